@@ -1,0 +1,227 @@
+"""Benchmark: device-resident batched CRC32C (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config headline|wal32k|blocks1m|host]
+
+One step = one launch of the batch kernel over one batch of blocks already
+resident in HBM (the headline batch: 10,000 x 4096 B). Consecutive steps read
+different windows of a >= 1 GiB rotation so every launch is cold in the
+256 MiB Infinity Cache. N > 1: one process per GPU (torchrun), every rank
+checksums its own 10k-block batch (independent slices, weak scaling, no
+collective on the data path); time = max over ranks of the barrier-bracketed
+K steps. Rank 0 prints ONE JSON line.
+
+roofline.achieved = algorithmic bytes per launch (nblocks x (block + 4 B
+CRC out)) / average kernel duration measured with HIP
+events on the launch stream. cpu_baseline = the reference's own
+util/crc32c.cc (compiled in place into oracle/_ref) timed on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+GIB = float(1 << 30)
+
+CONFIGS = {
+    # name: (nblocks, block_bytes, stride, crc_offset_in_block, description)
+    "headline": (10_000, 4096, 4096, 0, "10k x 4 KiB blocks (BASELINE headline)"),
+    "wal32k": (16_384, 32762, 32768, 6, "16384 x 32 KiB WAL blocks, CRC over [6, 32768) (config 3)"),
+    "blocks1m": (1_000_000, 4096, 4096, 0, "1M x 4 KiB blocks (config 4)"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return world, rank, local
+
+
+def cpu_baseline(seconds: float = 8.0):
+    """The reference's util/crc32c.cc (oracle/_ref, kind 'reference'), or the
+    oracle restatement (kind 'port') if the reference build is absent, on a
+    bounded sample of the headline workload."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    import oracle  # checker / baseline only
+
+    nb, L = 10_000, 4096
+    data = oracle.splitmix_bytes(0x1EDC6F41, nb * L)
+    if oracle.reference_available():
+        ref = oracle.Reference()
+        fn = lambda: ref.uniform(data, nb, L, threads=1)  # noqa: E731
+        kind = "reference"
+    else:
+        fn = lambda: oracle.uniform(data, nb, L, threads=1)  # noqa: E731
+        kind = "port"
+    fn()
+    best, t_end, passes = float("inf"), time.perf_counter() + seconds, 0
+    while time.perf_counter() < t_end:
+        t0 = time.perf_counter()
+        fn()
+        best = min(best, time.perf_counter() - t0)
+        passes += 1
+    gibs = nb * L / best / GIB
+    return {"value": round(gibs, 3), "unit": "GiB/s", "cores": 1, "kind": kind,
+            "sample": f"{nb} x {L} B splitmix64 blocks, 1 thread, best of {passes} passes "
+                      f"over {seconds:.0f} s (util/crc32c.cc -O3 -DNDEBUG)",
+            "cpu_model": _cpu_model()}
+
+
+def _cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def load_pmc_traffic():
+    p = REPO / "profiles" / "pmc_traffic.json"
+    if p.exists():
+        try:
+            return json.loads(p.read_text()).get("hbm_bytes_per_launch")
+        except (ValueError, OSError):
+            return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="headline", choices=sorted(CONFIGS))
+    ap.add_argument("--rotate-bytes", type=float, default=1.25 * GIB)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    args = ap.parse_args()
+
+    world, rank, local = dist_env()
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import __graft_entry__ as g
+    lvkv = g.load_package()
+
+    nb, L, stride, crc_off, desc = CONFIGS[args.config]
+    batch_bytes = nb * stride
+    nrot = max(1, int(np.ceil(args.rotate_bytes / batch_bytes)))
+    gen = torch.Generator(device=dev).manual_seed(0x1EDC6F41 + 17 * rank)
+    buf = torch.randint(0, 256, (nrot * batch_bytes + 64,), dtype=torch.uint8,
+                        device=dev, generator=gen)
+    outs = [torch.empty(nb, dtype=torch.int32, device=dev) for _ in range(2)]
+    stream = torch.cuda.current_stream(dev)
+
+    def launch(i):
+        w = i % nrot
+        base = buf[w * batch_bytes + crc_off:]
+        lvkv.crc32c_uniform(base, nb, L, stride, out=outs[i & 1], stream=stream)
+
+    # correctness spot check (outside the timed region) against the oracle
+    sys.path.insert(0, str(REPO / "oracle"))
+    import oracle
+    launch(0)
+    torch.cuda.synchronize()
+    check_n = min(nb, 2000)
+    host = buf[crc_off: crc_off + (check_n - 1) * stride + L].cpu().numpy()
+    want = oracle.uniform(host, check_n, L, stride, threads=8)
+    got = outs[0][:check_n].cpu().numpy().view(np.uint32)
+    if not np.array_equal(got, want):
+        raise SystemExit(f"bench: parity check FAILED on rank {rank}")
+
+    for i in range(args.warmup):
+        launch(i + 1)
+    torch.cuda.synchronize()
+
+    # per-launch kernel duration with HIP events on the launch stream
+    n_ev = min(args.steps, 100)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(n_ev)]
+    for i, (a, b) in enumerate(evs):
+        a.record(stream)
+        launch(i + 7)
+        b.record(stream)
+    torch.cuda.synchronize()
+    durs_ms = np.array([a.elapsed_time(b) for a, b in evs])
+    kern_ms = float(np.median(durs_ms))
+
+    # timed region: K back-to-back steps, barrier + sync on both sides
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        launch(i + 3)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ms_per_step = elapsed / args.steps * 1e3
+    data_bytes = nb * L
+    value = world * data_bytes * args.steps / elapsed / GIB
+    algo_bytes = nb * (L + 4)
+    achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.cpu_seconds)
+        traffic = load_pmc_traffic() if args.config == "headline" else None
+        line = {
+            "metric": "device-resident CRC32C GiB/s over 10k×4KiB blocks; % of MI355X HBM peak",
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (uniform random bytes, device-generated), resident in HBM",
+            "pct_hbm_peak": round(100.0 * value * GIB / 1e9 / HBM_PEAK_GBS, 2),
+            "config": {"workload": desc, "nblocks_per_gpu": nb, "block_bytes": L,
+                       "stride": stride, "rotation_buffers": nrot,
+                       "rotation_bytes": nrot * batch_bytes,
+                       "parallelism": f"{world} independent block slices (no collective)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "kernel_us_median": round(kern_ms * 1e3, 3),
+                         "kernel_us_min": round(float(durs_ms.min()) * 1e3, 3),
+                         "algo_bytes_per_launch": algo_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,118 @@
+/*
+ * lvkv_crc32c.h — C-ABI of the MI355X batched CRC32C engine for
+ * ArcueidType/LevelDB-KV-Separation (reference snapshot at /root/reference).
+ *
+ * Library: leveldb-kv-separation_amd/liblvkv_crc32c.so (built by
+ * __graft_entry__.build()). Plain pointers and sizes only; no C++ or torch
+ * types cross this boundary. Every function is reentrant; device state is
+ * initialised once per device on first use. Nothing here throws or aborts:
+ * failures are negative return codes (see lvkv_strerror).
+ *
+ * Which reference interface each entry replaces is cited per declaration.
+ * The C++ symbol leveldb::crc32c::Extend (util/crc32c.h:17) is exported by the
+ * same library; see INTEGRATION.md for the link recipe and FFI stubs.
+ */
+#ifndef LVKV_CRC32C_H_
+#define LVKV_CRC32C_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes ---------------------------------------------------- */
+#define LVKV_OK 0
+#define LVKV_ERR_INVALID (-1)   /* null pointer / bad argument            */
+#define LVKV_ERR_NO_DEVICE (-2) /* no HIP device (the batch API never falls
+                                   back to the CPU)                        */
+#define LVKV_ERR_HIP (-3)       /* HIP runtime error; see lvkv_last_hip_error */
+#define LVKV_ERR_RANGE (-4)     /* a block longer than 4 GiB - 1           */
+
+/* ---- flags ------------------------------------------------------------ */
+/* Store crc32c::Mask(crc) instead of crc (util/crc32c.h:29-32): the value
+ * TableBuilder::WriteRawBlock / log::Writer put on disk. */
+#define LVKV_FLAG_MASK 1u
+
+/* ---- per-call, host CPU: the drop-in for the reference's own symbols ---- */
+
+/* Replaces leveldb::crc32c::Extend (util/crc32c.h:17, util/crc32c.cc:276).
+ * CRC32C of A||data[0,n) given init_crc = CRC32C(A). Runs on the host CPU
+ * (SSE4.2 crc32 or portable slicing-by-8): one synchronous buffer per call is
+ * latency-bound, so a GPU round trip would lose. */
+uint32_t lvkv_crc32c_extend(uint32_t init_crc, const char* data, size_t n);
+/* Replaces leveldb::crc32c::Value (util/crc32c.h:20). */
+uint32_t lvkv_crc32c_value(const char* data, size_t n);
+/* Replace leveldb::crc32c::Mask / Unmask (util/crc32c.h:29-38). */
+uint32_t lvkv_crc32c_mask(uint32_t crc);
+uint32_t lvkv_crc32c_unmask(uint32_t masked_crc);
+
+/* ---- batched, device-resident (the GPU hot path) ---------------------- */
+/* All d_* pointers are device memory of the CURRENT HIP device; `stream` is a
+ * hipStream_t (NULL = the null stream). Calls are asynchronous on `stream`;
+ * results are valid after the stream is synchronised. No allocation or
+ * synchronisation happens inside, so the calls are graph-capturable after
+ * the first call on a device (which uploads the tables). */
+
+/* Batched leveldb::crc32c::Extend (util/crc32c.cc:276) over block i =
+ * d_base[d_offsets[i], d_offsets[i] + d_lengths[i]) with init
+ * d_init ? d_init[i] : init. Any offset alignment and length (0..4 GiB-1).
+ * d_out[i] = CRC (or Mask(CRC) with LVKV_FLAG_MASK). This is the loop of
+ * TableBuilder::WriteRawBlock (table/table_builder.cc:199-203) and
+ * log::Writer::EmitPhysicalRecord (db/log_writer.cc:94-95) run for many
+ * blocks in one launch. */
+int lvkv_crc32c_batch_device(const void* d_base, const uint64_t* d_offsets,
+                             const uint32_t* d_lengths, const uint32_t* d_init,
+                             uint32_t init, uint32_t* d_out, size_t nblocks,
+                             uint32_t flags, void* stream);
+
+/* Same, for nblocks blocks of `length` bytes at d_base + i*stride (no
+ * descriptor arrays; the benchmark's 10k x 4 KiB layout). */
+int lvkv_crc32c_uniform_device(const void* d_base, uint64_t stride,
+                               uint32_t length, uint32_t init, uint32_t* d_out,
+                               size_t nblocks, uint32_t flags, void* stream);
+
+/* Batched leveldb::ReadBlock checksum test (table/format.cc:92-99): block i
+ * is the BlockHandle {d_offsets[i], d_sizes[i]} of an SST image at d_file;
+ * the CRC covers contents + type byte (size+1 bytes) and is compared with
+ * Unmask(DecodeFixed32(trailer+1)). d_actual[i] = computed CRC (unmasked),
+ * d_status[i] = 0 on match, 1 on "block checksum mismatch". */
+int lvkv_sst_verify_device(const void* d_file, const uint64_t* d_offsets,
+                           const uint32_t* d_sizes, uint32_t* d_actual,
+                           uint8_t* d_status, size_t nblocks, void* stream);
+
+/* Batched log::Reader::ReadPhysicalRecord checksum test
+ * (db/log_reader.cc:217-247): record i has its 7-byte header at
+ * d_file + d_hdr_offsets[i]; the length is parsed on the device from header
+ * bytes 4..5, the CRC covers type byte + payload and is compared with
+ * Unmask(DecodeFixed32(header)). The caller guarantees header and payload
+ * are inside the image (the reader's "bad record length" check, :225-236). */
+int lvkv_log_verify_device(const void* d_file, const uint64_t* d_hdr_offsets,
+                           uint32_t* d_actual, uint8_t* d_status,
+                           size_t nrecords, void* stream);
+
+/* ---- batched, host-resident (end-to-end incl. PCIe) ------------------- */
+/* Blocks live in host memory (pageable or pinned). The library packs them
+ * into pinned staging buffers, copies them to the current device with
+ * hipMemcpyAsync in double-buffered chunks, runs the batch kernel and copies
+ * the CRCs back. Synchronous: returns when h_out is filled. This is the
+ * shape of a caller that reads blocks with pread (table/format.cc:78-80). */
+int lvkv_crc32c_batch_host(const void* h_base, const uint64_t* offsets,
+                           const uint32_t* lengths, const uint32_t* init_arr,
+                           uint32_t init, uint32_t* h_out, size_t nblocks,
+                           uint32_t flags);
+
+/* ---- diagnostics ------------------------------------------------------ */
+const char* lvkv_strerror(int code);
+int lvkv_last_hip_error(void);      /* hipError_t of the last LVKV_ERR_HIP */
+const char* lvkv_cpu_impl(void);    /* "sse4.2" or "portable-slice8"      */
+/* Number of workgroups (one per CU) the batch kernel launches on the current
+ * device, or a negative error code. */
+int lvkv_device_groups(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LVKV_CRC32C_H_ */

@@ -1,0 +1,281 @@
+"""MI355X batched CRC32C engine for ArcueidType/LevelDB-KV-Separation.
+
+Host-side mirror of the reference's checksum interface (util/crc32c.h:17-38)
+over the C-ABI in include/lvkv_crc32c.h, plus the batched device API that the
+SST writer/reader (table/table_builder.cc:199-203, table/format.cc:92-99) and
+WAL writer/reader (db/log_writer.cc:94-95, db/log_reader.cc:243-257) checksum
+paths map onto.
+
+The package directory name contains dashes, so import it through
+``load()`` (or ``importlib``); it registers itself as
+``leveldb_kv_separation_amd``. Every call goes to the native library
+``liblvkv_crc32c.so``; if it is missing, importing fails loudly — there is no
+Python or CPU fallback for the batch (GPU) path.
+"""
+from __future__ import annotations
+
+import ctypes
+from pathlib import Path
+from typing import Optional, Tuple
+
+__all__ = [
+    "Extend", "Value", "Mask", "Unmask", "kMaskDelta",
+    "crc32c_batch", "crc32c_uniform", "sst_verify", "log_verify",
+    "crc32c_batch_host", "LvkvError", "lib", "LIB_PATH", "device_groups",
+]
+
+LIB_PATH = Path(__file__).resolve().parent / "liblvkv_crc32c.so"
+kMaskDelta = 0xA282EAD8  # util/crc32c.h:22
+
+LVKV_OK = 0
+LVKV_FLAG_MASK = 1
+
+
+class LvkvError(RuntimeError):
+    """A C-ABI call returned a negative code (see lvkv_strerror)."""
+
+    def __init__(self, fn: str, code: int):
+        msg = _lib.lvkv_strerror(code).decode()
+        if code == -3:
+            msg += f" (hipError_t {_lib.lvkv_last_hip_error()})"
+        super().__init__(f"{fn}: {msg} [{code}]")
+        self.code = code
+
+
+def _load() -> ctypes.CDLL:
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"{LIB_PATH} is not built; run `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(the GPU path has no fallback)")
+    L = ctypes.CDLL(str(LIB_PATH))
+    u32, u64, sz, vp, i32 = (ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t,
+                             ctypes.c_void_p, ctypes.c_int)
+    L.lvkv_crc32c_extend.argtypes = [u32, ctypes.c_char_p, sz]
+    L.lvkv_crc32c_extend.restype = u32
+    L.lvkv_crc32c_value.argtypes = [ctypes.c_char_p, sz]
+    L.lvkv_crc32c_value.restype = u32
+    L.lvkv_crc32c_mask.argtypes = [u32]
+    L.lvkv_crc32c_mask.restype = u32
+    L.lvkv_crc32c_unmask.argtypes = [u32]
+    L.lvkv_crc32c_unmask.restype = u32
+    L.lvkv_crc32c_batch_device.argtypes = [vp, vp, vp, vp, u32, vp, sz, u32, vp]
+    L.lvkv_crc32c_batch_device.restype = i32
+    L.lvkv_crc32c_uniform_device.argtypes = [vp, u64, u32, u32, vp, sz, u32, vp]
+    L.lvkv_crc32c_uniform_device.restype = i32
+    L.lvkv_sst_verify_device.argtypes = [vp, vp, vp, vp, vp, sz, vp]
+    L.lvkv_sst_verify_device.restype = i32
+    L.lvkv_log_verify_device.argtypes = [vp, vp, vp, vp, sz, vp]
+    L.lvkv_log_verify_device.restype = i32
+    L.lvkv_crc32c_batch_host.argtypes = [vp, vp, vp, vp, u32, vp, sz, u32]
+    L.lvkv_crc32c_batch_host.restype = i32
+    L.lvkv_strerror.argtypes = [i32]
+    L.lvkv_strerror.restype = ctypes.c_char_p
+    L.lvkv_last_hip_error.argtypes = []
+    L.lvkv_last_hip_error.restype = i32
+    L.lvkv_cpu_impl.argtypes = []
+    L.lvkv_cpu_impl.restype = ctypes.c_char_p
+    L.lvkv_device_groups.argtypes = []
+    L.lvkv_device_groups.restype = i32
+    # Link-level drop-ins (C++ / Google ABI) — resolved to check they exist.
+    L.crc32c_extend.argtypes = [u32, ctypes.c_char_p, sz]
+    L.crc32c_extend.restype = u32
+    L.crc32c_value.argtypes = [ctypes.c_char_p, sz]
+    L.crc32c_value.restype = u32
+    return L
+
+
+_lib = _load()
+lib = _lib
+
+
+def _check(fn: str, rc: int) -> None:
+    if rc != LVKV_OK:
+        raise LvkvError(fn, rc)
+
+
+# --------------------------------------------------------------------------
+# util/crc32c.h mirror (per call, host)
+
+
+def _as_bytes(data) -> bytes:
+    if isinstance(data, (bytes, bytearray)):
+        return bytes(data)
+    if isinstance(data, str):
+        return data.encode()
+    return memoryview(data).tobytes()
+
+
+def Extend(init_crc: int, data, n: Optional[int] = None) -> int:
+    """leveldb::crc32c::Extend (util/crc32c.h:17): crc32c of A||data given
+    init_crc = crc32c(A)."""
+    b = _as_bytes(data)
+    if n is None:
+        n = len(b)
+    if n > len(b):
+        raise ValueError("n exceeds data length")
+    return int(_lib.lvkv_crc32c_extend(init_crc & 0xFFFFFFFF, b, n))
+
+
+def Value(data, n: Optional[int] = None) -> int:
+    """leveldb::crc32c::Value (util/crc32c.h:20)."""
+    return Extend(0, data, n)
+
+
+def Mask(crc: int) -> int:
+    """leveldb::crc32c::Mask (util/crc32c.h:29-32)."""
+    return int(_lib.lvkv_crc32c_mask(crc & 0xFFFFFFFF))
+
+
+def Unmask(masked_crc: int) -> int:
+    """leveldb::crc32c::Unmask (util/crc32c.h:35-38)."""
+    return int(_lib.lvkv_crc32c_unmask(masked_crc & 0xFFFFFFFF))
+
+
+def cpu_impl() -> str:
+    return _lib.lvkv_cpu_impl().decode()
+
+
+def device_groups() -> int:
+    g = int(_lib.lvkv_device_groups())
+    _check("lvkv_device_groups", g if g < 0 else 0)
+    return g
+
+
+# --------------------------------------------------------------------------
+# batched device API (torch tensors are only device-memory plumbing)
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _dev_ptr(t, name: str, dtype=None, numel: Optional[int] = None):
+    torch = _torch()
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise TypeError(f"{name} must be a CUDA (HIP) tensor")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if dtype is not None and t.dtype not in dtype:
+        raise TypeError(f"{name} must have dtype in {dtype}, got {t.dtype}")
+    if numel is not None and t.numel() < numel:
+        raise ValueError(f"{name} has {t.numel()} elements, need {numel}")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream_handle(stream, device):
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _u32_out(torch, n, device, out):
+    if out is None:
+        return torch.empty(n, dtype=torch.int32, device=device)
+    return out
+
+
+def crc32c_batch(buf, offsets, lengths, *, init: int = 0, inits=None,
+                 mask: bool = False, out=None, stream=None):
+    """Batched Extend over block i = buf[offsets[i] : offsets[i]+lengths[i]].
+
+    buf: uint8/int8 CUDA tensor; offsets: int64 CUDA tensor; lengths, inits:
+    int32 CUDA tensors (bit patterns of u32). Returns an int32 tensor of CRC
+    bit patterns (Mask()ed if mask=True)."""
+    torch = _torch()
+    n = offsets.numel()
+    if lengths.numel() != n:
+        raise ValueError("offsets and lengths differ in length")
+    out = _u32_out(torch, n, buf.device, out)
+    with torch.cuda.device(buf.device):
+        rc = _lib.lvkv_crc32c_batch_device(
+            _dev_ptr(buf, "buf", (torch.uint8, torch.int8)),
+            _dev_ptr(offsets, "offsets", (torch.int64,)),
+            _dev_ptr(lengths, "lengths", (torch.int32,)),
+            _dev_ptr(inits, "inits", (torch.int32,), n) if inits is not None else None,
+            init & 0xFFFFFFFF,
+            _dev_ptr(out, "out", (torch.int32,), n), n,
+            LVKV_FLAG_MASK if mask else 0, _stream_handle(stream, buf.device))
+    _check("lvkv_crc32c_batch_device", rc)
+    return out
+
+
+def crc32c_uniform(buf, nblocks: int, length: int, stride: Optional[int] = None, *,
+                   init: int = 0, mask: bool = False, out=None, stream=None):
+    """Batched Extend over nblocks blocks of `length` bytes at buf + i*stride."""
+    torch = _torch()
+    stride = length if stride is None else stride
+    if nblocks and (nblocks - 1) * stride + length > buf.numel():
+        raise ValueError("blocks exceed the buffer")
+    out = _u32_out(torch, nblocks, buf.device, out)
+    with torch.cuda.device(buf.device):
+        rc = _lib.lvkv_crc32c_uniform_device(
+            _dev_ptr(buf, "buf", (torch.uint8, torch.int8)), stride, length,
+            init & 0xFFFFFFFF, _dev_ptr(out, "out", (torch.int32,), nblocks),
+            nblocks, LVKV_FLAG_MASK if mask else 0,
+            _stream_handle(stream, buf.device))
+    _check("lvkv_crc32c_uniform_device", rc)
+    return out
+
+
+def sst_verify(file_buf, offsets, sizes, *, stream=None) -> Tuple["object", "object"]:
+    """Batched ReadBlock checksum test (table/format.cc:92-99) over the
+    BlockHandles {offsets[i], sizes[i]} of an SST image. Returns (actual crc
+    int32 tensor, status uint8 tensor: 0 ok / 1 'block checksum mismatch')."""
+    torch = _torch()
+    n = offsets.numel()
+    actual = torch.empty(n, dtype=torch.int32, device=file_buf.device)
+    status = torch.empty(n, dtype=torch.uint8, device=file_buf.device)
+    with torch.cuda.device(file_buf.device):
+        rc = _lib.lvkv_sst_verify_device(
+            _dev_ptr(file_buf, "file_buf", (torch.uint8, torch.int8)),
+            _dev_ptr(offsets, "offsets", (torch.int64,)),
+            _dev_ptr(sizes, "sizes", (torch.int32,), n),
+            _dev_ptr(actual, "actual"), _dev_ptr(status, "status"), n,
+            _stream_handle(stream, file_buf.device))
+    _check("lvkv_sst_verify_device", rc)
+    return actual, status
+
+
+def log_verify(file_buf, hdr_offsets, *, stream=None):
+    """Batched ReadPhysicalRecord checksum test (db/log_reader.cc:243-257)
+    over physical records whose 7-byte headers start at hdr_offsets[i]."""
+    torch = _torch()
+    n = hdr_offsets.numel()
+    actual = torch.empty(n, dtype=torch.int32, device=file_buf.device)
+    status = torch.empty(n, dtype=torch.uint8, device=file_buf.device)
+    with torch.cuda.device(file_buf.device):
+        rc = _lib.lvkv_log_verify_device(
+            _dev_ptr(file_buf, "file_buf", (torch.uint8, torch.int8)),
+            _dev_ptr(hdr_offsets, "hdr_offsets", (torch.int64,)),
+            _dev_ptr(actual, "actual"), _dev_ptr(status, "status"), n,
+            _stream_handle(stream, file_buf.device))
+    _check("lvkv_log_verify_device", rc)
+    return actual, status
+
+
+def crc32c_batch_host(data, offsets, lengths, *, init: int = 0, inits=None,
+                      mask: bool = False):
+    """Host-resident batch: numpy uint8 buffer + numpy offsets/lengths; the
+    library stages through pinned memory to the current device and back.
+    Returns a numpy uint32 array."""
+    import numpy as np
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+    n = offsets.size
+    if lengths.size != n:
+        raise ValueError("offsets and lengths differ in length")
+    if n and int((offsets + lengths).max()) > data.size:
+        raise ValueError("blocks exceed the buffer")
+    out = np.empty(n, dtype=np.uint32)
+    ip = None
+    if inits is not None:
+        inits = np.ascontiguousarray(inits, dtype=np.uint32)
+        ip = ctypes.c_void_p(inits.ctypes.data)
+    rc = _lib.lvkv_crc32c_batch_host(
+        ctypes.c_void_p(data.ctypes.data), ctypes.c_void_p(offsets.ctypes.data),
+        ctypes.c_void_p(lengths.ctypes.data), ip, init & 0xFFFFFFFF,
+        ctypes.c_void_p(out.ctypes.data), n, LVKV_FLAG_MASK if mask else 0)
+    _check("lvkv_crc32c_batch_host", rc)
+    return out

@@ -1,0 +1,87 @@
+"""In-tree build of liblvkv_crc32c.so (gfx950) and of the oracle checker.
+
+Used by __graft_entry__.build() and tests/conftest.py. Plain subprocess calls
+to hipcc / g++ / make — no cmake, no JIT cache outside the repo — so the built
+.so files travel with the repo snapshot to the GPU box.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+REPO = PKG.parent
+CSRC = PKG / "csrc"
+INCLUDE = REPO / "include"
+BUILD = REPO / "build" / "lvkv"
+LIB = PKG / "liblvkv_crc32c.so"
+ORACLE_DIR = REPO / "oracle"
+ORACLE_LIB = ORACLE_DIR / "liboracle_crc32c.so"
+REF_LIB = ORACLE_DIR / "_ref" / "libref_crc32c.so"
+REFERENCE = Path("/root/reference")
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("LVKV_OFFLOAD_ARCH", "gfx950")
+
+# Host-only C++ (no device code): built with g++.
+HOST_SOURCES = ["lvkv_tables.cpp", "lvkv_cpu_crc32c.cpp", "leveldb_crc32c_shim.cc"]
+# HIP sources: kernels and the runtime-facing C-ABI.
+HIP_SOURCES = ["crc32c_kernel.hip", "lvkv_capi.cpp"]
+HEADERS = ["lvkv_kernel_args.h", "lvkv_tables.h"]
+
+
+def _run(cmd: list[str], verbose: bool) -> None:
+    if verbose:
+        print("+", " ".join(str(c) for c in cmd), flush=True)
+    subprocess.run([str(c) for c in cmd], check=True)
+
+
+def _newer(target: Path, deps: list[Path]) -> bool:
+    if not target.exists():
+        return False
+    t = target.stat().st_mtime
+    return all(d.stat().st_mtime <= t for d in deps)
+
+
+def build_lib(verbose: bool = False, force: bool = False) -> Path:
+    deps = [CSRC / s for s in HOST_SOURCES + HIP_SOURCES + HEADERS]
+    deps += sorted(INCLUDE.glob("*.h")) + [Path(__file__)]
+    if not force and _newer(LIB, deps):
+        return LIB
+    BUILD.mkdir(parents=True, exist_ok=True)
+    objs = []
+    common = ["-O3", "-fPIC", "-std=c++17", "-Wall", "-I", INCLUDE, "-I", CSRC]
+    for src in HOST_SOURCES:
+        obj = BUILD / (Path(src).stem + ".o")
+        _run(["g++", *common, "-c", CSRC / src, "-o", obj], verbose)
+        objs.append(obj)
+    for src in HIP_SOURCES:
+        obj = BUILD / (Path(src).stem + ".hip.o")
+        _run([HIPCC, f"--offload-arch={ARCH}", *common, "-c", CSRC / src, "-o", obj], verbose)
+        objs.append(obj)
+    tmp = LIB.with_suffix(".so.tmp")
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp, "-lpthread"], verbose)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+def build_oracle(verbose: bool = False) -> Path:
+    """Build the C restatement (always) and the reference-backed checker
+    oracle/_ref (only where /root/reference exists, i.e. this container)."""
+    _run(["make", "-s", "-C", ORACLE_DIR, "all"], verbose)
+    if REFERENCE.is_dir() and shutil.which("g++"):
+        _run(["make", "-s", "-C", ORACLE_DIR, "ref", f"REF={REFERENCE}"], verbose)
+    return ORACLE_LIB
+
+
+def build_all(verbose: bool = False, force: bool = False) -> None:
+    build_lib(verbose=verbose, force=force)
+    build_oracle(verbose=verbose)
+
+
+if __name__ == "__main__":
+    import sys
+
+    build_all(verbose=True, force="--force" in sys.argv)

@@ -1,0 +1,439 @@
+// C-ABI of the batched CRC32C engine (declarations: include/lvkv_crc32c.h).
+//
+// Device state per HIP device (tables, CU count, staging for the host API) is
+// created once, lazily, under std::call_once; the per-call paths take no lock
+// and allocate nothing, so device-resident calls can be captured in a graph.
+// Errors are return codes: this library backs a -fno-exceptions caller
+// (reference CMakeLists.txt:71-77) and never throws or aborts.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "lvkv_crc32c.h"
+#include "lvkv_kernel_args.h"
+#include "lvkv_tables.h"
+
+namespace lvkv {
+
+hipError_t launch_crc32c_batch(const KernelArgs& args, int num_groups,
+                               hipStream_t stream);
+uint32_t cpu_crc32c_extend(uint32_t crc, const uint8_t* data, size_t n);
+const char* cpu_crc32c_impl_name();
+
+namespace {
+
+constexpr int kMaxDevices = 64;
+// Blocks per launch: the kernel indexes blocks with u32.
+constexpr size_t kMaxBlocksPerLaunch = size_t{1} << 30;
+
+// Host-API staging (double-buffered chunks).
+constexpr size_t kStageBytes = size_t{64} << 20;
+constexpr size_t kStageBlocks = 1u << 16;
+
+struct Stage {
+  uint8_t* h_data = nullptr;  // pinned
+  uint8_t* d_data = nullptr;
+  size_t cap = 0;
+  uint64_t* h_off = nullptr;  // pinned descriptors
+  uint32_t* h_len = nullptr;
+  uint32_t* h_init = nullptr;
+  uint32_t* h_out = nullptr;
+  uint64_t* d_off = nullptr;
+  uint32_t* d_len = nullptr;
+  uint32_t* d_init = nullptr;
+  uint32_t* d_out = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  size_t first = 0, count = 0;  // blocks of the batch held by this stage
+  bool busy = false;
+};
+
+struct DeviceCtx {
+  std::once_flag once;
+  int status = LVKV_ERR_NO_DEVICE;
+  int groups = 0;  // one workgroup per CU
+  uint32_t* d_tables = nullptr;
+  std::mutex host_mu;  // serialises lvkv_crc32c_batch_host per device
+  bool stages_ready = false;
+  Stage stage[2];
+};
+
+DeviceCtx g_dev[kMaxDevices];
+thread_local int t_last_hip_error = 0;
+
+int hip_fail(hipError_t e) {
+  t_last_hip_error = static_cast<int>(e);
+  return LVKV_ERR_HIP;
+}
+
+void init_ctx(DeviceCtx& c, int dev) {
+  int ncu = 0;
+  hipError_t e =
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess || ncu <= 0) {
+    c.status = hip_fail(e);
+    return;
+  }
+  std::vector<uint32_t> tab(kRowTabDwords + kLaneTabDwords);
+  build_row_table(tab.data());
+  build_lane_table(tab.data() + kRowTabDwords);
+  void* p = nullptr;
+  e = hipMalloc(&p, tab.size() * sizeof(uint32_t));
+  if (e != hipSuccess) {
+    c.status = hip_fail(e);
+    return;
+  }
+  e = hipMemcpy(p, tab.data(), tab.size() * sizeof(uint32_t),
+                hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(p);
+    c.status = hip_fail(e);
+    return;
+  }
+  c.d_tables = static_cast<uint32_t*>(p);
+  c.groups = ncu;
+  c.status = LVKV_OK;
+}
+
+DeviceCtx* current_ctx(int* rc) {
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count <= 0) {
+    t_last_hip_error = static_cast<int>(e);
+    *rc = LVKV_ERR_NO_DEVICE;
+    return nullptr;
+  }
+  int dev = -1;
+  e = hipGetDevice(&dev);
+  if (e != hipSuccess) {
+    *rc = hip_fail(e);
+    return nullptr;
+  }
+  if (dev < 0 || dev >= kMaxDevices) {
+    *rc = LVKV_ERR_INVALID;
+    return nullptr;
+  }
+  DeviceCtx& c = g_dev[dev];
+  std::call_once(c.once, [&] { init_ctx(c, dev); });
+  *rc = c.status;
+  return c.status == LVKV_OK ? &c : nullptr;
+}
+
+int run_batch(KernelArgs a, size_t nblocks, hipStream_t stream) {
+  if (nblocks == 0) return LVKV_OK;
+  int rc = LVKV_OK;
+  DeviceCtx* c = current_ctx(&rc);
+  if (c == nullptr) return rc;
+  a.row_tab = c->d_tables;
+  a.lane_tab = c->d_tables + kRowTabDwords;
+  for (size_t done = 0; done < nblocks;) {
+    const size_t n = std::min(nblocks - done, kMaxBlocksPerLaunch);
+    KernelArgs b = a;
+    b.nblocks = static_cast<uint32_t>(n);
+    if (a.offsets != nullptr) {
+      b.offsets = a.offsets + done;
+      if (a.lengths != nullptr) b.lengths = a.lengths + done;
+    } else {
+      b.base = a.base + done * a.stride;
+    }
+    if (a.inits != nullptr) b.inits = a.inits + done;
+    b.out_crc = a.out_crc + done;
+    if (a.out_status != nullptr) b.out_status = a.out_status + done;
+    const size_t want = (n + kWavesPerGroup - 1) / kWavesPerGroup;
+    const int groups = static_cast<int>(
+        std::min<size_t>(static_cast<size_t>(c->groups), want));
+    hipError_t e = launch_crc32c_batch(b, groups, stream);
+    if (e != hipSuccess) return hip_fail(e);
+    done += n;
+  }
+  return LVKV_OK;
+}
+
+KernelArgs blank_args() {
+  KernelArgs a;
+  memset(&a, 0, sizeof(a));
+  return a;
+}
+
+// ---- host-resident pipeline ------------------------------------------
+
+void free_stage(Stage& s) {
+  if (s.h_data) (void)hipHostFree(s.h_data);
+  if (s.d_data) (void)hipFree(s.d_data);
+  s.h_data = s.d_data = nullptr;
+  s.cap = 0;
+}
+
+int alloc_stage_data(Stage& s, size_t cap) {
+  free_stage(s);
+  hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&s.h_data), cap,
+                               hipHostMallocDefault);
+  if (e != hipSuccess) return hip_fail(e);
+  e = hipMalloc(reinterpret_cast<void**>(&s.d_data), cap);
+  if (e != hipSuccess) return hip_fail(e);
+  s.cap = cap;
+  return LVKV_OK;
+}
+
+int ensure_stages(DeviceCtx& c, size_t need_bytes) {
+  const size_t cap = std::max(kStageBytes, (need_bytes + 4095) & ~size_t{4095});
+  for (Stage& s : c.stage) {
+    if (!c.stages_ready) {
+      hipError_t e;
+      if ((e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) !=
+          hipSuccess)
+        return hip_fail(e);
+      if ((e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming)) !=
+          hipSuccess)
+        return hip_fail(e);
+      const size_t nb = kStageBlocks;
+      if ((e = hipHostMalloc(reinterpret_cast<void**>(&s.h_off), nb * 8,
+                             hipHostMallocDefault)) != hipSuccess ||
+          (e = hipHostMalloc(reinterpret_cast<void**>(&s.h_len), nb * 4,
+                             hipHostMallocDefault)) != hipSuccess ||
+          (e = hipHostMalloc(reinterpret_cast<void**>(&s.h_init), nb * 4,
+                             hipHostMallocDefault)) != hipSuccess ||
+          (e = hipHostMalloc(reinterpret_cast<void**>(&s.h_out), nb * 4,
+                             hipHostMallocDefault)) != hipSuccess ||
+          (e = hipMalloc(reinterpret_cast<void**>(&s.d_off), nb * 8)) !=
+              hipSuccess ||
+          (e = hipMalloc(reinterpret_cast<void**>(&s.d_len), nb * 4)) !=
+              hipSuccess ||
+          (e = hipMalloc(reinterpret_cast<void**>(&s.d_init), nb * 4)) !=
+              hipSuccess ||
+          (e = hipMalloc(reinterpret_cast<void**>(&s.d_out), nb * 4)) !=
+              hipSuccess)
+        return hip_fail(e);
+    }
+    if (s.cap < cap) {
+      int rc = alloc_stage_data(s, cap);
+      if (rc != LVKV_OK) return rc;
+    }
+  }
+  c.stages_ready = true;
+  return LVKV_OK;
+}
+
+// Copy blocks into the pinned buffer; big chunks are split over threads.
+void pack_parallel(uint8_t* dst, const uint8_t* src, const uint64_t* src_off,
+                   const uint32_t* len, const uint64_t* dst_off, size_t n,
+                   size_t bytes) {
+  const size_t kPerThread = size_t{8} << 20;
+  unsigned hw = std::thread::hardware_concurrency();
+  size_t nt = std::min<size_t>(hw ? hw : 1, 16);
+  nt = std::min(nt, std::max<size_t>(1, bytes / kPerThread));
+  auto work = [&](size_t t) {
+    for (size_t i = t; i < n; i += nt)
+      memcpy(dst + dst_off[i], src + src_off[i], len[i]);
+  };
+  if (nt <= 1) {
+    work(0);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < nt; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+}
+
+int drain_stage(Stage& s, uint32_t* h_out) {
+  if (!s.busy) return LVKV_OK;
+  hipError_t e = hipEventSynchronize(s.done);
+  s.busy = false;
+  if (e != hipSuccess) return hip_fail(e);
+  memcpy(h_out + s.first, s.h_out, s.count * sizeof(uint32_t));
+  return LVKV_OK;
+}
+
+}  // namespace
+}  // namespace lvkv
+
+using namespace lvkv;
+
+extern "C" {
+
+uint32_t lvkv_crc32c_extend(uint32_t init_crc, const char* data, size_t n) {
+  return cpu_crc32c_extend(init_crc, reinterpret_cast<const uint8_t*>(data), n);
+}
+
+uint32_t lvkv_crc32c_value(const char* data, size_t n) {
+  return cpu_crc32c_extend(0, reinterpret_cast<const uint8_t*>(data), n);
+}
+
+uint32_t lvkv_crc32c_mask(uint32_t crc) {
+  return ((crc >> 15) | (crc << 17)) + kMaskDelta;
+}
+
+uint32_t lvkv_crc32c_unmask(uint32_t masked_crc) {
+  const uint32_t r = masked_crc - kMaskDelta;
+  return (r >> 17) | (r << 15);
+}
+
+int lvkv_crc32c_batch_device(const void* d_base, const uint64_t* d_offsets,
+                             const uint32_t* d_lengths, const uint32_t* d_init,
+                             uint32_t init, uint32_t* d_out, size_t nblocks,
+                             uint32_t flags, void* stream) {
+  if (nblocks == 0) return LVKV_OK;
+  if (!d_base || !d_offsets || !d_lengths || !d_out) return LVKV_ERR_INVALID;
+  KernelArgs a = blank_args();
+  a.base = static_cast<const uint8_t*>(d_base);
+  a.offsets = d_offsets;
+  a.lengths = d_lengths;
+  a.inits = d_init;
+  a.init = init;
+  a.out_crc = d_out;
+  a.mode = kModeCompute;
+  a.mask = (flags & LVKV_FLAG_MASK) ? 1u : 0u;
+  return run_batch(a, nblocks, static_cast<hipStream_t>(stream));
+}
+
+int lvkv_crc32c_uniform_device(const void* d_base, uint64_t stride,
+                               uint32_t length, uint32_t init, uint32_t* d_out,
+                               size_t nblocks, uint32_t flags, void* stream) {
+  if (nblocks == 0) return LVKV_OK;
+  if (!d_base || !d_out) return LVKV_ERR_INVALID;
+  KernelArgs a = blank_args();
+  a.base = static_cast<const uint8_t*>(d_base);
+  a.stride = stride;
+  a.length = length;
+  a.init = init;
+  a.out_crc = d_out;
+  a.mode = kModeCompute;
+  a.mask = (flags & LVKV_FLAG_MASK) ? 1u : 0u;
+  return run_batch(a, nblocks, static_cast<hipStream_t>(stream));
+}
+
+int lvkv_sst_verify_device(const void* d_file, const uint64_t* d_offsets,
+                           const uint32_t* d_sizes, uint32_t* d_actual,
+                           uint8_t* d_status, size_t nblocks, void* stream) {
+  if (nblocks == 0) return LVKV_OK;
+  if (!d_file || !d_offsets || !d_sizes || !d_actual || !d_status)
+    return LVKV_ERR_INVALID;
+  KernelArgs a = blank_args();
+  a.base = static_cast<const uint8_t*>(d_file);
+  a.offsets = d_offsets;
+  a.lengths = d_sizes;
+  a.out_crc = d_actual;
+  a.out_status = d_status;
+  a.mode = kModeSstVerify;
+  return run_batch(a, nblocks, static_cast<hipStream_t>(stream));
+}
+
+int lvkv_log_verify_device(const void* d_file, const uint64_t* d_hdr_offsets,
+                           uint32_t* d_actual, uint8_t* d_status,
+                           size_t nrecords, void* stream) {
+  if (nrecords == 0) return LVKV_OK;
+  if (!d_file || !d_hdr_offsets || !d_actual || !d_status)
+    return LVKV_ERR_INVALID;
+  KernelArgs a = blank_args();
+  a.base = static_cast<const uint8_t*>(d_file);
+  a.offsets = d_hdr_offsets;
+  a.out_crc = d_actual;
+  a.out_status = d_status;
+  a.mode = kModeLogVerify;
+  return run_batch(a, nrecords, static_cast<hipStream_t>(stream));
+}
+
+int lvkv_crc32c_batch_host(const void* h_base, const uint64_t* offsets,
+                           const uint32_t* lengths, const uint32_t* init_arr,
+                           uint32_t init, uint32_t* h_out, size_t nblocks,
+                           uint32_t flags) {
+  if (nblocks == 0) return LVKV_OK;
+  if (!h_base || !offsets || !lengths || !h_out) return LVKV_ERR_INVALID;
+  int rc = LVKV_OK;
+  DeviceCtx* c = current_ctx(&rc);
+  if (c == nullptr) return rc;
+  std::lock_guard<std::mutex> lock(c->host_mu);
+  size_t biggest = 0;
+  for (size_t i = 0; i < nblocks; ++i)
+    biggest = std::max<size_t>(biggest, lengths[i]);
+  rc = ensure_stages(*c, biggest + 8);
+  if (rc != LVKV_OK) return rc;
+  const uint8_t* src = static_cast<const uint8_t*>(h_base);
+
+  size_t next = 0;
+  int k = 0;
+  std::vector<uint64_t> src_off;
+  while (next < nblocks) {
+    Stage& s = c->stage[k];
+    rc = drain_stage(s, h_out);
+    if (rc != LVKV_OK) return rc;
+    // Pack blocks so each one ENDS on a 4-byte boundary (the kernel's
+    // aligned fast path), as many as fit.
+    size_t n = 0, cursor = 0;
+    src_off.clear();
+    while (next + n < nblocks && n < kStageBlocks) {
+      const size_t len = lengths[next + n];
+      const size_t end = (cursor + len + 3) & ~size_t{3};
+      if (end > s.cap) break;
+      s.h_off[n] = end - len;
+      s.h_len[n] = static_cast<uint32_t>(len);
+      s.h_init[n] = init_arr ? init_arr[next + n] : init;
+      src_off.push_back(offsets[next + n]);
+      cursor = end;
+      ++n;
+    }
+    pack_parallel(s.h_data, src, src_off.data(), s.h_len, s.h_off, n, cursor);
+    hipError_t e;
+    if ((e = hipMemcpyAsync(s.d_data, s.h_data, cursor, hipMemcpyHostToDevice,
+                            s.stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(s.d_off, s.h_off, n * 8, hipMemcpyHostToDevice,
+                            s.stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(s.d_len, s.h_len, n * 4, hipMemcpyHostToDevice,
+                            s.stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(s.d_init, s.h_init, n * 4, hipMemcpyHostToDevice,
+                            s.stream)) != hipSuccess)
+      return hip_fail(e);
+    rc = lvkv_crc32c_batch_device(s.d_data, s.d_off, s.d_len, s.d_init, 0,
+                                  s.d_out, n, flags, s.stream);
+    if (rc != LVKV_OK) return rc;
+    if ((e = hipMemcpyAsync(s.h_out, s.d_out, n * 4, hipMemcpyDeviceToHost,
+                            s.stream)) != hipSuccess ||
+        (e = hipEventRecord(s.done, s.stream)) != hipSuccess)
+      return hip_fail(e);
+    s.first = next;
+    s.count = n;
+    s.busy = true;
+    next += n;
+    k ^= 1;
+  }
+  for (Stage& s : c->stage) {
+    rc = drain_stage(s, h_out);
+    if (rc != LVKV_OK) return rc;
+  }
+  return LVKV_OK;
+}
+
+const char* lvkv_strerror(int code) {
+  switch (code) {
+    case LVKV_OK:
+      return "ok";
+    case LVKV_ERR_INVALID:
+      return "invalid argument";
+    case LVKV_ERR_NO_DEVICE:
+      return "no HIP device available (the batch API has no CPU fallback)";
+    case LVKV_ERR_HIP:
+      return "HIP runtime error";
+    case LVKV_ERR_RANGE:
+      return "block too large";
+    default:
+      return "unknown error";
+  }
+}
+
+int lvkv_last_hip_error(void) { return t_last_hip_error; }
+
+const char* lvkv_cpu_impl(void) { return cpu_crc32c_impl_name(); }
+
+int lvkv_device_groups(void) {
+  int rc = LVKV_OK;
+  DeviceCtx* c = current_ctx(&rc);
+  return c ? c->groups : rc;
+}
+
+}  // extern "C"

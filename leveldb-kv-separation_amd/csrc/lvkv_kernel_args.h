@@ -1,0 +1,64 @@
+// Shared host/device definitions for the batched CRC32C engine.
+//
+// LDS image of one workgroup (gfx950: 160 KiB per CU, all of it used):
+//
+//   [0, 128 KiB)    row operator Z_256 ("advance the CRC register over 256
+//                   zero bytes") as four byte tables A_t[i] = Z_256(i << 8t),
+//                   each replicated 32x so that lane l always reads bank l%32:
+//                   byte address (t, i, copy c) =
+//                       (t >> 1) * 64 KiB + i * 256 + (t & 1) * 128 + c * 4
+//   [128, 160 KiB)  per-lane end shift Z_{256-4s} as eight nibble tables,
+//                   private to lane s:  byte address (k, nib, s) =
+//                       128 KiB + ((k * 16 + nib) * 64 + s) * 4
+//
+// The tables are generated on the host (lvkv_tables.cpp) and copied once per
+// device; each workgroup of the persistent grid replicates them into LDS.
+#ifndef LVKV_KERNEL_ARGS_H_
+#define LVKV_KERNEL_ARGS_H_
+
+#include <stdint.h>
+
+namespace lvkv {
+
+constexpr int kWaveLanes = 64;
+constexpr int kWavesPerGroup = 16;
+constexpr int kGroupThreads = kWaveLanes * kWavesPerGroup;  // 1024
+constexpr int kRowBytes = 256;      // one wave-wide row: 64 lanes x 4 B
+constexpr int kRowsPerChunk = 16;   // one pipeline stage = 4 KiB per wave
+constexpr uint32_t kRowTabDwords = 4 * 256;
+constexpr uint32_t kLaneTabDwords = 8 * 16 * 64;
+constexpr uint32_t kLdsRowRegionBytes = 64 * 1024;
+constexpr uint32_t kLdsLaneTabBase = 128 * 1024;
+constexpr uint32_t kLdsBytes = 160 * 1024;
+
+constexpr uint32_t kCastagnoliReflected = 0x82f63b78u;
+constexpr uint32_t kMaskDelta = 0xa282ead8u;  // util/crc32c.h:22
+
+// Kernel modes (KernelArgs::mode).
+enum : uint32_t {
+  kModeCompute = 0,    // out_crc[i] = Extend(init_i, base + off_i, len_i)
+  kModeSstVerify = 1,  // table/format.cc:92-99: covers n+1, trailer after it
+  kModeLogVerify = 2,  // db/log_reader.cc:243-257: header at off, len parsed
+};
+
+struct KernelArgs {
+  const uint8_t* base;        // device bytes all offsets are relative to
+  const uint64_t* offsets;    // per-block offsets; nullptr = uniform stride
+  const uint32_t* lengths;    // per-block lengths (ignored in uniform mode)
+  const uint32_t* inits;      // per-block init CRCs; nullptr = `init`
+  uint64_t stride;            // uniform mode: block i at base + i*stride
+  uint32_t length;            // uniform mode length
+  uint32_t init;              // init CRC when inits == nullptr
+  uint32_t* out_crc;          // nblocks u32 (masked if `mask`)
+  uint8_t* out_status;        // verify modes: 0 = match, 1 = mismatch
+  const uint32_t* row_tab;    // kRowTabDwords
+  const uint32_t* lane_tab;   // kLaneTabDwords, already in LDS order
+  uint32_t nblocks;
+  uint32_t mode;
+  uint32_t mask;              // 1: store Mask(crc) (util/crc32c.h:29-32)
+  uint32_t pad_;
+};
+
+}  // namespace lvkv
+
+#endif  // LVKV_KERNEL_ARGS_H_
