@@ -6,6 +6,7 @@
 #ifndef LVKV_CRC32C_DEBUG_H_
 #define LVKV_CRC32C_DEBUG_H_
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -17,6 +18,29 @@ extern "C" {
  * Z_d = advance the reflected CRC32C register over d zero bytes.
  * Either pointer may be NULL. */
 void lvkv_debug_tables(uint32_t* row_tab, uint32_t* lane_tab);
+
+/* Timing probes (tools/probe.py). Launch a variant of the batch kernel on the
+ * uniform layout: variant bit 1 = no table work, 2 = no global loads, 4 = no
+ * LDS fill, 8 = shuffle-based wave reduction, 16 = empty kernel, 32 = the
+ * uniform end-aligned specialisation (combines with 1, 2, 4), 64 = record
+ * per-wave timestamps (see lvkv_debug_set_stamps), 256 = the dedicated
+ * uniform kernel (crc32c_uniform.hip; combines with 64, and 128 = row tables
+ * before the loads), 512 (with 256) = its one-round small-batch kernel;
+ * 0, 8, 32, 96, 256, 320, 384, 448, 768, 832, 896, 960 compute correct CRCs.
+ * groups <= 0 uses one workgroup per CU. Returns an LVKV_* code. */
+int lvkv_debug_uniform_variant(int variant, int groups, const void* d_base,
+                               uint64_t stride, uint32_t length,
+                               uint32_t* d_out, size_t nblocks, void* stream);
+
+/* Timestamp buffer for variant bit 64: 8 u64 per wave (grid waves x 8). */
+void lvkv_debug_set_stamps(uint64_t* d_stamps);
+
+/* Read `bytes` (multiple of 16) of device memory once, 16 B per lane, grid
+ * stride over `groups` x 256 threads (0: 8 per CU; negative: -groups blocks
+ * reading 4 B per lane instead): the measured HBM read ceiling. d_scratch
+ * receives at most one u32. */
+int lvkv_debug_read_bw(const void* d_data, uint64_t bytes, uint32_t* d_scratch,
+                       int groups, void* stream);
 
 #ifdef __cplusplus
 }

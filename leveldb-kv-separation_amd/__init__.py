@@ -36,13 +36,22 @@ class LvkvError(RuntimeError):
 
     def __init__(self, fn: str, code: int):
         msg = _lib.lvkv_strerror(code).decode()
-        if code == -3:
+        if code in (-2, -3):
             msg += f" (hipError_t {_lib.lvkv_last_hip_error()})"
         super().__init__(f"{fn}: {msg} [{code}]")
         self.code = code
 
 
 def _load() -> ctypes.CDLL:
+    # One HIP runtime per process: torch bundles its own libamdhip64.so.7.
+    # Loading torch FIRST makes this library's NEEDED libamdhip64.so.7 bind to
+    # that same (already loaded) runtime, so device pointers and streams are
+    # shared. Loading this library first would map /opt/rocm's runtime and
+    # torch would then map a second one (device enumeration then fails).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not LIB_PATH.exists():
         raise ImportError(
             f"{LIB_PATH} is not built; run `python -c 'import __graft_entry__ as g; g.build()'` "

@@ -34,52 +34,45 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "crc32c_device_common.h"
 #include "lvkv_kernel_args.h"
 
 namespace lvkv {
 namespace {
 
-typedef __attribute__((address_space(4))) const uint32_t ConstU32;
 
-constexpr uint32_t kBufferDword3 = 0x00020000u;  // gfx9 raw buffer config
-constexpr uint32_t kOobOffset = 0x80000000u;     // >= any num_records
+// Cache policy of the block loads: nt (non-temporal). Block bytes are read
+// exactly once; streaming them with nt keeps the 36 KiB of tables that every
+// workgroup reloads at kernel start resident in the XCD's L2 across launches
+// (without it the table loads miss and queue behind the whole batch in HBM).
+constexpr int kDataCachePolicy = 2;
 
-__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+// Probe variants (timing experiments only; results are wrong except for 0
+// and kProbeShflReduce). Bits combine.
+enum : int {
+  kProbeNone = 0,
+  kProbeNoCompute = 1,    // loads + xor of the words, no LDS table work
+  kProbeNoLoads = 2,      // no global loads, words = lane constants
+  kProbeNoFill = 4,       // skip the LDS table fill
+  kProbeShflReduce = 8,   // wave reduction via ds_bpermute shuffles
+  kProbeEmpty = 16,       // return at once: launch + dispatch cost only
+  // Not a probe: the uniform-stride specialisation (every block `length`
+  // bytes at base + i*stride, every block END 4-byte aligned, length >= 4,
+  // compute mode). All geometry is loop-invariant except the block address.
+  kUniformAligned = 32,
+  kProbeStamps = 64,      // record s_memrealtime per wave at phase edges
+  kProbeLateLoads = 128,  // issue the first round only after the LDS fill
+};
 
-typedef __attribute__((address_space(4))) const uint64_t ConstU64;
-
-// Wave-uniform dword load through the scalar cache. `addr` must be 4-aligned.
-__device__ __forceinline__ uint32_t sload32(uint64_t addr) {
-  return *reinterpret_cast<ConstU32*>(addr);
-}
-// Wave-uniform element loads of the descriptor arrays (s_load, lgkmcnt).
-__device__ __forceinline__ uint32_t sload_u32(const uint32_t* p, uint32_t i) {
-  return reinterpret_cast<ConstU32*>(reinterpret_cast<uint64_t>(p))[i];
-}
-__device__ __forceinline__ uint64_t sload_u64(const uint64_t* p, uint32_t i) {
-  return reinterpret_cast<ConstU64*>(reinterpret_cast<uint64_t>(p))[i];
-}
-
-// Wave-uniform little-endian load of n (1..4) bytes at any address, touching
-// only the dwords that contain [addr, addr + n).
-__device__ __forceinline__ uint32_t sload_le(uint64_t addr, uint32_t n) {
-  const uint64_t a0 = addr & ~uint64_t{3};
-  const uint64_t a1 = (addr + n - 1) & ~uint64_t{3};
-  const uint32_t lo = sload32(a0);
-  const uint32_t hi = (a1 != a0) ? sload32(a1) : 0u;
-  const uint32_t sh = static_cast<uint32_t>(addr & 3u) * 8u;
-  const uint64_t v = (static_cast<uint64_t>(hi) << 32) | lo;
-  uint32_t r = static_cast<uint32_t>(v >> sh);
-  if (n < 4) r &= (1u << (8u * n)) - 1u;
-  return r;
-}
-
-__device__ __forceinline__ uint32_t crc_mask(uint32_t c) {
-  return ((c >> 15) | (c << 17)) + kMaskDelta;
-}
-__device__ __forceinline__ uint32_t crc_unmask(uint32_t m) {
-  const uint32_t r = m - kMaskDelta;
-  return (r >> 17) | (r << 15);
+// Probe timeline: lane 0 of each wave writes 8 u64 slots (100 MHz realtime
+// clock): 0 entry, 1 after the LDS fill barrier, 2.. after each round
+// (capped), 7 exit.
+template <int V>
+__device__ __forceinline__ void stamp(const KernelArgs& a, uint32_t gw, int slot) {
+  if (V & kProbeStamps) {
+    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63u) == 0) a.stamps[gw * 8u + slot] = t;
+  }
 }
 
 // Wave-uniform geometry of one block (lives in SGPRs).
@@ -105,10 +98,16 @@ struct Geo {
   __device__ __forceinline__ uint64_t ptr() const {
     return (static_cast<uint64_t>(ptr_hi) << 32) | ptr_lo;
   }
+  // The descriptor inputs go through readfirstlane so the compiler can prove
+  // the SRD wave-uniform; otherwise it wraps every buffer load in a
+  // waterfall loop (cdna_hip_programming.md T20).
   __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const {
-    const uint64_t b = (static_cast<uint64_t>(b4_hi) << 32) | b4_lo;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(b4_lo);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(b4_hi);
+    const uint32_t n = __builtin_amdgcn_readfirstlane(nrec);
+    const uint64_t b = (static_cast<uint64_t>(hi) << 32) | lo;
     return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(b), 0,
-                                             static_cast<int>(nrec),
+                                             static_cast<int>(n),
                                              kBufferDword3);
   }
 };
@@ -140,7 +139,35 @@ __device__ __forceinline__ Geo null_geo() {
   return g;
 }
 
+template <int V>
 __device__ __forceinline__ Geo make_geo(const KernelArgs& a, uint32_t b) {
+  if (V & kUniformAligned) {
+    // Same shape for every block; only the window base moves.
+    Geo g;
+    const uint32_t len = a.length;
+    const uint32_t q = (len + 3u) >> 2;
+    const uint32_t rows = (q + 63u) >> 6;
+    g.delta = 4u * q - len;
+    g.s0l = 64u * rows - q;
+    g.s0 = a.init ^ 0xffffffffu;
+    g.spill = g.delta ? (g.s0 >> (32u - 8u * g.delta)) : 0u;
+    g.e = 0;
+    g.tiny = 0;
+    g.len = len;
+    g.expected = 0;
+    g.nrec = (b < a.nblocks) ? 4u * q : 0u;
+    g.vb0 = -4 * static_cast<int32_t>(g.s0l);
+    g.rows = rows;
+    g.nchunks = (rows + kRowsPerChunk - 1) / kRowsPerChunk;
+    const uint64_t ptr = reinterpret_cast<uint64_t>(a.base) +
+                         static_cast<uint64_t>(b) * a.stride;
+    const uint64_t b4 = ptr - g.delta;  // end-aligned: floor4(ptr)
+    g.ptr_lo = static_cast<uint32_t>(ptr);
+    g.ptr_hi = static_cast<uint32_t>(ptr >> 32);
+    g.b4_lo = static_cast<uint32_t>(b4);
+    g.b4_hi = static_cast<uint32_t>(b4 >> 32);
+    return g;
+  }
   if (b >= a.nblocks) return null_geo();
   const uint64_t base = reinterpret_cast<uint64_t>(a.base);
   uint64_t off;
@@ -213,25 +240,33 @@ __device__ __forceinline__ Geo make_geo(const KernelArgs& a, uint32_t b) {
   return g;
 }
 
+template <int V>
 __device__ __forceinline__ Item next_item(const KernelArgs& a, const Item& it,
-                                          uint32_t nwaves) {
+                                          uint32_t block_stride) {
   Item n;
   if (it.chunk + 1 < it.g.nchunks) {
     n.block = it.block;
     n.chunk = it.chunk + 1;
     n.g = it.g;
   } else {
-    n.block = it.block + nwaves;
+    n.block = it.block + block_stride;
     n.chunk = 0;
-    n.g = make_geo(a, n.block);
+    n.g = make_geo<V>(a, n.block);
   }
   return n;
 }
 
 // Issue the 16 row loads of one chunk plus, for lane 0 only, the first dword
 // of the row after it (the high neighbour of lane 63 when re-aligning).
+template <int V>
 __device__ __forceinline__ void issue(uint32_t (&buf)[kRowsPerChunk + 1],
                                       const Item& it) {
+  if (V & kProbeNoLoads) {
+#pragma unroll
+    for (int j = 0; j <= kRowsPerChunk; ++j)
+      buf[j] = (lane_id() * 0x9E3779B1u) ^ (j * 0x85EBCA6Bu) ^ it.block;
+    return;
+  }
   const int32_t row0 =
       it.g.vb0 + kRowBytes * kRowsPerChunk * static_cast<int32_t>(it.chunk);
   const uint32_t lane = lane_id();
@@ -243,7 +278,7 @@ __device__ __forceinline__ void issue(uint32_t (&buf)[kRowsPerChunk + 1],
 #pragma unroll
     for (int j = 0; j < kRowsPerChunk; ++j)
       buf[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, vo + 256 * j,
-                                                    0, 0);
+                                                    0, kDataCachePolicy);
   } else {
     // Some lanes start before the block: keep each offset whole so that the
     // bounds check sees the negative (= huge) value.
@@ -251,108 +286,49 @@ __device__ __forceinline__ void issue(uint32_t (&buf)[kRowsPerChunk + 1],
     for (int j = 0; j < kRowsPerChunk; ++j) {
       int32_t o = vo + 256 * j;
       asm volatile("" : "+v"(o));
-      buf[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, o, 0, 0);
+      buf[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, o, 0, kDataCachePolicy);
     }
   }
   int32_t o16 = row0 + 256 * kRowsPerChunk;
   o16 = (lane == 0 && o16 >= 0) ? o16 : static_cast<int32_t>(kOobOffset);
   asm volatile("" : "+v"(o16));
   buf[kRowsPerChunk] =
-      __builtin_amdgcn_raw_buffer_load_b32(rsrc, o16, 0, 0);
+      __builtin_amdgcn_raw_buffer_load_b32(rsrc, o16, 0, kDataCachePolicy);
 }
 
-__device__ __forceinline__ uint32_t lds_ld(const uint32_t* lds,
-                                           uint32_t byte_addr) {
-  return *reinterpret_cast<const uint32_t*>(
-      reinterpret_cast<const char*>(lds) + byte_addr);
-}
-
-// S -> Z_256(S): one bank-private LDS lookup per byte of S.
-// k0 = (lane & 31) * 4, k1 = k0 | 0x10000. v_perm_b32 builds
-// {k.byte0, S.byte_t, k.byte2, 0} = S.byte_t * 256 + copy*4 + region.
-__device__ __forceinline__ uint32_t row_advance(const uint32_t* lds,
-                                                uint32_t s, uint32_t k0,
-                                                uint32_t k1) {
-  const uint32_t a0 = __builtin_amdgcn_perm(s, k0, 0x0C020400u);
-  const uint32_t a1 = __builtin_amdgcn_perm(s, k0, 0x0C020500u);
-  const uint32_t a2 = __builtin_amdgcn_perm(s, k1, 0x0C020600u);
-  const uint32_t a3 = __builtin_amdgcn_perm(s, k1, 0x0C020700u);
-  return lds_ld(lds, a0) ^ lds_ld(lds, a1 + 128u) ^ lds_ld(lds, a2) ^
-         lds_ld(lds, a3 + 128u);
-}
-
-// S -> Z_{256-4s}(S) for this lane s: eight lane-private nibble lookups.
-__device__ __forceinline__ uint32_t lane_end_shift(const uint32_t* lds,
-                                                   uint32_t s,
-                                                   uint32_t lane_base) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const uint32_t nib = (s >> (4 * k)) & 15u;
-    r ^= lds_ld(lds, (lane_base | (nib << 8)) + 4096u * k);
-  }
-  return r;
-}
-
-__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v ^= __shfl_xor(v, m, 64);
-  return v;
-}
-
-// Word j of a chunk, re-aligned to the grid when the block end is not
-// 4-byte aligned (the high neighbour of lane s is lane s+1's dword; lane 63
-// takes lane 0's dword of the next row).
-template <bool kMisaligned>
-__device__ __forceinline__ uint32_t grid_word(
-    const uint32_t (&buf)[kRowsPerChunk + 1], int j, uint32_t lane,
-    uint32_t nb_addr, uint32_t e) {
-  if (!kMisaligned) return buf[j];
-  const uint32_t src = (lane == 0) ? buf[j + 1] : buf[j];
-  const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(
-      static_cast<int>(nb_addr), static_cast<int>(src)));
-  return __builtin_amdgcn_alignbyte(hi, buf[j], e);
-}
-
-// Row 0 of a block: zero the words before the block, clear the padding bytes
-// of the first data word and xor in the init state (s0) at the first data
-// byte; the high part of s0 spills into the next word.
-__device__ __forceinline__ uint32_t fix_row0(uint32_t w, const Geo& g,
-                                            uint32_t lane) {
-  const uint32_t sh = 8u * g.delta;
-  w = (lane < g.s0l) ? 0u : w;
-  w = (lane == g.s0l) ? ((w & (0xffffffffu << sh)) ^ (g.s0 << sh)) : w;
-  w = (lane == g.s0l + 1u) ? (w ^ g.spill) : w;
-  return w;
-}
-
-template <bool kMisaligned>
-__device__ __forceinline__ uint32_t consume_rows(
-    const uint32_t* lds, const uint32_t (&buf)[kRowsPerChunk + 1],
-    const Item& it, uint32_t s, uint32_t k0, uint32_t k1) {
+// Prepare a loaded chunk in place, before any table work (so it overlaps the
+// other stream's lookups):
+//  * blocks whose end is not 4-byte aligned: re-align every row to the grid
+//    (high neighbour of lane s = lane s+1's dword; lane 63 takes lane 0's
+//    dword of the next row, the extra slot for the last row);
+//  * chunk 0: zero the words before the block, clear the padding bytes of the
+//    first data word and xor the init state s0 into the first 4 data bytes;
+//    the high part of s0 spills into the next word (row 1, lane 0 when the
+//    first data word is lane 63's).
+template <int V>
+__device__ __forceinline__ void prep_chunk(uint32_t (&buf)[kRowsPerChunk + 1],
+                                           const Item& it) {
   const uint32_t lane = lane_id();
-  const uint32_t nb_addr = ((lane + 1u) & 63u) * 4u;
-  const uint32_t e = it.g.e;
-  const uint32_t left = it.g.rows - kRowsPerChunk * it.chunk;  // >= 1
-  uint32_t w = grid_word<kMisaligned>(buf, 0, lane, nb_addr, e);
-  if (it.chunk == 0) {
-    s = fix_row0(w, it.g, lane);
-  } else {
-    s = row_advance(lds, s, k0, k1) ^ w;
-  }
-  if (left > 1) {
-    w = grid_word<kMisaligned>(buf, 1, lane, nb_addr, e);
-    if (it.chunk == 0 && it.g.s0l == 63u) w = (lane == 0) ? (w ^ it.g.spill) : w;
-    s = row_advance(lds, s, k0, k1) ^ w;
-  }
+  if (!(V & kUniformAligned) && it.g.e != 0) {
+    const int nb_addr = static_cast<int>(((lane + 1u) & 63u) * 4u);
 #pragma unroll
-  for (int j = 2; j < kRowsPerChunk; ++j) {
-    if (static_cast<uint32_t>(j) < left) {  // wave-uniform
-      w = grid_word<kMisaligned>(buf, j, lane, nb_addr, e);
-      s = row_advance(lds, s, k0, k1) ^ w;
+    for (int j = 0; j < kRowsPerChunk; ++j) {
+      const uint32_t src = (lane == 0) ? buf[j + 1] : buf[j];
+      const uint32_t hi = static_cast<uint32_t>(
+          __builtin_amdgcn_ds_bpermute(nb_addr, static_cast<int>(src)));
+      buf[j] = __builtin_amdgcn_alignbyte(hi, buf[j], it.g.e);
     }
   }
-  return s;
+  if (it.chunk == 0) {
+    const Geo& g = it.g;
+    const uint32_t sh = 8u * g.delta;
+    uint32_t w = buf[0];
+    w = (lane < g.s0l) ? 0u : w;
+    w = (lane == g.s0l) ? ((w & (0xffffffffu << sh)) ^ (g.s0 << sh)) : w;
+    w = (lane == g.s0l + 1u) ? (w ^ g.spill) : w;
+    buf[0] = w;
+    if (g.s0l == 63u) buf[1] = (lane == 0) ? (buf[1] ^ g.spill) : buf[1];
+  }
 }
 
 __device__ __forceinline__ uint32_t tiny_crc(const Geo& g) {
@@ -369,18 +345,11 @@ __device__ __forceinline__ uint32_t tiny_crc(const Geo& g) {
   return reg ^ 0xffffffffu;
 }
 
-__device__ __forceinline__ void finish_block(const KernelArgs& a,
-                                             const uint32_t* lds,
-                                             const Item& it, uint32_t s,
-                                             uint32_t lane_base) {
-  uint32_t crc;
-  if (it.g.tiny) {
-    crc = tiny_crc(it.g);
-  } else {
-    crc = wave_xor(lane_end_shift(lds, s, lane_base)) ^ 0xffffffffu;
-  }
+template <int V>
+__device__ __forceinline__ void store_result(const KernelArgs& a,
+                                             const Item& it, uint32_t crc) {
   if (lane_id() == 0) {
-    if (a.mode == kModeCompute) {
+    if ((V & kUniformAligned) || a.mode == kModeCompute) {
       a.out_crc[it.block] = a.mask ? crc_mask(crc) : crc;
     } else {
       a.out_crc[it.block] = crc;
@@ -389,33 +358,119 @@ __device__ __forceinline__ void finish_block(const KernelArgs& a,
   }
 }
 
-__device__ __forceinline__ uint32_t consume(const KernelArgs& a,
-                                           const uint32_t* lds,
-                                           const uint32_t (&buf)[kRowsPerChunk + 1],
-                                           const Item& it, uint32_t s,
-                                           uint32_t k0, uint32_t k1,
-                                           uint32_t lane_base) {
-  if (!it.g.tiny) {
-    if (it.g.e == 0)
-      s = consume_rows<false>(lds, buf, it, s, k0, k1);
-    else
-      s = consume_rows<true>(lds, buf, it, s, k0, k1);
+template <int V>
+__device__ __forceinline__ uint32_t finish_value(const uint32_t* lds,
+                                                 uint32_t s,
+                                                 uint32_t lane_base) {
+  if (V & kProbeNoCompute) return wave_xor_dpp(s);
+  if (V & kProbeShflReduce)
+    return wave_xor_shfl(lane_end_shift(lds, s, lane_base)) ^ 0xffffffffu;
+  return wave_xor_dpp(lane_end_shift(lds, s, lane_base)) ^ 0xffffffffu;
+}
+
+// One round: the current chunk of stream A and of stream B, two independent
+// Horner chains interleaved row by row (latency of one chain hides behind the
+// other's LDS lookups). A stream whose block is past the batch is idle.
+template <int V>
+__device__ __forceinline__ void consume2(
+    const KernelArgs& a, const uint32_t* lds,
+    uint32_t (&ba)[kRowsPerChunk + 1], const Item& ia, uint32_t& sa,
+    uint32_t (&bb)[kRowsPerChunk + 1], const Item& ib, uint32_t& sb,
+    uint32_t k0, uint32_t k1, uint32_t lane_base) {
+  const bool live_a = ia.block < a.nblocks;
+  const bool live_b = ib.block < a.nblocks;
+  const bool rows_a = live_a && ((V & kUniformAligned) || !ia.g.tiny);
+  const bool rows_b = live_b && ((V & kUniformAligned) || !ib.g.tiny);
+  if (V & kProbeNoCompute) {
+#pragma unroll
+    for (int j = 0; j < kRowsPerChunk; ++j) {
+      sa ^= ba[j];
+      sb ^= bb[j];
+    }
+  } else {
+    if (rows_a) prep_chunk<V>(ba, ia);
+    if (rows_b) prep_chunk<V>(bb, ib);
+    const uint32_t na =
+        rows_a ? min(static_cast<uint32_t>(kRowsPerChunk),
+                     ia.g.rows - kRowsPerChunk * ia.chunk)
+               : 0u;
+    const uint32_t nb =
+        rows_b ? min(static_cast<uint32_t>(kRowsPerChunk),
+                     ib.g.rows - kRowsPerChunk * ib.chunk)
+               : 0u;
+    // Row 0 of the chunk: starts the chain (chunk 0) or continues it.
+    if (na != 0) sa = (ia.chunk == 0) ? ba[0] : row_step(lds, sa, ba[0], k0, k1);
+    if (nb != 0) sb = (ib.chunk == 0) ? bb[0] : row_step(lds, sb, bb[0], k0, k1);
+    if (na == kRowsPerChunk && nb == kRowsPerChunk) {
+      // Straight-line body: both chains in one basic block.
+#pragma unroll
+      for (int j = 1; j < kRowsPerChunk; ++j) {
+        sa = row_step(lds, sa, ba[j], k0, k1);
+        sb = row_step(lds, sb, bb[j], k0, k1);
+      }
+    } else {
+      // Ragged chunks: both chains up to the shorter one, then the rest of
+      // each (three simple loops unroll fully; one three-way loop does not).
+      const uint32_t nab = min(na, nb);
+#pragma unroll
+      for (int j = 1; j < kRowsPerChunk; ++j) {
+        if (static_cast<uint32_t>(j) < nab) {
+          sa = row_step(lds, sa, ba[j], k0, k1);
+          sb = row_step(lds, sb, bb[j], k0, k1);
+        }
+      }
+#pragma unroll
+      for (int j = 1; j < kRowsPerChunk; ++j) {
+        const uint32_t u = static_cast<uint32_t>(j);
+        if (u >= nab && u < na) sa = row_step(lds, sa, ba[j], k0, k1);
+      }
+#pragma unroll
+      for (int j = 1; j < kRowsPerChunk; ++j) {
+        const uint32_t u = static_cast<uint32_t>(j);
+        if (u >= nab && u < nb) sb = row_step(lds, sb, bb[j], k0, k1);
+      }
+    }
   }
-  if (it.chunk + 1 == it.g.nchunks) finish_block(a, lds, it, s, lane_base);
-  return s;
+  const bool fin_a = live_a && ia.chunk + 1 == ia.g.nchunks;
+  const bool fin_b = live_b && ib.chunk + 1 == ib.g.nchunks;
+  if (fin_a && fin_b && ((V & kUniformAligned) || (!ia.g.tiny && !ib.g.tiny))) {
+    const uint32_t ca = finish_value<V>(lds, sa, lane_base);
+    const uint32_t cb = finish_value<V>(lds, sb, lane_base);
+    store_result<V>(a, ia, ca);
+    store_result<V>(a, ib, cb);
+  } else {
+    if (fin_a)
+      store_result<V>(a, ia, (!(V & kUniformAligned) && ia.g.tiny)
+                                 ? tiny_crc(ia.g) : finish_value<V>(lds, sa, lane_base));
+    if (fin_b)
+      store_result<V>(a, ib, (!(V & kUniformAligned) && ib.g.tiny)
+                                 ? tiny_crc(ib.g) : finish_value<V>(lds, sb, lane_base));
+  }
 }
 
 }  // namespace
 
+// Persistent grid, one 1024-thread workgroup per CU (all 160 KiB of LDS).
+// Wave gw runs two block streams: A = blocks gw, gw + 2W, ... and
+// B = blocks gw + W, gw + 3W, ... (W = waves in the grid); each stream walks
+// its blocks in 4 KiB chunks and keeps one chunk in flight while the current
+// chunks of both streams are consumed.
+template <int V>
 __global__ void __launch_bounds__(kGroupThreads, 1)
     crc32c_batch_kernel(KernelArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
 
+  if (V & kProbeEmpty) {
+    if (a.nblocks == 0xffffffffu) lds[threadIdx.x] = 0;  // keep the LDS request
+    return;
+  }
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = lane_id();
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t nwaves = gridDim.x * kWavesPerGroup;
   const uint32_t gw = blockIdx.x * kWavesPerGroup + wave;
+  const uint32_t stream_stride = 2u * nwaves;
+  stamp<V>(a, gw, 0);
 
   // 1. table values for this thread's share of the LDS image (L2 hits).
   constexpr int kRowIters = (kLdsRowRegionBytes * 2 / 16) / kGroupThreads;  // 8
@@ -424,6 +479,7 @@ __global__ void __launch_bounds__(kGroupThreads, 1)
   uint32_t lv[kLaneIters][4];
 #pragma unroll
   for (int k = 0; k < kRowIters; ++k) {
+    if (V & kProbeNoFill) break;
     const uint32_t dw = (tid + kGroupThreads * k) * 4u;
     const uint32_t t = ((dw >> 14) << 1) | ((dw >> 5) & 1u);
     const uint32_t i = (dw >> 6) & 255u;
@@ -431,56 +487,179 @@ __global__ void __launch_bounds__(kGroupThreads, 1)
   }
 #pragma unroll
   for (int k = 0; k < kLaneIters; ++k) {
+    if (V & kProbeNoFill) break;
     const uint32_t* src = a.lane_tab + 4u * (tid + kGroupThreads * k);
 #pragma unroll
     for (int x = 0; x < 4; ++x) lv[k][x] = src[x];
   }
+  // Every wave's table loads enter the CU's memory queue before any block
+  // load of the workgroup; otherwise they queue behind the batch's block
+  // stream and the fill (on every wave's critical path) waits ~5 us.
+  __builtin_amdgcn_sched_barrier(0);
+  if (!(V & kProbeNoFill)) __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
 
-  // 2. first two pipeline stages in flight before the LDS fill.
-  uint32_t bufA[kRowsPerChunk + 1], bufB[kRowsPerChunk + 1];
-  Item ia;
-  ia.block = gw;
-  ia.chunk = 0;
-  ia.g = make_geo(a, gw);
-  issue(bufA, ia);
-  Item ib = next_item(a, ia, nwaves);
-  issue(bufB, ib);
+  // 2. both streams' first chunk in flight before the LDS fill. Only one
+  //    round: the table loads + 34 block loads stay under the 63 loads the
+  //    vmcnt counter can track, so the fill waits for its table values only
+  //    (with both rounds in flight the wait before the first ds_write would
+  //    cover most of the block data).
+  uint32_t a0[kRowsPerChunk + 1], a1[kRowsPerChunk + 1];
+  uint32_t b0[kRowsPerChunk + 1], b1[kRowsPerChunk + 1];
+  Item ia0, ib0;
+  ia0.block = gw;
+  ia0.chunk = 0;
+  ia0.g = make_geo<V>(a, ia0.block);
+  ib0.block = gw + nwaves;
+  ib0.chunk = 0;
+  ib0.g = make_geo<V>(a, ib0.block);
+  if (!(V & kProbeLateLoads)) {
+    issue<V>(a0, ia0);
+    issue<V>(b0, ib0);
+  }
   __builtin_amdgcn_sched_barrier(0);
 
   // 3. LDS fill: row tables replicated 4 copies per ds_write_b128.
+  if (!(V & kProbeNoFill)) {
 #pragma unroll
-  for (int k = 0; k < kRowIters; ++k)
-    reinterpret_cast<uint4*>(lds)[tid + kGroupThreads * k] =
-        make_uint4(rv[k], rv[k], rv[k], rv[k]);
+    for (int k = 0; k < kRowIters; ++k)
+      reinterpret_cast<uint4*>(lds)[tid + kGroupThreads * k] =
+          make_uint4(rv[k], rv[k], rv[k], rv[k]);
 #pragma unroll
-  for (int k = 0; k < kLaneIters; ++k)
-    reinterpret_cast<uint4*>(lds + kLdsLaneTabBase / 4)[tid + kGroupThreads * k] =
-        make_uint4(lv[k][0], lv[k][1], lv[k][2], lv[k][3]);
+    for (int k = 0; k < kLaneIters; ++k)
+      reinterpret_cast<uint4*>(lds + kLdsLaneTabBase / 4)[tid + kGroupThreads * k] =
+          make_uint4(lv[k][0], lv[k][1], lv[k][2], lv[k][3]);
+  }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  stamp<V>(a, gw, 1);
+
+  if (V & kProbeLateLoads) {
+    issue<V>(a0, ia0);
+    issue<V>(b0, ib0);
+  }
+  // 4. second round in flight.
+  Item ia1 = next_item<V>(a, ia0, stream_stride);
+  Item ib1 = next_item<V>(a, ib0, stream_stride);
+  issue<V>(a1, ia1);
+  issue<V>(b1, ib1);
 
   const uint32_t k0 = (lane & 31u) * 4u;
   const uint32_t k1 = k0 | 0x10000u;
   const uint32_t lane_base = kLdsLaneTabBase + lane * 4u;
 
-  uint32_t s = 0;
+  uint32_t sa = 0, sb = 0;
+  int round = 0;
   while (true) {
-    if (ia.block >= a.nblocks) break;
-    s = consume(a, lds, bufA, ia, s, k0, k1, lane_base);
-    ia = next_item(a, ib, nwaves);
-    issue(bufA, ia);
-    if (ib.block >= a.nblocks) break;
-    s = consume(a, lds, bufB, ib, s, k0, k1, lane_base);
-    ib = next_item(a, ia, nwaves);
-    issue(bufB, ib);
+    if (ia0.block >= a.nblocks && ib0.block >= a.nblocks) break;
+    consume2<V>(a, lds, a0, ia0, sa, b0, ib0, sb, k0, k1, lane_base);
+    if (V & kProbeStamps) stamp<V>(a, gw, 2 + min(round++, 4));
+    ia0 = next_item<V>(a, ia1, stream_stride);
+    ib0 = next_item<V>(a, ib1, stream_stride);
+    issue<V>(a0, ia0);
+    issue<V>(b0, ib0);
+    if (ia1.block >= a.nblocks && ib1.block >= a.nblocks) break;
+    consume2<V>(a, lds, a1, ia1, sa, b1, ib1, sb, k0, k1, lane_base);
+    if (V & kProbeStamps) stamp<V>(a, gw, 2 + min(round++, 4));
+    ia1 = next_item<V>(a, ia0, stream_stride);
+    ib1 = next_item<V>(a, ib0, stream_stride);
+    issue<V>(a1, ia1);
+    issue<V>(b1, ib1);
   }
+  stamp<V>(a, gw, 7);
 }
 
-// Host-side launcher (compiled in this TU so the kernel symbol stays local).
-hipError_t launch_crc32c_batch(const KernelArgs& args, int num_groups,
-                               hipStream_t stream) {
-  hipLaunchKernelGGL(crc32c_batch_kernel, dim3(num_groups),
-                     dim3(kGroupThreads), 0, stream, args);
+// Read-bandwidth ceiling: every byte read once with 16 B per lane, grid
+// stride; nothing is stored unless the xor of the data hits a magic value, so
+// the loads cannot be dropped. Used to state the measured HBM ceiling next to
+// the 8 TB/s spec.
+// 4 B per lane variant of the same (the batch kernel's load width).
+__global__ void __launch_bounds__(256)
+    read_bw_dword_kernel(const uint32_t* __restrict__ p, uint64_t n4,
+                         uint32_t* out) {
+  const uint64_t nth = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  uint32_t acc = 0;
+  for (; i + 7 * nth < n4; i += 8 * nth) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc ^= p[i + k * nth];
+  }
+  for (; i < n4; i += nth) acc ^= p[i];
+  if (acc == 0x9E3779B9u) out[0] = acc;
+}
+
+__global__ void __launch_bounds__(256)
+    read_bw_kernel(const uint4* __restrict__ p, uint64_t n16, uint32_t* out) {
+  const uint64_t nth = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  for (; i + 3 * nth < n16; i += 4 * nth) {
+    const uint4 x0 = p[i], x1 = p[i + nth], x2 = p[i + 2 * nth], x3 = p[i + 3 * nth];
+    acc.x ^= x0.x ^ x1.x ^ x2.x ^ x3.x;
+    acc.y ^= x0.y ^ x1.y ^ x2.y ^ x3.y;
+    acc.z ^= x0.z ^ x1.z ^ x2.z ^ x3.z;
+    acc.w ^= x0.w ^ x1.w ^ x2.w ^ x3.w;
+  }
+  for (; i < n16; i += nth) {
+    const uint4 x = p[i];
+    acc.x ^= x.x; acc.y ^= x.y; acc.z ^= x.z; acc.w ^= x.w;
+  }
+  if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9E3779B9u) out[0] = acc.x;
+}
+
+// Host-side launchers (compiled in this TU so the kernel symbols stay local).
+hipError_t launch_crc32c_batch(const KernelArgs& args, bool uniform_aligned,
+                               int num_groups, hipStream_t stream) {
+  if (uniform_aligned) {
+    hipLaunchKernelGGL(crc32c_batch_kernel<kUniformAligned>, dim3(num_groups),
+                       dim3(kGroupThreads), 0, stream, args);
+  } else {
+    hipLaunchKernelGGL(crc32c_batch_kernel<kProbeNone>, dim3(num_groups),
+                       dim3(kGroupThreads), 0, stream, args);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_crc32c_probe(const KernelArgs& args, int variant,
+                               int num_groups, hipStream_t stream) {
+  switch (variant) {
+#define LVKV_PROBE_CASE(v)                                                  \
+  case v:                                                                   \
+    hipLaunchKernelGGL(crc32c_batch_kernel<v>, dim3(num_groups),            \
+                       dim3(kGroupThreads), 0, stream, args);               \
+    break;
+    LVKV_PROBE_CASE(0)
+    LVKV_PROBE_CASE(1)
+    LVKV_PROBE_CASE(2)
+    LVKV_PROBE_CASE(3)
+    LVKV_PROBE_CASE(4)
+    LVKV_PROBE_CASE(5)
+    LVKV_PROBE_CASE(6)
+    LVKV_PROBE_CASE(8)
+    LVKV_PROBE_CASE(16)
+    LVKV_PROBE_CASE(32)
+    LVKV_PROBE_CASE(33)
+    LVKV_PROBE_CASE(34)
+    LVKV_PROBE_CASE(38)
+    LVKV_PROBE_CASE(96)
+    LVKV_PROBE_CASE(97)
+    LVKV_PROBE_CASE(160)
+    LVKV_PROBE_CASE(224)
+#undef LVKV_PROBE_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_read_bw(const void* p, uint64_t bytes, uint32_t* out,
+                          int num_groups, hipStream_t stream) {
+  if (num_groups < 0) {  // negative: the dword-per-lane variant
+    hipLaunchKernelGGL(read_bw_dword_kernel, dim3(-num_groups), dim3(256), 0,
+                       stream, static_cast<const uint32_t*>(p), bytes / 4, out);
+  } else {
+    hipLaunchKernelGGL(read_bw_kernel, dim3(num_groups), dim3(256), 0, stream,
+                       static_cast<const uint4*>(p), bytes / 16, out);
+  }
   return hipGetLastError();
 }
 

@@ -1,0 +1,564 @@
+// Uniform-layout batch CRC32C for gfx950: nblocks blocks of `length` bytes at
+// base + i*stride, every block END 4-byte aligned (the benchmark's 10k x 4 KiB
+// batch, an SST region of equal-size blocks, 32 KiB WAL blocks at +6).
+//
+// Same arithmetic as crc32c_kernel.hip (see its header): end-aligned word
+// grid, Horner over 256-byte rows with the Z_256 LDS tables, per-lane end
+// shift Z_{256-4s}, wave xor-reduce. What differs is the schedule, built from
+// measurements (tools/timeline.py, tools/probe.py):
+//
+//  * The row tables are GENERATED in-kernel from the 32 columns of Z_256
+//    passed as kernel arguments: loading them from memory at kernel start put
+//    them behind the whole batch's block stream (fill done at ~6 us).
+//  * The lane tables (32 KiB) are loaded after the first round's block loads
+//    and written to LDS only when the first finished blocks are flushed (one
+//    barrier per wave, at its first flush or at exit).
+//  * Finished blocks are queued (up to 4) and flushed together, so their
+//    lane-shift lookups and reductions interleave.
+//  * Loads: 16 dword loads per 4 KiB chunk (no re-alignment slot), chunks of
+//    the next round issued unconditionally (out-of-range chunks read nothing)
+//    so the compiler's vmcnt bookkeeping stays exact; at most 2 rounds = 64
+//    loads in flight per wave.
+//  * Two block streams per wave (A: gw, gw+2W, ...; B: gw+W, gw+3W, ...), their
+//    row chains interleaved, as in the general kernel.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "crc32c_device_common.h"
+#include "lvkv_kernel_args.h"
+
+namespace lvkv {
+namespace {
+
+constexpr int kUniCachePolicy = 2;  // nt: block bytes are read once
+
+enum : int {
+  kUniProbeStamps = 64,
+  kUniFillFirst = 128,  // probe: generate the row tables before any load
+  kUniNoCompute = 1,    // probe: xor the words instead of the table walk
+  kUniNoLoads = 2,      // probe: synthetic words instead of block loads
+};
+
+struct UniGeo {  // wave-uniform, loop-invariant
+  uint32_t rows, nchunks, delta, s0l, s0, spill, nrec;
+  int32_t vb0;
+};
+
+struct Cursor {  // one block stream: current block and chunk
+  uint32_t block;
+  uint32_t chunk;
+};
+
+__device__ __forceinline__ UniGeo uni_geo(const UniformArgs& a) {
+  UniGeo g;
+  const uint32_t q = (a.length + 3u) >> 2;
+  g.rows = (q + 63u) >> 6;
+  g.nchunks = (g.rows + kRowsPerChunk - 1) / kRowsPerChunk;
+  g.delta = 4u * q - a.length;
+  g.s0l = 64u * g.rows - q;
+  g.s0 = a.init ^ 0xffffffffu;
+  g.spill = g.delta ? (g.s0 >> (32u - 8u * g.delta)) : 0u;
+  g.nrec = 4u * q;
+  g.vb0 = -4 * static_cast<int32_t>(g.s0l);
+  return g;
+}
+
+__device__ __forceinline__ Cursor advance(const Cursor& c, const UniGeo& g,
+                                          uint32_t block_stride) {
+  Cursor n;
+  const bool same = c.chunk + 1 < g.nchunks;
+  n.block = same ? c.block : c.block + block_stride;
+  n.chunk = same ? c.chunk + 1 : 0u;
+  return n;
+}
+
+// 16 row loads of one chunk; a chunk past the batch gets an empty window so
+// its loads return zeros without touching memory (keeps the issue count, and
+// so the compiler's vmcnt accounting, the same on every path).
+template <int P>
+__device__ __forceinline__ void issue16(uint32_t (&buf)[kRowsPerChunk],
+                                        const UniformArgs& a, const UniGeo& g,
+                                        const Cursor& c) {
+  if (P & kUniNoLoads) {
+#pragma unroll
+    for (int j = 0; j < kRowsPerChunk; ++j)
+      buf[j] = (lane_id() * 0x9E3779B1u) ^ (static_cast<uint32_t>(j) * 0x85EBCA6Bu) ^ c.block;
+    return;
+  }
+  const bool valid = c.block < a.nblocks;
+  const uint64_t ptr = reinterpret_cast<uint64_t>(a.base) +
+                       static_cast<uint64_t>(valid ? c.block : 0u) * a.stride -
+                       g.delta;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(ptr));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(ptr >> 32));
+  const uint32_t n = __builtin_amdgcn_readfirstlane(valid ? g.nrec : 0u);
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0,
+      static_cast<int>(n), kBufferDword3);
+  const int32_t row0 = g.vb0 + kRowBytes * kRowsPerChunk * static_cast<int32_t>(c.chunk);
+  const int32_t vo = row0 + 4 * static_cast<int32_t>(lane_id());
+  if (row0 >= 0) {
+#pragma unroll
+    for (int j = 0; j < kRowsPerChunk; ++j)
+      buf[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, vo + 256 * j, 0,
+                                                    kUniCachePolicy);
+  } else {
+#pragma unroll
+    for (int j = 0; j < kRowsPerChunk; ++j) {
+      int32_t o = vo + 256 * j;
+      asm volatile("" : "+v"(o));
+      buf[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, o, 0, kUniCachePolicy);
+    }
+  }
+}
+
+// Row-0 fix-ups of a block's first chunk (see prep_chunk in crc32c_kernel.hip).
+__device__ __forceinline__ void fix_first_chunk(uint32_t (&buf)[kRowsPerChunk],
+                                                const UniGeo& g) {
+  const uint32_t lane = lane_id();
+  const uint32_t sh = 8u * g.delta;
+  uint32_t w = buf[0];
+  w = (lane < g.s0l) ? 0u : w;
+  w = (lane == g.s0l) ? ((w & (0xffffffffu << sh)) ^ (g.s0 << sh)) : w;
+  w = (lane == g.s0l + 1u) ? (w ^ g.spill) : w;
+  buf[0] = w;
+  if (g.s0l == 63u) buf[1] = (lane == 0) ? (buf[1] ^ g.spill) : buf[1];
+}
+
+// Horner rows of the current chunks of streams A and B, interleaved.
+__device__ __forceinline__ void rows2(const uint32_t* lds,
+                                      uint32_t (&ba)[kRowsPerChunk], uint32_t na,
+                                      bool first_a, uint32_t& sa,
+                                      uint32_t (&bb)[kRowsPerChunk], uint32_t nb,
+                                      bool first_b, uint32_t& sb,
+                                      uint32_t k0, uint32_t k1) {
+  if (na != 0) sa = first_a ? ba[0] : row_step(lds, sa, ba[0], k0, k1);
+  if (nb != 0) sb = first_b ? bb[0] : row_step(lds, sb, bb[0], k0, k1);
+  if (na == kRowsPerChunk && nb == kRowsPerChunk) {
+#pragma unroll
+    for (int j = 1; j < kRowsPerChunk; ++j) {
+      sa = row_step(lds, sa, ba[j], k0, k1);
+      sb = row_step(lds, sb, bb[j], k0, k1);
+    }
+  } else {
+    const uint32_t nab = min(na, nb);
+#pragma unroll
+    for (int j = 1; j < kRowsPerChunk; ++j) {
+      if (static_cast<uint32_t>(j) < nab) {
+        sa = row_step(lds, sa, ba[j], k0, k1);
+        sb = row_step(lds, sb, bb[j], k0, k1);
+      }
+    }
+#pragma unroll
+    for (int j = 1; j < kRowsPerChunk; ++j) {
+      const uint32_t u = static_cast<uint32_t>(j);
+      if (u >= nab && u < na) sa = row_step(lds, sa, ba[j], k0, k1);
+    }
+#pragma unroll
+    for (int j = 1; j < kRowsPerChunk; ++j) {
+      const uint32_t u = static_cast<uint32_t>(j);
+      if (u >= nab && u < nb) sb = row_step(lds, sb, bb[j], k0, k1);
+    }
+  }
+}
+
+// Finished-block queue (static register slots, shifted on push).
+struct Pending {
+  uint32_t s0, s1, s2, s3;  // per-lane Horner states
+  uint32_t b0, b1, b2, b3;  // block indices (uniform)
+  uint32_t count;
+};
+
+template <int P>
+__device__ __forceinline__ void stamp_uni(const UniformArgs& a, uint32_t gw, int slot) {
+  if (P & kUniProbeStamps) {
+    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    if (lane_id() == 0) a.stamps[gw * 8u + slot] = t;
+  }
+}
+
+}  // namespace
+
+template <int P>
+__global__ void __launch_bounds__(kGroupThreads, 1)
+    crc32c_uniform_kernel(UniformArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
+
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t nwaves = gridDim.x * kWavesPerGroup;
+  const uint32_t gw = blockIdx.x * kWavesPerGroup + wave;
+  const uint32_t sstride = 2u * nwaves;
+  stamp_uni<P>(a, gw, 0);
+  const UniGeo g = uni_geo(a);
+
+  // Round counts of the two streams (chunks of their blocks).
+  const uint32_t nblk_a = gw < a.nblocks ? (a.nblocks - gw + sstride - 1) / sstride : 0u;
+  const uint32_t gwb = gw + nwaves;
+  const uint32_t nblk_b = gwb < a.nblocks ? (a.nblocks - gwb + sstride - 1) / sstride : 0u;
+  const uint32_t nrounds = max(nblk_a, nblk_b) * g.nchunks;
+
+  // 1. First round in flight.
+  uint32_t a0[kRowsPerChunk], b0[kRowsPerChunk], a1[kRowsPerChunk], b1[kRowsPerChunk];
+  Cursor ca0 = {gw, 0u}, cb0 = {gwb, 0u};
+  if (!(P & kUniFillFirst)) {
+    issue16<P>(a0, a, g, ca0);
+    issue16<P>(b0, a, g, cb0);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+
+  // 2. Row tables from the Z_256 columns: wave w fills table t = w / 4,
+  //    uint4 slots [(w % 4) * 512, +512) of that table's 2048 (8 per lane).
+  {
+    const uint32_t t = wave >> 2;
+    const uint32_t region = (t >> 1) * kLdsRowRegionBytes + (t & 1u) * 128u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t v = (wave & 3u) * 512u + static_cast<uint32_t>(k) * 64u + lane;
+      const uint32_t i = v >> 3;          // table index (8 slots of 4 copies)
+      const uint32_t c4 = v & 7u;         // copies 4*c4 .. 4*c4+3
+      uint32_t e = 0;
+#pragma unroll
+      for (int bit = 0; bit < 8; ++bit) {
+        const uint32_t m = 0u - ((i >> bit) & 1u);
+        e ^= m & a.zcol[8u * t + bit];
+      }
+      *reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds) + region + i * 256u + c4 * 16u) =
+          make_uint4(e, e, e, e);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  stamp_uni<P>(a, gw, 1);
+  if (P & kUniFillFirst) {
+    issue16<P>(a0, a, g, ca0);
+    issue16<P>(b0, a, g, cb0);
+  }
+
+  // 3. Lane tables (needed at the first flush), then the second round.
+  constexpr int kLaneIters = (kLaneTabDwords / 4) / kGroupThreads;  // 2
+  uint32_t lt[kLaneIters][4];
+#pragma unroll
+  for (int k = 0; k < kLaneIters; ++k) {
+    const uint32_t* src = a.lane_tab + 4u * (tid + kGroupThreads * k);
+#pragma unroll
+    for (int x = 0; x < 4; ++x) lt[k][x] = src[x];
+  }
+  Cursor ca1 = advance(ca0, g, sstride), cb1 = advance(cb0, g, sstride);
+  issue16<P>(a1, a, g, ca1);
+  issue16<P>(b1, a, g, cb1);
+
+  const uint32_t k0 = (lane & 31u) * 4u;
+  const uint32_t k1 = k0 | 0x10000u;
+  const uint32_t lane_base = kLdsLaneTabBase + lane * 4u;
+  bool lane_ready = false;
+  Pending pq = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+
+  auto flush = [&]() {
+    if (!lane_ready) {
+#pragma unroll
+      for (int k = 0; k < kLaneIters; ++k)
+        reinterpret_cast<uint4*>(lds + kLdsLaneTabBase / 4)[tid + kGroupThreads * k] =
+            make_uint4(lt[k][0], lt[k][1], lt[k][2], lt[k][3]);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      lane_ready = true;
+    }
+    // Up to four finishes; their lookups and reductions interleave.
+    const uint32_t c0 = wave_xor_dpp(lane_end_shift(lds, pq.s0, lane_base)) ^ 0xffffffffu;
+    uint32_t c1 = 0, c2 = 0, c3 = 0;
+    if (pq.count > 1) c1 = wave_xor_dpp(lane_end_shift(lds, pq.s1, lane_base)) ^ 0xffffffffu;
+    if (pq.count > 2) c2 = wave_xor_dpp(lane_end_shift(lds, pq.s2, lane_base)) ^ 0xffffffffu;
+    if (pq.count > 3) c3 = wave_xor_dpp(lane_end_shift(lds, pq.s3, lane_base)) ^ 0xffffffffu;
+    if (lane == 0) {
+      a.out[pq.b0] = a.mask ? crc_mask(c0) : c0;
+      if (pq.count > 1) a.out[pq.b1] = a.mask ? crc_mask(c1) : c1;
+      if (pq.count > 2) a.out[pq.b2] = a.mask ? crc_mask(c2) : c2;
+      if (pq.count > 3) a.out[pq.b3] = a.mask ? crc_mask(c3) : c3;
+    }
+    pq.count = 0;
+  };
+  auto push = [&](uint32_t s, uint32_t b) {
+    pq.s3 = pq.s2; pq.b3 = pq.b2;
+    pq.s2 = pq.s1; pq.b2 = pq.b1;
+    pq.s1 = pq.s0; pq.b1 = pq.b0;
+    pq.s0 = s; pq.b0 = b;
+    pq.count += 1;
+    if (pq.count == 4) flush();
+  };
+
+  uint32_t sa = 0, sb = 0;
+  auto consume = [&](uint32_t (&ba)[kRowsPerChunk], const Cursor& ca,
+                     uint32_t (&bb)[kRowsPerChunk], const Cursor& cb) {
+    const bool va = ca.block < a.nblocks, vb = cb.block < a.nblocks;
+    if (va && ca.chunk == 0) fix_first_chunk(ba, g);
+    if (vb && cb.chunk == 0) fix_first_chunk(bb, g);
+    const uint32_t na = va ? min(static_cast<uint32_t>(kRowsPerChunk),
+                                 g.rows - kRowsPerChunk * ca.chunk) : 0u;
+    const uint32_t nb = vb ? min(static_cast<uint32_t>(kRowsPerChunk),
+                                 g.rows - kRowsPerChunk * cb.chunk) : 0u;
+    if (P & kUniNoCompute) {
+#pragma unroll
+      for (int j = 0; j < kRowsPerChunk; ++j) {
+        sa ^= ba[j];
+        sb ^= bb[j];
+      }
+    } else {
+      rows2(lds, ba, na, ca.chunk == 0, sa, bb, nb, cb.chunk == 0, sb, k0, k1);
+    }
+    if (va && ca.chunk + 1 == g.nchunks) push(sa, ca.block);
+    if (vb && cb.chunk + 1 == g.nchunks) push(sb, cb.block);
+  };
+
+  // 4. Steady state: consume round k, issue round k+2 unconditionally.
+  uint32_t k = 0;
+  while (k + 2 < nrounds) {
+    consume(a0, ca0, b0, cb0);
+    ca0 = advance(ca1, g, sstride);
+    cb0 = advance(cb1, g, sstride);
+    issue16<P>(a0, a, g, ca0);
+    issue16<P>(b0, a, g, cb0);
+    ++k;
+    if (!(k + 2 < nrounds)) {
+      // Tail with the buffers swapped: rounds k (in a1/b1) and k+1 (a0/b0).
+      consume(a1, ca1, b1, cb1);
+      if (k + 1 < nrounds) consume(a0, ca0, b0, cb0);
+      k = nrounds;
+      break;
+    }
+    consume(a1, ca1, b1, cb1);
+    ca1 = advance(ca0, g, sstride);
+    cb1 = advance(cb0, g, sstride);
+    issue16<P>(a1, a, g, ca1);
+    issue16<P>(b1, a, g, cb1);
+    ++k;
+  }
+  // 5. Tail: the last (up to) two rounds, nothing more to issue.
+  if (k < nrounds) {
+    consume(a0, ca0, b0, cb0);
+    if (k + 1 < nrounds) consume(a1, ca1, b1, cb1);
+  }
+  stamp_uni<P>(a, gw, 2);
+  if (pq.count != 0 || !lane_ready) {
+    if (pq.count != 0) {
+      flush();
+    } else {
+      // No block to finish: still write this wave's share of the lane
+      // tables and pass the barrier every wave executes once.
+#pragma unroll
+      for (int k2 = 0; k2 < kLaneIters; ++k2)
+        reinterpret_cast<uint4*>(lds + kLdsLaneTabBase / 4)[tid + kGroupThreads * k2] =
+            make_uint4(lt[k2][0], lt[k2][1], lt[k2][2], lt[k2][3]);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  }
+  stamp_uni<P>(a, gw, 7);
+}
+
+// ---------------------------------------------------------------------------
+// Small batches (nblocks <= 3 x waves in the grid, blocks of <= 16 rows =
+// <= 4 KiB + 252 B): ONE round per wave. Wave gw owns blocks gw, gw+W, gw+2W
+// (W = waves in the grid) as three interleaved Horner chains; its 48 loads
+// are issued row-interleaved (A_j, B_j, C_j) so row j can be processed as
+// soon as its three words land, and everything a wave needs is in flight at
+// once (48 block loads + 2 lane-table loads <= 63).
+
+namespace {
+
+template <int P>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t block_rsrc(
+    const UniformArgs& a, const UniGeo& g, uint32_t block, bool valid) {
+  const uint64_t ptr = reinterpret_cast<uint64_t>(a.base) +
+                       static_cast<uint64_t>(valid ? block : 0u) * a.stride -
+                       g.delta;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(ptr));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(ptr >> 32));
+  const uint32_t n = __builtin_amdgcn_readfirstlane(valid ? g.nrec : 0u);
+  return __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0,
+      static_cast<int>(n), kBufferDword3);
+}
+
+__device__ __forceinline__ uint32_t load_word(__amdgpu_buffer_rsrc_t r,
+                                              int32_t vo, int j, bool fold) {
+  if (fold)
+    return __builtin_amdgcn_raw_buffer_load_b32(r, vo + 256 * j, 0, kUniCachePolicy);
+  int32_t o = vo + 256 * j;
+  asm volatile("" : "+v"(o));
+  return __builtin_amdgcn_raw_buffer_load_b32(r, o, 0, kUniCachePolicy);
+}
+
+template <int P>
+__device__ __forceinline__ void row_tables_from_columns(uint32_t* lds,
+                                                        const UniformArgs& a,
+                                                        uint32_t wave,
+                                                        uint32_t lane) {
+  const uint32_t t = wave >> 2;
+  const uint32_t region = (t >> 1) * kLdsRowRegionBytes + (t & 1u) * 128u;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t v = (wave & 3u) * 512u + static_cast<uint32_t>(k) * 64u + lane;
+    const uint32_t i = v >> 3;
+    const uint32_t c4 = v & 7u;
+    uint32_t e = 0;
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+      const uint32_t m = 0u - ((i >> bit) & 1u);
+      e ^= m & a.zcol[8u * t + bit];
+    }
+    *reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds) + region + i * 256u + c4 * 16u) =
+        make_uint4(e, e, e, e);
+  }
+}
+
+}  // namespace
+
+template <int P>
+__global__ void __launch_bounds__(kGroupThreads, 1)
+    crc32c_uniform_small_kernel(UniformArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
+
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t nwaves = gridDim.x * kWavesPerGroup;
+  const uint32_t gw = blockIdx.x * kWavesPerGroup + wave;
+  stamp_uni<P>(a, gw, 0);
+  const UniGeo g = uni_geo(a);
+  const uint32_t blk_a = gw, blk_b = gw + nwaves, blk_c = gw + 2u * nwaves;
+  const bool va = blk_a < a.nblocks, vb = blk_b < a.nblocks, vc = blk_c < a.nblocks;
+
+  if (P & kUniFillFirst) {
+    row_tables_from_columns<P>(lds, a, wave, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    stamp_uni<P>(a, gw, 1);
+  }
+
+  // 1. All of this wave's block words, row-interleaved, then the lane tables.
+  const __amdgpu_buffer_rsrc_t ra = block_rsrc<P>(a, g, blk_a, va);
+  const __amdgpu_buffer_rsrc_t rb = block_rsrc<P>(a, g, blk_b, vb);
+  const __amdgpu_buffer_rsrc_t rc = block_rsrc<P>(a, g, blk_c, vc);
+  const int32_t vo = g.vb0 + 4 * static_cast<int32_t>(lane);
+  const bool fold = g.vb0 >= 0;  // no lane starts before its block
+  uint32_t wa[kRowsPerChunk], wb[kRowsPerChunk], wc[kRowsPerChunk];
+#pragma unroll
+  for (int j = 0; j < kRowsPerChunk; ++j) {
+    wa[j] = load_word(ra, vo, j, fold);
+    wb[j] = load_word(rb, vo, j, fold);
+    wc[j] = load_word(rc, vo, j, fold);
+  }
+  constexpr int kLaneIters = (kLaneTabDwords / 4) / kGroupThreads;  // 2
+  uint32_t lt[kLaneIters][4];
+#pragma unroll
+  for (int k = 0; k < kLaneIters; ++k) {
+    const uint32_t* src = a.lane_tab + 4u * (tid + kGroupThreads * k);
+#pragma unroll
+    for (int x = 0; x < 4; ++x) lt[k][x] = src[x];
+  }
+
+  // 2. Row tables (if not generated first).
+  if (!(P & kUniFillFirst)) {
+    row_tables_from_columns<P>(lds, a, wave, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    stamp_uni<P>(a, gw, 1);
+  }
+
+  // 3. Rows: three (or two) chains interleaved; row-0 fix-ups first.
+  const uint32_t k0 = (lane & 31u) * 4u;
+  const uint32_t k1 = k0 | 0x10000u;
+  fix_first_chunk(wa, g);
+  fix_first_chunk(wb, g);
+  fix_first_chunk(wc, g);
+  uint32_t sa = wa[0], sb = wb[0], sc = wc[0];
+  if (vc) {
+#pragma unroll
+    for (int j = 1; j < kRowsPerChunk; ++j) {
+      if (static_cast<uint32_t>(j) < g.rows) {
+        sa = row_step(lds, sa, wa[j], k0, k1);
+        sb = row_step(lds, sb, wb[j], k0, k1);
+        sc = row_step(lds, sc, wc[j], k0, k1);
+      }
+    }
+  } else if (vb) {
+#pragma unroll
+    for (int j = 1; j < kRowsPerChunk; ++j) {
+      if (static_cast<uint32_t>(j) < g.rows) {
+        sa = row_step(lds, sa, wa[j], k0, k1);
+        sb = row_step(lds, sb, wb[j], k0, k1);
+      }
+    }
+  } else if (va) {
+#pragma unroll
+    for (int j = 1; j < kRowsPerChunk; ++j)
+      if (static_cast<uint32_t>(j) < g.rows) sa = row_step(lds, sa, wa[j], k0, k1);
+  }
+  stamp_uni<P>(a, gw, 2);
+
+  // 4. Lane tables into LDS (every wave writes its share, one barrier), then
+  //    the end shift + reduction of the wave's blocks.
+#pragma unroll
+  for (int k = 0; k < kLaneIters; ++k)
+    reinterpret_cast<uint4*>(lds + kLdsLaneTabBase / 4)[tid + kGroupThreads * k] =
+        make_uint4(lt[k][0], lt[k][1], lt[k][2], lt[k][3]);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  const uint32_t lane_base = kLdsLaneTabBase + lane * 4u;
+  if (va) {
+    const uint32_t ca = wave_xor_dpp(lane_end_shift(lds, sa, lane_base)) ^ 0xffffffffu;
+    uint32_t cb = 0, cc = 0;
+    if (vb) cb = wave_xor_dpp(lane_end_shift(lds, sb, lane_base)) ^ 0xffffffffu;
+    if (vc) cc = wave_xor_dpp(lane_end_shift(lds, sc, lane_base)) ^ 0xffffffffu;
+    if (lane == 0) {
+      a.out[blk_a] = a.mask ? crc_mask(ca) : ca;
+      if (vb) a.out[blk_b] = a.mask ? crc_mask(cb) : cb;
+      if (vc) a.out[blk_c] = a.mask ? crc_mask(cc) : cc;
+    }
+  }
+  stamp_uni<P>(a, gw, 7);
+}
+
+hipError_t launch_crc32c_uniform_small(const UniformArgs& args, int variant,
+                                       int num_groups, hipStream_t stream) {
+  switch (variant & (kUniProbeStamps | kUniFillFirst)) {
+#define LVKV_UNI_SMALL_CASE(v)                                               \
+  case v:                                                                    \
+    hipLaunchKernelGGL(crc32c_uniform_small_kernel<v>, dim3(num_groups),     \
+                       dim3(kGroupThreads), 0, stream, args);                \
+    break;
+    LVKV_UNI_SMALL_CASE(0)
+    LVKV_UNI_SMALL_CASE(64)
+    LVKV_UNI_SMALL_CASE(128)
+    LVKV_UNI_SMALL_CASE(192)
+#undef LVKV_UNI_SMALL_CASE
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_crc32c_uniform(const UniformArgs& args, int variant,
+                                 int num_groups, hipStream_t stream) {
+  switch (variant & (kUniProbeStamps | kUniFillFirst | kUniNoCompute | kUniNoLoads)) {
+#define LVKV_UNI_CASE(v)                                                     \
+  case v:                                                                    \
+    hipLaunchKernelGGL(crc32c_uniform_kernel<v>, dim3(num_groups),           \
+                       dim3(kGroupThreads), 0, stream, args);                \
+    break;
+    LVKV_UNI_CASE(0)
+    LVKV_UNI_CASE(1)
+    LVKV_UNI_CASE(2)
+    LVKV_UNI_CASE(3)
+    LVKV_UNI_CASE(64)
+    LVKV_UNI_CASE(65)
+    LVKV_UNI_CASE(66)
+    LVKV_UNI_CASE(67)
+    LVKV_UNI_CASE(128)
+    LVKV_UNI_CASE(129)
+    LVKV_UNI_CASE(130)
+    LVKV_UNI_CASE(131)
+    LVKV_UNI_CASE(192)
+    LVKV_UNI_CASE(193)
+    LVKV_UNI_CASE(194)
+    LVKV_UNI_CASE(195)
+#undef LVKV_UNI_CASE
+  }
+  return hipGetLastError();
+}
+
+}  // namespace lvkv

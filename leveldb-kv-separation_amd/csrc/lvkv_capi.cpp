@@ -20,8 +20,16 @@
 
 namespace lvkv {
 
-hipError_t launch_crc32c_batch(const KernelArgs& args, int num_groups,
-                               hipStream_t stream);
+hipError_t launch_crc32c_batch(const KernelArgs& args, bool uniform_aligned,
+                               int num_groups, hipStream_t stream);
+hipError_t launch_crc32c_probe(const KernelArgs& args, int variant,
+                               int num_groups, hipStream_t stream);
+hipError_t launch_read_bw(const void* p, uint64_t bytes, uint32_t* out,
+                          int num_groups, hipStream_t stream);
+hipError_t launch_crc32c_uniform(const UniformArgs& args, int variant,
+                                 int num_groups, hipStream_t stream);
+hipError_t launch_crc32c_uniform_small(const UniformArgs& args, int variant,
+                                       int num_groups, hipStream_t stream);
 uint32_t cpu_crc32c_extend(uint32_t crc, const uint8_t* data, size_t n);
 const char* cpu_crc32c_impl_name();
 
@@ -58,6 +66,7 @@ struct DeviceCtx {
   int status = LVKV_ERR_NO_DEVICE;
   int groups = 0;  // one workgroup per CU
   uint32_t* d_tables = nullptr;
+  uint32_t zcol[32];  // columns of Z_256 (uniform kernel's row tables)
   std::mutex host_mu;  // serialises lvkv_crc32c_batch_host per device
   bool stages_ready = false;
   Stage stage[2];
@@ -96,6 +105,8 @@ void init_ctx(DeviceCtx& c, int dev) {
     return;
   }
   c.d_tables = static_cast<uint32_t*>(p);
+  const Gf2Op z256 = gf2_zero_advance(kRowBytes);
+  for (int b = 0; b < 32; ++b) c.zcol[b] = z256.col[b];
   c.groups = ncu;
   c.status = LVKV_OK;
 }
@@ -124,6 +135,22 @@ DeviceCtx* current_ctx(int* rc) {
   return c.status == LVKV_OK ? &c : nullptr;
 }
 
+UniformArgs uniform_args(const DeviceCtx& c, const KernelArgs& b) {
+  UniformArgs u;
+  memset(&u, 0, sizeof(u));
+  u.base = b.base;
+  u.stride = b.stride;
+  u.out = b.out_crc;
+  u.lane_tab = c.d_tables + kRowTabDwords;
+  u.stamps = b.stamps;
+  u.length = b.length;
+  u.init = b.init;
+  u.nblocks = b.nblocks;
+  u.mask = b.mask;
+  memcpy(u.zcol, c.zcol, sizeof(u.zcol));
+  return u;
+}
+
 int run_batch(KernelArgs a, size_t nblocks, hipStream_t stream) {
   if (nblocks == 0) return LVKV_OK;
   int rc = LVKV_OK;
@@ -147,7 +174,23 @@ int run_batch(KernelArgs a, size_t nblocks, hipStream_t stream) {
     const size_t want = (n + kWavesPerGroup - 1) / kWavesPerGroup;
     const int groups = static_cast<int>(
         std::min<size_t>(static_cast<size_t>(c->groups), want));
-    hipError_t e = launch_crc32c_batch(b, groups, stream);
+    // Uniform layout whose every block END is 4-byte aligned: the dedicated
+    // uniform kernel (crc32c_uniform.hip).
+    const bool uni_aligned =
+        a.offsets == nullptr && a.mode == kModeCompute && a.length >= 4 &&
+        (a.stride % 4) == 0 &&
+        ((reinterpret_cast<uintptr_t>(b.base) + a.length) % 4) == 0;
+    hipError_t e;
+    if (uni_aligned) {
+      // One round per wave when every wave owns <= 3 single-chunk blocks.
+      const size_t waves = static_cast<size_t>(groups) * kWavesPerGroup;
+      if (a.length <= kRowsPerChunk * kRowBytes && n <= 3 * waves)
+        e = launch_crc32c_uniform_small(uniform_args(*c, b), 0, groups, stream);
+      else
+        e = launch_crc32c_uniform(uniform_args(*c, b), 0, groups, stream);
+    } else {
+      e = launch_crc32c_batch(b, false, groups, stream);
+    }
     if (e != hipSuccess) return hip_fail(e);
     done += n;
   }
@@ -429,6 +472,62 @@ const char* lvkv_strerror(int code) {
 int lvkv_last_hip_error(void) { return t_last_hip_error; }
 
 const char* lvkv_cpu_impl(void) { return cpu_crc32c_impl_name(); }
+
+static uint64_t* g_debug_stamps = nullptr;
+
+void lvkv_debug_set_stamps(uint64_t* d_stamps) { g_debug_stamps = d_stamps; }
+
+int lvkv_debug_uniform_variant(int variant, int groups, const void* d_base,
+                               uint64_t stride, uint32_t length,
+                               uint32_t* d_out, size_t nblocks, void* stream) {
+  if (nblocks == 0) return LVKV_OK;
+  if (!d_base || !d_out || nblocks > kMaxBlocksPerLaunch) return LVKV_ERR_INVALID;
+  int rc = LVKV_OK;
+  DeviceCtx* c = current_ctx(&rc);
+  if (c == nullptr) return rc;
+  KernelArgs a = blank_args();
+  a.base = static_cast<const uint8_t*>(d_base);
+  a.stride = stride;
+  a.length = length;
+  a.out_crc = d_out;
+  a.nblocks = static_cast<uint32_t>(nblocks);
+  a.row_tab = c->d_tables;
+  a.lane_tab = c->d_tables + kRowTabDwords;
+  a.stamps = g_debug_stamps;
+  if ((variant & 64) && g_debug_stamps == nullptr) return LVKV_ERR_INVALID;
+  const int g = groups > 0 ? groups : c->groups;
+  hipError_t e;
+  if (variant & 256) {
+    if (length < 4 || (stride % 4) != 0 ||
+        ((reinterpret_cast<uintptr_t>(d_base) + length) % 4) != 0)
+      return LVKV_ERR_INVALID;
+    if (variant & 512) {
+      if (length > kRowsPerChunk * kRowBytes ||
+          nblocks > 3 * static_cast<size_t>(g) * kWavesPerGroup)
+        return LVKV_ERR_INVALID;
+      e = launch_crc32c_uniform_small(uniform_args(*c, a), variant & 255, g,
+                                      static_cast<hipStream_t>(stream));
+    } else {
+      e = launch_crc32c_uniform(uniform_args(*c, a), variant & 255, g,
+                                static_cast<hipStream_t>(stream));
+    }
+  } else {
+    e = launch_crc32c_probe(a, variant, g, static_cast<hipStream_t>(stream));
+  }
+  return e == hipSuccess ? LVKV_OK : hip_fail(e);
+}
+
+int lvkv_debug_read_bw(const void* d_data, uint64_t bytes, uint32_t* d_scratch,
+                       int groups, void* stream) {
+  if (!d_data || !d_scratch || (bytes & 15u)) return LVKV_ERR_INVALID;
+  int rc = LVKV_OK;
+  DeviceCtx* c = current_ctx(&rc);
+  if (c == nullptr) return rc;
+  const int g = groups != 0 ? groups : 8 * c->groups;
+  hipError_t e = launch_read_bw(d_data, bytes, d_scratch, g,
+                                static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? LVKV_OK : hip_fail(e);
+}
 
 int lvkv_device_groups(void) {
   int rc = LVKV_OK;

@@ -57,6 +57,23 @@ struct KernelArgs {
   uint32_t mode;
   uint32_t mask;              // 1: store Mask(crc) (util/crc32c.h:29-32)
   uint32_t pad_;
+  uint64_t* stamps;           // probe builds only: per-wave timestamps
+};
+
+// Arguments of the uniform-layout kernel (crc32c_uniform.hip): nblocks
+// blocks of `length` bytes at base + i*stride, every block END 4-byte aligned.
+struct UniformArgs {
+  const uint8_t* base;
+  uint64_t stride;
+  uint32_t* out;              // nblocks u32 (masked if `mask`)
+  const uint32_t* lane_tab;   // kLaneTabDwords, LDS order (loaded per launch)
+  uint64_t* stamps;           // probe builds only
+  uint32_t length;            // >= 4
+  uint32_t init;
+  uint32_t nblocks;
+  uint32_t mask;
+  uint32_t zcol[32];          // zcol[k] = Z_256(1 << k): the row tables are
+                              // generated in-kernel from these columns
 };
 
 }  // namespace lvkv

@@ -209,3 +209,24 @@ def test_all_zero_and_x_blocks(lvkv, oracle, gpu):
         assert np.array_equal(_u32(got), oracle.uniform(h, 64, 4096))
     z = torch.zeros(64, dtype=torch.uint8, device=gpu)
     assert _u32(lvkv.crc32c_uniform(z, 1, 32))[0] == 0x8A9136AA
+
+
+@pytest.mark.parametrize("length,nblocks", [
+    (4, 5000), (5, 1), (7, 777), (8, 33), (255, 20000), (256, 9000), (257, 4097),
+    (259, 300), (1021, 1000), (4093, 2500), (4096, 20000), (4097, 10001), (4100, 123),
+    (8188, 700), (32762, 300), (65536, 64), (70001, 50)])
+def test_uniform_kernel_shapes(lvkv, oracle, gpu, length, nblocks):
+    # The dedicated uniform kernel (block END 4-byte aligned): every residue of
+    # length mod 4 (front padding + init spill, incl. the s0l == 63 case at
+    # 257), multi-chunk blocks, batches of 1..5 rounds per wave.
+    import torch
+    stride = (length + 3) // 4 * 4 + 4 * (length % 3)
+    pad = (-length) % 4            # base + pad + length is 4-aligned
+    nbytes = pad + (nblocks - 1) * stride + length
+    g = torch.Generator(device=gpu).manual_seed(length * 31 + nblocks)
+    d = torch.randint(0, 256, (nbytes + 64,), dtype=torch.uint8, device=gpu, generator=g)
+    init = (length * 2654435761) & 0xFFFFFFFF
+    got = lvkv.crc32c_uniform(d[pad:], nblocks, length, stride, init=init, mask=bool(length & 1))
+    h = d.cpu().numpy()[pad:]
+    want = oracle.uniform(h, nblocks, length, stride, init=init, mask=bool(length & 1), threads=8)
+    assert np.array_equal(_u32(got), want)
