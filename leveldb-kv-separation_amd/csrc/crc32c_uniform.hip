@@ -378,13 +378,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t block_rsrc(
       static_cast<int>(n), kBufferDword3);
 }
 
+// Row j of a block, j >= 0. Only row 0 can start before the block (vo < 0:
+// those lanes read zeros through the bounded window and are masked by
+// fix_first_chunk); rows >= 1 are addressed from vo1 = vo + 256 >= 4, kept
+// opaque so the compiler cannot re-fold it into a negative voffset with a
+// positive immediate (the range check would then reject the whole load).
 __device__ __forceinline__ uint32_t load_word(__amdgpu_buffer_rsrc_t r,
-                                              int32_t vo, int j, bool fold) {
-  if (fold)
-    return __builtin_amdgcn_raw_buffer_load_b32(r, vo + 256 * j, 0, kUniCachePolicy);
-  int32_t o = vo + 256 * j;
-  asm volatile("" : "+v"(o));
-  return __builtin_amdgcn_raw_buffer_load_b32(r, o, 0, kUniCachePolicy);
+                                              int32_t vo, int32_t vo1, int j) {
+  if (j == 0) return __builtin_amdgcn_raw_buffer_load_b32(r, vo, 0, kUniCachePolicy);
+  return __builtin_amdgcn_raw_buffer_load_b32(r, vo1 + 256 * (j - 1), 0, kUniCachePolicy);
 }
 
 template <int P>
@@ -412,11 +414,196 @@ __device__ __forceinline__ void row_tables_from_columns(uint32_t* lds,
 
 }  // namespace
 
+enum : int {
+  kSmallLaneEarly = 4,  // lane tables loaded first, written with the row
+                        // tables (one barrier; none at the end)
+  kSmallEarlyA = 8,     // chain A's loads issued before the row-table fill
+  kSmallOneBarrier = 16,  // lane tables first, chain A, fill, chains B/C,
+                          // write lane tables, then the only barrier
+  kSmallSkipFill = 32,    // probe: no row-table fill (CRCs wrong)
+  kSmallHalfA = 256,      // with kSmallEarlyA: only waves 0-7 load chain A
+                          // before the fill
+  kSmallBare = 4096,      // probe: loads + xor only (no tables, no walk)
+};
+
+// Body of the small kernel for a wave with NCH valid chains (1..3). Every
+// value a body loads is consumed unconditionally, so the compiler cannot sink
+// a load into the branch that uses it; FULL = 16-row (4 KiB-class) blocks,
+// no per-row guards. Every body executes the same barriers.
+template <int P, int NCH, bool FULL>
+__device__ __forceinline__ void small_body(const UniformArgs& a, const UniGeo& g,
+                                           uint32_t* lds, uint32_t tid,
+                                           uint32_t lane, uint32_t wave,
+                                           uint32_t gw, const uint32_t (&blk)[3]) {
+  constexpr bool kLaneEarly = (P & kSmallLaneEarly) != 0;
+  constexpr bool kEarlyA = (P & kSmallEarlyA) != 0;
+  constexpr bool kFillBeforeBC = (P & (kUniFillFirst | kSmallEarlyA)) != 0;
+  constexpr int kLaneIters = (kLaneTabDwords / 4) / kGroupThreads;  // 2
+
+  uint32_t lt[kLaneIters][4];
+  auto load_lane_tables = [&]() {
+#pragma unroll
+    for (int k = 0; k < kLaneIters; ++k) {
+      const uint32_t* src = a.lane_tab + 4u * (tid + kGroupThreads * k);
+#pragma unroll
+      for (int x = 0; x < 4; ++x) lt[k][x] = src[x];
+    }
+  };
+  auto write_lane_tables = [&]() {
+#pragma unroll
+    for (int k = 0; k < kLaneIters; ++k)
+      reinterpret_cast<uint4*>(lds + kLdsLaneTabBase / 4)[tid + kGroupThreads * k] =
+          make_uint4(lt[k][0], lt[k][1], lt[k][2], lt[k][3]);
+  };
+
+  __amdgpu_buffer_rsrc_t r[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)  // invalid only for NCH == 1 past the batch
+    r[c] = block_rsrc<P>(a, g, blk[c], NCH > 1 || blk[c] < a.nblocks);
+  const int32_t vo = g.vb0 + 4 * static_cast<int32_t>(lane);
+  int32_t vo1 = vo + kRowBytes;
+  asm volatile("" : "+v"(vo1));
+  uint32_t w[NCH][kRowsPerChunk];
+  auto load_rows = [&](int c_lo, int c_hi) {  // row-interleaved over chains
+#pragma unroll
+    for (int j = 0; j < kRowsPerChunk; ++j)
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+        if (c >= c_lo && c < c_hi)
+          w[c][j] = (P & kUniNoLoads)
+                        ? (lane * 0x9E3779B1u) ^ (static_cast<uint32_t>(j) * 0x85EBCA6Bu) ^ blk[c]
+                        : load_word(r[c], vo, vo1, j);
+  };
+  auto fill = [&]() {
+    stamp_uni<P>(a, gw, 3);
+    if (!(P & kSmallSkipFill)) row_tables_from_columns<P>(lds, a, wave, lane);
+    if (kLaneEarly) write_lane_tables();
+    stamp_uni<P>(a, gw, 4);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);  // nothing that waits on loads moves up
+    stamp_uni<P>(a, gw, 1);
+  };
+
+  // 1. Loads and the LDS image, in the order the variant asks for.
+  if (P & kSmallOneBarrier) {
+    load_lane_tables();
+    __builtin_amdgcn_sched_barrier(0);
+    load_rows(0, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    row_tables_from_columns<P>(lds, a, wave, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    load_rows(1, NCH);
+    __builtin_amdgcn_sched_barrier(0);
+    write_lane_tables();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    stamp_uni<P>(a, gw, 1);
+  } else if (kFillBeforeBC) {
+    if (kLaneEarly) {
+      load_lane_tables();
+      __builtin_amdgcn_sched_barrier(0);  // keep them ahead of the block loads
+    }
+    // kSmallHalfA: waves 8-15 leave chain A until after the fill
+    const bool early_a = kEarlyA && (!(P & kSmallHalfA) || wave < kWavesPerGroup / 2);
+    if (early_a) {
+      load_rows(0, 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    fill();
+    if (early_a) load_rows(1, NCH); else load_rows(0, NCH);
+    stamp_uni<P>(a, gw, 5);
+    if (!kLaneEarly) load_lane_tables();
+  } else {
+    if (kLaneEarly) {
+      load_lane_tables();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    load_rows(0, NCH);
+    if (!kLaneEarly) load_lane_tables();
+    fill();
+  }
+
+  // 2. Rows: the chains interleaved; row-0 fix-ups first.
+  const uint32_t k0 = (lane & 31u) * 4u;
+  const uint32_t k1 = k0 | 0x10000u;
+  uint32_t st[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    fix_first_chunk(w[c], g);
+    st[c] = w[c][0];
+  }
+#pragma unroll
+  for (int j = 1; j < kRowsPerChunk; ++j) {
+    if (FULL || static_cast<uint32_t>(j) < g.rows) {
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+        st[c] = (P & kUniNoCompute) ? (st[c] * 0x01000193u) ^ w[c][j]
+                                    : row_step(lds, st[c], w[c][j], k0, k1);
+    }
+  }
+  stamp_uni<P>(a, gw, 2);
+
+  // 3. Lane tables (unless already in LDS), end shift + reduction, store.
+  if (!kLaneEarly && !(P & kSmallOneBarrier)) {
+    write_lane_tables();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  const uint32_t lane_base = kLdsLaneTabBase + lane * 4u;
+  uint32_t crc[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+    crc[c] = wave_xor_dpp(lane_end_shift(lds, st[c], lane_base)) ^ 0xffffffffu;
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+      if (NCH > 1 || blk[c] < a.nblocks) a.out[blk[c]] = a.mask ? crc_mask(crc[c]) : crc[c];
+  }
+}
+
+// Probe: the memory side alone (same loads, mapping and LDS footprint).
+template <int P, int NCH>
+__device__ __forceinline__ void small_body_bare(const UniformArgs& a, const UniGeo& g,
+                                                uint32_t* lds, uint32_t lane,
+                                                const uint32_t (&blk)[3]) {
+  __amdgpu_buffer_rsrc_t r[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+    r[c] = block_rsrc<P>(a, g, blk[c], NCH > 1 || blk[c] < a.nblocks);
+  const int32_t vo = g.vb0 + 4 * static_cast<int32_t>(lane);
+  int32_t vo1 = vo + kRowBytes;
+  asm volatile("" : "+v"(vo1));
+  uint32_t w[NCH][kRowsPerChunk];
+#pragma unroll
+  for (int j = 0; j < kRowsPerChunk; ++j)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) w[c][j] = load_word(r[c], vo, vo1, j);
+  uint32_t x = 0;
+#pragma unroll
+  for (int j = 0; j < kRowsPerChunk; ++j)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) x ^= w[c][j];
+  lds[lane] = x;  // keeps the LDS allocation live
+  if (lane == 0)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+      if (NCH > 1 || blk[c] < a.nblocks) a.out[blk[c]] = x;
+}
+
+template <int P, int NCH, bool FULL>
+__device__ __forceinline__ void small_dispatch(const UniformArgs& a, const UniGeo& g,
+                                               uint32_t* lds, uint32_t tid, uint32_t lane,
+                                               uint32_t wave, uint32_t gw,
+                                               const uint32_t (&blk)[3]) {
+  if (P & kSmallBare)
+    small_body_bare<P, NCH>(a, g, lds, lane, blk);
+  else
+    small_body<P, NCH, FULL>(a, g, lds, tid, lane, wave, gw, blk);
+}
+
 template <int P>
 __global__ void __launch_bounds__(kGroupThreads, 1)
     crc32c_uniform_small_kernel(UniformArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
-
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = lane_id();
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -424,110 +611,62 @@ __global__ void __launch_bounds__(kGroupThreads, 1)
   const uint32_t gw = blockIdx.x * kWavesPerGroup + wave;
   stamp_uni<P>(a, gw, 0);
   const UniGeo g = uni_geo(a);
-  const uint32_t blk_a = gw, blk_b = gw + nwaves, blk_c = gw + 2u * nwaves;
-  const bool va = blk_a < a.nblocks, vb = blk_b < a.nblocks, vc = blk_c < a.nblocks;
-
-  if (P & kUniFillFirst) {
-    row_tables_from_columns<P>(lds, a, wave, lane);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    stamp_uni<P>(a, gw, 1);
-  }
-
-  // 1. All of this wave's block words, row-interleaved, then the lane tables.
-  const __amdgpu_buffer_rsrc_t ra = block_rsrc<P>(a, g, blk_a, va);
-  const __amdgpu_buffer_rsrc_t rb = block_rsrc<P>(a, g, blk_b, vb);
-  const __amdgpu_buffer_rsrc_t rc = block_rsrc<P>(a, g, blk_c, vc);
-  const int32_t vo = g.vb0 + 4 * static_cast<int32_t>(lane);
-  const bool fold = g.vb0 >= 0;  // no lane starts before its block
-  uint32_t wa[kRowsPerChunk], wb[kRowsPerChunk], wc[kRowsPerChunk];
-#pragma unroll
-  for (int j = 0; j < kRowsPerChunk; ++j) {
-    wa[j] = load_word(ra, vo, j, fold);
-    wb[j] = load_word(rb, vo, j, fold);
-    wc[j] = load_word(rc, vo, j, fold);
-  }
-  constexpr int kLaneIters = (kLaneTabDwords / 4) / kGroupThreads;  // 2
-  uint32_t lt[kLaneIters][4];
-#pragma unroll
-  for (int k = 0; k < kLaneIters; ++k) {
-    const uint32_t* src = a.lane_tab + 4u * (tid + kGroupThreads * k);
-#pragma unroll
-    for (int x = 0; x < 4; ++x) lt[k][x] = src[x];
-  }
-
-  // 2. Row tables (if not generated first).
-  if (!(P & kUniFillFirst)) {
-    row_tables_from_columns<P>(lds, a, wave, lane);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    stamp_uni<P>(a, gw, 1);
-  }
-
-  // 3. Rows: three (or two) chains interleaved; row-0 fix-ups first.
-  const uint32_t k0 = (lane & 31u) * 4u;
-  const uint32_t k1 = k0 | 0x10000u;
-  fix_first_chunk(wa, g);
-  fix_first_chunk(wb, g);
-  fix_first_chunk(wc, g);
-  uint32_t sa = wa[0], sb = wb[0], sc = wc[0];
-  if (vc) {
-#pragma unroll
-    for (int j = 1; j < kRowsPerChunk; ++j) {
-      if (static_cast<uint32_t>(j) < g.rows) {
-        sa = row_step(lds, sa, wa[j], k0, k1);
-        sb = row_step(lds, sb, wb[j], k0, k1);
-        sc = row_step(lds, sc, wc[j], k0, k1);
-      }
-    }
-  } else if (vb) {
-#pragma unroll
-    for (int j = 1; j < kRowsPerChunk; ++j) {
-      if (static_cast<uint32_t>(j) < g.rows) {
-        sa = row_step(lds, sa, wa[j], k0, k1);
-        sb = row_step(lds, sb, wb[j], k0, k1);
-      }
-    }
-  } else if (va) {
-#pragma unroll
-    for (int j = 1; j < kRowsPerChunk; ++j)
-      if (static_cast<uint32_t>(j) < g.rows) sa = row_step(lds, sa, wa[j], k0, k1);
-  }
-  stamp_uni<P>(a, gw, 2);
-
-  // 4. Lane tables into LDS (every wave writes its share, one barrier), then
-  //    the end shift + reduction of the wave's blocks.
-#pragma unroll
-  for (int k = 0; k < kLaneIters; ++k)
-    reinterpret_cast<uint4*>(lds + kLdsLaneTabBase / 4)[tid + kGroupThreads * k] =
-        make_uint4(lt[k][0], lt[k][1], lt[k][2], lt[k][3]);
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  const uint32_t lane_base = kLdsLaneTabBase + lane * 4u;
-  if (va) {
-    const uint32_t ca = wave_xor_dpp(lane_end_shift(lds, sa, lane_base)) ^ 0xffffffffu;
-    uint32_t cb = 0, cc = 0;
-    if (vb) cb = wave_xor_dpp(lane_end_shift(lds, sb, lane_base)) ^ 0xffffffffu;
-    if (vc) cc = wave_xor_dpp(lane_end_shift(lds, sc, lane_base)) ^ 0xffffffffu;
-    if (lane == 0) {
-      a.out[blk_a] = a.mask ? crc_mask(ca) : ca;
-      if (vb) a.out[blk_b] = a.mask ? crc_mask(cb) : cb;
-      if (vc) a.out[blk_c] = a.mask ? crc_mask(cc) : cc;
-    }
+  // Chains A and B: 16 contiguous blocks per workgroup each. Chain C (the
+  // partial third round, nc = nblocks - 2W blocks) is split into equal
+  // contiguous runs per workgroup (waves 0.. of group g take run g), so every
+  // CU gets the same share and each CU's CRC stores stay in one run. A
+  // wave's valid chains are a prefix (C valid => B valid => A valid).
+  const uint32_t nc = a.nblocks > 2u * nwaves ? a.nblocks - 2u * nwaves : 0u;
+  const uint32_t per = nc / gridDim.x, extra = nc % gridDim.x;
+  const uint32_t run_len = per + (blockIdx.x < extra ? 1u : 0u);
+  const uint32_t run_start = blockIdx.x * per + min(blockIdx.x, extra);
+  const uint32_t blk_c = wave < run_len ? 2u * nwaves + run_start + wave : 0xffffffffu;
+  const uint32_t blk[3] = {gw, gw + nwaves, blk_c};
+  const bool full = g.rows == static_cast<uint32_t>(kRowsPerChunk);
+  if (blk[2] < a.nblocks) {
+    if (full) small_dispatch<P, 3, true>(a, g, lds, tid, lane, wave, gw, blk);
+    else small_dispatch<P, 3, false>(a, g, lds, tid, lane, wave, gw, blk);
+  } else if (blk[1] < a.nblocks) {
+    if (full) small_dispatch<P, 2, true>(a, g, lds, tid, lane, wave, gw, blk);
+    else small_dispatch<P, 2, false>(a, g, lds, tid, lane, wave, gw, blk);
+  } else {
+    // One chain; a wave past the batch (only in the last workgroup) runs it
+    // over an empty window and stores nothing, keeping the barrier count.
+    const uint32_t one[3] = {blk[0] < a.nblocks ? blk[0] : 0xffffffffu, 0, 0};
+    if (full) small_dispatch<P, 1, true>(a, g, lds, tid, lane, wave, gw, one);
+    else small_dispatch<P, 1, false>(a, g, lds, tid, lane, wave, gw, one);
   }
   stamp_uni<P>(a, gw, 7);
 }
 
 hipError_t launch_crc32c_uniform_small(const UniformArgs& args, int variant,
                                        int num_groups, hipStream_t stream) {
-  switch (variant & (kUniProbeStamps | kUniFillFirst)) {
+  switch (variant & (kUniProbeStamps | kUniFillFirst | kSmallLaneEarly | kSmallEarlyA |
+                     kSmallOneBarrier | kSmallSkipFill | kUniNoCompute | kUniNoLoads |
+                     kSmallHalfA | kSmallBare)) {
 #define LVKV_UNI_SMALL_CASE(v)                                               \
   case v:                                                                    \
     hipLaunchKernelGGL(crc32c_uniform_small_kernel<v>, dim3(num_groups),     \
                        dim3(kGroupThreads), 0, stream, args);                \
     break;
-    LVKV_UNI_SMALL_CASE(0)
-    LVKV_UNI_SMALL_CASE(64)
-    LVKV_UNI_SMALL_CASE(128)
-    LVKV_UNI_SMALL_CASE(192)
+#define LVKV_UNI_SMALL_PAIR(v) LVKV_UNI_SMALL_CASE(v) LVKV_UNI_SMALL_CASE(v + 64)
+    LVKV_UNI_SMALL_PAIR(0)    // all loads, then the fill
+    LVKV_UNI_SMALL_PAIR(4)    // + lane tables first
+    LVKV_UNI_SMALL_PAIR(8)    // chain A before the fill
+    LVKV_UNI_SMALL_PAIR(12)   // production: 4 | 8
+    LVKV_UNI_SMALL_PAIR(16)   // one barrier after chains B/C
+    LVKV_UNI_SMALL_PAIR(128)  // fill first
+    LVKV_UNI_SMALL_PAIR(132)
+    LVKV_UNI_SMALL_PAIR(268)  // 12, chain A early in waves 0-7 only
+    LVKV_UNI_SMALL_PAIR(13)   // probes: 12 without the table walk,
+    LVKV_UNI_SMALL_PAIR(14)   //   without block loads,
+    LVKV_UNI_SMALL_PAIR(44)   //   without the row-table fill,
+    LVKV_UNI_SMALL_PAIR(15)   //   loads and walk both off
+    LVKV_UNI_SMALL_PAIR(4096)  // memory side only
+#undef LVKV_UNI_SMALL_PAIR
 #undef LVKV_UNI_SMALL_CASE
+    default:
+      return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }

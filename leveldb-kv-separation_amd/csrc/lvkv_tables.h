@@ -28,6 +28,7 @@ Gf2Op gf2_compose(const Gf2Op& outer, const Gf2Op& inner);  // outer(inner(v))
 void build_row_table(uint32_t* row_tab);
 void build_lane_table(uint32_t* lane_tab);
 
+
 }  // namespace lvkv
 
 #endif  // LVKV_TABLES_H_

@@ -230,3 +230,35 @@ def test_uniform_kernel_shapes(lvkv, oracle, gpu, length, nblocks):
     h = d.cpu().numpy()[pad:]
     want = oracle.uniform(h, nblocks, length, stride, init=init, mask=bool(length & 1), threads=8)
     assert np.array_equal(_u32(got), want)
+
+
+@pytest.mark.parametrize("length,nblocks,groups", [
+    (4, 700, 0), (6, 3000, 64), (255, 12288, 0), (1021, 999, 3), (4093, 48, 1),
+    (4096, 10000, 0), (4096, 3 * 16 * 17, 17)])
+def test_every_uniform_variant(lvkv, oracle, gpu, length, nblocks, groups):
+    # Force each kernel that can serve a uniform end-aligned batch (the general
+    # kernel's uniform specialisation, the two-stream uniform kernel loads-first
+    # and fill-first, the one-round small kernel both ways) onto the same input
+    # and grid; all must match the oracle bit for bit.
+    import ctypes
+    import torch
+    L = lvkv.lib
+    L.lvkv_debug_uniform_variant.argtypes = [
+        ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+        ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    L.lvkv_debug_uniform_variant.restype = ctypes.c_int
+    stride = (length + 3) // 4 * 4
+    pad = (-length) % 4
+    g = torch.Generator(device=gpu).manual_seed(length + 7 * nblocks)
+    d = torch.randint(0, 256, (pad + nblocks * stride + 64,), dtype=torch.uint8,
+                      device=gpu, generator=g)
+    want = oracle.uniform(d.cpu().numpy()[pad:], nblocks, length, stride, threads=8)
+    waves = 16 * (groups or lvkv.device_groups())
+    small_fits = length <= 4096 and nblocks <= 3 * waves
+    for variant in (32, 256, 384) + ((768, 772, 776, 780, 784, 896, 900, 1804) if small_fits else ()):
+        out = torch.full((nblocks,), -1, dtype=torch.int32, device=gpu)
+        rc = L.lvkv_debug_uniform_variant(variant, groups, d.data_ptr() + pad, stride, length,
+                                          out.data_ptr(), nblocks, None)
+        assert rc == 0, (variant, rc)
+        torch.cuda.synchronize()
+        assert np.array_equal(_u32(out), want), variant

@@ -69,8 +69,19 @@ def timed(fn, n=60):
 
 cases = {
     "v256 uniform kernel": lambda i: run_variant(256, 0, i),
-    "v768 small kernel": lambda i: run_variant(768, 0, i),
-    "v896 small kernel fill-first": lambda i: run_variant(896, 0, i),
+    "v768 small kernel loads-first": lambda i: run_variant(768, 0, i),
+    "v772 small lane-early": lambda i: run_variant(772, 0, i),
+    "v776 small early-A": lambda i: run_variant(776, 0, i),
+    "v780 small early-A lane-early": lambda i: run_variant(780, 0, i),
+    "v784 small one-barrier": lambda i: run_variant(784, 0, i),
+    "v1804 small half-early-A": lambda i: run_variant(1804, 0, i),
+    "v17152 small bare loads": lambda i: run_variant(17152, 0, i),
+    "v781 small 12 no-walk": lambda i: run_variant(781, 0, i),
+    "v782 small 12 no-loads": lambda i: run_variant(782, 0, i),
+    "v812 small 12 no-fill": lambda i: run_variant(812, 0, i),
+    "v783 small 12 no-loads no-walk": lambda i: run_variant(783, 0, i),
+    "v896 small fill-first": lambda i: run_variant(896, 0, i),
+    "v900 small fill-first lane-early": lambda i: run_variant(900, 0, i),
     "v384 uniform fill-first": lambda i: run_variant(384, 0, i),
     "v257 uniform no-compute": lambda i: run_variant(257, 0, i),
     "v258 uniform no-loads": lambda i: run_variant(258, 0, i),
@@ -102,7 +113,7 @@ if len(sys.argv) > 1:  # optional substring filter, e.g. "v0 full" "v6"
     cases = {k: v for k, v in cases.items() if any(f in k for f in sys.argv[1:])}
 
 # correctness of the production variant first
-for v in (0, 8, 32, 256, 768, 896):
+for v in (0, 8, 32, 256, 768, 772, 776, 780, 784, 896, 900, 1804):
     run_variant(v, 0, 0)
     torch.cuda.synchronize()
     ref = lvkv.crc32c_uniform(buf, NB, BL)

@@ -33,11 +33,23 @@ for variant in [int(x) for x in (sys.argv[1:] or ["96", "97"])]:
         t0 = a[:, 0].min()
         rel = np.where(a > 0, (a - t0) * 10, -1)  # ns (100 MHz clock)
         runs.append(rel)
+    # per-workgroup tails: the launch ends with its slowest workgroup
+    wg_exit = np.stack([r[:, 7].reshape(-1, 16).max(axis=1) for r in runs[2:]])  # [run, wg]
+    wg_rows = np.stack([r[:, 2].reshape(-1, 16).max(axis=1) for r in runs[2:]])
+    ng = wg_exit.shape[1]
+    xcd = np.arange(ng) % 8
+    print(f"variant {variant}: per-WG exit (max over its waves), mean over runs; by XCD (g % 8):")
+    print("   ", " ".join(f"x{x}:{int(wg_exit[:, xcd == x].mean())}" for x in range(8)))
+    print("    by g-octile:", " ".join(str(int(wg_exit[:, k * ng // 8:(k + 1) * ng // 8].mean())) for k in range(8)))
+    slow = np.argsort(-wg_exit.mean(axis=0))[:8]
+    print("    slowest WGs:", " ".join(f"g{g}:{int(wg_exit[:, g].mean())}/{int(wg_rows[:, g].mean())}" for g in slow))
+    per_run_end = wg_exit.max(axis=1)
+    print("    launch end (max WG exit) per run:", [int(x) for x in per_run_end])
     rel = np.concatenate(runs[2:])
     def pct(col):
         v = rel[:, col]; v = v[v >= 0]
         return [int(x) for x in np.percentile(v, [0, 10, 50, 90, 100])] if v.size else None
-    res[variant] = {k: pct(c) for k, c in [("entry", 0), ("fill_done", 1), ("slot2", 2), ("slot3", 3), ("exit", 7)]}
+    res[variant] = {k: pct(c) for k, c in [("entry", 0), ("pre_fill", 3), ("fill_issued", 4), ("barrier", 1), ("bc_issued", 5), ("rows_done", 2), ("exit", 7)]}
     print("variant", variant, "percentiles [0,10,50,90,100] ns from first wave entry")
     for k, v in res[variant].items():
         print(f"  {k:10s} {v}")
