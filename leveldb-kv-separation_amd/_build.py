@@ -9,6 +9,7 @@ from __future__ import annotations
 import os
 import shutil
 import subprocess
+from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
@@ -29,7 +30,8 @@ ARCH = os.environ.get("LVKV_OFFLOAD_ARCH", "gfx950")
 HOST_SOURCES = ["lvkv_tables.cpp", "lvkv_cpu_crc32c.cpp", "leveldb_crc32c_shim.cc"]
 # HIP sources: kernels and the runtime-facing C-ABI.
 HIP_SOURCES = ["crc32c_kernel.hip", "crc32c_uniform.hip", "lvkv_capi.cpp"]
-HEADERS = ["lvkv_kernel_args.h", "lvkv_tables.h", "crc32c_device_common.h"]
+HEADERS = ["lvkv_kernel_args.h", "lvkv_tables.h", "crc32c_device_common.h",
+           "crc32c_uniform_common.h"]
 
 
 def _run(cmd: list[str], verbose: bool) -> None:
@@ -51,16 +53,19 @@ def build_lib(verbose: bool = False, force: bool = False) -> Path:
     if not force and _newer(LIB, deps):
         return LIB
     BUILD.mkdir(parents=True, exist_ok=True)
-    objs = []
+    objs, cmds = [], []
     common = ["-O3", "-fPIC", "-std=c++17", "-Wall", "-I", INCLUDE, "-I", CSRC]
     for src in HOST_SOURCES:
         obj = BUILD / (Path(src).stem + ".o")
-        _run(["g++", *common, "-c", CSRC / src, "-o", obj], verbose)
+        cmds.append(["g++", *common, "-c", CSRC / src, "-o", obj])
         objs.append(obj)
     for src in HIP_SOURCES:
         obj = BUILD / (Path(src).stem + ".hip.o")
-        _run([HIPCC, f"--offload-arch={ARCH}", *common, "-c", CSRC / src, "-o", obj], verbose)
+        cmds.append([HIPCC, f"--offload-arch={ARCH}", *common, "-c", CSRC / src, "-o", obj])
         objs.append(obj)
+    # translation units are independent: compile them concurrently
+    with ThreadPoolExecutor(max_workers=min(len(cmds), os.cpu_count() or 1, 8)) as ex:
+        list(ex.map(lambda c: _run(c, verbose), cmds))
     tmp = LIB.with_suffix(".so.tmp")
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp, "-lpthread"], verbose)
     os.replace(tmp, LIB)
