@@ -5,15 +5,22 @@
 One step = one launch of the batch kernel over one batch of blocks already
 resident in HBM (the headline batch: 10,000 x 4096 B). Consecutive steps read
 different windows of a >= 1 GiB rotation so every launch is cold in the
-256 MiB Infinity Cache. N > 1: one process per GPU (torchrun), every rank
-checksums its own 10k-block batch (independent slices, weak scaling, no
-collective on the data path); time = max over ranks of the barrier-bracketed
-K steps. Rank 0 prints ONE JSON line.
+256 MiB Infinity Cache. Steps are independent batches: step i is issued on
+stream i % S (--streams, default 2), so one batch's kernel can start on the
+CUs the previous batch's kernel has released (a checksum service with two
+batches in flight); --streams 1 serialises them. N > 1: one process per GPU
+(torchrun), every rank checksums its own 10k-block batch (independent slices,
+weak scaling, no collective on the data path); time = max over ranks of the
+barrier-bracketed K steps. Rank 0 prints ONE JSON line.
 
-roofline.achieved = algorithmic bytes per launch (nblocks x (block + 4 B
-CRC out)) / average launch duration = HIP-event time on the
-launch stream across the K timed launches / K. cpu_baseline = the reference's own
-util/crc32c.cc (compiled in place into oracle/_ref) timed on this host.
+value = whole-job GiB/s of the K steps (all streams, barrier + synchronize
+on both sides). roofline.achieved = algorithmic bytes per launch (nblocks x
+(block + 4 B CRC out)) / the kernel's own average launch
+duration, measured by a HIP event pair around K launches issued back to back
+on ONE stream (so it agrees with a rocprofv3 kernel trace of --streams 1);
+roofline.pipelined prices the same bytes on the S-stream launch period.
+cpu_baseline = the reference's own util/crc32c.cc (compiled in place into
+oracle/_ref) timed on this host.
 """
 from __future__ import annotations
 
@@ -118,12 +125,14 @@ def load_pmc_traffic():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="headline", choices=sorted(CONFIGS))
     ap.add_argument("--rotate-bytes", type=float, default=1.25 * GIB)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--streams", type=int, default=2,
+                    help="independent batches in flight: step i runs on stream i %% S")
     args = ap.parse_args()
 
     world, rank, local = dist_env()
@@ -142,8 +151,11 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(0x1EDC6F41 + 17 * rank)
     buf = torch.randint(0, 256, (nrot * batch_bytes + 64,), dtype=torch.uint8,
                         device=dev, generator=gen)
-    outs = [torch.empty(nb, dtype=torch.int32, device=dev) for _ in range(2)]
+    nstreams = max(1, args.streams)
+    outs = [torch.empty(nb, dtype=torch.int32, device=dev) for _ in range(2 * nstreams)]
     stream = torch.cuda.current_stream(dev)
+    side = [torch.cuda.Stream(dev) for _ in range(nstreams - 1)]
+    hstreams = [stream.cuda_stream] + [s.cuda_stream for s in side]
 
     # Steps call the C-ABI entry point directly (lvkv_crc32c_uniform_device,
     # include/lvkv_crc32c.h) with pre-computed device pointers, so the host
@@ -154,7 +166,8 @@ def main():
     hstream = stream.cuda_stream
 
     def launch(i):
-        rc = c_uniform(bases[i % nrot], stride, L, 0, out_ptrs[i & 1], nb, 0, hstream)
+        rc = c_uniform(bases[i % nrot], stride, L, 0, out_ptrs[i % len(out_ptrs)], nb, 0,
+                       hstreams[i % nstreams])
         if rc != 0:
             raise SystemExit(f"bench: lvkv_crc32c_uniform_device failed ({rc})")
 
@@ -170,32 +183,20 @@ def main():
     if not np.array_equal(got, want):
         raise SystemExit(f"bench: parity check FAILED on rank {rank}")
 
+    # The kernel's own launch duration (roofline): K launches issued back to
+    # back on ONE stream, before any side stream is used (a process whose
+    # side streams have run measured ~10 % longer single-stream launches).
     for i in range(args.warmup):
-        launch(i + 1)
+        c_uniform(bases[(i + 1) % nrot], stride, L, 0, out_ptrs[i & 1], nb, 0, hstream)
+    k0 = torch.cuda.Event(enable_timing=True)
+    k1 = torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
-
-    # timed region: K back-to-back steps, barrier + sync on both sides; a HIP
-    # event pair on the launch stream brackets the same K launches, giving
-    # the average launch duration the roofline is priced on.
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
+    k0.record(stream)
     for i in range(args.steps):
-        launch(i + 3)
-    ev1.record(stream)
+        c_uniform(bases[(i + 5) % nrot], stride, L, 0, out_ptrs[i & 1], nb, 0, hstream)
+    k1.record(stream)
     torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+    kern_ms = k0.elapsed_time(k1) / args.steps
 
     # Labelled secondary figure: the same batch re-read while resident in the
     # 256 MiB MALL (not the headline; the headline rotates >= 1.25 GiB).
@@ -213,11 +214,43 @@ def main():
         torch.cuda.synchronize()
         warm_us = w0.elapsed_time(w1) * 10.0
 
+    for i in range(args.warmup):
+        launch(i + 1)
+    torch.cuda.synchronize()
+
+    # timed region: K back-to-back steps over S streams, barrier + sync on
+    # both sides; an event pair on the default stream (the side streams fork
+    # from and join into it) gives the device-side launch period.
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for s in side:
+        s.wait_stream(stream)
+    for i in range(args.steps):
+        launch(i + 3)
+    for s in side:
+        stream.wait_stream(s)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    period_ms = ev0.elapsed_time(ev1) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+
     ms_per_step = elapsed / args.steps * 1e3
     data_bytes = nb * L
     value = world * data_bytes * args.steps / elapsed / GIB
     algo_bytes = nb * (L + 4)
     achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
+    achieved_pipe = algo_bytes / (period_ms * 1e-3) / 1e9
 
     if rank == 0:
         cpu = None
@@ -241,11 +274,16 @@ def main():
             "config": {"workload": desc, "nblocks_per_gpu": nb, "block_bytes": L,
                        "stride": stride, "rotation_buffers": nrot,
                        "rotation_bytes": nrot * batch_bytes,
+                       "streams": nstreams,
                        "parallelism": f"{world} independent block slices (no collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
                          "kernel_us_avg": round(kern_ms * 1e3, 3),
+                         "pipelined": {"streams": nstreams,
+                                       "period_us": round(period_ms * 1e3, 3),
+                                       "achieved": round(achieved_pipe, 1),
+                                       "frac": round(achieved_pipe / HBM_PEAK_GBS, 4)},
                          "warm_mall_us_avg": None if warm_us is None else round(warm_us, 3),
                          "algo_bytes_per_launch": algo_bytes},
             "cpu_baseline": cpu,

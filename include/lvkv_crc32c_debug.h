@@ -25,7 +25,9 @@ void lvkv_debug_tables(uint32_t* row_tab, uint32_t* lane_tab);
  * uniform end-aligned specialisation (combines with 1, 2, 4), 64 = record
  * per-wave timestamps (see lvkv_debug_set_stamps), 256 = the dedicated
  * uniform kernel (crc32c_uniform.hip; combines with 64, and 128 = row tables
- * before the loads), 512 (with 256) = its one-round small-batch kernel;
+ * before the loads), 512 (with 256) = its one-round small-batch kernel
+ * (with 256|512 and variant >= 1 << 16, bits 16..30 are the small kernel's
+ * own schedule flags, crc32c_uniform.hip);
  * 0, 8, 32, 96, 256, 320, 384, 448, 768, 832, 896, 960 compute correct CRCs.
  * groups <= 0 uses one workgroup per CU. Returns an LVKV_* code. */
 int lvkv_debug_uniform_variant(int variant, int groups, const void* d_base,

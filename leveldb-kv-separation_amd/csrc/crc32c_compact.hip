@@ -1,0 +1,290 @@
+// Uniform-layout batch CRC32C for gfx950 with a 64 KiB LDS image, so two
+// workgroups fit on one CU (the 160 KiB image of crc32c_uniform.hip allows
+// one). Same arithmetic as the other kernels (end-aligned word grid, Horner
+// over 256-byte rows with Z_256 byte tables, per-lane end shift Z_{256-4s},
+// wave xor-reduce); what changes is how the row tables avoid bank conflicts.
+//
+// Row tables: ds_read_b32 banks are (addr/4) mod 32 per 32-lane half-wave.
+// Instead of 32 copies of each table (lane l -> copy l), lane l looks up, in
+// its p-th lookup of a row step, byte t = (l + p) & 3 of the state in table t,
+// copy c = (l >> 2) & 7. Over one half-wave the pairs (t, c) are all 32
+// distinct, and copy c of table t sits in bank 8t + c of every 256-byte bank
+// row, so each lookup instruction is conflict-free with 8 copies per table:
+//
+//   LDS row b (256 B), bytes [0, 128):   T_t[b] copy c at 32t + 4c
+//   LDS row r (256 B), bytes [128, 256): lane nibble table r>>1 = k*16 + nib,
+//                                        lane s (r & 1 = s >> 5) at 128 + 4(s & 31)
+//
+// The address of a lookup is one v_perm_b32 with a per-lane selector:
+// {kpack.byte[p], S.byte[t], 0, 0} = S.byte[t] * 256 + 32t + 4c, where kpack
+// holds 32t_p + 4c for p = 0..3. XOR order does not matter, so lane l's four
+// lookups still cover the four bytes of its state.
+//
+// Work map: the batch is split into `gridDim.x` contiguous runs of equal
+// length (+1 for the first nblocks % G). Run element i goes to wave i % W,
+// chain i / W, so a wave's valid chains are a prefix and every CU gets the
+// same number of blocks. Chain 0's loads are issued before the LDS fill, the
+// other chains' after the barrier (row-interleaved), then all chains are
+// walked interleaved (crc32c_uniform.hip's measured schedule).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "crc32c_device_common.h"
+#include "crc32c_uniform_common.h"
+#include "lvkv_kernel_args.h"
+
+namespace lvkv {
+
+constexpr uint32_t kCompactLdsBytes = 64 * 1024;
+
+namespace {
+
+enum : int {
+  kCmpBare = 1,  // probe: loads + xor only (no tables, no walk)
+};
+
+struct LaneKeys {
+  uint32_t kpack;   // byte p = 32 * t_p + 4 * c
+  uint32_t sel[4];  // v_perm selectors {kpack.byte[p], S.byte[t_p], 0, 0}
+};
+
+__device__ __forceinline__ LaneKeys lane_keys(uint32_t lane) {
+  LaneKeys k;
+  const uint32_t c = (lane >> 2) & 7u;
+  k.kpack = 0;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const uint32_t t = (lane + static_cast<uint32_t>(p)) & 3u;
+    k.kpack |= (32u * t + 4u * c) << (8 * p);
+    k.sel[p] = 0x0C0C0000u | ((4u + t) << 8) | static_cast<uint32_t>(p);
+  }
+  return k;
+}
+
+// S -> Z_256(S) ^ w on the compact image.
+__device__ __forceinline__ uint32_t row_step_c(const uint32_t* lds, uint32_t s, uint32_t w,
+                                               const LaneKeys& k) {
+  const uint32_t a0 = __builtin_amdgcn_perm(s, k.kpack, k.sel[0]);
+  const uint32_t a1 = __builtin_amdgcn_perm(s, k.kpack, k.sel[1]);
+  const uint32_t a2 = __builtin_amdgcn_perm(s, k.kpack, k.sel[2]);
+  const uint32_t a3 = __builtin_amdgcn_perm(s, k.kpack, k.sel[3]);
+  const uint32_t x = xor3(lds_ld(lds, a0), lds_ld(lds, a1), w);
+  return xor3(x, lds_ld(lds, a2), lds_ld(lds, a3));
+}
+
+// S -> Z_{256-4s}(S) for this lane s (eight lane-private nibble lookups).
+__device__ __forceinline__ uint32_t lane_end_shift_c(const uint32_t* lds, uint32_t s,
+                                                     uint32_t lane_base) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t nib = (s >> (4 * k)) & 15u;
+    r ^= lds_ld(lds, (lane_base | (nib << 9)) + 8192u * k);
+  }
+  return r;
+}
+
+// Row tables: 2048 16-byte slots q -> row b = q >> 3, table t = (q >> 1) & 3,
+// copies 4h..4h+3 with h = q & 1 (address b*256 + 32t + 16h). Eight
+// consecutive lanes cover one row's 128 B: conflict-free ds_write_b128.
+template <int W>
+__device__ __forceinline__ void fill_rows_c(uint32_t* lds, const UniformArgs& a, uint32_t tid) {
+  constexpr int kThreads = 64 * W;
+  constexpr int kIters = 2048 / kThreads;
+  const uint32_t t = (tid >> 1) & 3u;  // the same for every iteration
+  uint32_t col[8];
+#pragma unroll
+  for (int bit = 0; bit < 8; ++bit) {
+    const uint32_t c01 = (t & 1u) ? a.zcol[8 + bit] : a.zcol[bit];
+    const uint32_t c23 = (t & 1u) ? a.zcol[24 + bit] : a.zcol[16 + bit];
+    col[bit] = (t & 2u) ? c23 : c01;
+  }
+#pragma unroll
+  for (int it = 0; it < kIters; ++it) {
+    const uint32_t q = tid + static_cast<uint32_t>(kThreads * it);
+    const uint32_t b = q >> 3;
+    uint32_t e = 0;
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) e ^= (0u - ((b >> bit) & 1u)) & col[bit];
+    *reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds) + b * 256u + (q & 7u) * 16u) =
+        make_uint4(e, e, e, e);
+  }
+}
+
+// Lane tables from HBM (lane_tab[(k*16 + nib)*64 + s], kLaneTabDwords) into
+// the upper halves of the bank rows.
+template <int W>
+struct LaneTabStage {
+  static constexpr int kThreads = 64 * W;
+  static constexpr int kIters = (kLaneTabDwords / 4) / kThreads;
+  uint32_t v[kIters][4];
+
+  __device__ __forceinline__ void load(const UniformArgs& a, uint32_t tid) {
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) {
+      const uint32_t* src = a.lane_tab + 4u * (tid + kThreads * it);
+#pragma unroll
+      for (int x = 0; x < 4; ++x) v[it][x] = src[x];
+    }
+  }
+  __device__ __forceinline__ void store(uint32_t* lds, uint32_t tid) const {
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) {
+      const uint32_t d = 4u * (tid + kThreads * it);
+      const uint32_t r = d >> 6, s = d & 63u;
+      *reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds) + (2u * r + (s >> 5)) * 256u +
+                                128u + (s & 31u) * 4u) =
+          make_uint4(v[it][0], v[it][1], v[it][2], v[it][3]);
+    }
+  }
+};
+
+// One wave with NV (1..NCH) valid chains; blocks blk[0..NV).
+// `live` false: a wave past the batch (tiny batches only) runs chain 0 over an
+// empty window (loads return zeros, no memory traffic) and stores nothing.
+template <int P, int W, int NV, bool FULL>
+__device__ __forceinline__ void compact_body(const UniformArgs& a, const UniGeo& g,
+                                             uint32_t* lds, uint32_t tid, uint32_t lane,
+                                             const uint32_t* blk, bool live) {
+  LaneTabStage<W> lt;
+  __amdgpu_buffer_rsrc_t r[NV];
+#pragma unroll
+  for (int c = 0; c < NV; ++c) r[c] = block_rsrc<0>(a, g, blk[c], live);
+  const int32_t vo = g.vb0 + 4 * static_cast<int32_t>(lane);
+  int32_t vo1 = vo + kRowBytes;
+  asm volatile("" : "+v"(vo1));
+  uint32_t w[NV][kRowsPerChunk];
+  auto load_rows = [&](int c_lo, int c_hi) {
+#pragma unroll
+    for (int j = 0; j < kRowsPerChunk; ++j)
+#pragma unroll
+      for (int c = 0; c < NV; ++c)
+        if (c >= c_lo && c < c_hi && (FULL || static_cast<uint32_t>(j) < g.rows))
+          w[c][j] = load_word(r[c], vo, vo1, j);
+  };
+
+  if (P & kCmpBare) {
+    load_rows(0, NV);
+    uint32_t x = 0;
+#pragma unroll
+    for (int j = 0; j < kRowsPerChunk; ++j)
+#pragma unroll
+      for (int c = 0; c < NV; ++c)
+        if (FULL || static_cast<uint32_t>(j) < g.rows) x ^= w[c][j];
+    asm volatile("s_barrier" ::: "memory");
+    lds[tid] = x;
+    if (lane == 0 && live)
+#pragma unroll
+      for (int c = 0; c < NV; ++c) a.out[blk[c]] = x;
+    return;
+  }
+
+  // 1. Lane tables, chain 0, the LDS image, one barrier, the other chains.
+  lt.load(a, tid);
+  __builtin_amdgcn_sched_barrier(0);
+  load_rows(0, 1);
+  __builtin_amdgcn_sched_barrier(0);
+  fill_rows_c<W>(lds, a, tid);
+  lt.store(lds, tid);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  load_rows(1, NV);
+
+  // 2. Rows, chains interleaved; row-0 fix-ups first.
+  const LaneKeys keys = lane_keys(lane);
+  uint32_t st[NV];
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    fix_first_chunk(w[c], g);
+    st[c] = w[c][0];
+  }
+#pragma unroll
+  for (int j = 1; j < kRowsPerChunk; ++j) {
+    if (FULL || static_cast<uint32_t>(j) < g.rows) {
+#pragma unroll
+      for (int c = 0; c < NV; ++c) st[c] = row_step_c(lds, st[c], w[c][j], keys);
+    }
+  }
+
+  // 3. End shift, reduction, store.
+  const uint32_t lane_base = (lane >> 5) * 256u + 128u + (lane & 31u) * 4u;
+  uint32_t crc[NV];
+#pragma unroll
+  for (int c = 0; c < NV; ++c)
+    crc[c] = wave_xor_dpp(lane_end_shift_c(lds, st[c], lane_base)) ^ 0xffffffffu;
+  if (lane == 0 && live) {
+#pragma unroll
+    for (int c = 0; c < NV; ++c) a.out[blk[c]] = a.mask ? crc_mask(crc[c]) : crc[c];
+  }
+}
+
+}  // namespace
+
+template <int P, int W, int NCH, int OCC>
+__global__ void __launch_bounds__(64 * W, OCC) crc32c_compact_kernel(UniformArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kCompactLdsBytes / 4];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const UniGeo g = uni_geo(a);
+  // Equal contiguous runs per workgroup.
+  const uint32_t G = gridDim.x;
+  const uint32_t per = a.nblocks / G, extra = a.nblocks % G;
+  const uint32_t n = per + (blockIdx.x < extra ? 1u : 0u);
+  const uint32_t start = blockIdx.x * per + min(blockIdx.x, extra);
+  uint32_t blk[NCH];
+  uint32_t nv = 0;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const uint32_t i = static_cast<uint32_t>(c) * W + wave;
+    blk[c] = start + i;
+    nv += i < n ? 1u : 0u;
+  }
+  const bool full = g.rows == static_cast<uint32_t>(kRowsPerChunk);
+  // Every body runs the same single barrier.
+  if (NCH >= 3 && nv >= 3) {
+    if (full) compact_body<P, W, (NCH >= 3 ? 3 : 1), true>(a, g, lds, tid, lane, blk, true);
+    else compact_body<P, W, (NCH >= 3 ? 3 : 1), false>(a, g, lds, tid, lane, blk, true);
+  } else if (NCH >= 2 && nv >= 2) {
+    if (full) compact_body<P, W, (NCH >= 2 ? 2 : 1), true>(a, g, lds, tid, lane, blk, true);
+    else compact_body<P, W, (NCH >= 2 ? 2 : 1), false>(a, g, lds, tid, lane, blk, true);
+  } else {
+    if (full) compact_body<P, W, 1, true>(a, g, lds, tid, lane, blk, nv != 0);
+    else compact_body<P, W, 1, false>(a, g, lds, tid, lane, blk, nv != 0);
+  }
+}
+
+// cfg: bits 0-1 = shape (0: 16 waves x 3 chains, 1 WG/CU; 1: 8 waves x 3
+// chains, 2 WGs/CU; 2: 16 waves x 2 chains, 2 WGs/CU); bit 2 = bare probe.
+int compact_capacity(int cfg) {
+  switch (cfg & 3) {
+    case 0: return 16 * 3;
+    case 1: return 8 * 3;
+    case 2: return 16 * 2;
+  }
+  return 0;
+}
+int compact_occupancy(int cfg) { return (cfg & 3) == 0 ? 1 : 2; }
+
+hipError_t launch_crc32c_compact(const UniformArgs& args, int cfg, int num_groups,
+                                 hipStream_t stream) {
+  switch (cfg & 7) {
+#define LVKV_CMP_CASE(c, p, w, nch, occ)                                        \
+  case c:                                                                       \
+    hipLaunchKernelGGL((crc32c_compact_kernel<p, w, nch, occ>), dim3(num_groups), \
+                       dim3(64 * w), 0, stream, args);                          \
+    break;
+    LVKV_CMP_CASE(0, 0, 16, 3, 1)
+    LVKV_CMP_CASE(1, 0, 8, 3, 2)
+    LVKV_CMP_CASE(2, 0, 16, 2, 2)
+    LVKV_CMP_CASE(4, kCmpBare, 16, 3, 1)
+    LVKV_CMP_CASE(5, kCmpBare, 8, 3, 2)
+    LVKV_CMP_CASE(6, kCmpBare, 16, 2, 2)
+#undef LVKV_CMP_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace lvkv

@@ -459,15 +459,36 @@ __device__ __forceinline__ void small_body(const UniformArgs& a, const UniGeo& g
     fix_first_chunk(w[c], g);
     st[c] = w[c][0];
   }
+  auto walk = [&](int c_lo, int c_hi) {  // rows 1.., chains [c_lo, c_hi) interleaved
 #pragma unroll
-  for (int j = 1; j < kRowsPerChunk; ++j) {
-    if (FULL || static_cast<uint32_t>(j) < g.rows) {
+    for (int j = 1; j < kRowsPerChunk; ++j) {
+      if (FULL || static_cast<uint32_t>(j) < g.rows) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+          if (c >= c_lo && c < c_hi)
+            st[c] = (P & kUniNoCompute) ? (st[c] * 0x01000193u) ^ w[c][j]
+                                        : row_step(lds, st[c], w[c][j], k0, k1);
+      }
+    }
+  };
+  const uint32_t lane_base = kLdsLaneTabBase + lane * 4u;
+  uint32_t crc[NCH];
+  auto reduce = [&](int c_lo, int c_hi) {  // end shift + reduction
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+      if (c >= c_lo && c < c_hi)
+        crc[c] = wave_xor_dpp(lane_end_shift(lds, st[c], lane_base)) ^ 0xffffffffu;
+  };
+  // One store pass at the very end: a global store between the chains'
+  // waits would make the compiler's vmcnt accounting conservative.
+  auto store = [&]() {
+    if (lane == 0) {
 #pragma unroll
       for (int c = 0; c < NCH; ++c)
-        st[c] = (P & kUniNoCompute) ? (st[c] * 0x01000193u) ^ w[c][j]
-                                    : row_step(lds, st[c], w[c][j], k0, k1);
+        if (NCH > 1 || blk[c] < a.nblocks) a.out[blk[c]] = a.mask ? crc_mask(crc[c]) : crc[c];
     }
-  }
+  };
+  walk(0, NCH);
   stamp_uni<P>(a, gw, 2);
 
   // 3. Lane tables (unless already in LDS), end shift + reduction, store.
@@ -475,16 +496,8 @@ __device__ __forceinline__ void small_body(const UniformArgs& a, const UniGeo& g
     write_lane_tables();
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
-  const uint32_t lane_base = kLdsLaneTabBase + lane * 4u;
-  uint32_t crc[NCH];
-#pragma unroll
-  for (int c = 0; c < NCH; ++c)
-    crc[c] = wave_xor_dpp(lane_end_shift(lds, st[c], lane_base)) ^ 0xffffffffu;
-  if (lane == 0) {
-#pragma unroll
-    for (int c = 0; c < NCH; ++c)
-      if (NCH > 1 || blk[c] < a.nblocks) a.out[blk[c]] = a.mask ? crc_mask(crc[c]) : crc[c];
-  }
+  reduce(0, NCH);
+  store();
 }
 
 // Probe: the memory side alone (same loads, mapping and LDS footprint).

@@ -34,6 +34,11 @@ hipError_t launch_crc32c_uniform(const UniformArgs& args, int variant,
 constexpr int kSmallProductionVariant = 4 | 8;
 hipError_t launch_crc32c_uniform_small(const UniformArgs& args, int variant,
                                        int num_groups, hipStream_t stream);
+hipError_t launch_crc32c_compact(const UniformArgs& args, int cfg, int num_groups,
+                                 hipStream_t stream);
+int compact_capacity(int cfg);
+int compact_occupancy(int cfg);
+constexpr int kCompactProductionCfg = 1;  // 8 waves x 3 chains, 2 workgroups per CU
 uint32_t cpu_crc32c_extend(uint32_t crc, const uint8_t* data, size_t n);
 const char* cpu_crc32c_impl_name();
 
@@ -186,9 +191,18 @@ int run_batch(KernelArgs a, size_t nblocks, hipStream_t stream) {
         ((reinterpret_cast<uintptr_t>(b.base) + a.length) % 4) == 0;
     hipError_t e;
     if (uni_aligned) {
-      // One round per wave when every wave owns <= 3 single-chunk blocks.
+      // Blocks of <= 16 rows (4 KiB + 252 B) that fit one round of the
+      // compact-LDS kernel (two 512-thread workgroups per CU, 24 blocks
+      // each): crc32c_compact.hip. At least 3 blocks per workgroup.
+      const int cgroups = static_cast<int>(std::min<size_t>(
+          static_cast<size_t>(c->groups) * compact_occupancy(kCompactProductionCfg),
+          (n + 2) / 3));
       const size_t waves = static_cast<size_t>(groups) * kWavesPerGroup;
-      if (a.length <= kRowsPerChunk * kRowBytes && n <= 3 * waves)
+      if (a.length <= kRowsPerChunk * kRowBytes &&
+          n <= static_cast<size_t>(cgroups) * compact_capacity(kCompactProductionCfg))
+        e = launch_crc32c_compact(uniform_args(*c, b), kCompactProductionCfg, cgroups, stream);
+      // One round per wave when every wave owns <= 3 single-chunk blocks.
+      else if (a.length <= kRowsPerChunk * kRowBytes && n <= 3 * waves)
         e = launch_crc32c_uniform_small(uniform_args(*c, b), kSmallProductionVariant,
                                         groups, stream);
       else
@@ -506,12 +520,23 @@ int lvkv_debug_uniform_variant(int variant, int groups, const void* d_base,
     if (length < 4 || (stride % 4) != 0 ||
         ((reinterpret_cast<uintptr_t>(d_base) + length) % 4) != 0)
       return LVKV_ERR_INVALID;
-    if (variant & 512) {
+    if (variant & 2048) {
+      // compact-LDS kernel (crc32c_compact.hip), cfg in bits 16..22
+      const int cfg = (variant >> 16) & 0x7f;
+      const int gg = groups > 0 ? groups : c->groups * compact_occupancy(cfg);
+      if (length > kRowsPerChunk * kRowBytes ||
+          nblocks > static_cast<size_t>(gg) * compact_capacity(cfg))
+        return LVKV_ERR_INVALID;
+      e = launch_crc32c_compact(uniform_args(*c, a), cfg, gg, static_cast<hipStream_t>(stream));
+    } else if (variant & 512) {
       if (length > kRowsPerChunk * kRowBytes ||
           nblocks > 3 * static_cast<size_t>(g) * kWavesPerGroup)
         return LVKV_ERR_INVALID;
       // debug bit 1024 -> kernel bit 256 (kSmallHalfA), 16384 -> 4096 (memory-only probe)
-      const int sv = (variant & 255) | ((variant & 1024) >> 2) | ((variant & 16384) >> 2);
+      // variant >= 1 << 16: kernel bits given directly in bits 16..30
+      const int sv = variant >= (1 << 16)
+                         ? (variant >> 16) | (variant & 64)
+                         : (variant & 255) | ((variant & 1024) >> 2) | ((variant & 16384) >> 2);
       e = launch_crc32c_uniform_small(uniform_args(*c, a), sv, g,
                                       static_cast<hipStream_t>(stream));
     } else {

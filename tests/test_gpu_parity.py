@@ -255,7 +255,11 @@ def test_every_uniform_variant(lvkv, oracle, gpu, length, nblocks, groups):
     want = oracle.uniform(d.cpu().numpy()[pad:], nblocks, length, stride, threads=8)
     waves = 16 * (groups or lvkv.device_groups())
     small_fits = length <= 4096 and nblocks <= 3 * waves
-    for variant in (32, 256, 384) + ((768, 772, 776, 780, 784, 896, 900, 1804) if small_fits else ()):
+    # compact-LDS kernel shapes (crc32c_compact.hip): (cfg, blocks per group, groups per CU)
+    compact = tuple((cfg << 16) | 2048 | 256 for cfg, cap, occ in ((0, 48, 1), (1, 24, 2), (2, 32, 2))
+                    if length <= 4096 and nblocks <= cap * (groups or occ * lvkv.device_groups()))
+    for variant in ((32, 256, 384) + ((768, 772, 776, 780, 784, 896, 900, 1804) if small_fits else ())
+                    + compact):
         out = torch.full((nblocks,), -1, dtype=torch.int32, device=gpu)
         rc = L.lvkv_debug_uniform_variant(variant, groups, d.data_ptr() + pad, stride, length,
                                           out.data_ptr(), nblocks, None)

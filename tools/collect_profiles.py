@@ -21,7 +21,7 @@ import sys
 from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
-HEADLINE = "crc32c_uniform_small_kernel"
+HEADLINE = "crc32c_compact_kernel"
 
 
 def short(name):

@@ -35,32 +35,97 @@ nrot = 33
 buf = torch.randint(0, 256, (nrot * BATCH,), dtype=torch.uint8, device=dev)
 out = torch.empty(NB, dtype=torch.int32, device=dev)
 stream = torch.cuda.current_stream()
-sh = vp(stream.cuda_stream)
+# --streams S: launch i goes to stream i % S (independent batches in flight,
+# as bench.py --streams); timing brackets all streams.
+NSTREAMS = next((int(a.split("=")[1]) for a in sys.argv[1:] if a.startswith("--streams=")), 1)
+side = [torch.cuda.Stream() for _ in range(NSTREAMS - 1)]
+handles = [vp(stream.cuda_stream)] + [vp(x.cuda_stream) for x in side]
+sh = handles[0]
 cu = lvkv.device_groups()
 
 
 def run_variant(variant, groups, i, warm=False):
     w = 0 if warm else i % nrot
     rc = L.lvkv_debug_uniform_variant(variant, groups, vp(buf.data_ptr() + w * BATCH), BL, BL,
-                                      vp(out.data_ptr()), NB, sh)
+                                      vp(out.data_ptr()), NB, handles[i % NSTREAMS])
     assert rc == 0, rc
 
 
 def run_readbw(groups, i, nbytes=BATCH, warm=False):
     w = 0 if warm else i % nrot
-    rc = L.lvkv_debug_read_bw(vp(buf.data_ptr() + w * BATCH), nbytes, vp(out.data_ptr()), groups, sh)
+    rc = L.lvkv_debug_read_bw(vp(buf.data_ptr() + w * BATCH), nbytes, vp(out.data_ptr()), groups,
+                              handles[i % NSTREAMS])
     assert rc == 0, rc
+
+
+def small_variant(kernel_bits):
+    """Small-kernel schedule flags (crc32c_uniform.hip enum) via the debug entry."""
+    return (kernel_bits << 16) | 768
+
+
+SMALL_CASES = {}  # e.g. {12: "production"}: kernel bits of crc32c_uniform.hip's small kernel
+SMALL_CORRECT = ()
+
+
+def compact_variant(cfg):
+    return (cfg << 16) | 2048 | 256
+
+
+COMPACT_CASES = {0: "16w x3 occ1", 1: "8w x3 occ2", 2: "16w x2 occ2", 4: "16w x3 occ1 bare",
+                 5: "8w x3 occ2 bare", 6: "16w x2 occ2 bare"}
+COMPACT_CORRECT = (0, 1, 2)
+
+GRAPH = "--graph" in sys.argv
 
 
 def timed(fn, n=60):
     """Average per launch over n back-to-back launches (events only around
-    the whole run, as in bench.py's timed region), repeated 5 times."""
+    the whole run, as in bench.py's timed region), repeated 5 times.
+    --graph: the n launches (over all streams) are captured once into a HIP
+    graph and replayed, so the host launch rate drops out."""
+    if GRAPH:
+        return timed_graph(fn, n)
     out = []
     for _ in range(5):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
+        for x in side:
+            x.wait_stream(stream)
         for i in range(n):
             fn(i + 1)
+        for x in side:
+            stream.wait_stream(x)
+        b.record(stream)
+        torch.cuda.synchronize()
+        out.append(a.elapsed_time(b) * 1e3 / n)
+    return out
+
+
+def timed_graph(fn, n):
+    g = torch.cuda.CUDAGraph()
+    cap = torch.cuda.Stream()
+    cap.wait_stream(stream)
+    global handles, side
+    saved = (handles, side)
+    with torch.cuda.stream(cap):
+        cside = [torch.cuda.Stream() for _ in range(NSTREAMS - 1)]
+        handles = [vp(cap.cuda_stream)] + [vp(x.cuda_stream) for x in cside]
+        side = cside
+        g.capture_begin()
+        for x in cside:
+            x.wait_stream(cap)
+        for i in range(n):
+            fn(i + 1)
+        for x in cside:
+            cap.wait_stream(x)
+        g.capture_end()
+    handles, side = saved
+    torch.cuda.synchronize()
+    out = []
+    for _ in range(5):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        g.replay()
         b.record(stream)
         torch.cuda.synchronize()
         out.append(a.elapsed_time(b) * 1e3 / n)
@@ -73,6 +138,11 @@ cases = {
     "v772 small lane-early": lambda i: run_variant(772, 0, i),
     "v776 small early-A": lambda i: run_variant(776, 0, i),
     "v780 small early-A lane-early": lambda i: run_variant(780, 0, i),
+    "v780 warm(MALL)": lambda i: run_variant(780, 0, i, warm=True),
+    **{f"k{kb} {d}": (lambda i, kb=kb: run_variant(small_variant(kb), 0, i))
+       for kb, d in SMALL_CASES.items()},
+    **{f"c{cf} compact {d}": (lambda i, cf=cf: run_variant(compact_variant(cf), 0, i))
+       for cf, d in COMPACT_CASES.items()},
     "v784 small one-barrier": lambda i: run_variant(784, 0, i),
     "v1804 small half-early-A": lambda i: run_variant(1804, 0, i),
     "v17152 small bare loads": lambda i: run_variant(17152, 0, i),
@@ -109,12 +179,15 @@ cases = {
     "readbw 1.3GB": lambda i: run_readbw(8 * cu, 0, nbytes=nrot * BATCH - 16 * 1024),
 }
 
-if len(sys.argv) > 1:  # optional substring filter, e.g. "v0 full" "v6"
-    cases = {k: v for k, v in cases.items() if any(f in k for f in sys.argv[1:])}
+FILTERS = [a for a in sys.argv[1:] if not a.startswith("--")]
+if FILTERS:  # optional substring filter, e.g. "v0 full" "v6"
+    cases = {k: v for k, v in cases.items() if any(f in k for f in FILTERS)}
 
 # correctness of the production variant first
-for v in (0, 8, 32, 256, 768, 772, 776, 780, 784, 896, 900, 1804):
-    run_variant(v, 0, 0)
+for v in (0, 8, 32, 256, 768, 772, 776, 780, 784, 896, 900, 1804,
+          *[small_variant(kb) for kb in SMALL_CORRECT],
+          *[compact_variant(cf) for cf in COMPACT_CORRECT]):
+    run_variant(v, 0, 0)  # stream 0
     torch.cuda.synchronize()
     ref = lvkv.crc32c_uniform(buf, NB, BL)
     torch.cuda.synchronize()
