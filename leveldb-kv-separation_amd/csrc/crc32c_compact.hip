@@ -40,7 +40,9 @@ constexpr uint32_t kCompactLdsBytes = 64 * 1024;
 namespace {
 
 enum : int {
-  kCmpBare = 1,  // probe: loads + xor only (no tables, no walk)
+  kCmpBare = 1,     // probe: loads + xor only (no tables, no walk)
+  kCmpGenLane = 2,  // lane tables generated from 4 columns per lane and
+                    // nibble position (8 KiB of loads per workgroup, not 32)
 };
 
 struct LaneKeys {
@@ -139,6 +141,41 @@ struct LaneTabStage {
   }
 };
 
+// Lane tables generated in-kernel: wave w owns nibble position k = w % 8
+// (and, with 16 waves, nibbles 8 (w / 8) .. +7), loads the 4 columns of
+// Z_{256-4s} it needs (lane_cols[(k*64 + s)*4 + j], one 16-byte load per
+// lane), and writes its entries in Gray-code order, one xor each. For a fixed
+// (k, nib) the 64 lanes write two contiguous 128-byte half rows:
+// conflict-free ds_write_b32.
+template <int W>
+struct LaneTabGen {
+  static constexpr int kNibs = 16 * 8 / W;  // entries per lane
+  uint32_t col[4];
+
+  __device__ __forceinline__ void load(const UniformArgs& a, uint32_t wave, uint32_t lane) {
+    const uint32_t k = wave & 7u;
+    const uint4 v = *reinterpret_cast<const uint4*>(a.lane_cols + (k * 64u + lane) * 4u);
+    col[0] = v.x;
+    col[1] = v.y;
+    col[2] = v.z;
+    col[3] = v.w;
+  }
+  __device__ __forceinline__ void store(uint32_t* lds, uint32_t wave, uint32_t lane) const {
+    const uint32_t k = wave & 7u;
+    const uint32_t nib0 = (W == 16) ? (wave >> 3) * 8u : 0u;
+    char* base = reinterpret_cast<char*>(lds) + (lane >> 5) * 256u + 128u + (lane & 31u) * 4u +
+                 (k * 16u + nib0) * 512u;
+    uint32_t e = 0;
+    if (W == 16 && nib0) e = col[3];  // entry nib0 = 8
+#pragma unroll
+    for (int i = 0; i < kNibs; ++i) {
+      if (i) e ^= col[__builtin_ctz(i)];
+      const int g = i ^ (i >> 1);  // Gray code: nib = nib0 + g
+      *reinterpret_cast<uint32_t*>(base + g * 512) = e;
+    }
+  }
+};
+
 // One wave with NV (1..NCH) valid chains; blocks blk[0..NV).
 // `live` false: a wave past the batch (tiny batches only) runs chain 0 over an
 // empty window (loads return zeros, no memory traffic) and stores nothing.
@@ -147,6 +184,8 @@ __device__ __forceinline__ void compact_body(const UniformArgs& a, const UniGeo&
                                              uint32_t* lds, uint32_t tid, uint32_t lane,
                                              const uint32_t* blk, bool live) {
   LaneTabStage<W> lt;
+  LaneTabGen<W> lg;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   __amdgpu_buffer_rsrc_t r[NV];
 #pragma unroll
   for (int c = 0; c < NV; ++c) r[c] = block_rsrc<0>(a, g, blk[c], live);
@@ -180,12 +219,18 @@ __device__ __forceinline__ void compact_body(const UniformArgs& a, const UniGeo&
   }
 
   // 1. Lane tables, chain 0, the LDS image, one barrier, the other chains.
-  lt.load(a, tid);
+  if (P & kCmpGenLane)
+    lg.load(a, wave, lane);
+  else
+    lt.load(a, tid);
   __builtin_amdgcn_sched_barrier(0);
   load_rows(0, 1);
   __builtin_amdgcn_sched_barrier(0);
   fill_rows_c<W>(lds, a, tid);
-  lt.store(lds, tid);
+  if (P & kCmpGenLane)
+    lg.store(lds, wave, lane);
+  else
+    lt.store(lds, tid);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   load_rows(1, NV);
@@ -255,7 +300,8 @@ __global__ void __launch_bounds__(64 * W, OCC) crc32c_compact_kernel(UniformArgs
 }
 
 // cfg: bits 0-1 = shape (0: 16 waves x 3 chains, 1 WG/CU; 1: 8 waves x 3
-// chains, 2 WGs/CU; 2: 16 waves x 2 chains, 2 WGs/CU); bit 2 = bare probe.
+// chains, 2 WGs/CU; 2: 16 waves x 2 chains, 2 WGs/CU); bit 2 = bare probe;
+// bit 3 = generated lane tables.
 int compact_capacity(int cfg) {
   switch (cfg & 3) {
     case 0: return 16 * 3;
@@ -268,7 +314,7 @@ int compact_occupancy(int cfg) { return (cfg & 3) == 0 ? 1 : 2; }
 
 hipError_t launch_crc32c_compact(const UniformArgs& args, int cfg, int num_groups,
                                  hipStream_t stream) {
-  switch (cfg & 7) {
+  switch (cfg & 15) {
 #define LVKV_CMP_CASE(c, p, w, nch, occ)                                        \
   case c:                                                                       \
     hipLaunchKernelGGL((crc32c_compact_kernel<p, w, nch, occ>), dim3(num_groups), \
@@ -280,6 +326,8 @@ hipError_t launch_crc32c_compact(const UniformArgs& args, int cfg, int num_group
     LVKV_CMP_CASE(4, kCmpBare, 16, 3, 1)
     LVKV_CMP_CASE(5, kCmpBare, 8, 3, 2)
     LVKV_CMP_CASE(6, kCmpBare, 16, 2, 2)
+    LVKV_CMP_CASE(8, kCmpGenLane, 16, 3, 1)
+    LVKV_CMP_CASE(9, kCmpGenLane, 8, 3, 2)
 #undef LVKV_CMP_CASE
     default:
       return hipErrorInvalidValue;

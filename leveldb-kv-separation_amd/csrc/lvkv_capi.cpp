@@ -38,7 +38,8 @@ hipError_t launch_crc32c_compact(const UniformArgs& args, int cfg, int num_group
                                  hipStream_t stream);
 int compact_capacity(int cfg);
 int compact_occupancy(int cfg);
-constexpr int kCompactProductionCfg = 1;  // 8 waves x 3 chains, 2 workgroups per CU
+// 8 waves x 3 chains, two workgroups per CU, generated lane tables
+constexpr int kCompactProductionCfg = 9;
 uint32_t cpu_crc32c_extend(uint32_t crc, const uint8_t* data, size_t n);
 const char* cpu_crc32c_impl_name();
 
@@ -97,9 +98,10 @@ void init_ctx(DeviceCtx& c, int dev) {
     c.status = hip_fail(e);
     return;
   }
-  std::vector<uint32_t> tab(kRowTabDwords + kLaneTabDwords);
+  std::vector<uint32_t> tab(kRowTabDwords + kLaneTabDwords + kLaneColDwords);
   build_row_table(tab.data());
   build_lane_table(tab.data() + kRowTabDwords);
+  build_lane_columns(tab.data() + kRowTabDwords + kLaneTabDwords);
   void* p = nullptr;
   e = hipMalloc(&p, tab.size() * sizeof(uint32_t));
   if (e != hipSuccess) {
@@ -151,6 +153,7 @@ UniformArgs uniform_args(const DeviceCtx& c, const KernelArgs& b) {
   u.stride = b.stride;
   u.out = b.out_crc;
   u.lane_tab = c.d_tables + kRowTabDwords;
+  u.lane_cols = c.d_tables + kRowTabDwords + kLaneTabDwords;
   u.stamps = b.stamps;
   u.length = b.length;
   u.init = b.init;

@@ -27,6 +27,7 @@ constexpr int kRowBytes = 256;      // one wave-wide row: 64 lanes x 4 B
 constexpr int kRowsPerChunk = 16;   // one pipeline stage = 4 KiB per wave
 constexpr uint32_t kRowTabDwords = 4 * 256;
 constexpr uint32_t kLaneTabDwords = 8 * 16 * 64;
+constexpr uint32_t kLaneColDwords = 8 * 64 * 4;  // lane_cols (lvkv_tables.h)
 constexpr uint32_t kLdsRowRegionBytes = 64 * 1024;
 constexpr uint32_t kLdsLaneTabBase = 128 * 1024;
 constexpr uint32_t kLdsBytes = 160 * 1024;
@@ -67,6 +68,8 @@ struct UniformArgs {
   uint64_t stride;
   uint32_t* out;              // nblocks u32 (masked if `mask`)
   const uint32_t* lane_tab;   // kLaneTabDwords, LDS order (loaded per launch)
+  const uint32_t* lane_cols;  // kLaneColDwords (compact kernel generates the
+                              // lane tables from these)
   uint64_t* stamps;           // probe builds only
   uint32_t length;            // >= 4
   uint32_t init;

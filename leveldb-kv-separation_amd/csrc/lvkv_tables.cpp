@@ -69,6 +69,14 @@ void build_lane_table(uint32_t* lane_tab) {
   }
 }
 
+void build_lane_columns(uint32_t* lane_cols) {
+  for (uint32_t s = 0; s < 64; ++s) {
+    const Gf2Op z = gf2_zero_advance(kRowBytes - 4 * s);
+    for (uint32_t k = 0; k < 8; ++k)
+      for (uint32_t j = 0; j < 4; ++j) lane_cols[(k * 64 + s) * 4 + j] = z.col[4 * k + j];
+  }
+}
+
 }  // namespace lvkv
 
 extern "C" __attribute__((visibility("default"))) void lvkv_debug_tables(

@@ -27,6 +27,9 @@ Gf2Op gf2_compose(const Gf2Op& outer, const Gf2Op& inner);  // outer(inner(v))
 //   lane_tab[(k*16 + nib)*64 + s]   = Z_{256-4s}(nib << 4k)   (8192 dwords)
 void build_row_table(uint32_t* row_tab);
 void build_lane_table(uint32_t* lane_tab);
+//   lane_cols[(k*64 + s)*4 + j]     = Z_{256-4s}(1 << (4k + j)) (2048 dwords):
+//   the columns lane s needs to generate its lane-table entries of nibble k
+void build_lane_columns(uint32_t* lane_cols);
 
 
 }  // namespace lvkv

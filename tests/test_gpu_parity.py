@@ -256,7 +256,8 @@ def test_every_uniform_variant(lvkv, oracle, gpu, length, nblocks, groups):
     waves = 16 * (groups or lvkv.device_groups())
     small_fits = length <= 4096 and nblocks <= 3 * waves
     # compact-LDS kernel shapes (crc32c_compact.hip): (cfg, blocks per group, groups per CU)
-    compact = tuple((cfg << 16) | 2048 | 256 for cfg, cap, occ in ((0, 48, 1), (1, 24, 2), (2, 32, 2))
+    compact = tuple((cfg << 16) | 2048 | 256 for cfg, cap, occ in ((0, 48, 1), (1, 24, 2), (2, 32, 2),
+                                                                   (8, 48, 1), (9, 24, 2))
                     if length <= 4096 and nblocks <= cap * (groups or occ * lvkv.device_groups()))
     for variant in ((32, 256, 384) + ((768, 772, 776, 780, 784, 896, 900, 1804) if small_fits else ())
                     + compact):

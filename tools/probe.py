@@ -72,8 +72,9 @@ def compact_variant(cfg):
 
 
 COMPACT_CASES = {0: "16w x3 occ1", 1: "8w x3 occ2", 2: "16w x2 occ2", 4: "16w x3 occ1 bare",
-                 5: "8w x3 occ2 bare", 6: "16w x2 occ2 bare"}
-COMPACT_CORRECT = (0, 1, 2)
+                 5: "8w x3 occ2 bare", 6: "16w x2 occ2 bare", 8: "16w x3 occ1 genlane",
+                 9: "8w x3 occ2 genlane"}
+COMPACT_CORRECT = (0, 1, 2, 8, 9)
 
 GRAPH = "--graph" in sys.argv
 
