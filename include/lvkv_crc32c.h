@@ -92,6 +92,69 @@ int lvkv_log_verify_device(const void* d_file, const uint64_t* d_hdr_offsets,
                            uint32_t* d_actual, uint8_t* d_status,
                            size_t nrecords, void* stream);
 
+/* ---- whole-SSTable verify, device-resident ------- */
+/* report.status: what Table::Open / ReadBlock would return for the table. */
+#define LVKV_SST_OK 0
+#define LVKV_SST_TOO_SHORT 1       /* "file is too short to be an sstable" (table/table.cc:41) */
+#define LVKV_SST_BAD_MAGIC 2       /* "not an sstable (bad magic number)" (table/format.cc:54) */
+#define LVKV_SST_BAD_HANDLE 3      /* "bad block handle" in the footer (table/format.cc:28) */
+#define LVKV_SST_INDEX_TRUNCATED 4 /* "truncated block read" of the index (table/format.cc:86) */
+#define LVKV_SST_INDEX_CHECKSUM 5  /* "block checksum mismatch" on the index (table/format.cc:96) */
+#define LVKV_SST_INDEX_TYPE 6      /* index block compressed (no codec on this path) or
+                                      "bad block type" (table/format.cc:157) */
+#define LVKV_SST_INDEX_CORRUPT 7   /* restart array or an entry unusable (table/block.cc:25-75) */
+#define LVKV_SST_CAPACITY 8        /* more blocks than the caller's arrays hold (ndata says
+                                      how many data blocks the index lists) */
+/* Per-block status (d_status). */
+#define LVKV_BLOCK_OK 0
+#define LVKV_BLOCK_CHECKSUM 1      /* "block checksum mismatch" (table/format.cc:96) */
+#define LVKV_BLOCK_TRUNCATED 2     /* "truncated block read": handle past the file (:86) */
+#define LVKV_BLOCK_BAD_TYPE 3      /* "bad block type": type byte not 0/1/2 (:157) */
+#define LVKV_BLOCK_BAD_HANDLE 4    /* index entry value is not a BlockHandle (:28) */
+#define LVKV_BLOCK_BAD_ENTRY 5     /* "bad entry in block" for the index entry (block.cc:236) */
+
+/* Written by lvkv_sst_verify_table_device into device memory. */
+typedef struct lvkv_sst_report {
+  int32_t status;          /* LVKV_SST_* */
+  uint32_t nblocks;        /* entries in the per-block arrays: ndata + has_filter */
+  uint32_t ndata;          /* data blocks the index lists */
+  uint32_t has_filter;     /* 1: entry ndata is the filter block ("filter." in the metaindex) */
+  uint32_t nbad;           /* entries with status != LVKV_BLOCK_OK */
+  uint32_t first_bad;      /* lowest such entry, or 0xffffffff */
+  uint32_t index_crc;      /* computed CRC (contents + type byte) of the index block */
+  uint32_t meta_crc;       /* same, metaindex block */
+  uint8_t index_status;    /* LVKV_BLOCK_* of the index block */
+  uint8_t meta_status;     /* LVKV_BLOCK_* of the metaindex (Table::ReadMeta ignores its
+                              errors, table/table.cc:92-94; reported, not fatal) */
+  uint8_t reserved0_[6];
+  uint64_t index_offset, index_size, meta_offset, meta_size;  /* footer handles */
+  /* library-internal scratch: the index + metaindex verify before the parse */
+  uint64_t scratch_off_[2];
+  uint32_t scratch_size_[2];
+  uint32_t scratch_crc_[2];
+  uint8_t scratch_status_[2];
+  uint8_t reserved1_[2];
+  uint32_t scratch_count_;
+} lvkv_sst_report;
+
+/* Verifies a whole SSTable image already in device memory, as Table::Open
+ * (table/table.cc:38-79) + Table::ReadMeta (:81-105) + ReadBlock on every
+ * block (table/format.cc:69-160) would with verify_checksums: footer and
+ * magic, index and metaindex checksums, then every data block the index lists
+ * and the filter block, all on the device (footer kernel -> verify of index
+ * and metaindex -> parallel index parse, one entry per restart point as
+ * table_builder.cc:35 writes it -> one batched verify -> merge). Per-block
+ * outputs (arrays of `capacity` entries, device memory), in index order, then
+ * the filter block: d_offsets/d_sizes = the BlockHandle (0/0 for an entry
+ * that is not a usable handle), d_actual = computed CRC of contents + type
+ * byte, d_status = LVKV_BLOCK_*. Asynchronous on `stream` and graph-capturable
+ * (no host synchronisation; counts live in *d_report). Returns LVKV_OK when
+ * the work was enqueued; the table's verdict is d_report->status. */
+int lvkv_sst_verify_table_device(const void* d_file, uint64_t file_size,
+                                 uint64_t* d_offsets, uint32_t* d_sizes,
+                                 uint32_t* d_actual, uint8_t* d_status, size_t capacity,
+                                 lvkv_sst_report* d_report, void* stream);
+
 /* ---- batched, host-resident (end-to-end incl. PCIe) ------------------- */
 /* Blocks live in host memory (pageable or pinned). The library packs them
  * into pinned staging buffers, copies them to the current device with

@@ -73,6 +73,8 @@ def _load() -> ctypes.CDLL:
     L.lvkv_crc32c_uniform_device.restype = i32
     L.lvkv_sst_verify_device.argtypes = [vp, vp, vp, vp, vp, sz, vp]
     L.lvkv_sst_verify_device.restype = i32
+    L.lvkv_sst_verify_table_device.argtypes = [vp, u64, vp, vp, vp, vp, sz, vp, vp]
+    L.lvkv_sst_verify_table_device.restype = i32
     L.lvkv_log_verify_device.argtypes = [vp, vp, vp, vp, sz, vp]
     L.lvkv_log_verify_device.restype = i32
     L.lvkv_crc32c_batch_host.argtypes = [vp, vp, vp, vp, u32, vp, sz, u32]
@@ -244,6 +246,67 @@ def sst_verify(file_buf, offsets, sizes, *, stream=None) -> Tuple["object", "obj
             _stream_handle(stream, file_buf.device))
     _check("lvkv_sst_verify_device", rc)
     return actual, status
+
+
+class SstReport(ctypes.Structure):
+    """lvkv_sst_report (include/lvkv_crc32c.h)."""
+    _fields_ = [("status", ctypes.c_int32), ("nblocks", ctypes.c_uint32),
+                ("ndata", ctypes.c_uint32), ("has_filter", ctypes.c_uint32),
+                ("nbad", ctypes.c_uint32), ("first_bad", ctypes.c_uint32),
+                ("index_crc", ctypes.c_uint32), ("meta_crc", ctypes.c_uint32),
+                ("index_status", ctypes.c_uint8), ("meta_status", ctypes.c_uint8),
+                ("reserved0_", ctypes.c_uint8 * 6),
+                ("index_offset", ctypes.c_uint64), ("index_size", ctypes.c_uint64),
+                ("meta_offset", ctypes.c_uint64), ("meta_size", ctypes.c_uint64),
+                ("scratch_off_", ctypes.c_uint64 * 2), ("scratch_size_", ctypes.c_uint32 * 2),
+                ("scratch_crc_", ctypes.c_uint32 * 2), ("scratch_status_", ctypes.c_uint8 * 2),
+                ("reserved1_", ctypes.c_uint8 * 2), ("scratch_count_", ctypes.c_uint32)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_
+                if not k.endswith("_")}
+
+
+SST_STATUS = {0: "OK", 1: "file is too short to be an sstable",
+              2: "not an sstable (bad magic number)", 3: "bad block handle",
+              4: "truncated block read (index)", 5: "block checksum mismatch (index)",
+              6: "index block type not readable here", 7: "bad index block contents",
+              8: "capacity too small"}
+BLOCK_STATUS = {0: "OK", 1: "block checksum mismatch", 2: "truncated block read",
+                3: "bad block type", 4: "bad block handle", 5: "bad entry in block"}
+
+
+def sst_verify_table(file_buf, *, capacity: Optional[int] = None, stream=None):
+    """Whole-SSTable verify on the device (lvkv_sst_verify_table_device):
+    footer, index, metaindex, filter and every data block of the SST image
+    in `file_buf` (uint8 CUDA tensor). Returns (report dict, offsets int64,
+    sizes int32, actual int32, status uint8) — the per-block tensors cut to
+    report['nblocks'] entries (data blocks in index order, then the filter).
+    With capacity=None a first guess is retried once at the index's size."""
+    torch = _torch()
+    dev = file_buf.device
+    size = file_buf.numel()
+    cap = capacity if capacity is not None else max(64, size // 2048 + 2)
+    for attempt in range(2):
+        off = torch.empty(cap, dtype=torch.int64, device=dev)
+        sizes = torch.empty(cap, dtype=torch.int32, device=dev)
+        actual = torch.empty(cap, dtype=torch.int32, device=dev)
+        status = torch.empty(cap, dtype=torch.uint8, device=dev)
+        rep = torch.zeros(ctypes.sizeof(SstReport), dtype=torch.uint8, device=dev)
+        with torch.cuda.device(dev):
+            rc = _lib.lvkv_sst_verify_table_device(
+                _dev_ptr(file_buf, "file_buf", (torch.uint8, torch.int8)), size,
+                _dev_ptr(off, "offsets"), _dev_ptr(sizes, "sizes"), _dev_ptr(actual, "actual"),
+                _dev_ptr(status, "status"), cap, _dev_ptr(rep, "report"),
+                _stream_handle(stream, dev))
+        _check("lvkv_sst_verify_table_device", rc)
+        r = SstReport.from_buffer_copy(bytes(rep.cpu().numpy()))
+        if r.status == 8 and capacity is None and attempt == 0:
+            cap = r.ndata + 1
+            continue
+        break
+    n = r.nblocks
+    return r.as_dict(), off[:n], sizes[:n], actual[:n], status[:n]
 
 
 def log_verify(file_buf, hdr_offsets, *, stream=None):

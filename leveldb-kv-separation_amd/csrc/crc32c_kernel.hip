@@ -353,7 +353,7 @@ __device__ __forceinline__ void store_result(const KernelArgs& a,
       a.out_crc[it.block] = a.mask ? crc_mask(crc) : crc;
     } else {
       a.out_crc[it.block] = crc;
-      a.out_status[it.block] = (crc != it.g.expected) ? 1 : 0;
+      if (a.out_status != nullptr) a.out_status[it.block] = (crc != it.g.expected) ? 1 : 0;
     }
   }
 }
@@ -460,6 +460,7 @@ __global__ void __launch_bounds__(kGroupThreads, 1)
     crc32c_batch_kernel(KernelArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
 
+  if (a.count != nullptr) a.nblocks = min(a.nblocks, sload_u32(a.count, 0));
   if (V & kProbeEmpty) {
     if (a.nblocks == 0xffffffffu) lds[threadIdx.x] = 0;  // keep the LDS request
     return;

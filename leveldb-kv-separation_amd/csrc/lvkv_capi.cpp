@@ -36,6 +36,10 @@ hipError_t launch_crc32c_uniform_small(const UniformArgs& args, int variant,
                                        int num_groups, hipStream_t stream);
 hipError_t launch_crc32c_compact(const UniformArgs& args, int cfg, int num_groups,
                                  hipStream_t stream);
+hipError_t launch_sst_table(const uint8_t* file, uint64_t file_size, uint64_t* d_off,
+                            uint32_t* d_size, uint32_t* d_actual, uint8_t* d_status,
+                            uint32_t capacity, lvkv_sst_report* r, const KernelArgs& verify,
+                            int groups, hipStream_t stream);
 int compact_capacity(int cfg);
 int compact_occupancy(int cfg);
 // 8 waves x 3 chains, two workgroups per CU, generated lane tables
@@ -387,6 +391,27 @@ int lvkv_sst_verify_device(const void* d_file, const uint64_t* d_offsets,
   a.out_status = d_status;
   a.mode = kModeSstVerify;
   return run_batch(a, nblocks, static_cast<hipStream_t>(stream));
+}
+
+int lvkv_sst_verify_table_device(const void* d_file, uint64_t file_size,
+                                 uint64_t* d_offsets, uint32_t* d_sizes,
+                                 uint32_t* d_actual, uint8_t* d_status, size_t capacity,
+                                 lvkv_sst_report* d_report, void* stream) {
+  if (!d_file || !d_offsets || !d_sizes || !d_actual || !d_status || !d_report ||
+      capacity == 0 || capacity > kMaxBlocksPerLaunch)
+    return LVKV_ERR_INVALID;
+  int rc = LVKV_OK;
+  DeviceCtx* c = current_ctx(&rc);
+  if (c == nullptr) return rc;
+  KernelArgs a = blank_args();
+  a.row_tab = c->d_tables;
+  a.lane_tab = c->d_tables + kRowTabDwords;
+  a.mode = kModeSstVerify;
+  const hipError_t e = launch_sst_table(
+      static_cast<const uint8_t*>(d_file), file_size, d_offsets, d_sizes, d_actual, d_status,
+      static_cast<uint32_t>(capacity), d_report, a, c->groups,
+      static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? LVKV_OK : hip_fail(e);
 }
 
 int lvkv_log_verify_device(const void* d_file, const uint64_t* d_hdr_offsets,

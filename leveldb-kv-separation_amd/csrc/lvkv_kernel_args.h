@@ -59,6 +59,10 @@ struct KernelArgs {
   uint32_t mask;              // 1: store Mask(crc) (util/crc32c.h:29-32)
   uint32_t pad_;
   uint64_t* stamps;           // probe builds only: per-wave timestamps
+  const uint32_t* count;      // optional device-side block count: the launch
+                              // covers min(nblocks, *count) blocks (a count
+                              // produced by an earlier kernel, e.g. an index
+                              // parse); nullptr = nblocks
 };
 
 // Arguments of the uniform-layout kernel (crc32c_uniform.hip): nblocks
