@@ -155,6 +155,46 @@ int lvkv_sst_verify_table_device(const void* d_file, uint64_t file_size,
                                  uint32_t* d_actual, uint8_t* d_status, size_t capacity,
                                  lvkv_sst_report* d_report, void* stream);
 
+/* ---- WAL / MANIFEST verify, device-resident ----- */
+#define LVKV_LOG_CAPACITY 1        /* report.status: more records than `capacity` */
+/* Per physical record (d_rec_status). */
+#define LVKV_REC_OK 0              /* returned by ReadPhysicalRecord */
+#define LVKV_REC_CHECKSUM 1        /* "checksum mismatch" (db/log_reader.cc:243-255) */
+#define LVKV_REC_DROPPED 2         /* after a mismatch in the same block: never read */
+/* Per 32 KiB block (d_block_status). */
+#define LVKV_LOGBLK_OK 0
+#define LVKV_LOGBLK_CHECKSUM 1     /* reported, drop = bytes from that header to block end */
+#define LVKV_LOGBLK_BAD_LENGTH 2   /* "bad record length", reported (:221-232) */
+#define LVKV_LOGBLK_ZERO 3         /* zero-type zero-length record: rest skipped, silent (:234-240) */
+#define LVKV_LOGBLK_EOF 4          /* truncated record or header at the end of the file: kEof */
+
+typedef struct lvkv_log_report {
+  int32_t status;            /* LVKV_OK or LVKV_LOG_CAPACITY */
+  uint32_t nblocks;          /* ceil(file_size / 32768) */
+  uint32_t nrecords;         /* candidate physical records (d_hdr_offsets entries) */
+  uint32_t ngood;            /* records the reader returns */
+  uint32_t ncorrupt;         /* Reporter::Corruption calls */
+  uint32_t first_bad_block;  /* lowest block with a reported corruption, or 0xffffffff */
+  uint64_t dropped_bytes;    /* sum of the reported drop sizes */
+  uint32_t count_;           /* library-internal */
+  uint32_t reserved_;
+} lvkv_log_report;
+
+/* Verifies every physical record of a log image in device memory, as
+ * log::Reader(checksum = true) reading from offset 0 would (ReadPhysicalRecord,
+ * db/log_reader.cc:189-271): the image is cut into 32 KiB blocks
+ * (db/log_format.h), each block's headers are walked on the device, all
+ * candidate records are checksummed in one batched launch, and a mismatch
+ * drops the rest of its block. Outputs: d_hdr_offsets / d_actual (CRC of type
+ * + payload) / d_rec_status for up to `capacity` candidates in file order;
+ * d_block_status / d_block_drop for ceil(file_size / 32768) blocks; totals in
+ * *d_report. Asynchronous on `stream`, no host synchronisation. */
+int lvkv_log_verify_blocks_device(const void* d_file, uint64_t file_size,
+                                  uint64_t* d_hdr_offsets, uint32_t* d_actual,
+                                  uint8_t* d_rec_status, size_t capacity,
+                                  uint8_t* d_block_status, uint32_t* d_block_drop,
+                                  lvkv_log_report* d_report, void* stream);
+
 /* ---- batched, host-resident (end-to-end incl. PCIe) ------------------- */
 /* Blocks live in host memory (pageable or pinned). The library packs them
  * into pinned staging buffers, copies them to the current device with

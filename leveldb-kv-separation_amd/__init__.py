@@ -75,6 +75,8 @@ def _load() -> ctypes.CDLL:
     L.lvkv_sst_verify_device.restype = i32
     L.lvkv_sst_verify_table_device.argtypes = [vp, u64, vp, vp, vp, vp, sz, vp, vp]
     L.lvkv_sst_verify_table_device.restype = i32
+    L.lvkv_log_verify_blocks_device.argtypes = [vp, u64, vp, vp, vp, sz, vp, vp, vp, vp]
+    L.lvkv_log_verify_blocks_device.restype = i32
     L.lvkv_log_verify_device.argtypes = [vp, vp, vp, vp, sz, vp]
     L.lvkv_log_verify_device.restype = i32
     L.lvkv_crc32c_batch_host.argtypes = [vp, vp, vp, vp, u32, vp, sz, u32]
@@ -324,6 +326,51 @@ def log_verify(file_buf, hdr_offsets, *, stream=None):
             _stream_handle(stream, file_buf.device))
     _check("lvkv_log_verify_device", rc)
     return actual, status
+
+
+class LogReport(ctypes.Structure):
+    """lvkv_log_report (include/lvkv_crc32c.h)."""
+    _fields_ = [("status", ctypes.c_int32), ("nblocks", ctypes.c_uint32),
+                ("nrecords", ctypes.c_uint32), ("ngood", ctypes.c_uint32),
+                ("ncorrupt", ctypes.c_uint32), ("first_bad_block", ctypes.c_uint32),
+                ("dropped_bytes", ctypes.c_uint64), ("count_", ctypes.c_uint32),
+                ("reserved_", ctypes.c_uint32)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_ if not k.endswith("_")}
+
+
+def log_verify_blocks(file_buf, *, capacity: Optional[int] = None, stream=None):
+    """Every physical record of the log image in `file_buf` (uint8 CUDA
+    tensor), walked and verified on the device (lvkv_log_verify_blocks_device).
+    Returns (report dict, hdr_offsets int64, actual int32, rec_status uint8 —
+    cut to report['nrecords'] — block_status uint8, block_drop int32)."""
+    torch = _torch()
+    dev = file_buf.device
+    size = file_buf.numel()
+    nblocks = (size + 32767) // 32768
+    cap = capacity if capacity is not None else max(64, size // 256)
+    for attempt in range(2):
+        hdr = torch.empty(cap, dtype=torch.int64, device=dev)
+        actual = torch.empty(cap, dtype=torch.int32, device=dev)
+        rst = torch.empty(cap, dtype=torch.uint8, device=dev)
+        bst = torch.empty(max(1, nblocks), dtype=torch.uint8, device=dev)
+        bdrop = torch.empty(max(1, nblocks), dtype=torch.int32, device=dev)
+        rep = torch.zeros(ctypes.sizeof(LogReport), dtype=torch.uint8, device=dev)
+        with torch.cuda.device(dev):
+            rc = _lib.lvkv_log_verify_blocks_device(
+                _dev_ptr(file_buf, "file_buf", (torch.uint8, torch.int8)), size,
+                _dev_ptr(hdr, "hdr"), _dev_ptr(actual, "actual"), _dev_ptr(rst, "rec_status"),
+                cap, _dev_ptr(bst, "block_status"), _dev_ptr(bdrop, "block_drop"),
+                _dev_ptr(rep, "report"), _stream_handle(stream, dev))
+        _check("lvkv_log_verify_blocks_device", rc)
+        r = LogReport.from_buffer_copy(bytes(rep.cpu().numpy()))
+        if r.status == 1 and capacity is None and attempt == 0:
+            cap = r.nrecords
+            continue
+        break
+    n = r.nrecords if r.status == 0 else 0
+    return r.as_dict(), hdr[:n], actual[:n], rst[:n], bst[:nblocks], bdrop[:nblocks]
 
 
 def crc32c_batch_host(data, offsets, lengths, *, init: int = 0, inits=None,

@@ -40,6 +40,10 @@ hipError_t launch_sst_table(const uint8_t* file, uint64_t file_size, uint64_t* d
                             uint32_t* d_size, uint32_t* d_actual, uint8_t* d_status,
                             uint32_t capacity, lvkv_sst_report* r, const KernelArgs& verify,
                             int groups, hipStream_t stream);
+hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_off,
+                             uint32_t* actual, uint8_t* rec_status, uint32_t capacity,
+                             uint8_t* block_status, uint32_t* block_drop, lvkv_log_report* r,
+                             const KernelArgs& verify, int groups, hipStream_t stream);
 int compact_capacity(int cfg);
 int compact_occupancy(int cfg);
 // 8 waves x 3 chains, two workgroups per CU, generated lane tables
@@ -410,6 +414,29 @@ int lvkv_sst_verify_table_device(const void* d_file, uint64_t file_size,
   const hipError_t e = launch_sst_table(
       static_cast<const uint8_t*>(d_file), file_size, d_offsets, d_sizes, d_actual, d_status,
       static_cast<uint32_t>(capacity), d_report, a, c->groups,
+      static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? LVKV_OK : hip_fail(e);
+}
+
+int lvkv_log_verify_blocks_device(const void* d_file, uint64_t file_size,
+                                  uint64_t* d_hdr_offsets, uint32_t* d_actual,
+                                  uint8_t* d_rec_status, size_t capacity,
+                                  uint8_t* d_block_status, uint32_t* d_block_drop,
+                                  lvkv_log_report* d_report, void* stream) {
+  if ((!d_file && file_size) || !d_hdr_offsets || !d_actual || !d_rec_status || !d_block_status ||
+      !d_block_drop || !d_report || capacity == 0 || capacity > kMaxBlocksPerLaunch ||
+      file_size > (uint64_t{1} << 46))
+    return LVKV_ERR_INVALID;
+  int rc = LVKV_OK;
+  DeviceCtx* c = current_ctx(&rc);
+  if (c == nullptr) return rc;
+  KernelArgs a = blank_args();
+  a.row_tab = c->d_tables;
+  a.lane_tab = c->d_tables + kRowTabDwords;
+  a.mode = kModeLogVerify;
+  const hipError_t e = launch_log_blocks(
+      static_cast<const uint8_t*>(d_file), file_size, d_hdr_offsets, d_actual, d_rec_status,
+      static_cast<uint32_t>(capacity), d_block_status, d_block_drop, d_report, a, c->groups,
       static_cast<hipStream_t>(stream));
   return e == hipSuccess ? LVKV_OK : hip_fail(e);
 }

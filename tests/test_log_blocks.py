@@ -1,0 +1,201 @@
+"""WAL / MANIFEST block verify: the CPU restatement of
+log::Reader::ReadPhysicalRecord (oracle/log_walk.py) pinned by the
+reference-written golden log and the reference's own log_test.cc cases, and
+the device path lvkv_log_verify_blocks_device checked against it.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import random
+import subprocess
+import textwrap
+
+import numpy as np
+import pytest
+
+import log_synth
+import log_walk as lw
+from conftest import GOLDEN, REPO
+
+
+def _golden_log() -> bytes:
+    return (GOLDEN / "wal.log").read_bytes()
+
+
+def _check_equivalent(img: bytes) -> None:
+    """The per-block form (what the device computes) yields exactly the
+    sequential reader's returned records and reported corruptions."""
+    w = lw.read_physical_records(img)
+    v = lw.block_verdicts(img)
+    assert [h for h, s in zip(v.hdrs, v.rec_status) if s == lw.REC_OK] == [r[0] for r in w.records]
+    reported = [(d, "checksum mismatch" if s == lw.BLK_CHECKSUM else "bad record length")
+                for s, d in zip(v.block_status, v.block_drop)
+                if s in (lw.BLK_CHECKSUM, lw.BLK_BAD_LENGTH)]
+    assert reported == w.corruptions
+
+
+# ---------------------------------------------------------------- CPU -----
+
+def test_oracle_reads_reference_log():
+    # oracle/gen_golden.cc wrote wal.log with log::Writer and listed every
+    # physical record log::Reader returned.
+    fx = json.loads((GOLDEN / "wal_records.json").read_text())
+    w = lw.read_physical_records(_golden_log())
+    assert w.records == [(r["offset"], r["length"], r["type"]) for r in fx["records"]]
+    assert w.corruptions == []
+    v = lw.block_verdicts(_golden_log())
+    assert v.hdrs == [r["offset"] for r in fx["records"]]
+
+
+def test_oracle_log_test_cases():
+    # db/log_test.cc, restated on images built like its Writer does.
+    def one(payload):
+        wr = log_synth.LogWriter()
+        wr.add_record(payload)
+        return bytearray(wr.buf)
+    img = one(b"foo")                                  # ChecksumMismatch (:412-418)
+    img[0] = (img[0] + 10) & 0xFF
+    w = lw.read_physical_records(bytes(img))
+    assert w.records == [] and w.corruptions == [(10, "checksum mismatch")]
+    wr = log_synth.LogWriter()                         # BadLength (:393-402)
+    wr.add_record(b"b" * (32768 - 7))
+    wr.add_record(b"foo")
+    img = bytearray(wr.buf)
+    img[4] = (img[4] + 1) & 0xFF
+    w = lw.read_physical_records(bytes(img))
+    assert [r[1] for r in w.records] == [3] and w.corruptions == [(32768, "bad record length")]
+    img = one(b"foo")[:-1]                             # BadLengthAtEndIsIgnored (:404-410)
+    assert lw.read_physical_records(bytes(img)).corruptions == []
+    img = one(b"foo")[:-4]                             # TruncatedTrailingRecordIsIgnored
+    w = lw.read_physical_records(bytes(img))
+    assert w.records == [] and w.corruptions == []
+    wr = log_synth.LogWriter()                         # MarginalTrailer (:296-307)
+    wr.add_record(b"a" * (32768 - 2 * 7))
+    wr.add_record(b"")
+    wr.add_record(b"bar")
+    w = lw.read_physical_records(bytes(wr.buf))
+    assert [r[1] for r in w.records] == [32768 - 14, 0, 3]
+    for img in (_golden_log(), log_synth.build_log(200, seed=2, big_every=37)):
+        _check_equivalent(img)
+
+
+def test_oracle_block_form_equivalent_under_random_damage():
+    img = log_synth.build_log(300, seed=5, max_len=4000, big_every=53)
+    rng = random.Random(7)
+    for _ in range(200):
+        b = bytearray(img)
+        for _ in range(rng.randint(1, 4)):
+            p = rng.randrange(len(b))
+            b[p] ^= 1 << rng.randrange(8)
+        if rng.random() < 0.3:
+            b = b[: rng.randrange(len(b))]
+        if rng.random() < 0.2:  # a preallocated zero region
+            p = rng.randrange(len(b))
+            b[p: p + 64] = b"\0" * len(b[p: p + 64])
+        _check_equivalent(bytes(b))
+
+
+def test_log_report_struct_layout(tmp_path, lvkv):
+    src = tmp_path / "layout.c"
+    src.write_text(textwrap.dedent("""
+        #include <stddef.h>
+        #include <stdio.h>
+        #include "lvkv_crc32c.h"
+        #define F(x) printf("%s %zu\\n", #x, offsetof(lvkv_log_report, x));
+        int main(void) {
+          printf("size %zu\\n", sizeof(lvkv_log_report));
+          F(status) F(nblocks) F(nrecords) F(ngood) F(ncorrupt) F(first_bad_block)
+          F(dropped_bytes) F(count_)
+          return 0;
+        }"""))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", str(REPO / "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(l.split() for l in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                  check=True).stdout.splitlines())
+    S = lvkv.LogReport
+    assert int(got.pop("size")) == ctypes.sizeof(S)
+    for name, off in got.items():
+        assert getattr(S, name).offset == int(off), name
+
+
+# ---------------------------------------------------------------- GPU -----
+
+def _device(lvkv, img: bytes, gpu, capacity=None):
+    import torch
+    buf = torch.from_numpy(np.frombuffer(img, dtype=np.uint8).copy()).to(gpu)
+    rep, hdr, actual, rst, bst, bdrop = lvkv.log_verify_blocks(buf, capacity=capacity)
+    torch.cuda.synchronize()
+    return (rep, hdr.cpu().numpy(), actual.cpu().numpy().view(np.uint32), rst.cpu().numpy(),
+            bst.cpu().numpy(), bdrop.cpu().numpy().view(np.uint32))
+
+
+def _assert_matches(lvkv, img: bytes, gpu):
+    import oracle
+    v = lw.block_verdicts(img)
+    w = lw.read_physical_records(img)
+    rep, hdr, actual, rst, bst, bdrop = _device(lvkv, img, gpu)
+    assert rep["status"] == 0
+    assert rep["nrecords"] == len(v.hdrs) and list(hdr) == v.hdrs
+    assert list(rst) == v.rec_status
+    assert list(bst) == v.block_status and list(bdrop) == v.block_drop
+    assert rep["ngood"] == len(w.records) and rep["ncorrupt"] == len(w.corruptions)
+    assert rep["dropped_bytes"] == sum(d for d, _ in w.corruptions)
+    bad = [i for i, s in enumerate(v.block_status) if s in (lw.BLK_CHECKSUM, lw.BLK_BAD_LENGTH)]
+    assert rep["first_bad_block"] == (bad[0] if bad else 0xFFFFFFFF)
+    for i, (h, s) in enumerate(zip(v.hdrs, v.rec_status)):
+        if s != lw.REC_DROPPED:
+            n = img[h + 4] | (img[h + 5] << 8)
+            assert int(actual[i]) == oracle.value(img[h + 6: h + 7 + n]), i
+    return rep
+
+
+@pytest.mark.gpu
+def test_device_log_golden(lvkv, gpu):
+    rep = _assert_matches(lvkv, _golden_log(), gpu)
+    assert rep["ngood"] == 18 and rep["ncorrupt"] == 0
+
+
+@pytest.mark.gpu
+def test_device_log_reference_cases(lvkv, gpu):
+    def one(payload):
+        wr = log_synth.LogWriter()
+        wr.add_record(payload)
+        return bytearray(wr.buf)
+    cases = []
+    img = one(b"foo"); img[0] = (img[0] + 10) & 0xFF; cases.append(img)
+    wr = log_synth.LogWriter(); wr.add_record(b"b" * (32768 - 7)); wr.add_record(b"foo")
+    img = bytearray(wr.buf); img[4] = (img[4] + 1) & 0xFF; cases.append(img)
+    cases += [one(b"foo")[:-1], one(b"foo")[:-4], bytearray()]
+    wr = log_synth.LogWriter(); wr.add_record(b"a" * (32768 - 14)); wr.add_record(b"")
+    wr.add_record(b"bar"); cases.append(bytearray(wr.buf))
+    wr = log_synth.LogWriter(); wr.add_record(b"c" * (32768 - 7)); cases.append(bytearray(wr.buf))
+    img = one(b"foo"); img[6] = 100; log_synth.fix_header_crc(img, 0); cases.append(img)
+    for c in cases:
+        _assert_matches(lvkv, bytes(c), gpu)
+
+
+@pytest.mark.gpu
+def test_device_log_random_damage(lvkv, gpu):
+    img = log_synth.build_log(400, seed=9, max_len=5000, big_every=61)
+    rng = random.Random(11)
+    for _ in range(40):
+        b = bytearray(img)
+        for _ in range(rng.randint(1, 4)):
+            p = rng.randrange(len(b))
+            b[p] ^= 1 << rng.randrange(8)
+        if rng.random() < 0.3:
+            b = b[: rng.randrange(len(b))]
+        if rng.random() < 0.2:
+            p = rng.randrange(len(b))
+            b[p: p + 64] = b"\0" * len(b[p: p + 64])
+        _assert_matches(lvkv, bytes(b), gpu)
+
+
+@pytest.mark.gpu
+def test_device_log_large_and_capacity(lvkv, gpu):
+    img = log_synth.build_log(20_000, seed=3, max_len=600, big_every=997)  # ~6 MB, ~190 blocks
+    rep = _assert_matches(lvkv, img, gpu)
+    assert rep["ncorrupt"] == 0 and rep["nblocks"] == (len(img) + 32767) // 32768
+    rep2, *_ = _device(lvkv, img, gpu, capacity=100)
+    assert rep2["status"] == 1 and rep2["nrecords"] == rep["nrecords"]
