@@ -92,6 +92,24 @@ int lvkv_log_verify_device(const void* d_file, const uint64_t* d_hdr_offsets,
                            uint32_t* d_actual, uint8_t* d_status,
                            size_t nrecords, void* stream);
 
+/* ---- write side: batched trailer / header emission */
+/* TableBuilder::WriteRawBlock's checksum (table/table_builder.cc:192-209) for
+ * many finished blocks at once: block i occupies d_file[d_offsets[i],
+ * + d_sizes[i]) followed by its 5-byte trailer whose type byte (byte 0) the
+ * caller has written; writes Mask(CRC32C(contents + type)) little-endian into
+ * trailer bytes 1..4. d_crc (nullable) receives the unmasked CRCs. Blocks
+ * must not overlap each other's trailers. */
+int lvkv_sst_fill_trailers_device(void* d_file, const uint64_t* d_offsets,
+                                  const uint32_t* d_sizes, uint32_t* d_crc, size_t nblocks,
+                                  void* stream);
+
+/* log::Writer::EmitPhysicalRecord's checksum (db/log_writer.cc:82-108) for many
+ * records: record i has its 7-byte header at d_file + d_hdr_offsets[i] with
+ * the length (bytes 4..5) and type (byte 6) written and its payload after it;
+ * writes Mask(CRC32C(type + payload)) into header bytes 0..3. */
+int lvkv_log_fill_headers_device(void* d_file, const uint64_t* d_hdr_offsets, uint32_t* d_crc,
+                                 size_t nrecords, void* stream);
+
 /* ---- whole-SSTable verify, device-resident ------- */
 /* report.status: what Table::Open / ReadBlock would return for the table. */
 #define LVKV_SST_OK 0

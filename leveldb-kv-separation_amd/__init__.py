@@ -75,6 +75,10 @@ def _load() -> ctypes.CDLL:
     L.lvkv_sst_verify_device.restype = i32
     L.lvkv_sst_verify_table_device.argtypes = [vp, u64, vp, vp, vp, vp, sz, vp, vp]
     L.lvkv_sst_verify_table_device.restype = i32
+    L.lvkv_sst_fill_trailers_device.argtypes = [vp, vp, vp, vp, sz, vp]
+    L.lvkv_sst_fill_trailers_device.restype = i32
+    L.lvkv_log_fill_headers_device.argtypes = [vp, vp, vp, sz, vp]
+    L.lvkv_log_fill_headers_device.restype = i32
     L.lvkv_log_verify_blocks_device.argtypes = [vp, u64, vp, vp, vp, sz, vp, vp, vp, vp]
     L.lvkv_log_verify_blocks_device.restype = i32
     L.lvkv_log_verify_device.argtypes = [vp, vp, vp, vp, sz, vp]
@@ -326,6 +330,40 @@ def log_verify(file_buf, hdr_offsets, *, stream=None):
             _stream_handle(stream, file_buf.device))
     _check("lvkv_log_verify_device", rc)
     return actual, status
+
+
+def sst_fill_trailers(file_buf, offsets, sizes, *, stream=None):
+    """Batched TableBuilder::WriteRawBlock checksum (table_builder.cc:192-209):
+    for each block handle (offsets int64, sizes int32 CUDA tensors) whose type
+    byte is already in file_buf, writes Mask(CRC32C(contents + type)) into
+    the trailer in place. Returns the unmasked CRCs (int32 tensor)."""
+    torch = _torch()
+    n = offsets.numel()
+    crc = torch.empty(n, dtype=torch.int32, device=file_buf.device)
+    with torch.cuda.device(file_buf.device):
+        rc = _lib.lvkv_sst_fill_trailers_device(
+            _dev_ptr(file_buf, "file_buf", (torch.uint8, torch.int8)),
+            _dev_ptr(offsets, "offsets", (torch.int64,)),
+            _dev_ptr(sizes, "sizes", (torch.int32,), n), _dev_ptr(crc, "crc"), n,
+            _stream_handle(stream, file_buf.device))
+    _check("lvkv_sst_fill_trailers_device", rc)
+    return crc
+
+
+def log_fill_headers(file_buf, hdr_offsets, *, stream=None):
+    """Batched log::Writer::EmitPhysicalRecord checksum (log_writer.cc:82-108):
+    fills header bytes 0..3 of every record in place. Returns the unmasked
+    CRCs (int32 tensor)."""
+    torch = _torch()
+    n = hdr_offsets.numel()
+    crc = torch.empty(n, dtype=torch.int32, device=file_buf.device)
+    with torch.cuda.device(file_buf.device):
+        rc = _lib.lvkv_log_fill_headers_device(
+            _dev_ptr(file_buf, "file_buf", (torch.uint8, torch.int8)),
+            _dev_ptr(hdr_offsets, "hdr_offsets", (torch.int64,)), _dev_ptr(crc, "crc"), n,
+            _stream_handle(stream, file_buf.device))
+    _check("lvkv_log_fill_headers_device", rc)
+    return crc
 
 
 class LogReport(ctypes.Structure):

@@ -172,13 +172,13 @@ __device__ __forceinline__ Geo make_geo(const KernelArgs& a, uint32_t b) {
   const uint64_t base = reinterpret_cast<uint64_t>(a.base);
   uint64_t off;
   uint32_t len, init = a.init, expected = 0;
-  if (a.mode == kModeLogVerify) {
+  if (a.mode == kModeLogVerify || a.mode == kModeLogFill) {
     // Header [masked crc u32][len u16][type u8]; CRC covers type + payload
     // (db/log_reader.cc:217-221, 243-247).
     const uint64_t hoff = sload_u64(a.offsets, b);
     const uint64_t hdr = base + hoff;
     const uint32_t len_type = sload_le(hdr + 4, 3);
-    expected = crc_unmask(sload_le(hdr, 4));
+    if (a.mode == kModeLogVerify) expected = crc_unmask(sload_le(hdr, 4));
     off = hoff + 6;
     len = 1u + (len_type & 0xffffu);
     init = 0;
@@ -190,12 +190,12 @@ __device__ __forceinline__ Geo make_geo(const KernelArgs& a, uint32_t b) {
     off = static_cast<uint64_t>(b) * a.stride;
     len = a.length;
   }
-  if (a.mode == kModeSstVerify) {
+  if (a.mode == kModeSstVerify || a.mode == kModeSstFill) {
     // Block contents n bytes + type byte are covered; the masked CRC follows
     // (table/format.cc:92-94, table/table_builder.cc:199-203).
     len += 1;
     init = 0;
-    expected = crc_unmask(sload_le(base + off + len, 4));
+    if (a.mode == kModeSstVerify) expected = crc_unmask(sload_le(base + off + len, 4));
   }
 
   Geo g;
@@ -351,6 +351,16 @@ __device__ __forceinline__ void store_result(const KernelArgs& a,
   if (lane_id() == 0) {
     if ((V & kUniformAligned) || a.mode == kModeCompute) {
       a.out_crc[it.block] = a.mask ? crc_mask(crc) : crc;
+    } else if (a.mode == kModeSstFill || a.mode == kModeLogFill) {
+      // The stored form (Mask, little-endian) into the trailer / header hole:
+      // trailer bytes 1..4 follow the covered n+1 bytes; the header CRC sits
+      // 6 bytes before the covered type byte.
+      const uint64_t ptr = (static_cast<uint64_t>(it.g.ptr_hi) << 32) | it.g.ptr_lo;
+      uint8_t* dst = reinterpret_cast<uint8_t*>(a.mode == kModeSstFill ? ptr + it.g.len : ptr - 6);
+      const uint32_t m = crc_mask(crc);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) dst[k] = static_cast<uint8_t>(m >> (8 * k));
+      if (a.out_crc != nullptr) a.out_crc[it.block] = crc;
     } else {
       a.out_crc[it.block] = crc;
       if (a.out_status != nullptr) a.out_status[it.block] = (crc != it.g.expected) ? 1 : 0;

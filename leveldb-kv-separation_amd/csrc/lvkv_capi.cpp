@@ -189,7 +189,7 @@ int run_batch(KernelArgs a, size_t nblocks, hipStream_t stream) {
       b.base = a.base + done * a.stride;
     }
     if (a.inits != nullptr) b.inits = a.inits + done;
-    b.out_crc = a.out_crc + done;
+    if (a.out_crc != nullptr) b.out_crc = a.out_crc + done;
     if (a.out_status != nullptr) b.out_status = a.out_status + done;
     const size_t want = (n + kWavesPerGroup - 1) / kWavesPerGroup;
     const int groups = static_cast<int>(
@@ -439,6 +439,32 @@ int lvkv_log_verify_blocks_device(const void* d_file, uint64_t file_size,
       static_cast<uint32_t>(capacity), d_block_status, d_block_drop, d_report, a, c->groups,
       static_cast<hipStream_t>(stream));
   return e == hipSuccess ? LVKV_OK : hip_fail(e);
+}
+
+int lvkv_sst_fill_trailers_device(void* d_file, const uint64_t* d_offsets,
+                                  const uint32_t* d_sizes, uint32_t* d_crc, size_t nblocks,
+                                  void* stream) {
+  if (nblocks == 0) return LVKV_OK;
+  if (!d_file || !d_offsets || !d_sizes) return LVKV_ERR_INVALID;
+  KernelArgs a = blank_args();
+  a.base = static_cast<const uint8_t*>(d_file);
+  a.offsets = d_offsets;
+  a.lengths = d_sizes;
+  a.out_crc = d_crc;
+  a.mode = kModeSstFill;
+  return run_batch(a, nblocks, static_cast<hipStream_t>(stream));
+}
+
+int lvkv_log_fill_headers_device(void* d_file, const uint64_t* d_hdr_offsets, uint32_t* d_crc,
+                                 size_t nrecords, void* stream) {
+  if (nrecords == 0) return LVKV_OK;
+  if (!d_file || !d_hdr_offsets) return LVKV_ERR_INVALID;
+  KernelArgs a = blank_args();
+  a.base = static_cast<const uint8_t*>(d_file);
+  a.offsets = d_hdr_offsets;
+  a.out_crc = d_crc;
+  a.mode = kModeLogFill;
+  return run_batch(a, nrecords, static_cast<hipStream_t>(stream));
 }
 
 int lvkv_log_verify_device(const void* d_file, const uint64_t* d_hdr_offsets,

@@ -40,6 +40,10 @@ enum : uint32_t {
   kModeCompute = 0,    // out_crc[i] = Extend(init_i, base + off_i, len_i)
   kModeSstVerify = 1,  // table/format.cc:92-99: covers n+1, trailer after it
   kModeLogVerify = 2,  // db/log_reader.cc:243-257: header at off, len parsed
+  kModeSstFill = 3,    // table_builder.cc:199-203: covers n+1, writes the
+                       // masked CRC into trailer bytes 1..4
+  kModeLogFill = 4,    // log_writer.cc:94-96: header at off, writes the
+                       // masked CRC into header bytes 0..3
 };
 
 struct KernelArgs {

@@ -199,3 +199,24 @@ def test_device_log_large_and_capacity(lvkv, gpu):
     assert rep["ncorrupt"] == 0 and rep["nblocks"] == (len(img) + 32767) // 32768
     rep2, *_ = _device(lvkv, img, gpu, capacity=100)
     assert rep2["status"] == 1 and rep2["nrecords"] == rep["nrecords"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("source", ["golden", "synthetic"])
+def test_device_fill_headers_rebuilds_the_log(lvkv, gpu, source):
+    # log::Writer::EmitPhysicalRecord (log_writer.cc:82-108) wrote these
+    # headers; wipe every header CRC and let the device refill them.
+    import torch
+    import oracle
+    img = _golden_log() if source == "golden" else log_synth.build_log(3000, seed=4,
+                                                                         big_every=101)
+    hdrs = lw.block_verdicts(img).hdrs
+    wiped = bytearray(img)
+    for h in hdrs:
+        wiped[h: h + 4] = b"\0\0\0\0"
+    buf = torch.from_numpy(np.frombuffer(bytes(wiped), dtype=np.uint8).copy()).to(gpu)
+    crc = lvkv.log_fill_headers(buf, torch.tensor(hdrs, dtype=torch.int64, device=gpu))
+    torch.cuda.synchronize()
+    assert bytes(buf.cpu().numpy()) == img
+    want = [oracle.value(img[h + 6: h + 7 + (img[h + 4] | img[h + 5] << 8)]) for h in hdrs]
+    assert list(crc.cpu().numpy().view(np.uint32)) == want

@@ -213,3 +213,32 @@ def test_device_table_verify_synthetic(lvkv, gpu, n, bs, filt):
     if n > 1:
         rep2, *_ = _device_verify(lvkv, img, gpu, capacity=n // 2)
         assert rep2["status"] == st.SST_CAPACITY and rep2["ndata"] == n
+
+
+# --------------------------------------------- write side (§8f row 3) -----
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("source", ["golden", "synthetic"])
+def test_device_fill_trailers_rebuilds_the_table(lvkv, gpu, source):
+    # TableBuilder::WriteRawBlock (table_builder.cc:192-209) wrote these
+    # trailers; wipe every CRC (types kept) and let the device refill them.
+    import torch
+    if source == "golden":
+        img = _golden_img()
+        blocks = [(b["offset"], b["size"]) for b in _golden_blocks()]
+    else:
+        img = sst_synth.build_sst(3000, 4096, seed=21)
+        r = st.verify_table(img)
+        blocks = r.handles + [r.meta, r.index]
+    wiped = bytearray(img)
+    for off, size in blocks:
+        wiped[off + size + 1: off + size + 5] = b"\0\0\0\0"
+    buf = torch.from_numpy(np.frombuffer(bytes(wiped), dtype=np.uint8).copy()).to(gpu)
+    offs = torch.tensor([o for o, _ in blocks], dtype=torch.int64, device=gpu)
+    sizes = torch.tensor([s for _, s in blocks], dtype=torch.int32, device=gpu)
+    crc = lvkv.sst_fill_trailers(buf, offs, sizes)
+    torch.cuda.synchronize()
+    assert bytes(buf.cpu().numpy()) == img
+    import oracle
+    want = [oracle.value(img[o: o + s + 1]) for o, s in blocks]
+    assert list(crc.cpu().numpy().view(np.uint32)) == want
