@@ -146,13 +146,18 @@ typedef struct lvkv_sst_report {
                               errors, table/table.cc:92-94; reported, not fatal) */
   uint8_t reserved0_[6];
   uint64_t index_offset, index_size, meta_offset, meta_size;  /* footer handles */
-  /* library-internal scratch: the index + metaindex verify before the parse */
-  uint64_t scratch_off_[2];
-  uint32_t scratch_size_[2];
+  /* library-internal scratch: the index + metaindex verify before the parse,
+   * each block cut into up to 64 segments checksummed in parallel */
   uint32_t scratch_crc_[2];
   uint8_t scratch_status_[2];
   uint8_t reserved1_[2];
-  uint32_t scratch_count_;
+  uint32_t scratch_count_;     /* segments in use */
+  uint32_t scratch_nseg_[2];   /* segments of the index / metaindex */
+  uint32_t reserved2_;
+  uint64_t seg_off_[128];
+  uint32_t seg_len_[128];
+  uint32_t seg_init_[128];
+  uint32_t seg_crc_[128];
 } lvkv_sst_report;
 
 /* Verifies a whole SSTable image already in device memory, as Table::Open

@@ -264,9 +264,11 @@ class SstReport(ctypes.Structure):
                 ("reserved0_", ctypes.c_uint8 * 6),
                 ("index_offset", ctypes.c_uint64), ("index_size", ctypes.c_uint64),
                 ("meta_offset", ctypes.c_uint64), ("meta_size", ctypes.c_uint64),
-                ("scratch_off_", ctypes.c_uint64 * 2), ("scratch_size_", ctypes.c_uint32 * 2),
                 ("scratch_crc_", ctypes.c_uint32 * 2), ("scratch_status_", ctypes.c_uint8 * 2),
-                ("reserved1_", ctypes.c_uint8 * 2), ("scratch_count_", ctypes.c_uint32)]
+                ("reserved1_", ctypes.c_uint8 * 2), ("scratch_count_", ctypes.c_uint32),
+                ("scratch_nseg_", ctypes.c_uint32 * 2), ("reserved2_", ctypes.c_uint32),
+                ("seg_off_", ctypes.c_uint64 * 128), ("seg_len_", ctypes.c_uint32 * 128),
+                ("seg_init_", ctypes.c_uint32 * 128), ("seg_crc_", ctypes.c_uint32 * 128)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_

@@ -39,7 +39,7 @@ hipError_t launch_crc32c_compact(const UniformArgs& args, int cfg, int num_group
 hipError_t launch_sst_table(const uint8_t* file, uint64_t file_size, uint64_t* d_off,
                             uint32_t* d_size, uint32_t* d_actual, uint8_t* d_status,
                             uint32_t capacity, lvkv_sst_report* r, const KernelArgs& verify,
-                            int groups, hipStream_t stream);
+                            const uint32_t* zpow, int groups, hipStream_t stream);
 hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_off,
                              uint32_t* actual, uint8_t* rec_status, uint32_t capacity,
                              uint8_t* block_status, uint32_t* block_drop, lvkv_log_report* r,
@@ -106,10 +106,12 @@ void init_ctx(DeviceCtx& c, int dev) {
     c.status = hip_fail(e);
     return;
   }
-  std::vector<uint32_t> tab(kRowTabDwords + kLaneTabDwords + kLaneColDwords);
+  static_assert(kZPowOffset == kRowTabDwords + kLaneTabDwords + kLaneColDwords, "layout");
+  std::vector<uint32_t> tab(kZPowOffset + kZPowDwords);
   build_row_table(tab.data());
   build_lane_table(tab.data() + kRowTabDwords);
   build_lane_columns(tab.data() + kRowTabDwords + kLaneTabDwords);
+  build_zpow_tables(tab.data() + kZPowOffset);
   void* p = nullptr;
   e = hipMalloc(&p, tab.size() * sizeof(uint32_t));
   if (e != hipSuccess) {
@@ -413,7 +415,7 @@ int lvkv_sst_verify_table_device(const void* d_file, uint64_t file_size,
   a.mode = kModeSstVerify;
   const hipError_t e = launch_sst_table(
       static_cast<const uint8_t*>(d_file), file_size, d_offsets, d_sizes, d_actual, d_status,
-      static_cast<uint32_t>(capacity), d_report, a, c->groups,
+      static_cast<uint32_t>(capacity), d_report, a, c->d_tables + kZPowOffset, c->groups,
       static_cast<hipStream_t>(stream));
   return e == hipSuccess ? LVKV_OK : hip_fail(e);
 }

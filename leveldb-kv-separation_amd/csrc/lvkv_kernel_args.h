@@ -28,6 +28,9 @@ constexpr int kRowsPerChunk = 16;   // one pipeline stage = 4 KiB per wave
 constexpr uint32_t kRowTabDwords = 4 * 256;
 constexpr uint32_t kLaneTabDwords = 8 * 16 * 64;
 constexpr uint32_t kLaneColDwords = 8 * 64 * 4;  // lane_cols (lvkv_tables.h)
+constexpr uint32_t kZPowCount = 48;               // Z_{2^j}, j < 48 (256 TiB)
+constexpr uint32_t kZPowDwords = kZPowCount * 1024;
+constexpr uint32_t kZPowOffset = 1024 + 8 * 16 * 64 + 8 * 64 * 4;  // in d_tables
 constexpr uint32_t kLdsRowRegionBytes = 64 * 1024;
 constexpr uint32_t kLdsLaneTabBase = 128 * 1024;
 constexpr uint32_t kLdsBytes = 160 * 1024;

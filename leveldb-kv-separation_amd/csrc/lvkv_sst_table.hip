@@ -6,8 +6,11 @@
 //   1. sst_footer_kernel      one lane: size check, magic, the two footer
 //                             BlockHandles (format.cc:43-67); index and
 //                             metaindex handles into the report's scratch
-//   2. crc32c_batch_kernel    SST-verify mode over those two blocks (count
-//                             read from the report on the device)
+//   2. crc32c_batch_kernel    the index and metaindex cut into up to 64
+//                             segments each, checksummed in parallel
+//      sst_combine_kernel     one lane per segment: shift by the bytes after
+//                             it (Z_n as a product of Z_{2^j} byte tables),
+//                             wave xor -> the two block CRCs vs their trailers
 //   3. sst_index_kernel       one lane per index entry: the index is written
 //                             with block_restart_interval = 1
 //                             (table_builder.cc:35, :90), so restart point i
@@ -37,6 +40,21 @@ constexpr uint64_t kTableMagic = 0xdb4775248b80fb57ull;  // table/format.h:76
 constexpr uint64_t kFooterLen = 48;  // table/format.h:53 (2 * 20 + 8)
 constexpr uint64_t kTrailer = 5;     // table/format.h:79
 constexpr uint32_t kIndexThreads = 256;
+
+constexpr uint64_t kSegMin = 16384;
+
+// Z_n(v): the register advanced over n zero bytes, as the product of the
+// Z_{2^j} for the set bits j of n (zpow: kZPowCount byte-table sets).
+__device__ uint32_t zshift(const uint32_t* zpow, uint32_t v, uint64_t n) {
+  while (n) {
+    const uint32_t j = __builtin_ctzll(n);
+    const uint32_t* t = zpow + j * 1024u;
+    v = t[v & 255u] ^ t[256u + ((v >> 8) & 255u)] ^ t[512u + ((v >> 16) & 255u)] ^
+        t[768u + (v >> 24)];
+    n &= n - 1;
+  }
+  return v;
+}
 
 __device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {
   return static_cast<uint32_t>(p[0]) | (static_cast<uint32_t>(p[1]) << 8) |
@@ -112,6 +130,7 @@ __global__ void sst_footer_kernel(const uint8_t* file, uint64_t size, lvkv_sst_r
   r->meta_status = LVKV_BLOCK_OK;
   r->index_offset = r->index_size = r->meta_offset = r->meta_size = 0;
   r->scratch_count_ = 0;
+  r->scratch_nseg_[0] = r->scratch_nseg_[1] = 0;
   r->scratch_status_[0] = r->scratch_status_[1] = 0;
   if (size < kFooterLen) {  // table/table.cc:40-42
     r->status = LVKV_SST_TOO_SHORT;
@@ -142,11 +161,51 @@ __global__ void sst_footer_kernel(const uint8_t* file, uint64_t size, lvkv_sst_r
   }
   const bool meta_ok = handle_in_file(mo, ms, size);
   if (!meta_ok) r->meta_status = LVKV_BLOCK_TRUNCATED;
-  r->scratch_off_[0] = io;
-  r->scratch_size_[0] = static_cast<uint32_t>(is);
-  r->scratch_off_[1] = meta_ok ? mo : 0;
-  r->scratch_size_[1] = meta_ok ? static_cast<uint32_t>(ms) : 0;
-  r->scratch_count_ = 2;
+  // Covered ranges (contents + type byte) cut into m <= 64 segments of at
+  // least kSegMin bytes; segment k > 0 starts from register 0 (init ~0).
+  uint32_t n = 0;
+  for (int blk = 0; blk < 2; ++blk) {
+    const uint64_t off = blk == 0 ? io : mo;
+    const uint64_t len = blk == 0 ? is + 1 : (meta_ok ? ms + 1 : 0);
+    uint64_t m = len ? (len + kSegMin - 1) / kSegMin : 0;
+    if (m > 64) m = 64;
+    const uint64_t seg = m ? (len + m - 1) / m : 0;
+    for (uint64_t k = 0; k < m; ++k) {
+      const uint64_t a = k * seg;
+      r->seg_off_[n] = off + a;
+      r->seg_len_[n] = static_cast<uint32_t>(min(seg, len - a));
+      r->seg_init_[n] = k ? 0xffffffffu : 0u;
+      ++n;
+    }
+    r->scratch_nseg_[blk] = static_cast<uint32_t>(m);
+  }
+  r->scratch_count_ = n;
+}
+
+// Wave 0: the index block, wave 1: the metaindex. Lane k owns segment k:
+// its register (CRC ^ ~0) advanced over the bytes after the segment, then
+// xored over the wave: the block's register, so CRC = reg ^ ~0.
+__global__ void __launch_bounds__(128)
+    sst_combine_kernel(const uint8_t* file, lvkv_sst_report* r, const uint32_t* zpow) {
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  if (r->status != LVKV_SST_OK || r->scratch_count_ == 0) return;
+  const uint32_t m = r->scratch_nseg_[w];
+  if (m == 0) return;
+  const uint32_t first = w ? r->scratch_nseg_[0] : 0u;
+  uint32_t v = 0;
+  if (lane < m) {
+    const uint32_t i = first + lane;
+    const uint64_t end = (w ? r->meta_offset + r->meta_size : r->index_offset + r->index_size) + 1;
+    v = zshift(zpow, r->seg_crc_[i] ^ 0xffffffffu, end - (r->seg_off_[i] + r->seg_len_[i]));
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v ^= __shfl_xor(v, d, 64);
+  if (lane == 0) {
+    const uint32_t crc = v ^ 0xffffffffu;
+    const uint8_t* t = file + (w ? r->meta_offset + r->meta_size : r->index_offset + r->index_size);
+    r->scratch_crc_[w] = crc;
+    r->scratch_status_[w] = crc != crc_unmask(ld_le32(t + 1)) ? 1 : 0;
+  }
 }
 
 // Lane 0: Table::ReadMeta's lookup (table.cc:95-104) — the first key with
@@ -264,7 +323,7 @@ __global__ void __launch_bounds__(kIndexThreads)
     sst_merge_kernel(const uint8_t* file, lvkv_sst_report* r, const uint64_t* off,
                      const uint32_t* size, const uint32_t* actual, uint8_t* status) {
   const uint32_t gid = blockIdx.x * kIndexThreads + threadIdx.x;
-  if (gid == 0 && r->scratch_count_ == 2) {
+  if (gid == 0 && r->scratch_count_ > 0) {
     r->index_crc = r->scratch_crc_[0];
     if (r->meta_status == LVKV_BLOCK_OK) {
       r->meta_crc = r->scratch_crc_[1];
@@ -301,21 +360,27 @@ hipError_t launch_crc32c_batch(const KernelArgs& args, bool uniform_aligned, int
 hipError_t launch_sst_table(const uint8_t* file, uint64_t file_size, uint64_t* d_off,
                             uint32_t* d_size, uint32_t* d_actual, uint8_t* d_status,
                             uint32_t capacity, lvkv_sst_report* r, const KernelArgs& verify,
-                            int groups, hipStream_t stream) {
+                            const uint32_t* zpow, int groups, hipStream_t stream) {
   hipLaunchKernelGGL(sst_footer_kernel, dim3(1), dim3(64), 0, stream, file, file_size, r);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
 
   KernelArgs a = verify;
   a.base = file;
-  a.offsets = r->scratch_off_;
-  a.lengths = r->scratch_size_;
-  a.out_crc = r->scratch_crc_;
-  a.out_status = r->scratch_status_;
-  a.nblocks = 2;
+  a.mode = kModeCompute;
+  a.offsets = r->seg_off_;
+  a.lengths = r->seg_len_;
+  a.inits = r->seg_init_;
+  a.out_crc = r->seg_crc_;
+  a.out_status = nullptr;
+  a.nblocks = 128;
   a.count = &r->scratch_count_;
-  e = launch_crc32c_batch(a, false, 1, stream);
+  e = launch_crc32c_batch(a, false, 8, stream);  // 8 x 16 waves: one segment each
   if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(sst_combine_kernel, dim3(1), dim3(128), 0, stream, file, r, zpow);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  a.mode = verify.mode;
+  a.inits = nullptr;
 
   const uint32_t grid = (capacity + kIndexThreads - 1) / kIndexThreads;
   hipLaunchKernelGGL(sst_index_kernel, dim3(grid), dim3(kIndexThreads), 0, stream, file,

@@ -77,6 +77,14 @@ void build_lane_columns(uint32_t* lane_cols) {
   }
 }
 
+void build_zpow_tables(uint32_t* zpow) {
+  for (uint32_t j = 0; j < kZPowCount; ++j) {
+    const Gf2Op z = gf2_zero_advance(uint64_t{1} << j);
+    for (uint32_t t = 0; t < 4; ++t)
+      for (uint32_t b = 0; b < 256; ++b) zpow[j * 1024 + t * 256 + b] = gf2_apply(z, b << (8 * t));
+  }
+}
+
 }  // namespace lvkv
 
 extern "C" __attribute__((visibility("default"))) void lvkv_debug_tables(

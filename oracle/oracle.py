@@ -112,6 +112,8 @@ class Reference:
         L.ref_crc32c_mask.restype = _u32
         L.ref_crc32c_uniform.argtypes = [_vp, _u64, _u32, _u32, _vp, _sz, _int]
         L.ref_crc32c_uniform.restype = None
+        L.ref_crc32c_batch.argtypes = [_vp, _vp, _vp, _vp, _sz]
+        L.ref_crc32c_batch.restype = None
         self._L = L
 
     def extend(self, init: int, data: bytes) -> int:
@@ -128,6 +130,19 @@ class Reference:
         out = np.empty(nblocks, dtype=np.uint32)
         self._L.ref_crc32c_uniform(buf.ctypes.data, stride, length, init & 0xFFFFFFFF,
                                    out.ctypes.data, nblocks, threads)
+        return out
+
+
+    def batch(self, buf: np.ndarray, offsets, lengths) -> np.ndarray:
+        """Value() over block i = buf[offsets[i], + lengths[i]), 1 thread."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+        assert offsets.size == lengths.size
+        assert offsets.size == 0 or int((offsets + lengths).max()) <= buf.size
+        out = np.empty(offsets.size, dtype=np.uint32)
+        self._L.ref_crc32c_batch(buf.ctypes.data, offsets.ctypes.data, lengths.ctypes.data,
+                                 out.ctypes.data, offsets.size)
         return out
 
 

@@ -59,4 +59,10 @@ void ref_crc32c_uniform(const char* base, uint64_t stride, uint32_t length,
   for (int t = 0; t < threads; ++t) pthread_join(tids[t], nullptr);
 }
 
+// Ragged batch, 1 thread: block i = base[offsets[i], + lengths[i]).
+void ref_crc32c_batch(const char* base, const uint64_t* offsets, const uint32_t* lengths,
+                      uint32_t* out, size_t n) {
+  for (size_t i = 0; i < n; ++i) out[i] = leveldb::crc32c::Value(base + offsets[i], lengths[i]);
+}
+
 }  // extern "C"

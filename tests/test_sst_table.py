@@ -96,8 +96,8 @@ def test_report_struct_layout_matches_header(tmp_path, lvkv):
           printf("size %zu\\n", sizeof(lvkv_sst_report));
           F(status) F(nblocks) F(ndata) F(has_filter) F(nbad) F(first_bad) F(index_crc)
           F(meta_crc) F(index_status) F(meta_status) F(index_offset) F(index_size)
-          F(meta_offset) F(meta_size) F(scratch_off_) F(scratch_size_) F(scratch_crc_)
-          F(scratch_status_) F(scratch_count_)
+          F(meta_offset) F(meta_size) F(scratch_crc_) F(scratch_status_) F(scratch_count_)
+          F(scratch_nseg_) F(seg_off_) F(seg_len_) F(seg_init_) F(seg_crc_)
           return 0;
         }"""))
     exe = tmp_path / "layout"
