@@ -113,6 +113,21 @@ __device__ __forceinline__ void fill_rows_c(uint32_t* lds, const UniformArgs& a,
   }
 }
 
+// Same row image, entries read from the Z_256 tables in HBM (zpow set j = 8)
+// instead of generated from kernel-argument columns (crc32c_long_kernel).
+__device__ __forceinline__ void fill_rows_from_zpow(uint32_t* lds, const uint32_t* zpow,
+                                                    uint32_t tid) {
+  const uint32_t* z256 = zpow + 8u * 1024u;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const uint32_t q = tid + 1024u * static_cast<uint32_t>(it);
+    const uint32_t b = q >> 3, t = (q >> 1) & 3u;
+    const uint32_t e = z256[t * 256u + b];
+    *reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds) + b * 256u + (q & 7u) * 16u) =
+        make_uint4(e, e, e, e);
+  }
+}
+
 // Lane tables from HBM (lane_tab[(k*16 + nib)*64 + s], kLaneTabDwords) into
 // the upper halves of the bank rows.
 template <int W>
@@ -297,6 +312,189 @@ __global__ void __launch_bounds__(64 * W, OCC) crc32c_compact_kernel(UniformArgs
     if (full) compact_body<P, W, 1, true>(a, g, lds, tid, lane, blk, nv != 0);
     else compact_body<P, W, 1, false>(a, g, lds, tid, lane, blk, nv != 0);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Long blocks of the general batch (covered length > kLongBytes), one
+// workgroup per block instead of one wave: the bytes up to the last 4-byte
+// boundary are cut at absolute 4-byte-aligned points into kLongSeg segments;
+// wave w checksums segments w, w + 16, ... (segment 0 from init ^ ~0, the
+// others from register 0), shifts each register to that boundary with Z_n =
+// the product of the Z_{2^j} byte tables (zpow, HBM), and xors it into its
+// accumulator. Wave 0 combines the 16 accumulators, feeds the 0-3 tail bytes
+// through the byte table (Z_1) and stores in the batch's mode (compute, SST
+// verify, SST fill). The main batch kernel skips exactly these blocks
+// (KernelArgs::long_split). Bytes read per block: its covered length once.
+
+constexpr uint64_t kLongSeg = 16 * 1024;
+
+namespace {
+
+__device__ __forceinline__ uint32_t zshift_g(const uint32_t* zpow, uint32_t v, uint64_t n) {
+  while (n) {
+    const uint32_t j = __builtin_ctzll(n);
+    const uint32_t* t = zpow + j * 1024u;
+    v = t[v & 255u] ^ t[256u + ((v >> 8) & 255u)] ^ t[512u + ((v >> 16) & 255u)] ^
+        t[768u + (v >> 24)];
+    n &= n - 1;
+  }
+  return v;
+}
+
+// Register after [s, e) (e 4-byte aligned, e - s <= kLongSeg) from state
+// init ^ ~0: the end-aligned row walk of the uniform kernels, 16-row chunks,
+// the next chunk's loads in flight while one is walked.
+__device__ uint32_t segment_register(const uint32_t* lds, uint64_t s, uint64_t e, uint32_t init,
+                                     const LaneKeys& keys, uint32_t lane, uint32_t lane_base) {
+  const uint32_t len = static_cast<uint32_t>(e - s);
+  UniGeo g;
+  const uint32_t q = (len + 3u) >> 2;
+  g.rows = (q + 63u) >> 6;
+  g.delta = 4u * q - len;
+  g.s0l = 64u * g.rows - q;
+  g.s0 = init ^ 0xffffffffu;
+  g.spill = g.delta ? (g.s0 >> (32u - 8u * g.delta)) : 0u;
+  g.nrec = 4u * q;
+  g.vb0 = -4 * static_cast<int32_t>(g.s0l);
+  const uint64_t b4 = e - 4ull * q;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(b4));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(b4 >> 32));
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0,
+      static_cast<int>(g.nrec), kBufferDword3);
+  const int32_t vo = g.vb0 + 4 * static_cast<int32_t>(lane);
+  int32_t vo1 = vo + kRowBytes;
+  asm volatile("" : "+v"(vo1));
+  const uint32_t nchunks = (g.rows + kRowsPerChunk - 1) / kRowsPerChunk;
+  uint32_t buf[2][kRowsPerChunk];
+  auto issue = [&](uint32_t (&b)[kRowsPerChunk], uint32_t c) {
+#pragma unroll
+    for (int j = 0; j < kRowsPerChunk; ++j) {
+      const int32_t row = static_cast<int32_t>(c) * kRowsPerChunk + j;
+      b[j] = row == 0 ? __builtin_amdgcn_raw_buffer_load_b32(r, vo, 0, kUniCachePolicy)
+                      : __builtin_amdgcn_raw_buffer_load_b32(r, vo1 + 256 * (row - 1), 0,
+                                                             kUniCachePolicy);
+    }
+  };
+  uint32_t st = 0;
+  issue(buf[0], 0);
+  for (uint32_t c = 0; c < nchunks; c += 2) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t cc = c + h;
+      if (cc < nchunks) {
+        if (cc + 1 < nchunks) issue(buf[h ^ 1], cc + 1);
+        uint32_t(&b)[kRowsPerChunk] = buf[h];
+        if (cc == 0) {
+          fix_first_chunk(b, g);
+          st = b[0];
+        } else {
+          st = row_step_c(lds, st, b[0], keys);
+        }
+        const uint32_t nrow = min(static_cast<uint32_t>(kRowsPerChunk), g.rows - cc * kRowsPerChunk);
+#pragma unroll
+        for (int j = 1; j < kRowsPerChunk; ++j)
+          if (static_cast<uint32_t>(j) < nrow) st = row_step_c(lds, st, b[j], keys);
+      }
+    }
+  }
+  return wave_xor_dpp(lane_end_shift_c(lds, st, lane_base));
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(1024, 1)
+    crc32c_long_kernel(KernelArgs a, const uint32_t* zpow, const uint32_t* lane_cols) {
+  constexpr int W = 16;
+  // LDS: the compact image, one accumulator per wave, the slice's long-block
+  // list and its length.
+  constexpr uint32_t kAcc = kCompactLdsBytes / 4, kList = kAcc + W, kCount = kList + 1024;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kCount + 1];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t n = a.count != nullptr ? min(a.nblocks, sload_u32(a.count, 0)) : a.nblocks;
+  const uint64_t base = reinterpret_cast<uint64_t>(a.base);
+  const bool sst = a.mode == kModeSstVerify || a.mode == kModeSstFill;
+  const uint32_t extra = sst ? 1u : 0u;
+  bool built = false;
+  const LaneKeys keys = lane_keys(lane);
+  const uint32_t lane_base = (lane >> 5) * 256u + 128u + (lane & 31u) * 4u;
+  // Workgroup g scans blocks [g*per, (g+1)*per), 1024 lengths at a time
+  // (coalesced), and walks the long ones it finds.
+  const uint32_t per = (n + gridDim.x - 1) / gridDim.x;
+  const uint32_t first = min(n, blockIdx.x * per), last = min(n, first + per);
+  for (uint32_t slice = first; slice < last; slice += 1024) {
+    if (tid == 0) lds[kCount] = 0;
+    __syncthreads();
+    const uint32_t i = slice + tid;
+    if (i < last && a.lengths[i] + extra > kLongBytes) lds[kList + atomicAdd(&lds[kCount], 1u)] = i;
+    __syncthreads();
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(lds[kCount]);
+    for (uint32_t li = 0; li < cnt; ++li) {
+    const uint32_t b = __builtin_amdgcn_readfirstlane(lds[kList + li]);
+    const uint64_t off = sload_u64(a.offsets, b);
+    uint64_t len = static_cast<uint64_t>(sload_u32(a.lengths, b)) + extra;
+    const uint32_t init = sst ? 0u : (a.inits != nullptr ? sload_u32(a.inits, b) : a.init);
+    if (!built) {  // the compact LDS image, once per workgroup
+      UniformArgs u;
+      u.lane_cols = lane_cols;
+      LaneTabGen<W> lg;
+      lg.load(u, wave, lane);
+      fill_rows_from_zpow(lds, zpow, tid);
+      lg.store(lds, wave, lane);
+      __syncthreads();
+      built = true;
+    }
+    const uint64_t start = base + off, end = start + len, e4 = end & ~uint64_t{3};
+    const uint64_t a4 = start & ~uint64_t{3};
+    const uint32_t m = static_cast<uint32_t>((e4 - a4 + kLongSeg - 1) / kLongSeg);
+    uint32_t acc = 0;
+    for (uint32_t k = wave; k < m; k += W) {
+      const uint64_t s = k == 0 ? start : a4 + k * kLongSeg;
+      const uint64_t e = min(a4 + (k + 1) * kLongSeg, e4);
+      const uint32_t reg = segment_register(lds, s, e, k == 0 ? init : 0xffffffffu, keys, lane,
+                                            lane_base);
+      acc ^= zshift_g(zpow, reg, e4 - e);
+    }
+    if (lane == 0) lds[kAcc + wave] = acc;
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t reg = 0;
+#pragma unroll
+      for (int w = 0; w < W; ++w) reg ^= lds[kAcc + w];
+      for (uint64_t p = e4; p < end; ++p)  // tail bytes: the byte table = Z_1 on b
+        reg = zpow[(reg ^ *reinterpret_cast<const uint8_t*>(p)) & 255u] ^ (reg >> 8);
+      const uint32_t crc = reg ^ 0xffffffffu;
+      if (a.mode == kModeSstFill) {
+        uint8_t* dst = reinterpret_cast<uint8_t*>(end);
+        const uint32_t mcrc = crc_mask(crc);
+        for (int k = 0; k < 4; ++k) dst[k] = static_cast<uint8_t>(mcrc >> (8 * k));
+        if (a.out_crc != nullptr) a.out_crc[b] = crc;
+      } else if (a.mode == kModeSstVerify) {
+        a.out_crc[b] = crc;
+        if (a.out_status != nullptr) {
+          const uint8_t* t = reinterpret_cast<const uint8_t*>(end);
+          const uint32_t stored = static_cast<uint32_t>(t[0]) | (static_cast<uint32_t>(t[1]) << 8) |
+                                  (static_cast<uint32_t>(t[2]) << 16) |
+                                  (static_cast<uint32_t>(t[3]) << 24);
+          a.out_status[b] = crc != crc_unmask(stored) ? 1 : 0;
+        }
+      } else {
+        a.out_crc[b] = a.mask ? crc_mask(crc) : crc;
+      }
+    }
+    __syncthreads();
+    }
+    __syncthreads();
+  }
+}
+
+hipError_t launch_crc32c_long(const KernelArgs& args, const uint32_t* zpow,
+                              const uint32_t* lane_cols, int num_groups, hipStream_t stream) {
+  hipLaunchKernelGGL(crc32c_long_kernel, dim3(num_groups), dim3(1024), 0, stream, args, zpow,
+                     lane_cols);
+  return hipGetLastError();
 }
 
 // cfg: bits 0-1 = shape (0: 16 waves x 3 chains, 1 WG/CU; 1: 8 waves x 3

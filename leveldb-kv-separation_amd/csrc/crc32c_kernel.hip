@@ -90,7 +90,8 @@ struct Geo {
   uint32_t delta;     // bytes of front padding inside the first data word
   uint32_t s0;        // init ^ ~0, xored into the first 4 data bytes
   uint32_t spill;     // part of s0 that lands in the second data word
-  uint32_t tiny;      // 1: length < 4, computed bitwise
+  uint32_t tiny;      // 1: length < 4, computed bitwise; 2: a long block left
+                      //    to crc32c_long_kernel (no loads, no store)
   uint32_t len;
   uint32_t ptr_lo;    // absolute address of the first covered byte
   uint32_t ptr_hi;    //   (split: keeps the struct free of padding)
@@ -198,6 +199,11 @@ __device__ __forceinline__ Geo make_geo(const KernelArgs& a, uint32_t b) {
     if (a.mode == kModeSstVerify) expected = crc_unmask(sload_le(base + off + len, 4));
   }
 
+  if (a.long_split && len > kLongBytes) {  // crc32c_long_kernel's block
+    Geo g = null_geo();
+    g.tiny = 2;
+    return g;
+  }
   Geo g;
   const uint64_t ptr = base + off;
   g.ptr_lo = static_cast<uint32_t>(ptr);
@@ -348,6 +354,7 @@ __device__ __forceinline__ uint32_t tiny_crc(const Geo& g) {
 template <int V>
 __device__ __forceinline__ void store_result(const KernelArgs& a,
                                              const Item& it, uint32_t crc) {
+  if (!(V & kUniformAligned) && it.g.tiny == 2) return;
   if (lane_id() == 0) {
     if ((V & kUniformAligned) || a.mode == kModeCompute) {
       a.out_crc[it.block] = a.mask ? crc_mask(crc) : crc;

@@ -39,11 +39,14 @@ hipError_t launch_crc32c_compact(const UniformArgs& args, int cfg, int num_group
 hipError_t launch_sst_table(const uint8_t* file, uint64_t file_size, uint64_t* d_off,
                             uint32_t* d_size, uint32_t* d_actual, uint8_t* d_status,
                             uint32_t capacity, lvkv_sst_report* r, const KernelArgs& verify,
-                            const uint32_t* zpow, int groups, hipStream_t stream);
+                            const uint32_t* zpow, const uint32_t* lane_cols, int groups,
+                            hipStream_t stream);
 hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_off,
                              uint32_t* actual, uint8_t* rec_status, uint32_t capacity,
                              uint8_t* block_status, uint32_t* block_drop, lvkv_log_report* r,
                              const KernelArgs& verify, int groups, hipStream_t stream);
+hipError_t launch_crc32c_long(const KernelArgs& args, const uint32_t* zpow,
+                              const uint32_t* lane_cols, int num_groups, hipStream_t stream);
 int compact_capacity(int cfg);
 int compact_occupancy(int cfg);
 // 8 waves x 3 chains, two workgroups per CU, generated lane tables
@@ -220,6 +223,14 @@ int run_batch(KernelArgs a, size_t nblocks, hipStream_t stream) {
                                         groups, stream);
       else
         e = launch_crc32c_uniform(uniform_args(*c, b), 0, groups, stream);
+    } else if (b.offsets != nullptr && b.mode != kModeLogVerify && b.mode != kModeLogFill) {
+      // Blocks longer than kLongBytes go to one workgroup each (segments in
+      // parallel) instead of one wave; the main kernel leaves them alone.
+      b.long_split = 1;
+      e = launch_crc32c_batch(b, false, groups, stream);
+      if (e == hipSuccess)
+        e = launch_crc32c_long(b, c->d_tables + kZPowOffset,
+                               c->d_tables + kRowTabDwords + kLaneTabDwords, c->groups, stream);
     } else {
       e = launch_crc32c_batch(b, false, groups, stream);
     }
@@ -415,8 +426,8 @@ int lvkv_sst_verify_table_device(const void* d_file, uint64_t file_size,
   a.mode = kModeSstVerify;
   const hipError_t e = launch_sst_table(
       static_cast<const uint8_t*>(d_file), file_size, d_offsets, d_sizes, d_actual, d_status,
-      static_cast<uint32_t>(capacity), d_report, a, c->d_tables + kZPowOffset, c->groups,
-      static_cast<hipStream_t>(stream));
+      static_cast<uint32_t>(capacity), d_report, a, c->d_tables + kZPowOffset,
+      c->d_tables + kRowTabDwords + kLaneTabDwords, c->groups, static_cast<hipStream_t>(stream));
   return e == hipSuccess ? LVKV_OK : hip_fail(e);
 }
 

@@ -28,6 +28,9 @@ constexpr int kRowsPerChunk = 16;   // one pipeline stage = 4 KiB per wave
 constexpr uint32_t kRowTabDwords = 4 * 256;
 constexpr uint32_t kLaneTabDwords = 8 * 16 * 64;
 constexpr uint32_t kLaneColDwords = 8 * 64 * 4;  // lane_cols (lvkv_tables.h)
+// Blocks longer than this are split over a whole workgroup
+// (crc32c_long_kernel) instead of one wave walking them alone.
+constexpr uint32_t kLongBytes = 64 * 1024;
 constexpr uint32_t kZPowCount = 48;               // Z_{2^j}, j < 48 (256 TiB)
 constexpr uint32_t kZPowDwords = kZPowCount * 1024;
 constexpr uint32_t kZPowOffset = 1024 + 8 * 16 * 64 + 8 * 64 * 4;  // in d_tables
@@ -64,7 +67,9 @@ struct KernelArgs {
   uint32_t nblocks;
   uint32_t mode;
   uint32_t mask;              // 1: store Mask(crc) (util/crc32c.h:29-32)
-  uint32_t pad_;
+  uint32_t long_split;        // 1: blocks whose covered length exceeds
+                              // kLongBytes are left to crc32c_long_kernel
+                              // (no loads, no store here)
   uint64_t* stamps;           // probe builds only: per-wave timestamps
   const uint32_t* count;      // optional device-side block count: the launch
                               // covers min(nblocks, *count) blocks (a count

@@ -354,13 +354,16 @@ __global__ void __launch_bounds__(kIndexThreads)
 
 hipError_t launch_crc32c_batch(const KernelArgs& args, bool uniform_aligned, int num_groups,
                                hipStream_t stream);
+hipError_t launch_crc32c_long(const KernelArgs& args, const uint32_t* zpow,
+                              const uint32_t* lane_cols, int num_groups, hipStream_t stream);
 
 // The five launches; `verify` is the SST-verify KernelArgs template (tables,
 // mode) the caller filled.
 hipError_t launch_sst_table(const uint8_t* file, uint64_t file_size, uint64_t* d_off,
                             uint32_t* d_size, uint32_t* d_actual, uint8_t* d_status,
                             uint32_t capacity, lvkv_sst_report* r, const KernelArgs& verify,
-                            const uint32_t* zpow, int groups, hipStream_t stream) {
+                            const uint32_t* zpow, const uint32_t* lane_cols, int groups,
+                            hipStream_t stream) {
   hipLaunchKernelGGL(sst_footer_kernel, dim3(1), dim3(64), 0, stream, file, file_size, r);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -393,8 +396,10 @@ hipError_t launch_sst_table(const uint8_t* file, uint64_t file_size, uint64_t* d
   a.out_status = nullptr;  // merged below with the parse status
   a.nblocks = capacity;
   a.count = &r->nblocks;
+  a.long_split = 1;  // large data/filter blocks: one workgroup each
   e = launch_crc32c_batch(a, false, groups, stream);
   if (e != hipSuccess) return e;
+  if ((e = launch_crc32c_long(a, zpow, lane_cols, groups, stream)) != hipSuccess) return e;
 
   hipLaunchKernelGGL(sst_merge_kernel, dim3(grid), dim3(kIndexThreads), 0, stream, file, r,
                      d_off, d_size, d_actual, d_status);

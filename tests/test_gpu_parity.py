@@ -267,3 +267,24 @@ def test_every_uniform_variant(lvkv, oracle, gpu, length, nblocks, groups):
         assert rc == 0, (variant, rc)
         torch.cuda.synchronize()
         assert np.array_equal(_u32(out), want), variant
+
+
+def test_long_blocks_split_over_workgroups(lvkv, oracle, gpu):
+    # Blocks past kLongBytes (64 KiB) are cut into 16 KiB segments on 4-byte
+    # boundaries and combined with Z_{2^j} shifts (crc32c_long_kernel): every
+    # start and end alignment, segment-boundary lengths, mixed with short ones.
+    import torch
+    rng = np.random.default_rng(12)
+    data = rng.integers(0, 256, 24 << 20, dtype=np.uint8)
+    lens = [65536, 65537, 65538, 65539, 65540, 16384 * 5, 16384 * 5 + 1, 100003,
+            (1 << 20) + 1, (3 << 20) + 2, 7, 4096, 70000]
+    L = np.array([l for l in lens for _ in range(4)], dtype=np.uint32)
+    offs = np.array([rng.integers(0, (data.size - l) // 8) * 4 + k
+                     for l in lens for k in range(4)], dtype=np.uint64)
+    inits = rng.integers(0, 2**32, L.size, dtype=np.uint64).astype(np.uint32)
+    want = oracle.batch(data, offs, L, inits, threads=8)
+    got = lvkv.crc32c_batch(_to_dev(torch, data, gpu), _to_dev(torch, offs.astype(np.int64), gpu),
+                            _to_dev(torch, L.view(np.int32), gpu),
+                            inits=_to_dev(torch, inits.view(np.int32), gpu))
+    bad = np.nonzero(_u32(got) != want)[0]
+    assert bad.size == 0, [(int(L[i]), int(offs[i] % 4)) for i in bad[:10]]

@@ -242,3 +242,28 @@ def test_device_fill_trailers_rebuilds_the_table(lvkv, gpu, source):
     import oracle
     want = [oracle.value(img[o: o + s + 1]) for o, s in blocks]
     assert list(crc.cpu().numpy().view(np.uint32)) == want
+
+
+@pytest.mark.gpu
+def test_device_table_with_long_blocks(lvkv, gpu):
+    # Data blocks far beyond kLongBytes (one huge value per block, as a table
+    # with big values gets): verify, a corrupted long block, and the refill.
+    import torch
+    img = sst_synth.build_sst(24, 300_000, seed=8)
+    rep, want = _assert_matches_oracle(lvkv, img, gpu)
+    assert rep["nbad"] == 0
+    r0 = st.verify_table(img)
+    off, size = r0.handles[7]
+    bad = bytearray(img)
+    bad[off + size - 3] ^= 0x20
+    rep, want = _assert_matches_oracle(lvkv, bytes(bad), gpu)
+    assert rep["nbad"] == 1 and rep["first_bad"] == 7
+    blocks = r0.handles + [r0.meta, r0.index]
+    wiped = bytearray(img)
+    for o, s in blocks:
+        wiped[o + s + 1: o + s + 5] = b"\0\0\0\0"
+    buf = torch.from_numpy(np.frombuffer(bytes(wiped), dtype=np.uint8).copy()).to(gpu)
+    lvkv.sst_fill_trailers(buf, torch.tensor([o for o, _ in blocks], dtype=torch.int64, device=gpu),
+                           torch.tensor([s for _, s in blocks], dtype=torch.int32, device=gpu))
+    torch.cuda.synchronize()
+    assert bytes(buf.cpu().numpy()) == img
