@@ -18,6 +18,11 @@
 //   5. log_merge_kernel   per block: the first checksum mismatch drops the
 //                         rest of the block; per-block status and reported
 //                         drop bytes (Reporter::Corruption), report totals
+//
+// Measured and rejected: copying each block into LDS (coalesced) before the
+// walk. The three walks then read the whole image three times; walking the
+// headers straight from HBM/MALL reads a few bytes per record and was faster
+// (142 vs 178 us for a 66 MB log).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
