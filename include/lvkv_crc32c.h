@@ -131,33 +131,31 @@ int lvkv_log_fill_headers_device(void* d_file, const uint64_t* d_hdr_offsets, ui
 #define LVKV_BLOCK_BAD_HANDLE 4    /* index entry value is not a BlockHandle (:28) */
 #define LVKV_BLOCK_BAD_ENTRY 5     /* "bad entry in block" for the index entry (block.cc:236) */
 
-/* Written by lvkv_sst_verify_table_device into device memory. */
+/* Written by lvkv_sst_verify_table(s)_device into device memory. */
 typedef struct lvkv_sst_report {
   int32_t status;          /* LVKV_SST_* */
   uint32_t nblocks;        /* entries in the per-block arrays: ndata + has_filter */
   uint32_t ndata;          /* data blocks the index lists */
   uint32_t has_filter;     /* 1: entry ndata is the filter block ("filter." in the metaindex) */
   uint32_t nbad;           /* entries with status != LVKV_BLOCK_OK */
-  uint32_t first_bad;      /* lowest such entry, or 0xffffffff */
+  uint32_t first_bad;      /* lowest such entry (relative to `first`), or 0xffffffff */
   uint32_t index_crc;      /* computed CRC (contents + type byte) of the index block */
   uint32_t meta_crc;       /* same, metaindex block */
   uint8_t index_status;    /* LVKV_BLOCK_* of the index block */
   uint8_t meta_status;     /* LVKV_BLOCK_* of the metaindex (Table::ReadMeta ignores its
                               errors, table/table.cc:92-94; reported, not fatal) */
-  uint8_t reserved0_[6];
+  uint8_t reserved0_[2];
+  uint32_t first;          /* this table's first entry in the shared per-block arrays */
   uint64_t index_offset, index_size, meta_offset, meta_size;  /* footer handles */
-  /* library-internal scratch: the index + metaindex verify before the parse,
-   * each block cut into up to 64 segments checksummed in parallel */
-  uint32_t scratch_crc_[2];
+  /* library-internal */
+  uint64_t filter_off_;
+  uint32_t filter_size_;
   uint8_t scratch_status_[2];
-  uint8_t reserved1_[2];
-  uint32_t scratch_count_;     /* segments in use */
-  uint32_t scratch_nseg_[2];   /* segments of the index / metaindex */
+  uint8_t filter_status_;
+  uint8_t reserved1_;
+  uint32_t scratch_crc_[2];
+  uint32_t total_;         /* tables[0] only: entries verified over all tables */
   uint32_t reserved2_;
-  uint64_t seg_off_[128];
-  uint32_t seg_len_[128];
-  uint32_t seg_init_[128];
-  uint32_t seg_crc_[128];
 } lvkv_sst_report;
 
 /* Verifies a whole SSTable image already in device memory, as Table::Open
@@ -177,6 +175,21 @@ int lvkv_sst_verify_table_device(const void* d_file, uint64_t file_size,
                                  uint64_t* d_offsets, uint32_t* d_sizes,
                                  uint32_t* d_actual, uint8_t* d_status, size_t capacity,
                                  lvkv_sst_report* d_report, void* stream);
+
+/* Many SSTables at once: compaction inputs (paranoid checks), a repair scan.
+ * Table t is d_file[d_table_off[t], + d_table_size[t]) (device arrays). The
+ * same eight launches as one table serve all of them: footers, index and
+ * metaindex CRCs (one workgroup each), index heads, a scan that packs every
+ * table's entries into the shared per-block arrays (table t from
+ * d_reports[t].first on), the entry parse, one batched verify and the merge.
+ * d_offsets are offsets into d_file (table offset + BlockHandle offset). A
+ * table whose entries do not fit in `capacity` gets LVKV_SST_CAPACITY (with
+ * ndata set); so do the tables after it. Asynchronous; graph-capturable. */
+int lvkv_sst_verify_tables_device(const void* d_file, const uint64_t* d_table_off,
+                                  const uint64_t* d_table_size, size_t ntables,
+                                  uint64_t* d_offsets, uint32_t* d_sizes, uint32_t* d_actual,
+                                  uint8_t* d_status, size_t capacity,
+                                  lvkv_sst_report* d_reports, void* stream);
 
 /* ---- WAL / MANIFEST verify, device-resident ----- */
 #define LVKV_LOG_CAPACITY 1        /* report.status: more records than `capacity` */

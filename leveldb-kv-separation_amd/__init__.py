@@ -75,6 +75,8 @@ def _load() -> ctypes.CDLL:
     L.lvkv_sst_verify_device.restype = i32
     L.lvkv_sst_verify_table_device.argtypes = [vp, u64, vp, vp, vp, vp, sz, vp, vp]
     L.lvkv_sst_verify_table_device.restype = i32
+    L.lvkv_sst_verify_tables_device.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, sz, vp, vp]
+    L.lvkv_sst_verify_tables_device.restype = i32
     L.lvkv_sst_fill_trailers_device.argtypes = [vp, vp, vp, vp, sz, vp]
     L.lvkv_sst_fill_trailers_device.restype = i32
     L.lvkv_log_fill_headers_device.argtypes = [vp, vp, vp, sz, vp]
@@ -261,14 +263,13 @@ class SstReport(ctypes.Structure):
                 ("nbad", ctypes.c_uint32), ("first_bad", ctypes.c_uint32),
                 ("index_crc", ctypes.c_uint32), ("meta_crc", ctypes.c_uint32),
                 ("index_status", ctypes.c_uint8), ("meta_status", ctypes.c_uint8),
-                ("reserved0_", ctypes.c_uint8 * 6),
+                ("reserved0_", ctypes.c_uint8 * 2), ("first", ctypes.c_uint32),
                 ("index_offset", ctypes.c_uint64), ("index_size", ctypes.c_uint64),
                 ("meta_offset", ctypes.c_uint64), ("meta_size", ctypes.c_uint64),
-                ("scratch_crc_", ctypes.c_uint32 * 2), ("scratch_status_", ctypes.c_uint8 * 2),
-                ("reserved1_", ctypes.c_uint8 * 2), ("scratch_count_", ctypes.c_uint32),
-                ("scratch_nseg_", ctypes.c_uint32 * 2), ("reserved2_", ctypes.c_uint32),
-                ("seg_off_", ctypes.c_uint64 * 128), ("seg_len_", ctypes.c_uint32 * 128),
-                ("seg_init_", ctypes.c_uint32 * 128), ("seg_crc_", ctypes.c_uint32 * 128)]
+                ("filter_off_", ctypes.c_uint64), ("filter_size_", ctypes.c_uint32),
+                ("scratch_status_", ctypes.c_uint8 * 2), ("filter_status_", ctypes.c_uint8),
+                ("reserved1_", ctypes.c_uint8), ("scratch_crc_", ctypes.c_uint32 * 2),
+                ("total_", ctypes.c_uint32), ("reserved2_", ctypes.c_uint32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_
@@ -315,6 +316,41 @@ def sst_verify_table(file_buf, *, capacity: Optional[int] = None, stream=None):
         break
     n = r.nblocks
     return r.as_dict(), off[:n], sizes[:n], actual[:n], status[:n]
+
+
+def sst_verify_tables(file_buf, table_offsets, table_sizes, *, capacity=None, stream=None):
+    """Many SST images in one device buffer (lvkv_sst_verify_tables_device):
+    eight launches for all of them. Returns one (report dict, offsets, sizes,
+    actual, status) per table as sst_verify_table would for that image alone,
+    except that offsets are into file_buf. capacity (shared by all tables)
+    defaults to file_buf.numel() // 2048 + 64 per table; a table that does
+    not fit reports LVKV_SST_CAPACITY (8)."""
+    torch = _torch()
+    dev = file_buf.device
+    T = len(table_offsets)
+    toff = torch.tensor([int(x) for x in table_offsets], dtype=torch.int64, device=dev)
+    tsz = torch.tensor([int(x) for x in table_sizes], dtype=torch.int64, device=dev)
+    cap = capacity if capacity is not None else file_buf.numel() // 2048 + 64 * T
+    o = torch.empty(cap, dtype=torch.int64, device=dev)
+    sz = torch.empty(cap, dtype=torch.int32, device=dev)
+    act = torch.empty(cap, dtype=torch.int32, device=dev)
+    st = torch.empty(cap, dtype=torch.uint8, device=dev)
+    rsz = ctypes.sizeof(SstReport)
+    reps = torch.zeros(T * rsz, dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        rc = _lib.lvkv_sst_verify_tables_device(
+            _dev_ptr(file_buf, "file_buf", (torch.uint8, torch.int8)), _dev_ptr(toff, "toff"),
+            _dev_ptr(tsz, "tsize"), T, _dev_ptr(o, "offsets"), _dev_ptr(sz, "sizes"),
+            _dev_ptr(act, "actual"), _dev_ptr(st, "status"), cap, _dev_ptr(reps, "reports"),
+            _stream_handle(stream, dev))
+    _check("lvkv_sst_verify_tables_device", rc)
+    host = bytes(reps.cpu().numpy())
+    out = []
+    for t in range(T):
+        r = SstReport.from_buffer_copy(host[t * rsz:(t + 1) * rsz])
+        f, n = r.first, (r.nblocks if r.status == 0 else 0)
+        out.append((r.as_dict(), o[f:f + n], sz[f:f + n], act[f:f + n], st[f:f + n]))
+    return out
 
 
 def log_verify(file_buf, hdr_offsets, *, stream=None):

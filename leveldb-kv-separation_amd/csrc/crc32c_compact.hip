@@ -31,6 +31,7 @@
 
 #include "crc32c_device_common.h"
 #include "crc32c_uniform_common.h"
+#include "lvkv_crc32c.h"
 #include "lvkv_kernel_args.h"
 
 namespace lvkv {
@@ -403,9 +404,72 @@ __device__ uint32_t segment_register(const uint32_t* lds, uint64_t s, uint64_t e
 
 }  // namespace
 
+namespace {
+
+constexpr int kLongWaves = 16;
+
+// The compact LDS image for a 1024-thread workgroup: row tables from the
+// Z_256 set of zpow, lane tables generated from lane_cols.
+__device__ __forceinline__ void build_compact_image(uint32_t* lds, const uint32_t* zpow,
+                                                    const uint32_t* lane_cols, uint32_t tid,
+                                                    uint32_t wave, uint32_t lane) {
+  UniformArgs u;
+  u.lane_cols = lane_cols;
+  LaneTabGen<kLongWaves> lg;
+  lg.load(u, wave, lane);
+  fill_rows_from_zpow(lds, zpow, tid);
+  lg.store(lds, wave, lane);
+  __syncthreads();
+}
+
+// CRC32C of [start, end) from `init` by the whole workgroup: 16 KiB segments
+// on 4-byte boundaries, wave w takes segments w, w + 16, ...; each register
+// is shifted to the last 4-byte boundary (Z_n from zpow) and xored into the
+// wave's LDS slot; thread 0 combines, feeds the 0-3 tail bytes through Z_1
+// and returns the CRC (other threads: undefined). Two barriers; every thread
+// of the workgroup must call it.
+__device__ uint32_t workgroup_crc(const uint32_t* lds, uint32_t* acc_slots, uint64_t start,
+                                  uint64_t end, uint32_t init, const LaneKeys& keys,
+                                  uint32_t tid, uint32_t wave, uint32_t lane, uint32_t lane_base,
+                                  const uint32_t* zpow) {
+  const uint64_t e4 = end & ~uint64_t{3};
+  const uint64_t a4 = start & ~uint64_t{3};
+  const uint32_t m = e4 > start ? static_cast<uint32_t>((e4 - a4 + kLongSeg - 1) / kLongSeg) : 0u;
+  uint32_t acc = 0;
+  for (uint32_t k = wave; k < m; k += kLongWaves) {
+    const uint64_t s = k == 0 ? start : a4 + k * kLongSeg;
+    const uint64_t e = min(a4 + (k + 1) * kLongSeg, e4);
+    const uint32_t reg =
+        segment_register(lds, s, e, k == 0 ? init : 0xffffffffu, keys, lane, lane_base);
+    acc ^= zshift_g(zpow, reg, e4 - e);
+  }
+  if (lane == 0) acc_slots[wave] = acc;
+  __syncthreads();
+  uint32_t crc = 0;
+  if (tid == 0) {
+    // m == 0 (fewer than 4 bytes up to a boundary): the init state is the
+    // register, the bytes all go through the tail step
+    uint32_t reg = m ? 0u : init ^ 0xffffffffu;
+#pragma unroll
+    for (int w = 0; w < kLongWaves; ++w) reg ^= acc_slots[w];
+    for (uint64_t p = m ? e4 : start; p < end; ++p)  // tail bytes: Z_1 = the byte table
+      reg = zpow[(reg ^ *reinterpret_cast<const uint8_t*>(p)) & 255u] ^ (reg >> 8);
+    crc = reg ^ 0xffffffffu;
+  }
+  __syncthreads();
+  return crc;
+}
+
+__device__ __forceinline__ uint32_t ld_le32_g(const uint8_t* t) {
+  return static_cast<uint32_t>(t[0]) | (static_cast<uint32_t>(t[1]) << 8) |
+         (static_cast<uint32_t>(t[2]) << 16) | (static_cast<uint32_t>(t[3]) << 24);
+}
+
+}  // namespace
+
 __global__ void __launch_bounds__(1024, 1)
     crc32c_long_kernel(KernelArgs a, const uint32_t* zpow, const uint32_t* lane_cols) {
-  constexpr int W = 16;
+  constexpr int W = kLongWaves;
   // LDS: the compact image, one accumulator per wave, the slice's long-block
   // list and its length.
   constexpr uint32_t kAcc = kCompactLdsBytes / 4, kList = kAcc + W, kCount = kList + 1024;
@@ -432,62 +496,70 @@ __global__ void __launch_bounds__(1024, 1)
     __syncthreads();
     const uint32_t cnt = __builtin_amdgcn_readfirstlane(lds[kCount]);
     for (uint32_t li = 0; li < cnt; ++li) {
-    const uint32_t b = __builtin_amdgcn_readfirstlane(lds[kList + li]);
-    const uint64_t off = sload_u64(a.offsets, b);
-    uint64_t len = static_cast<uint64_t>(sload_u32(a.lengths, b)) + extra;
-    const uint32_t init = sst ? 0u : (a.inits != nullptr ? sload_u32(a.inits, b) : a.init);
-    if (!built) {  // the compact LDS image, once per workgroup
-      UniformArgs u;
-      u.lane_cols = lane_cols;
-      LaneTabGen<W> lg;
-      lg.load(u, wave, lane);
-      fill_rows_from_zpow(lds, zpow, tid);
-      lg.store(lds, wave, lane);
-      __syncthreads();
-      built = true;
-    }
-    const uint64_t start = base + off, end = start + len, e4 = end & ~uint64_t{3};
-    const uint64_t a4 = start & ~uint64_t{3};
-    const uint32_t m = static_cast<uint32_t>((e4 - a4 + kLongSeg - 1) / kLongSeg);
-    uint32_t acc = 0;
-    for (uint32_t k = wave; k < m; k += W) {
-      const uint64_t s = k == 0 ? start : a4 + k * kLongSeg;
-      const uint64_t e = min(a4 + (k + 1) * kLongSeg, e4);
-      const uint32_t reg = segment_register(lds, s, e, k == 0 ? init : 0xffffffffu, keys, lane,
-                                            lane_base);
-      acc ^= zshift_g(zpow, reg, e4 - e);
-    }
-    if (lane == 0) lds[kAcc + wave] = acc;
-    __syncthreads();
-    if (tid == 0) {
-      uint32_t reg = 0;
-#pragma unroll
-      for (int w = 0; w < W; ++w) reg ^= lds[kAcc + w];
-      for (uint64_t p = e4; p < end; ++p)  // tail bytes: the byte table = Z_1 on b
-        reg = zpow[(reg ^ *reinterpret_cast<const uint8_t*>(p)) & 255u] ^ (reg >> 8);
-      const uint32_t crc = reg ^ 0xffffffffu;
-      if (a.mode == kModeSstFill) {
-        uint8_t* dst = reinterpret_cast<uint8_t*>(end);
-        const uint32_t mcrc = crc_mask(crc);
-        for (int k = 0; k < 4; ++k) dst[k] = static_cast<uint8_t>(mcrc >> (8 * k));
-        if (a.out_crc != nullptr) a.out_crc[b] = crc;
-      } else if (a.mode == kModeSstVerify) {
-        a.out_crc[b] = crc;
-        if (a.out_status != nullptr) {
-          const uint8_t* t = reinterpret_cast<const uint8_t*>(end);
-          const uint32_t stored = static_cast<uint32_t>(t[0]) | (static_cast<uint32_t>(t[1]) << 8) |
-                                  (static_cast<uint32_t>(t[2]) << 16) |
-                                  (static_cast<uint32_t>(t[3]) << 24);
-          a.out_status[b] = crc != crc_unmask(stored) ? 1 : 0;
+      const uint32_t b = __builtin_amdgcn_readfirstlane(lds[kList + li]);
+      const uint64_t off = sload_u64(a.offsets, b);
+      const uint64_t len = static_cast<uint64_t>(sload_u32(a.lengths, b)) + extra;
+      const uint32_t init = sst ? 0u : (a.inits != nullptr ? sload_u32(a.inits, b) : a.init);
+      if (!built) {  // the compact LDS image, once per workgroup
+        build_compact_image(lds, zpow, lane_cols, tid, wave, lane);
+        built = true;
+      }
+      const uint64_t start = base + off, end = start + len;
+      const uint32_t crc =
+          workgroup_crc(lds, lds + kAcc, start, end, init, keys, tid, wave, lane, lane_base, zpow);
+      if (tid == 0) {
+        if (a.mode == kModeSstFill) {
+          uint8_t* dst = reinterpret_cast<uint8_t*>(end);
+          const uint32_t mcrc = crc_mask(crc);
+          for (int k = 0; k < 4; ++k) dst[k] = static_cast<uint8_t>(mcrc >> (8 * k));
+          if (a.out_crc != nullptr) a.out_crc[b] = crc;
+        } else if (a.mode == kModeSstVerify) {
+          a.out_crc[b] = crc;
+          if (a.out_status != nullptr)
+            a.out_status[b] = crc != crc_unmask(ld_le32_g(reinterpret_cast<const uint8_t*>(end)));
+        } else {
+          a.out_crc[b] = a.mask ? crc_mask(crc) : crc;
         }
-      } else {
-        a.out_crc[b] = a.mask ? crc_mask(crc) : crc;
       }
     }
     __syncthreads();
-    }
-    __syncthreads();
   }
+}
+
+// Index and metaindex CRCs of T tables (lvkv_sst_table.hip): workgroup 2t + w
+// checksums table t's index (w = 0) or metaindex (w = 1), contents + type
+// byte, and compares with the stored trailer (table/format.cc:92-97).
+__global__ void __launch_bounds__(1024, 1)
+    sst_meta_crc_kernel(const uint8_t* file, const uint64_t* table_off, lvkv_sst_report* reports,
+                        const uint32_t* zpow, const uint32_t* lane_cols) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kCompactLdsBytes / 4 + kLongWaves];
+  const uint32_t t = blockIdx.x >> 1, which = blockIdx.x & 1u;
+  lvkv_sst_report* r = reports + t;
+  if (r->status != LVKV_SST_OK) return;
+  if (which == 1 && r->meta_status != LVKV_BLOCK_OK) return;  // truncated metaindex
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  build_compact_image(lds, zpow, lane_cols, tid, wave, lane);
+  const uint8_t* img = file + (table_off != nullptr ? table_off[t] : 0);
+  const uint64_t off = which ? r->meta_offset : r->index_offset;
+  const uint64_t len = (which ? r->meta_size : r->index_size) + 1;
+  const uint64_t start = reinterpret_cast<uint64_t>(img) + off;
+  const uint32_t crc = workgroup_crc(lds, lds + kCompactLdsBytes / 4, start, start + len, 0u,
+                                     lane_keys(lane), tid, wave, lane,
+                                     (lane >> 5) * 256u + 128u + (lane & 31u) * 4u, zpow);
+  if (tid == 0) {
+    r->scratch_crc_[which] = crc;
+    r->scratch_status_[which] = crc != crc_unmask(ld_le32_g(img + off + len)) ? 1 : 0;
+  }
+}
+
+hipError_t launch_sst_meta_crc(const uint8_t* file, const uint64_t* table_off, uint32_t ntables,
+                               lvkv_sst_report* reports, const uint32_t* zpow,
+                               const uint32_t* lane_cols, hipStream_t stream) {
+  hipLaunchKernelGGL(sst_meta_crc_kernel, dim3(2 * ntables), dim3(1024), 0, stream, file,
+                     table_off, reports, zpow, lane_cols);
+  return hipGetLastError();
 }
 
 hipError_t launch_crc32c_long(const KernelArgs& args, const uint32_t* zpow,

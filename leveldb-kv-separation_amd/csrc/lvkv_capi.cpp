@@ -36,11 +36,12 @@ hipError_t launch_crc32c_uniform_small(const UniformArgs& args, int variant,
                                        int num_groups, hipStream_t stream);
 hipError_t launch_crc32c_compact(const UniformArgs& args, int cfg, int num_groups,
                                  hipStream_t stream);
-hipError_t launch_sst_table(const uint8_t* file, uint64_t file_size, uint64_t* d_off,
-                            uint32_t* d_size, uint32_t* d_actual, uint8_t* d_status,
-                            uint32_t capacity, lvkv_sst_report* r, const KernelArgs& verify,
-                            const uint32_t* zpow, const uint32_t* lane_cols, int groups,
-                            hipStream_t stream);
+hipError_t launch_sst_tables(const uint8_t* file, const uint64_t* toff, const uint64_t* tsize,
+                             uint64_t single_size, uint32_t ntables, uint64_t* d_off,
+                             uint32_t* d_size, uint32_t* d_actual, uint8_t* d_status,
+                             uint32_t capacity, lvkv_sst_report* reports,
+                             const KernelArgs& verify, const uint32_t* zpow,
+                             const uint32_t* lane_cols, int groups, hipStream_t stream);
 hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_off,
                              uint32_t* actual, uint8_t* rec_status, uint32_t capacity,
                              uint8_t* block_status, uint32_t* block_drop, lvkv_log_report* r,
@@ -424,9 +425,35 @@ int lvkv_sst_verify_table_device(const void* d_file, uint64_t file_size,
   a.row_tab = c->d_tables;
   a.lane_tab = c->d_tables + kRowTabDwords;
   a.mode = kModeSstVerify;
-  const hipError_t e = launch_sst_table(
-      static_cast<const uint8_t*>(d_file), file_size, d_offsets, d_sizes, d_actual, d_status,
-      static_cast<uint32_t>(capacity), d_report, a, c->d_tables + kZPowOffset,
+  const hipError_t e = launch_sst_tables(
+      static_cast<const uint8_t*>(d_file), nullptr, nullptr, file_size, 1, d_offsets, d_sizes,
+      d_actual, d_status, static_cast<uint32_t>(capacity), d_report, a,
+      c->d_tables + kZPowOffset, c->d_tables + kRowTabDwords + kLaneTabDwords, c->groups,
+      static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? LVKV_OK : hip_fail(e);
+}
+
+int lvkv_sst_verify_tables_device(const void* d_file, const uint64_t* d_table_off,
+                                  const uint64_t* d_table_size, size_t ntables,
+                                  uint64_t* d_offsets, uint32_t* d_sizes, uint32_t* d_actual,
+                                  uint8_t* d_status, size_t capacity,
+                                  lvkv_sst_report* d_reports, void* stream) {
+  if (ntables == 0) return LVKV_OK;
+  if (!d_file || !d_table_off || !d_table_size || !d_offsets || !d_sizes || !d_actual ||
+      !d_status || !d_reports || capacity == 0 || capacity > kMaxBlocksPerLaunch ||
+      ntables > (size_t{1} << 20))
+    return LVKV_ERR_INVALID;
+  int rc = LVKV_OK;
+  DeviceCtx* c = current_ctx(&rc);
+  if (c == nullptr) return rc;
+  KernelArgs a = blank_args();
+  a.row_tab = c->d_tables;
+  a.lane_tab = c->d_tables + kRowTabDwords;
+  a.mode = kModeSstVerify;
+  const hipError_t e = launch_sst_tables(
+      static_cast<const uint8_t*>(d_file), d_table_off, d_table_size, 0,
+      static_cast<uint32_t>(ntables), d_offsets, d_sizes, d_actual, d_status,
+      static_cast<uint32_t>(capacity), d_reports, a, c->d_tables + kZPowOffset,
       c->d_tables + kRowTabDwords + kLaneTabDwords, c->groups, static_cast<hipStream_t>(stream));
   return e == hipSuccess ? LVKV_OK : hip_fail(e);
 }

@@ -95,9 +95,9 @@ def test_report_struct_layout_matches_header(tmp_path, lvkv):
         int main(void) {
           printf("size %zu\\n", sizeof(lvkv_sst_report));
           F(status) F(nblocks) F(ndata) F(has_filter) F(nbad) F(first_bad) F(index_crc)
-          F(meta_crc) F(index_status) F(meta_status) F(index_offset) F(index_size)
-          F(meta_offset) F(meta_size) F(scratch_crc_) F(scratch_status_) F(scratch_count_)
-          F(scratch_nseg_) F(seg_off_) F(seg_len_) F(seg_init_) F(seg_crc_)
+          F(meta_crc) F(index_status) F(meta_status) F(first) F(index_offset) F(index_size)
+          F(meta_offset) F(meta_size) F(filter_off_) F(filter_size_) F(scratch_status_)
+          F(filter_status_) F(scratch_crc_) F(total_)
           return 0;
         }"""))
     exe = tmp_path / "layout"
@@ -121,9 +121,13 @@ def _device_verify(lvkv, img: bytes, gpu, capacity=None):
             actual.cpu().numpy().view(np.uint32), status.cpu().numpy())
 
 
-def _assert_matches_oracle(lvkv, img: bytes, gpu, capacity=None):
+def _assert_matches_oracle(lvkv, img: bytes, gpu, capacity=None, got=None, base=0):
     want = st.verify_table(img)
-    rep, off, size, actual, status = _device_verify(lvkv, img, gpu, capacity)
+    rep, off, size, actual, status = got if got is not None else _device_verify(
+        lvkv, img, gpu, capacity)
+    # handles come back as offsets into the device buffer, bad entries as
+    # (table start, 0)
+    off = np.array([int(x) - base for x in off], dtype=np.int64)
     assert rep["status"] == want.status
     if want.status not in (st.SST_OK,):
         return rep, want
@@ -267,3 +271,42 @@ def test_device_table_with_long_blocks(lvkv, gpu):
                            torch.tensor([s for _, s in blocks], dtype=torch.int32, device=gpu))
     torch.cuda.synchronize()
     assert bytes(buf.cpu().numpy()) == img
+
+
+@pytest.mark.gpu
+def test_device_multi_table_verify(lvkv, gpu):
+    # Compaction-input shape: many tables in one buffer, each checked exactly
+    # as the single-table call would (lvkv_sst_verify_tables_device).
+    import torch
+    gold = _golden_img()
+    r0 = st.verify_table(gold)
+    bad = bytearray(gold)
+    o, n = r0.handles[11]
+    bad[o + n // 3] ^= 4
+    imgs = [gold, sst_synth.build_sst(300, 4096, seed=30), bytes(bad),
+            b"\x07" * 2000, sst_synth.build_sst(1, 50, seed=31, with_filter=False),
+            sst_synth.build_sst(6, 200_000, seed=32)] * 3
+    offs, pos = [], 0
+    for im in imgs:
+        offs.append(pos)
+        pos += len(im) + 13  # unaligned table starts
+    buf = bytearray(pos)
+    for o_, im in zip(offs, imgs):
+        buf[o_: o_ + len(im)] = im
+    dbuf = torch.from_numpy(np.frombuffer(bytes(buf), dtype=np.uint8).copy()).to(gpu)
+    res = lvkv.sst_verify_tables(dbuf, offs, [len(im) for im in imgs])
+    torch.cuda.synchronize()
+    assert len(res) == len(imgs)
+    for o_, im, (rep, off, size, actual, status) in zip(offs, imgs, res):
+        got = (rep, off.cpu().numpy(), size.cpu().numpy().view(np.uint32),
+               actual.cpu().numpy().view(np.uint32), status.cpu().numpy())
+        _assert_matches_oracle(lvkv, im, gpu, got=got, base=o_)
+    # a shared capacity too small for all: the tables that fit are verified,
+    # the first that does not and every later one report LVKV_SST_CAPACITY
+    small = lvkv.sst_verify_tables(dbuf, offs, [len(im) for im in imgs], capacity=400)
+    torch.cuda.synchronize()
+    stats = [r[0]["status"] for r in small]
+    assert stats[0] == 0 and st.SST_CAPACITY in stats
+    k = stats.index(st.SST_CAPACITY)
+    assert all(s_ in (st.SST_CAPACITY, st.SST_BAD_MAGIC) for s_ in stats[k:])
+    assert res[2][0]["nbad"] == 1 and res[3][0]["status"] == st.SST_BAD_MAGIC

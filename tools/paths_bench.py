@@ -121,6 +121,53 @@ def main():
         report(f"sst_fill_trailers_{nblocks}x4KiB", len(img), us, cpu,
                "Mask(CRC32C(contents + type)) written into every trailer")
 
+    # compaction-input shape: 32 tables of ~2 MiB, one multi-table call vs
+    # 32 single-table calls on one stream
+    imgs = [sst_synth.build_sst(512, 4096, seed=100 + t) for t in range(32)]
+    offs, pos = [], 0
+    for im in imgs:
+        offs.append(pos)
+        pos += (len(im) + 255) // 256 * 256
+    host = np.zeros(pos, dtype=np.uint8)
+    for o_, im in zip(offs, imgs):
+        host[o_: o_ + len(im)] = np.frombuffer(im, dtype=np.uint8)
+    buf = torch.from_numpy(host).to(dev)
+    sizes_t = [len(im) for im in imgs]
+    tabs = lvkv.sst_verify_tables(buf, offs, sizes_t)
+    assert all(r[0]["status"] == 0 and r[0]["nbad"] == 0 for r in tabs)
+    L = lvkv.lib
+    vp = ctypes.c_void_p
+    h = vp(torch.cuda.current_stream().cuda_stream)
+    d_toff = torch.tensor(offs, dtype=torch.int64, device=dev)
+    d_tsz = torch.tensor(sizes_t, dtype=torch.int64, device=dev)
+    tot = 32 * 600
+    o3 = torch.empty(tot, dtype=torch.int64, device=dev)
+    s3 = torch.empty(tot, dtype=torch.int32, device=dev)
+    a3 = torch.empty(tot, dtype=torch.int32, device=dev)
+    st3 = torch.empty(tot, dtype=torch.uint8, device=dev)
+    rp3 = torch.zeros(32 * ctypes.sizeof(lvkv.SstReport), dtype=torch.uint8, device=dev)
+
+    def multi():
+        rc = L.lvkv_sst_verify_tables_device(
+            vp(buf.data_ptr()), vp(d_toff.data_ptr()), vp(d_tsz.data_ptr()), 32,
+            vp(o3.data_ptr()), vp(s3.data_ptr()), vp(a3.data_ptr()), vp(st3.data_ptr()), tot,
+            vp(rp3.data_ptr()), h)
+        assert rc == 0
+
+    def single():
+        for t in range(32):
+            f = 600 * t
+            rc = L.lvkv_sst_verify_table_device(
+                vp(buf.data_ptr() + offs[t]), sizes_t[t], vp(o3.data_ptr() + 8 * f),
+                vp(s3.data_ptr() + 4 * f), vp(a3.data_ptr() + 4 * f), vp(st3.data_ptr() + f),
+                600, vp(rp3.data_ptr() + t * ctypes.sizeof(lvkv.SstReport)), h)
+            assert rc == 0
+    nbytes = sum(sizes_t)
+    us_m = timed(multi, max(5, args.reps // 5))
+    us_s = timed(single, max(5, args.reps // 5))
+    report("sst_verify_tables_32x2MiB", nbytes, us_m, None,
+           f"one multi-table call (8 launches); 32 single-table calls: {us_s:.1f} us")
+
     for nrec in (2000, 60000):
         img = log_synth.build_log(nrec, seed=nrec, max_len=2000, big_every=997)
         v = log_walk.block_verdicts(img)
