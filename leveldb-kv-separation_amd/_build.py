@@ -30,9 +30,10 @@ ARCH = os.environ.get("LVKV_OFFLOAD_ARCH", "gfx950")
 HOST_SOURCES = ["lvkv_tables.cpp", "lvkv_cpu_crc32c.cpp", "leveldb_crc32c_shim.cc"]
 # HIP sources: kernels and the runtime-facing C-ABI.
 HIP_SOURCES = ["crc32c_kernel.hip", "crc32c_uniform.hip", "crc32c_compact.hip",
-               "lvkv_sst_table.hip", "lvkv_log_blocks.hip", "lvkv_capi.cpp"]
+               "crc32c_ragged.hip", "lvkv_sst_table.hip", "lvkv_log_blocks.hip",
+               "lvkv_capi.cpp"]
 HEADERS = ["lvkv_kernel_args.h", "lvkv_tables.h", "crc32c_device_common.h",
-           "crc32c_uniform_common.h"]
+           "crc32c_uniform_common.h", "crc32c_compact_common.h"]
 
 
 def _run(cmd: list[str], verbose: bool) -> None:

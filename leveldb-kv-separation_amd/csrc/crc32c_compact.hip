@@ -4,21 +4,7 @@
 // over 256-byte rows with Z_256 byte tables, per-lane end shift Z_{256-4s},
 // wave xor-reduce); what changes is how the row tables avoid bank conflicts.
 //
-// Row tables: ds_read_b32 banks are (addr/4) mod 32 per 32-lane half-wave.
-// Instead of 32 copies of each table (lane l -> copy l), lane l looks up, in
-// its p-th lookup of a row step, byte t = (l + p) & 3 of the state in table t,
-// copy c = (l >> 2) & 7. Over one half-wave the pairs (t, c) are all 32
-// distinct, and copy c of table t sits in bank 8t + c of every 256-byte bank
-// row, so each lookup instruction is conflict-free with 8 copies per table:
-//
-//   LDS row b (256 B), bytes [0, 128):   T_t[b] copy c at 32t + 4c
-//   LDS row r (256 B), bytes [128, 256): lane nibble table r>>1 = k*16 + nib,
-//                                        lane s (r & 1 = s >> 5) at 128 + 4(s & 31)
-//
-// The address of a lookup is one v_perm_b32 with a per-lane selector:
-// {kpack.byte[p], S.byte[t], 0, 0} = S.byte[t] * 256 + 32t + 4c, where kpack
-// holds 32t_p + 4c for p = 0..3. XOR order does not matter, so lane l's four
-// lookups still cover the four bytes of its state.
+// Row tables and lane tables: the compact image of crc32c_compact_common.h.
 //
 // Work map: the batch is split into `gridDim.x` contiguous runs of equal
 // length (+1 for the first nblocks % G). Run element i goes to wave i % W,
@@ -30,13 +16,12 @@
 #include <stdint.h>
 
 #include "crc32c_device_common.h"
+#include "crc32c_compact_common.h"
 #include "crc32c_uniform_common.h"
 #include "lvkv_crc32c.h"
 #include "lvkv_kernel_args.h"
 
 namespace lvkv {
-
-constexpr uint32_t kCompactLdsBytes = 64 * 1024;
 
 namespace {
 
@@ -45,47 +30,6 @@ enum : int {
   kCmpGenLane = 2,  // lane tables generated from 4 columns per lane and
                     // nibble position (8 KiB of loads per workgroup, not 32)
 };
-
-struct LaneKeys {
-  uint32_t kpack;   // byte p = 32 * t_p + 4 * c
-  uint32_t sel[4];  // v_perm selectors {kpack.byte[p], S.byte[t_p], 0, 0}
-};
-
-__device__ __forceinline__ LaneKeys lane_keys(uint32_t lane) {
-  LaneKeys k;
-  const uint32_t c = (lane >> 2) & 7u;
-  k.kpack = 0;
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const uint32_t t = (lane + static_cast<uint32_t>(p)) & 3u;
-    k.kpack |= (32u * t + 4u * c) << (8 * p);
-    k.sel[p] = 0x0C0C0000u | ((4u + t) << 8) | static_cast<uint32_t>(p);
-  }
-  return k;
-}
-
-// S -> Z_256(S) ^ w on the compact image.
-__device__ __forceinline__ uint32_t row_step_c(const uint32_t* lds, uint32_t s, uint32_t w,
-                                               const LaneKeys& k) {
-  const uint32_t a0 = __builtin_amdgcn_perm(s, k.kpack, k.sel[0]);
-  const uint32_t a1 = __builtin_amdgcn_perm(s, k.kpack, k.sel[1]);
-  const uint32_t a2 = __builtin_amdgcn_perm(s, k.kpack, k.sel[2]);
-  const uint32_t a3 = __builtin_amdgcn_perm(s, k.kpack, k.sel[3]);
-  const uint32_t x = xor3(lds_ld(lds, a0), lds_ld(lds, a1), w);
-  return xor3(x, lds_ld(lds, a2), lds_ld(lds, a3));
-}
-
-// S -> Z_{256-4s}(S) for this lane s (eight lane-private nibble lookups).
-__device__ __forceinline__ uint32_t lane_end_shift_c(const uint32_t* lds, uint32_t s,
-                                                     uint32_t lane_base) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const uint32_t nib = (s >> (4 * k)) & 15u;
-    r ^= lds_ld(lds, (lane_base | (nib << 9)) + 8192u * k);
-  }
-  return r;
-}
 
 // Row tables: 2048 16-byte slots q -> row b = q >> 3, table t = (q >> 1) & 3,
 // copies 4h..4h+3 with h = q & 1 (address b*256 + 32t + 16h). Eight
@@ -109,21 +53,6 @@ __device__ __forceinline__ void fill_rows_c(uint32_t* lds, const UniformArgs& a,
     uint32_t e = 0;
 #pragma unroll
     for (int bit = 0; bit < 8; ++bit) e ^= (0u - ((b >> bit) & 1u)) & col[bit];
-    *reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds) + b * 256u + (q & 7u) * 16u) =
-        make_uint4(e, e, e, e);
-  }
-}
-
-// Same row image, entries read from the Z_256 tables in HBM (zpow set j = 8)
-// instead of generated from kernel-argument columns (crc32c_long_kernel).
-__device__ __forceinline__ void fill_rows_from_zpow(uint32_t* lds, const uint32_t* zpow,
-                                                    uint32_t tid) {
-  const uint32_t* z256 = zpow + 8u * 1024u;
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const uint32_t q = tid + 1024u * static_cast<uint32_t>(it);
-    const uint32_t b = q >> 3, t = (q >> 1) & 3u;
-    const uint32_t e = z256[t * 256u + b];
     *reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds) + b * 256u + (q & 7u) * 16u) =
         make_uint4(e, e, e, e);
   }
@@ -153,41 +82,6 @@ struct LaneTabStage {
       *reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds) + (2u * r + (s >> 5)) * 256u +
                                 128u + (s & 31u) * 4u) =
           make_uint4(v[it][0], v[it][1], v[it][2], v[it][3]);
-    }
-  }
-};
-
-// Lane tables generated in-kernel: wave w owns nibble position k = w % 8
-// (and, with 16 waves, nibbles 8 (w / 8) .. +7), loads the 4 columns of
-// Z_{256-4s} it needs (lane_cols[(k*64 + s)*4 + j], one 16-byte load per
-// lane), and writes its entries in Gray-code order, one xor each. For a fixed
-// (k, nib) the 64 lanes write two contiguous 128-byte half rows:
-// conflict-free ds_write_b32.
-template <int W>
-struct LaneTabGen {
-  static constexpr int kNibs = 16 * 8 / W;  // entries per lane
-  uint32_t col[4];
-
-  __device__ __forceinline__ void load(const UniformArgs& a, uint32_t wave, uint32_t lane) {
-    const uint32_t k = wave & 7u;
-    const uint4 v = *reinterpret_cast<const uint4*>(a.lane_cols + (k * 64u + lane) * 4u);
-    col[0] = v.x;
-    col[1] = v.y;
-    col[2] = v.z;
-    col[3] = v.w;
-  }
-  __device__ __forceinline__ void store(uint32_t* lds, uint32_t wave, uint32_t lane) const {
-    const uint32_t k = wave & 7u;
-    const uint32_t nib0 = (W == 16) ? (wave >> 3) * 8u : 0u;
-    char* base = reinterpret_cast<char*>(lds) + (lane >> 5) * 256u + 128u + (lane & 31u) * 4u +
-                 (k * 16u + nib0) * 512u;
-    uint32_t e = 0;
-    if (W == 16 && nib0) e = col[3];  // entry nib0 = 8
-#pragma unroll
-    for (int i = 0; i < kNibs; ++i) {
-      if (i) e ^= col[__builtin_ctz(i)];
-      const int g = i ^ (i >> 1);  // Gray code: nib = nib0 + g
-      *reinterpret_cast<uint32_t*>(base + g * 512) = e;
     }
   }
 };
@@ -236,7 +130,7 @@ __device__ __forceinline__ void compact_body(const UniformArgs& a, const UniGeo&
 
   // 1. Lane tables, chain 0, the LDS image, one barrier, the other chains.
   if (P & kCmpGenLane)
-    lg.load(a, wave, lane);
+    lg.load(a.lane_cols, wave, lane);
   else
     lt.load(a, tid);
   __builtin_amdgcn_sched_barrier(0);
@@ -327,83 +221,6 @@ __global__ void __launch_bounds__(64 * W, OCC) crc32c_compact_kernel(UniformArgs
 // verify, SST fill). The main batch kernel skips exactly these blocks
 // (KernelArgs::long_split). Bytes read per block: its covered length once.
 
-constexpr uint64_t kLongSeg = 16 * 1024;
-
-namespace {
-
-__device__ __forceinline__ uint32_t zshift_g(const uint32_t* zpow, uint32_t v, uint64_t n) {
-  while (n) {
-    const uint32_t j = __builtin_ctzll(n);
-    const uint32_t* t = zpow + j * 1024u;
-    v = t[v & 255u] ^ t[256u + ((v >> 8) & 255u)] ^ t[512u + ((v >> 16) & 255u)] ^
-        t[768u + (v >> 24)];
-    n &= n - 1;
-  }
-  return v;
-}
-
-// Register after [s, e) (e 4-byte aligned, e - s <= kLongSeg) from state
-// init ^ ~0: the end-aligned row walk of the uniform kernels, 16-row chunks,
-// the next chunk's loads in flight while one is walked.
-__device__ uint32_t segment_register(const uint32_t* lds, uint64_t s, uint64_t e, uint32_t init,
-                                     const LaneKeys& keys, uint32_t lane, uint32_t lane_base) {
-  const uint32_t len = static_cast<uint32_t>(e - s);
-  UniGeo g;
-  const uint32_t q = (len + 3u) >> 2;
-  g.rows = (q + 63u) >> 6;
-  g.delta = 4u * q - len;
-  g.s0l = 64u * g.rows - q;
-  g.s0 = init ^ 0xffffffffu;
-  g.spill = g.delta ? (g.s0 >> (32u - 8u * g.delta)) : 0u;
-  g.nrec = 4u * q;
-  g.vb0 = -4 * static_cast<int32_t>(g.s0l);
-  const uint64_t b4 = e - 4ull * q;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(b4));
-  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(b4 >> 32));
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0,
-      static_cast<int>(g.nrec), kBufferDword3);
-  const int32_t vo = g.vb0 + 4 * static_cast<int32_t>(lane);
-  int32_t vo1 = vo + kRowBytes;
-  asm volatile("" : "+v"(vo1));
-  const uint32_t nchunks = (g.rows + kRowsPerChunk - 1) / kRowsPerChunk;
-  uint32_t buf[2][kRowsPerChunk];
-  auto issue = [&](uint32_t (&b)[kRowsPerChunk], uint32_t c) {
-#pragma unroll
-    for (int j = 0; j < kRowsPerChunk; ++j) {
-      const int32_t row = static_cast<int32_t>(c) * kRowsPerChunk + j;
-      b[j] = row == 0 ? __builtin_amdgcn_raw_buffer_load_b32(r, vo, 0, kUniCachePolicy)
-                      : __builtin_amdgcn_raw_buffer_load_b32(r, vo1 + 256 * (row - 1), 0,
-                                                             kUniCachePolicy);
-    }
-  };
-  uint32_t st = 0;
-  issue(buf[0], 0);
-  for (uint32_t c = 0; c < nchunks; c += 2) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint32_t cc = c + h;
-      if (cc < nchunks) {
-        if (cc + 1 < nchunks) issue(buf[h ^ 1], cc + 1);
-        uint32_t(&b)[kRowsPerChunk] = buf[h];
-        if (cc == 0) {
-          fix_first_chunk(b, g);
-          st = b[0];
-        } else {
-          st = row_step_c(lds, st, b[0], keys);
-        }
-        const uint32_t nrow = min(static_cast<uint32_t>(kRowsPerChunk), g.rows - cc * kRowsPerChunk);
-#pragma unroll
-        for (int j = 1; j < kRowsPerChunk; ++j)
-          if (static_cast<uint32_t>(j) < nrow) st = row_step_c(lds, st, b[j], keys);
-      }
-    }
-  }
-  return wave_xor_dpp(lane_end_shift_c(lds, st, lane_base));
-}
-
-}  // namespace
-
 namespace {
 
 constexpr int kLongWaves = 16;
@@ -413,51 +230,13 @@ constexpr int kLongWaves = 16;
 __device__ __forceinline__ void build_compact_image(uint32_t* lds, const uint32_t* zpow,
                                                     const uint32_t* lane_cols, uint32_t tid,
                                                     uint32_t wave, uint32_t lane) {
-  UniformArgs u;
-  u.lane_cols = lane_cols;
+  RowTabStage<1024> rt;
   LaneTabGen<kLongWaves> lg;
-  lg.load(u, wave, lane);
-  fill_rows_from_zpow(lds, zpow, tid);
+  rt.load(zpow, tid);
+  lg.load(lane_cols, wave, lane);
+  rt.store(lds, tid);
   lg.store(lds, wave, lane);
   __syncthreads();
-}
-
-// CRC32C of [start, end) from `init` by the whole workgroup: 16 KiB segments
-// on 4-byte boundaries, wave w takes segments w, w + 16, ...; each register
-// is shifted to the last 4-byte boundary (Z_n from zpow) and xored into the
-// wave's LDS slot; thread 0 combines, feeds the 0-3 tail bytes through Z_1
-// and returns the CRC (other threads: undefined). Two barriers; every thread
-// of the workgroup must call it.
-__device__ uint32_t workgroup_crc(const uint32_t* lds, uint32_t* acc_slots, uint64_t start,
-                                  uint64_t end, uint32_t init, const LaneKeys& keys,
-                                  uint32_t tid, uint32_t wave, uint32_t lane, uint32_t lane_base,
-                                  const uint32_t* zpow) {
-  const uint64_t e4 = end & ~uint64_t{3};
-  const uint64_t a4 = start & ~uint64_t{3};
-  const uint32_t m = e4 > start ? static_cast<uint32_t>((e4 - a4 + kLongSeg - 1) / kLongSeg) : 0u;
-  uint32_t acc = 0;
-  for (uint32_t k = wave; k < m; k += kLongWaves) {
-    const uint64_t s = k == 0 ? start : a4 + k * kLongSeg;
-    const uint64_t e = min(a4 + (k + 1) * kLongSeg, e4);
-    const uint32_t reg =
-        segment_register(lds, s, e, k == 0 ? init : 0xffffffffu, keys, lane, lane_base);
-    acc ^= zshift_g(zpow, reg, e4 - e);
-  }
-  if (lane == 0) acc_slots[wave] = acc;
-  __syncthreads();
-  uint32_t crc = 0;
-  if (tid == 0) {
-    // m == 0 (fewer than 4 bytes up to a boundary): the init state is the
-    // register, the bytes all go through the tail step
-    uint32_t reg = m ? 0u : init ^ 0xffffffffu;
-#pragma unroll
-    for (int w = 0; w < kLongWaves; ++w) reg ^= acc_slots[w];
-    for (uint64_t p = m ? e4 : start; p < end; ++p)  // tail bytes: Z_1 = the byte table
-      reg = zpow[(reg ^ *reinterpret_cast<const uint8_t*>(p)) & 255u] ^ (reg >> 8);
-    crc = reg ^ 0xffffffffu;
-  }
-  __syncthreads();
-  return crc;
 }
 
 __device__ __forceinline__ uint32_t ld_le32_g(const uint8_t* t) {
@@ -506,7 +285,7 @@ __global__ void __launch_bounds__(1024, 1)
       }
       const uint64_t start = base + off, end = start + len;
       const uint32_t crc =
-          workgroup_crc(lds, lds + kAcc, start, end, init, keys, tid, wave, lane, lane_base, zpow);
+          workgroup_crc<kLongWaves>(lds, lds + kAcc, start, end, init, keys, tid, wave, lane, lane_base, zpow);
       if (tid == 0) {
         if (a.mode == kModeSstFill) {
           uint8_t* dst = reinterpret_cast<uint8_t*>(end);
@@ -545,7 +324,7 @@ __global__ void __launch_bounds__(1024, 1)
   const uint64_t off = which ? r->meta_offset : r->index_offset;
   const uint64_t len = (which ? r->meta_size : r->index_size) + 1;
   const uint64_t start = reinterpret_cast<uint64_t>(img) + off;
-  const uint32_t crc = workgroup_crc(lds, lds + kCompactLdsBytes / 4, start, start + len, 0u,
+  const uint32_t crc = workgroup_crc<kLongWaves>(lds, lds + kCompactLdsBytes / 4, start, start + len, 0u,
                                      lane_keys(lane), tid, wave, lane,
                                      (lane >> 5) * 256u + 128u + (lane & 31u) * 4u, zpow);
   if (tid == 0) {

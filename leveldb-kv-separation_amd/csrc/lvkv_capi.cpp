@@ -22,6 +22,8 @@ namespace lvkv {
 
 hipError_t launch_crc32c_batch(const KernelArgs& args, bool uniform_aligned,
                                int num_groups, hipStream_t stream);
+hipError_t launch_crc32c_general(const KernelArgs& a, int cus, hipStream_t stream);
+extern int g_general_kernel;
 hipError_t launch_crc32c_probe(const KernelArgs& args, int variant,
                                int num_groups, hipStream_t stream);
 hipError_t launch_read_bw(const void* p, uint64_t bytes, uint32_t* out,
@@ -228,11 +230,10 @@ int run_batch(KernelArgs a, size_t nblocks, hipStream_t stream) {
       // Blocks longer than kLongBytes go to one workgroup each (segments in
       // parallel) instead of one wave; the main kernel leaves them alone.
       b.long_split = 1;
-      e = launch_crc32c_batch(b, false, groups, stream);
-      if (e == hipSuccess)
-        e = launch_crc32c_long(b, c->d_tables + kZPowOffset,
-                               c->d_tables + kRowTabDwords + kLaneTabDwords, c->groups, stream);
-    } else {
+      e = launch_crc32c_general(b, c->groups, stream);
+    } else if (b.offsets != nullptr) {  // log headers
+      e = launch_crc32c_general(b, c->groups, stream);
+    } else {  // uniform layout, block ends not 4-byte aligned
       e = launch_crc32c_batch(b, false, groups, stream);
     }
     if (e != hipSuccess) return hip_fail(e);
@@ -680,6 +681,14 @@ int lvkv_debug_read_bw(const void* d_data, uint64_t bytes, uint32_t* d_scratch,
   hipError_t e = launch_read_bw(d_data, bytes, d_scratch, g,
                                 static_cast<hipStream_t>(stream));
   return e == hipSuccess ? LVKV_OK : hip_fail(e);
+}
+
+// -1: crc32c_kernel.hip's persistent kernel for general-layout batches;
+// 0..7: crc32c_ragged.hip cfgs (launch_crc32c_ragged). Timing only.
+int lvkv_debug_set_general_kernel(int k) {
+  if (k < -1 || k > 7) return LVKV_ERR_INVALID;
+  g_general_kernel = k;
+  return LVKV_OK;
 }
 
 int lvkv_device_groups(void) {

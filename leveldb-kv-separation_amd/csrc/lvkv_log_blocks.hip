@@ -13,7 +13,7 @@
 //   2. log_scan_kernel    one workgroup: exclusive scan of the counts -> the
 //                         block's first record slot; total vs capacity
 //   3. log_emit_kernel    per block: walk again, write the header offsets
-//   4. crc32c_batch_kernel log-verify mode over all candidates (count read
+//   4. crc32c_ragged_kernel log-verify mode over all candidates (count read
 //                         on the device)
 //   5. log_merge_kernel   per block: the first checksum mismatch drops the
 //                         rest of the block; per-block status and reported
@@ -188,8 +188,7 @@ __global__ void __launch_bounds__(kWalkThreads)
 
 }  // namespace
 
-hipError_t launch_crc32c_batch(const KernelArgs& args, bool uniform_aligned, int num_groups,
-                               hipStream_t stream);
+hipError_t launch_crc32c_general(const KernelArgs& a, int cus, hipStream_t stream);
 
 hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_off,
                              uint32_t* actual, uint8_t* rec_status, uint32_t capacity,
@@ -214,7 +213,7 @@ hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_o
   a.out_status = rec_status;
   a.nblocks = capacity;
   a.count = &r->count_;
-  if ((e = launch_crc32c_batch(a, false, groups, stream)) != hipSuccess) return e;
+  if ((e = launch_crc32c_general(a, groups, stream)) != hipSuccess) return e;
   hipLaunchKernelGGL(log_merge_kernel, dim3(grid), dim3(kWalkThreads), 0, stream, file, size,
                      nblocks, block_drop, block_status, rec_status, r);
   return hipGetLastError();

@@ -1,7 +1,7 @@
 // Whole-SSTable verify on the device, for one table or
 // many at once: the footer, index and metaindex walk of Table::Open /
 // Table::ReadMeta (table/table.cc:38-105) and ReadBlock's checks
-// (table/format.cc:69-160) for every block, as eight launches on one stream
+// (table/format.cc:69-160) for every block, as seven launches on one stream
 // whatever the number of tables, with no host round trip:
 //
 //   1. sst_footer_kernel         one workgroup per table, lane 0: size check,
@@ -22,10 +22,10 @@
 //                                i IS entry i and the entries decode in
 //                                parallel (DecodeEntry, block.cc:55-75;
 //                                BlockHandle varints, format.cc:24-30)
-//   6-7. crc32c_batch_kernel + crc32c_long_kernel: SST-verify mode over all
-//                                entries (count read on the device), computed
-//                                CRC only
-//   8. sst_merge_kernel          stored trailer vs computed CRC, type byte,
+//   6. crc32c_ragged_kernel      SST-verify mode over all entries (count read
+//                                on the device), computed CRC only; blocks
+//                                over 64 KiB by a whole workgroup
+//   7. sst_merge_kernel          stored trailer vs computed CRC, type byte,
 //                                parse status -> LVKV_BLOCK_*, per-table
 //                                nbad / first_bad
 //
@@ -379,15 +379,12 @@ __global__ void __launch_bounds__(kThreads)
 
 }  // namespace
 
-hipError_t launch_crc32c_batch(const KernelArgs& args, bool uniform_aligned, int num_groups,
-                               hipStream_t stream);
-hipError_t launch_crc32c_long(const KernelArgs& args, const uint32_t* zpow,
-                              const uint32_t* lane_cols, int num_groups, hipStream_t stream);
+hipError_t launch_crc32c_general(const KernelArgs& a, int cus, hipStream_t stream);
 hipError_t launch_sst_meta_crc(const uint8_t* file, const uint64_t* table_off, uint32_t ntables,
                                lvkv_sst_report* reports, const uint32_t* zpow,
                                const uint32_t* lane_cols, hipStream_t stream);
 
-// The eight launches for `ntables` images (toff/tsize device arrays, or
+// The seven launches for `ntables` images (toff/tsize device arrays, or
 // nullptr and `single_size` for one image at d_file); `verify` carries the
 // SST-verify KernelArgs template (tables, mode) the caller filled.
 hipError_t launch_sst_tables(const uint8_t* file, const uint64_t* toff, const uint64_t* tsize,
@@ -424,8 +421,7 @@ hipError_t launch_sst_tables(const uint8_t* file, const uint64_t* toff, const ui
   a.nblocks = capacity;
   a.count = &reports[0].total_;
   a.long_split = 1;  // large data/filter blocks: one workgroup each
-  if ((e = launch_crc32c_batch(a, false, groups, stream)) != hipSuccess) return e;
-  if ((e = launch_crc32c_long(a, zpow, lane_cols, groups, stream)) != hipSuccess) return e;
+  if ((e = launch_crc32c_general(a, groups, stream)) != hipSuccess) return e;
 
   hipLaunchKernelGGL(sst_merge_kernel, dim3(egrid), dim3(kThreads), 0, stream, file, ntables,
                      reports, d_off, d_size, d_actual, d_status);

@@ -288,3 +288,45 @@ def test_long_blocks_split_over_workgroups(lvkv, oracle, gpu):
                             inits=_to_dev(torch, inits.view(np.int32), gpu))
     bad = np.nonzero(_u32(got) != want)[0]
     assert bad.size == 0, [(int(L[i]), int(offs[i] % 4)) for i in bad[:10]]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", [-1, 0, 1, 2, 3, 4, 7])
+def test_general_layout_kernels(lvkv, oracle, gpu, kernel):
+    # Every general-layout kernel (crc32c_kernel.hip: -1; crc32c_ragged.hip
+    # shapes 0-2) on every start/end alignment, lengths at and around the
+    # 16/24/32-row chunk edges, idle chains (batch sizes not a multiple of
+    # a round) and blocks up to 64 KiB + a few.
+    import torch
+    L_ = lvkv.lib
+    assert L_.lvkv_debug_set_general_kernel(kernel) == 0
+    try:
+        rng = np.random.default_rng(40 + kernel)
+        data = rng.integers(0, 256, 8 << 20, dtype=np.uint8)
+        edges = [r * 256 + d for r in (1, 15, 16, 17, 23, 24, 25, 31, 32, 33, 48, 64, 255, 256)
+                 for d in (-4, -3, -2, -1, 0, 1, 2, 3, 4)]
+        lens = np.array([0, 1, 2, 3, 4, 5, 7, 8] + edges + [65535, 65536, 65537, 70001],
+                        dtype=np.uint32)
+        L = np.repeat(lens, 4)
+        a = np.tile(np.arange(4, dtype=np.uint64), lens.size)
+        offs = (rng.integers(0, (data.size - 80000) // 4096, L.size).astype(np.uint64) * 4096
+                + a).astype(np.uint64)
+        inits = rng.integers(0, 2**32, L.size, dtype=np.uint64).astype(np.uint32)
+        for n in (L.size, 1, 5, 17, 33):
+            want = oracle.batch(data, offs[:n], L[:n], inits[:n])
+            got = lvkv.crc32c_batch(_to_dev(torch, data, gpu),
+                                    _to_dev(torch, offs[:n].astype(np.int64), gpu),
+                                    _to_dev(torch, L[:n].view(np.int32), gpu),
+                                    inits=_to_dev(torch, inits[:n].view(np.int32), gpu))
+            bad = np.nonzero(_u32(got) != want)[0]
+            assert bad.size == 0, [(int(L[i]), int(offs[i] % 4)) for i in bad[:10]]
+        # many rounds per workgroup: 20k random blocks of 0..9 KiB, masked
+        n = 20000
+        L2 = rng.integers(0, 9000, n).astype(np.uint32)
+        o2 = rng.integers(0, data.size - 9000, n).astype(np.uint64)
+        want = oracle.batch(data, o2, L2, np.full(n, 7, np.uint32), mask=True, threads=8)
+        got = lvkv.crc32c_batch(_to_dev(torch, data, gpu), _to_dev(torch, o2.astype(np.int64), gpu),
+                                _to_dev(torch, L2.view(np.int32), gpu), init=7, mask=True)
+        assert np.array_equal(_u32(got), want)
+    finally:
+        L_.lvkv_debug_set_general_kernel(0)

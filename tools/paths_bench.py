@@ -120,6 +120,18 @@ def main():
         assert bytes(buf.cpu().numpy()) == img
         report(f"sst_fill_trailers_{nblocks}x4KiB", len(img), us, cpu,
                "Mask(CRC32C(contents + type)) written into every trailer")
+        if nblocks == 16384:
+            # the general-layout kernels side by side on the same table
+            ab = {}
+            for k in (-1, 0, 1, 2, 3, 4, 5, 6, 7):
+                assert L.lvkv_debug_set_general_kernel(k) == 0
+                ab[k] = (round(timed(call, args.reps), 2), round(timed(fill, args.reps), 2))
+                assert bytes(buf.cpu().numpy()) == img
+            L.lvkv_debug_set_general_kernel(0)
+            res["general_kernel_ab_70MB_table"] = {
+                "us_verify_table_fill": {str(k): v for k, v in ab.items()},
+                "note": "-1 crc32c_kernel.hip; 0-3 crc32c_ragged.hip shapes (8x2x24, 8x3x16, 8x2x32, 8x3x24), +4: one round per workgroup"}
+            print("general_kernel_ab", json.dumps(ab), flush=True)
 
     # compaction-input shape: 32 tables of ~2 MiB, one multi-table call vs
     # 32 single-table calls on one stream
