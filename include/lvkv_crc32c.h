@@ -178,7 +178,7 @@ int lvkv_sst_verify_table_device(const void* d_file, uint64_t file_size,
 
 /* Many SSTables at once: compaction inputs (paranoid checks), a repair scan.
  * Table t is d_file[d_table_off[t], + d_table_size[t]) (device arrays). The
- * same eight launches as one table serve all of them: footers, index and
+ * same four launches as one table serve all of them: footers, index and
  * metaindex CRCs (one workgroup each), index heads, a scan that packs every
  * table's entries into the shared per-block arrays (table t from
  * d_reports[t].first on), the entry parse, one batched verify and the merge.

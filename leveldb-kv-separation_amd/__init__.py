@@ -320,7 +320,7 @@ def sst_verify_table(file_buf, *, capacity: Optional[int] = None, stream=None):
 
 def sst_verify_tables(file_buf, table_offsets, table_sizes, *, capacity=None, stream=None):
     """Many SST images in one device buffer (lvkv_sst_verify_tables_device):
-    eight launches for all of them. Returns one (report dict, offsets, sizes,
+    four launches for all of them. Returns one (report dict, offsets, sizes,
     actual, status) per table as sst_verify_table would for that image alone,
     except that offsets are into file_buf. capacity (shared by all tables)
     defaults to file_buf.numel() // 2048 + 64 per table; a table that does

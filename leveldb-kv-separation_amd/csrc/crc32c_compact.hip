@@ -225,20 +225,6 @@ namespace {
 
 constexpr int kLongWaves = 16;
 
-// The compact LDS image for a 1024-thread workgroup: row tables from the
-// Z_256 set of zpow, lane tables generated from lane_cols.
-__device__ __forceinline__ void build_compact_image(uint32_t* lds, const uint32_t* zpow,
-                                                    const uint32_t* lane_cols, uint32_t tid,
-                                                    uint32_t wave, uint32_t lane) {
-  RowTabStage<1024> rt;
-  LaneTabGen<kLongWaves> lg;
-  rt.load(zpow, tid);
-  lg.load(lane_cols, wave, lane);
-  rt.store(lds, tid);
-  lg.store(lds, wave, lane);
-  __syncthreads();
-}
-
 __device__ __forceinline__ uint32_t ld_le32_g(const uint8_t* t) {
   return static_cast<uint32_t>(t[0]) | (static_cast<uint32_t>(t[1]) << 8) |
          (static_cast<uint32_t>(t[2]) << 16) | (static_cast<uint32_t>(t[3]) << 24);
@@ -280,7 +266,7 @@ __global__ void __launch_bounds__(1024, 1)
       const uint64_t len = static_cast<uint64_t>(sload_u32(a.lengths, b)) + extra;
       const uint32_t init = sst ? 0u : (a.inits != nullptr ? sload_u32(a.inits, b) : a.init);
       if (!built) {  // the compact LDS image, once per workgroup
-        build_compact_image(lds, zpow, lane_cols, tid, wave, lane);
+        build_compact_image<kLongWaves>(lds, zpow, lane_cols, tid, wave, lane);
         built = true;
       }
       const uint64_t start = base + off, end = start + len;
@@ -303,42 +289,6 @@ __global__ void __launch_bounds__(1024, 1)
     }
     __syncthreads();
   }
-}
-
-// Index and metaindex CRCs of T tables (lvkv_sst_table.hip): workgroup 2t + w
-// checksums table t's index (w = 0) or metaindex (w = 1), contents + type
-// byte, and compares with the stored trailer (table/format.cc:92-97).
-__global__ void __launch_bounds__(1024, 1)
-    sst_meta_crc_kernel(const uint8_t* file, const uint64_t* table_off, lvkv_sst_report* reports,
-                        const uint32_t* zpow, const uint32_t* lane_cols) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kCompactLdsBytes / 4 + kLongWaves];
-  const uint32_t t = blockIdx.x >> 1, which = blockIdx.x & 1u;
-  lvkv_sst_report* r = reports + t;
-  if (r->status != LVKV_SST_OK) return;
-  if (which == 1 && r->meta_status != LVKV_BLOCK_OK) return;  // truncated metaindex
-  const uint32_t tid = threadIdx.x;
-  const uint32_t lane = lane_id();
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  build_compact_image(lds, zpow, lane_cols, tid, wave, lane);
-  const uint8_t* img = file + (table_off != nullptr ? table_off[t] : 0);
-  const uint64_t off = which ? r->meta_offset : r->index_offset;
-  const uint64_t len = (which ? r->meta_size : r->index_size) + 1;
-  const uint64_t start = reinterpret_cast<uint64_t>(img) + off;
-  const uint32_t crc = workgroup_crc<kLongWaves>(lds, lds + kCompactLdsBytes / 4, start, start + len, 0u,
-                                     lane_keys(lane), tid, wave, lane,
-                                     (lane >> 5) * 256u + 128u + (lane & 31u) * 4u, zpow);
-  if (tid == 0) {
-    r->scratch_crc_[which] = crc;
-    r->scratch_status_[which] = crc != crc_unmask(ld_le32_g(img + off + len)) ? 1 : 0;
-  }
-}
-
-hipError_t launch_sst_meta_crc(const uint8_t* file, const uint64_t* table_off, uint32_t ntables,
-                               lvkv_sst_report* reports, const uint32_t* zpow,
-                               const uint32_t* lane_cols, hipStream_t stream) {
-  hipLaunchKernelGGL(sst_meta_crc_kernel, dim3(2 * ntables), dim3(1024), 0, stream, file,
-                     table_off, reports, zpow, lane_cols);
-  return hipGetLastError();
 }
 
 hipError_t launch_crc32c_long(const KernelArgs& args, const uint32_t* zpow,

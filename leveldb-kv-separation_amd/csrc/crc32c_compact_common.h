@@ -143,6 +143,21 @@ struct LaneTabGen {
   }
 };
 
+// The compact image for a workgroup of W waves: row tables from the Z_256
+// set of zpow, lane tables generated from lane_cols; ends with a barrier.
+template <int W>
+__device__ __forceinline__ void build_compact_image(uint32_t* lds, const uint32_t* zpow,
+                                                    const uint32_t* lane_cols, uint32_t tid,
+                                                    uint32_t wave, uint32_t lane) {
+  RowTabStage<64 * W> rt;
+  LaneTabGen<W> lg;
+  rt.load(zpow, tid);
+  lg.load(lane_cols, wave, lane);
+  rt.store(lds, tid);
+  lg.store(lds, wave, lane);
+  __syncthreads();
+}
+
 // ---- long blocks: one workgroup per block -------------------------------
 
 __device__ __forceinline__ uint32_t zshift_g(const uint32_t* zpow, uint32_t v, uint64_t n) {
@@ -216,28 +231,43 @@ __device__ uint32_t segment_register(const uint32_t* lds, uint64_t s, uint64_t e
   return wave_xor_dpp(lane_end_shift_c(lds, st, lane_base));
 }
 
+// v -> Z_{2^j}(v) with zpow set j (one step of four lookups).
+__device__ __forceinline__ uint32_t zstep_g(const uint32_t* t, uint32_t v) {
+  return t[v & 255u] ^ t[256u + ((v >> 8) & 255u)] ^ t[512u + ((v >> 16) & 255u)] ^
+         t[768u + (v >> 24)];
+}
+
 // CRC32C of [start, end) from `init` by the whole workgroup: 16 KiB segments
-// on 4-byte boundaries, wave w of W takes segments w, w + W, ...; each register
-// is shifted to the last 4-byte boundary (Z_n from zpow) and xored into the
-// wave's LDS slot; thread 0 combines, feeds the 0-3 tail bytes through Z_1
-// and returns the CRC (other threads: undefined). Two barriers; every thread
-// of the workgroup must call it.
+// on 4-byte boundaries, wave w of W takes segments w, w + W, ... and folds
+// them Horner-style, acc <- Z_{W * 16 KiB}(acc) ^ reg (one zpow set, since
+// W * 16 KiB is a power of two; only the batch's last segment and the final
+// shift to the last 4-byte boundary are variable, Z_n as a product of zpow
+// sets). Thread 0 combines the waves' accumulators, feeds the 0-3 tail bytes
+// through Z_1 and returns the CRC (other threads: undefined). Two barriers;
+// every thread of the workgroup must call it.
 template <int W>
 __device__ uint32_t workgroup_crc(const uint32_t* lds, uint32_t* acc_slots, uint64_t start,
                                   uint64_t end, uint32_t init, const LaneKeys& keys,
                                   uint32_t tid, uint32_t wave, uint32_t lane, uint32_t lane_base,
                                   const uint32_t* zpow) {
+  static_assert(W == 8 || W == 16, "W * kLongSeg must be a power of two");
+  constexpr uint64_t kStride = W * kLongSeg;
+  const uint32_t* zstride = zpow + (W == 8 ? 17u : 18u) * 1024u;  // Z_{kStride}
   const uint64_t e4 = end & ~uint64_t{3};
   const uint64_t a4 = start & ~uint64_t{3};
   const uint32_t m = e4 > start ? static_cast<uint32_t>((e4 - a4 + kLongSeg - 1) / kLongSeg) : 0u;
   uint32_t acc = 0;
+  uint64_t at = 0;  // the boundary acc is the register at (0: nothing yet)
   for (uint32_t k = wave; k < m; k += W) {
     const uint64_t s = k == 0 ? start : a4 + k * kLongSeg;
     const uint64_t e = min(a4 + (k + 1) * kLongSeg, e4);
     const uint32_t reg =
         segment_register(lds, s, e, k == 0 ? init : 0xffffffffu, keys, lane, lane_base);
-    acc ^= zshift_g(zpow, reg, e4 - e);
+    if (at != 0) acc = e - at == kStride ? zstep_g(zstride, acc) : zshift_g(zpow, acc, e - at);
+    acc ^= reg;
+    at = e;
   }
+  if (at != 0) acc = zshift_g(zpow, acc, e4 - at);
   if (lane == 0) acc_slots[wave] = acc;
   __syncthreads();
   uint32_t crc = 0;

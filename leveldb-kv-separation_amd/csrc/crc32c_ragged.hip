@@ -27,6 +27,7 @@
 
 #include "crc32c_compact_common.h"
 #include "crc32c_device_common.h"
+#include "lvkv_crc32c.h"
 #include "lvkv_kernel_args.h"
 
 namespace lvkv {
@@ -99,12 +100,12 @@ __device__ __forceinline__ RagBlock rag_block(const KernelArgs& a, uint32_t b, b
     len = sload_u32(a.lengths, b);
     if (a.inits != nullptr) init = sload_u32(a.inits, b);
   }
-  if (a.mode == kModeSstVerify || a.mode == kModeSstFill) {
+  if (a.mode == kModeSstVerify || a.mode == kModeSstFill || a.mode == kModeSstTable) {
     // contents n bytes + type byte; the masked CRC follows
     // (table/format.cc:92-94, table/table_builder.cc:199-203)
     len += 1;
     init = 0;
-    if (a.mode == kModeSstVerify) expected = crc_unmask(sload_le(base + off + len, 4));
+    if (a.mode != kModeSstFill) expected = crc_unmask(sload_le(base + off + len, 4));
   }
   const uint64_t ptr = base + off;
   g.ptr_lo = static_cast<uint32_t>(ptr);
@@ -137,11 +138,40 @@ __device__ __forceinline__ uint32_t rag_tiny(const RagBlock& g) {
   return reg ^ 0xffffffffu;
 }
 
+// Table of entry e in kModeSstTable: the last report whose first <= e.
+__device__ __forceinline__ uint32_t sst_table_of(const lvkv_sst_report* reports, uint32_t ntables,
+                                                 uint32_t e) {
+  uint32_t lo = 0, hi = ntables;  // answer in [lo, hi)
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (reports[mid].first <= e) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
 // Lane 0 stores block b's result in the batch's mode.
 __device__ __forceinline__ void rag_store(const KernelArgs& a, uint32_t b, const RagBlock& g,
                                           uint32_t crc) {
   if (lane_id() != 0) return;
-  if (a.mode == kModeCompute) {
+  if (a.mode == kModeSstTable) {
+    // ReadBlock's order (format.cc:92-97, :104-158): the index parse status
+    // first, then the checksum, then the type byte
+    a.out_crc[b] = crc;
+    uint8_t st = a.out_status[b];
+    if (st == LVKV_BLOCK_OK) {
+      if (crc != g.expected)
+        st = LVKV_BLOCK_CHECKSUM;
+      else if (*reinterpret_cast<const uint8_t*>(g.ptr() + g.len - 1) > 2)
+        st = LVKV_BLOCK_BAD_TYPE;
+      if (st != LVKV_BLOCK_OK) a.out_status[b] = st;
+    }
+    if (st != LVKV_BLOCK_OK) {
+      lvkv_sst_report* reps = static_cast<lvkv_sst_report*>(a.sst_reports);
+      lvkv_sst_report* r = reps + sst_table_of(reps, a.sst_ntables, b);
+      atomicAdd(&r->nbad, 1u);
+      atomicMin(&r->first_bad, b - r->first);
+    }
+  } else if (a.mode == kModeCompute) {
     a.out_crc[b] = a.mask ? crc_mask(crc) : crc;
   } else if (a.mode == kModeSstFill || a.mode == kModeLogFill) {
     // the stored form (Mask, little-endian) into the trailer / header hole
@@ -333,7 +363,7 @@ __global__ void __launch_bounds__(64 * W, 2)
   //    64 * W at a time only when a wave met one.
   __syncthreads();
   if (lds[kFlag] == 0) return;
-  const bool sst = a.mode == kModeSstVerify || a.mode == kModeSstFill;
+  const bool sst = a.mode == kModeSstVerify || a.mode == kModeSstFill || a.mode == kModeSstTable;
   for (uint32_t slice = 0; slice < n; slice += 64 * W) {
     if (tid == 0) lds[kCount] = 0;
     __syncthreads();
@@ -396,7 +426,8 @@ hipError_t launch_crc32c_long(const KernelArgs& args, const uint32_t* zpow,
 hipError_t launch_crc32c_general(const KernelArgs& a, int cus, hipStream_t stream) {
   const uint32_t n = a.nblocks;
   if (n == 0) return hipSuccess;
-  const int cfg = g_general_kernel;
+  // (kModeSstTable exists in this kernel only)
+  const int cfg = a.mode == kModeSstTable && g_general_kernel < 0 ? 0 : g_general_kernel;
   if (cfg < 0) {  // the persistent kernel and, for long blocks, a second launch
     const uint32_t want = (n + kWavesPerGroup - 1) / kWavesPerGroup;
     hipError_t e = launch_crc32c_batch(

@@ -50,6 +50,9 @@ enum : uint32_t {
                        // masked CRC into trailer bytes 1..4
   kModeLogFill = 4,    // log_writer.cc:94-96: header at off, writes the
                        // masked CRC into header bytes 0..3
+  kModeSstTable = 5,   // kModeSstVerify whose store also merges the index
+                       // parse status (out_status in), the type byte and
+                       // the per-table totals (sst_reports)
 };
 
 struct KernelArgs {
@@ -75,6 +78,9 @@ struct KernelArgs {
                               // covers min(nblocks, *count) blocks (a count
                               // produced by an earlier kernel, e.g. an index
                               // parse); nullptr = nblocks
+  void* sst_reports;          // kModeSstTable: lvkv_sst_report[sst_ntables]
+  uint32_t sst_ntables;
+  uint32_t pad_;
 };
 
 // Arguments of the uniform-layout kernel (crc32c_uniform.hip): nblocks

@@ -178,7 +178,7 @@ def main():
     us_m = timed(multi, max(5, args.reps // 5))
     us_s = timed(single, max(5, args.reps // 5))
     report("sst_verify_tables_32x2MiB", nbytes, us_m, None,
-           f"one multi-table call (8 launches); 32 single-table calls: {us_s:.1f} us")
+           f"one multi-table call (4 launches); 32 single-table calls: {us_s:.1f} us")
 
     for nrec in (2000, 60000):
         img = log_synth.build_log(nrec, seed=nrec, max_len=2000, big_every=997)
