@@ -237,22 +237,24 @@ __device__ __forceinline__ uint32_t zstep_g(const uint32_t* t, uint32_t v) {
          t[768u + (v >> 24)];
 }
 
-// CRC32C of [start, end) from `init` by the whole workgroup: 16 KiB segments
-// on 4-byte boundaries, wave w of W takes segments w, w + W, ... and folds
-// them Horner-style, acc <- Z_{W * 16 KiB}(acc) ^ reg (one zpow set, since
-// W * 16 KiB is a power of two; only the batch's last segment and the final
+// CRC32C of [start, end) from `init` by the whole workgroup: SEG-byte
+// segments on 4-byte boundaries, wave w of W takes segments w, w + W, ... and
+// folds them Horner-style, acc <- Z_{W * SEG}(acc) ^ reg (one zpow set, since
+// W * SEG is a power of two; only the batch's last segment and the final
 // shift to the last 4-byte boundary are variable, Z_n as a product of zpow
 // sets). Thread 0 combines the waves' accumulators, feeds the 0-3 tail bytes
 // through Z_1 and returns the CRC (other threads: undefined). Two barriers;
 // every thread of the workgroup must call it.
-template <int W>
+template <int W, uint64_t SEG = kLongSeg>
 __device__ uint32_t workgroup_crc(const uint32_t* lds, uint32_t* acc_slots, uint64_t start,
                                   uint64_t end, uint32_t init, const LaneKeys& keys,
                                   uint32_t tid, uint32_t wave, uint32_t lane, uint32_t lane_base,
                                   const uint32_t* zpow) {
-  static_assert(W == 8 || W == 16, "W * kLongSeg must be a power of two");
+  constexpr uint64_t kLongSeg = SEG;
   constexpr uint64_t kStride = W * kLongSeg;
-  const uint32_t* zstride = zpow + (W == 8 ? 17u : 18u) * 1024u;  // Z_{kStride}
+  static_assert((kStride & (kStride - 1)) == 0 && kStride < (uint64_t{1} << kZPowCount),
+                "W * SEG must be a power of two");
+  const uint32_t* zstride = zpow + static_cast<uint32_t>(__builtin_ctzll(kStride)) * 1024u;
   const uint64_t e4 = end & ~uint64_t{3};
   const uint64_t a4 = start & ~uint64_t{3};
   const uint32_t m = e4 > start ? static_cast<uint32_t>((e4 - a4 + kLongSeg - 1) / kLongSeg) : 0u;

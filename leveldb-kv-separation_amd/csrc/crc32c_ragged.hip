@@ -113,7 +113,7 @@ __device__ __forceinline__ RagBlock rag_block(const KernelArgs& a, uint32_t b, b
   g.len = len;
   g.s0 = init ^ 0xffffffffu;
   g.expected = expected;
-  if (a.long_split && len > kLongBytes) {
+  if (a.long_split && len > a.long_split) {
     g.kind = kRagSkip;
     return g;
   }
@@ -195,14 +195,23 @@ struct RagRound {
   uint32_t nchunks;  // max over the chains, >= 1
   uint32_t w[NCH][R + 1];  // row R: the neighbour dwords of row R - 1
 
-  __device__ __forceinline__ void setup(const KernelArgs& a, uint32_t start, uint32_t n,
-                                        uint32_t r0, uint32_t wave, uint32_t W) {
-    nchunks = 1;
+  // Chain c of round r0 is block start + r0 + c * W + wave.
+  __device__ static __forceinline__ void fetch(RagBlock (&out)[NCH], const KernelArgs& a,
+                                               uint32_t start, uint32_t n, uint32_t r0,
+                                               uint32_t wave, uint32_t W) {
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const uint32_t i = r0 + static_cast<uint32_t>(c) * W + wave;
-      blk[c] = start + i;
-      g[c] = rag_block(a, blk[c], i < n);
+      out[c] = rag_block(a, start + i, i < n);
+    }
+  }
+  __device__ __forceinline__ void adopt(const RagBlock (&in)[NCH], uint32_t start, uint32_t r0,
+                                        uint32_t wave, uint32_t W) {
+    nchunks = 1;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      g[c] = in[c];
+      blk[c] = start + r0 + static_cast<uint32_t>(c) * W + wave;
       if (g[c].kind == kRagRows) nchunks = max(nchunks, (g[c].rows() + R - 1) / R);
     }
   }
@@ -261,9 +270,19 @@ __global__ void __launch_bounds__(64 * W, 2)
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t total = a.count != nullptr ? min(a.nblocks, sload_u32(a.count, 0)) : a.nblocks;
   const uint32_t G = gridDim.x;
-  const uint32_t per = total / G, extra = total % G;
-  const uint32_t n = per + (blockIdx.x < extra ? 1u : 0u);
-  const uint32_t start = blockIdx.x * per + min(blockIdx.x, extra);
+  uint32_t start, n;
+  if (a.run_base != nullptr) {  // runs of whole units (bytes balanced)
+    const uint32_t U = a.run_units;
+    const uint32_t u0 = static_cast<uint32_t>(static_cast<uint64_t>(blockIdx.x) * U / G);
+    const uint32_t u1 = static_cast<uint32_t>(static_cast<uint64_t>(blockIdx.x + 1) * U / G);
+    start = min(total, sload_u32(a.run_base, u0));
+    const uint32_t end = u1 < U ? min(total, sload_u32(a.run_base, u1)) : total;
+    n = end > start ? end - start : 0u;
+  } else {
+    const uint32_t per = total / G, extra = total % G;
+    n = per + (blockIdx.x < extra ? 1u : 0u);
+    start = blockIdx.x * per + min(blockIdx.x, extra);
+  }
   if (n == 0) return;  // the whole workgroup: no barrier is left waiting
 
   // 1. table loads, round 0's first chunk in flight, the LDS image, barrier
@@ -273,7 +292,11 @@ __global__ void __launch_bounds__(64 * W, 2)
     LaneTabGen<W> lg;
     rt.load(zpow, tid);
     lg.load(lane_cols, wave, lane);
-    rd.setup(a, start, n, 0, wave, W);
+    {
+      RagBlock g0[NCH];
+      RagRound<NCH, R>::fetch(g0, a, start, n, 0, wave, W);
+      rd.adopt(g0, start, 0, wave, W);
+    }
     __builtin_amdgcn_sched_barrier(0);
     rd.issue(0, lane);
     __builtin_amdgcn_sched_barrier(0);
@@ -288,9 +311,13 @@ __global__ void __launch_bounds__(64 * W, 2)
 
   uint32_t r0 = 0, k = 0;
   uint32_t st[NCH];
+  RagBlock gn[NCH];  // the next round's chains
   while (true) {
-    // 2. row 0: start every chain (fix-ups) or continue it. Idle chains walk
-    //    zeros and store nothing.
+    // 2. the next round's descriptors (offsets, lengths, headers, trailers:
+    //    dependent scalar loads) fetched while this round's rows are in
+    //    flight. Row 0: start every chain (fix-ups) or continue it. Idle
+    //    chains walk zeros and store nothing.
+    if (k == 0) RagRound<NCH, R>::fetch(gn, a, start, n, r0 + W * NCH, wave, W);
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
       if (rd.g[c].e() != 0) rd.realign(c, lane);
@@ -326,12 +353,14 @@ __global__ void __launch_bounds__(64 * W, 2)
         for (int c = 0; c < NCH; ++c) st[c] = row_step_c(lds, st[c], rd.w[c][j], keys);
       }
     }
+    // (row-major: the chains still running stay interleaved)
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
+    for (int j = 1; j < R; ++j) {
+      const uint32_t u = static_cast<uint32_t>(j);
+      if (u >= nab) {
 #pragma unroll
-      for (int j = 1; j < R; ++j) {
-        const uint32_t u = static_cast<uint32_t>(j);
-        if (u >= nab && u < nrow[c]) st[c] = row_step_c(lds, st[c], rd.w[c][j], keys);
+        for (int c = 0; c < NCH; ++c)
+          if (u < nrow[c]) st[c] = row_step_c(lds, st[c], rd.w[c][j], keys);
       }
     }
     // 4. chains whose last chunk this was; tiny blocks at the round's end
@@ -351,7 +380,7 @@ __global__ void __launch_bounds__(64 * W, 2)
       }
       r0 += W * NCH;
       if (r0 >= n) break;
-      rd.setup(a, start, n, r0, wave, W);
+      rd.adopt(gn, start, r0, wave, W);
       k = 0;
     }
     rd.issue(k, lane);
@@ -364,20 +393,34 @@ __global__ void __launch_bounds__(64 * W, 2)
   __syncthreads();
   if (lds[kFlag] == 0) return;
   const bool sst = a.mode == kModeSstVerify || a.mode == kModeSstFill || a.mode == kModeSstTable;
+  const bool log = a.mode == kModeLogVerify || a.mode == kModeLogFill;
   for (uint32_t slice = 0; slice < n; slice += 64 * W) {
     if (tid == 0) lds[kCount] = 0;
     __syncthreads();
     const uint32_t i = slice + tid;
-    if (i < n && a.lengths[start + i] + (sst ? 1u : 0u) > kLongBytes)
-      lds[kList + atomicAdd(&lds[kCount], 1u)] = start + i;
+    if (i < n) {
+      uint32_t clen;  // covered length, as rag_block computes it
+      if (log) {
+        const uint8_t* h = a.base + a.offsets[start + i];
+        clen = 1u + (static_cast<uint32_t>(h[4]) | (static_cast<uint32_t>(h[5]) << 8));
+      } else {
+        clen = a.lengths[start + i] + (sst ? 1u : 0u);
+      }
+      if (clen > a.long_split) lds[kList + atomicAdd(&lds[kCount], 1u)] = start + i;
+    }
     __syncthreads();
     const uint32_t cnt = __builtin_amdgcn_readfirstlane(lds[kCount]);
     for (uint32_t li = 0; li < cnt; ++li) {
       const uint32_t b = __builtin_amdgcn_readfirstlane(lds[kList + li]);
       const RagBlock g = rag_block(a, b, true);
-      const uint32_t crc = workgroup_crc<W>(lds, lds + kAcc, g.ptr(), g.ptr() + g.len,
-                                            g.s0 ^ 0xffffffffu, keys, tid, wave, lane, lane_base,
-                                            zpow);
+      // WAL fragments (<= 32 KiB): 4 KiB segments, one per wave; longer
+      // blocks: 16 KiB segments
+      const uint32_t crc =
+          g.len <= 32768u
+              ? workgroup_crc<W, 4096>(lds, lds + kAcc, g.ptr(), g.ptr() + g.len,
+                                       g.s0 ^ 0xffffffffu, keys, tid, wave, lane, lane_base, zpow)
+              : workgroup_crc<W>(lds, lds + kAcc, g.ptr(), g.ptr() + g.len, g.s0 ^ 0xffffffffu,
+                                 keys, tid, wave, lane, lane_base, zpow);
       if (tid == 0) rag_store(a, b, g, crc);
     }
     __syncthreads();
@@ -386,15 +429,25 @@ __global__ void __launch_bounds__(64 * W, 2)
 
 }  // namespace
 
-// cfg: shape = cfg & 3 (0: 8 waves x 2 chains x 24 rows; 1: 8 x 3 x 16;
-// 2: 8 x 2 x 32; 3: 8 x 3 x 24); cfg & 4: one round per workgroup (grid
-// sized to the batch) instead of at most two workgroups per CU.
-int ragged_blocks_per_round(int cfg) { return ((cfg & 3) == 1 || (cfg & 3) == 3) ? 8 * 3 : 8 * 2; }
+// cfg: shape = cfg & 3, or cfg >> 3 for the small-record shapes (1: 8 waves
+// x 4 chains x 8 rows; 2: 8 x 6 x 8; 3: 8 x 8 x 4); the large-record shapes
+// (cfg < 8) are 0: 8 x 2 x 24; 1: 8 x 3 x 16; 2: 8 x 2 x 32; 3: 8 x 3 x 24,
+// and cfg & 4 asks for one round per workgroup (grid sized to the batch)
+// instead of at most two workgroups per CU.
+int ragged_blocks_per_round(int cfg) {
+  switch (cfg >> 3) {
+    case 1: return 8 * 4;
+    case 2: return 8 * 6;
+    case 3: return 8 * 8;
+  }
+  return ((cfg & 3) == 1 || (cfg & 3) == 3) ? 8 * 3 : 8 * 2;
+}
 
 hipError_t launch_crc32c_ragged(const KernelArgs& a, const uint32_t* zpow,
                                 const uint32_t* lane_cols, int cfg, int num_groups,
                                 hipStream_t stream) {
-  switch (cfg & 3) {
+  const int shape = cfg >= 8 ? 4 + (cfg >> 3) : (cfg & 3);
+  switch (shape) {
 #define LVKV_RAG_CASE(c, w, nch, r)                                                            \
   case c:                                                                                      \
     hipLaunchKernelGGL((crc32c_ragged_kernel<w, nch, r>), dim3(num_groups), dim3(64 * w), 0,   \
@@ -404,7 +457,12 @@ hipError_t launch_crc32c_ragged(const KernelArgs& a, const uint32_t* zpow,
     LVKV_RAG_CASE(1, 8, 3, 16)
     LVKV_RAG_CASE(2, 8, 2, 32)
     LVKV_RAG_CASE(3, 8, 3, 24)
+    LVKV_RAG_CASE(5, 8, 4, 8)
+    LVKV_RAG_CASE(6, 8, 6, 8)
+    LVKV_RAG_CASE(7, 8, 8, 4)
 #undef LVKV_RAG_CASE
+    default:
+      return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
@@ -416,6 +474,8 @@ hipError_t launch_crc32c_batch(const KernelArgs& args, bool uniform_aligned, int
 // cfg (>= 0), or -1 for crc32c_kernel.hip's persistent kernel. Set only by
 // lvkv_debug_set_general_kernel (A/B timing).
 int g_general_kernel = 0;
+// The shape for WAL records (type + payload, mostly well under 2 KiB).
+int g_log_kernel = 8;
 
 hipError_t launch_crc32c_long(const KernelArgs& args, const uint32_t* zpow,
                               const uint32_t* lane_cols, int num_groups, hipStream_t stream);
@@ -427,14 +487,18 @@ hipError_t launch_crc32c_general(const KernelArgs& a, int cus, hipStream_t strea
   const uint32_t n = a.nblocks;
   if (n == 0) return hipSuccess;
   // (kModeSstTable exists in this kernel only)
-  const int cfg = a.mode == kModeSstTable && g_general_kernel < 0 ? 0 : g_general_kernel;
+  const bool log = a.mode == kModeLogVerify || a.mode == kModeLogFill;
+  int cfg = log && g_general_kernel >= 0 ? g_log_kernel : g_general_kernel;
+  if (a.mode == kModeSstTable && cfg < 0) cfg = 0;
   if (cfg < 0) {  // the persistent kernel and, for long blocks, a second launch
+    KernelArgs b = a;
+    if (log) b.long_split = 0;  // crc32c_long_kernel has no WAL modes
     const uint32_t want = (n + kWavesPerGroup - 1) / kWavesPerGroup;
     hipError_t e = launch_crc32c_batch(
-        a, false, static_cast<int>(min(static_cast<uint32_t>(cus), want)), stream);
-    if (e == hipSuccess && a.long_split)
-      e = launch_crc32c_long(a, a.row_tab + kZPowOffset,
-                             a.row_tab + kRowTabDwords + kLaneTabDwords, cus, stream);
+        b, false, static_cast<int>(min(static_cast<uint32_t>(cus), want)), stream);
+    if (e == hipSuccess && b.long_split)
+      e = launch_crc32c_long(b, b.row_tab + kZPowOffset,
+                             b.row_tab + kRowTabDwords + kLaneTabDwords, cus, stream);
     return e;
   }
   const uint32_t per = static_cast<uint32_t>(ragged_blocks_per_round(cfg));

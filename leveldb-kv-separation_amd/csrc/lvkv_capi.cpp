@@ -24,6 +24,7 @@ hipError_t launch_crc32c_batch(const KernelArgs& args, bool uniform_aligned,
                                int num_groups, hipStream_t stream);
 hipError_t launch_crc32c_general(const KernelArgs& a, int cus, hipStream_t stream);
 extern int g_general_kernel;
+extern int g_log_kernel;
 hipError_t launch_crc32c_probe(const KernelArgs& args, int variant,
                                int num_groups, hipStream_t stream);
 hipError_t launch_read_bw(const void* p, uint64_t bytes, uint32_t* out,
@@ -229,9 +230,10 @@ int run_batch(KernelArgs a, size_t nblocks, hipStream_t stream) {
     } else if (b.offsets != nullptr && b.mode != kModeLogVerify && b.mode != kModeLogFill) {
       // Blocks longer than kLongBytes go to one workgroup each (segments in
       // parallel) instead of one wave; the main kernel leaves them alone.
-      b.long_split = 1;
+      b.long_split = kLongBytes;
       e = launch_crc32c_general(b, c->groups, stream);
     } else if (b.offsets != nullptr) {  // log headers
+      b.long_split = kLogLongBytes;
       e = launch_crc32c_general(b, c->groups, stream);
     } else {  // uniform layout, block ends not 4-byte aligned
       e = launch_crc32c_batch(b, false, groups, stream);
@@ -684,10 +686,17 @@ int lvkv_debug_read_bw(const void* d_data, uint64_t bytes, uint32_t* d_scratch,
 }
 
 // -1: crc32c_kernel.hip's persistent kernel for general-layout batches;
-// 0..7: crc32c_ragged.hip cfgs (launch_crc32c_ragged). Timing only.
+// 0..31: crc32c_ragged.hip cfgs (launch_crc32c_ragged). Timing only.
 int lvkv_debug_set_general_kernel(int k) {
-  if (k < -1 || k > 7) return LVKV_ERR_INVALID;
+  if (k < -1 || k > 31) return LVKV_ERR_INVALID;
   g_general_kernel = k;
+  return LVKV_OK;
+}
+
+// The ragged cfg used for WAL records (8, 16, 24: small-record shapes).
+int lvkv_debug_set_log_kernel(int k) {
+  if (k < 0 || k > 31) return LVKV_ERR_INVALID;
+  g_log_kernel = k;
   return LVKV_OK;
 }
 

@@ -31,6 +31,9 @@ constexpr uint32_t kLaneColDwords = 8 * 64 * 4;  // lane_cols (lvkv_tables.h)
 // Blocks longer than this are split over a whole workgroup
 // (crc32c_long_kernel) instead of one wave walking them alone.
 constexpr uint32_t kLongBytes = 64 * 1024;
+// The same for WAL records (<= 32 KiB, most far smaller): a 32 KiB fragment
+// walked by one wave would hold up its workgroup.
+constexpr uint32_t kLogLongBytes = 8 * 1024;
 constexpr uint32_t kZPowCount = 48;               // Z_{2^j}, j < 48 (256 TiB)
 constexpr uint32_t kZPowDwords = kZPowCount * 1024;
 constexpr uint32_t kZPowOffset = 1024 + 8 * 16 * 64 + 8 * 64 * 4;  // in d_tables
@@ -70,9 +73,11 @@ struct KernelArgs {
   uint32_t nblocks;
   uint32_t mode;
   uint32_t mask;              // 1: store Mask(crc) (util/crc32c.h:29-32)
-  uint32_t long_split;        // 1: blocks whose covered length exceeds
-                              // kLongBytes are left to crc32c_long_kernel
-                              // (no loads, no store here)
+  uint32_t long_split;        // non-zero: blocks whose covered length
+                              // exceeds it (bytes) are walked by a whole
+                              // workgroup (crc32c_ragged.hip) or left to
+                              // crc32c_long_kernel (crc32c_kernel.hip, which
+                              // takes kLongBytes whatever the value)
   uint64_t* stamps;           // probe builds only: per-wave timestamps
   const uint32_t* count;      // optional device-side block count: the launch
                               // covers min(nblocks, *count) blocks (a count
@@ -80,7 +85,12 @@ struct KernelArgs {
                               // parse); nullptr = nblocks
   void* sst_reports;          // kModeSstTable: lvkv_sst_report[sst_ntables]
   uint32_t sst_ntables;
-  uint32_t pad_;
+  uint32_t run_units;         // with run_base: workgroup g of G walks blocks
+  const uint32_t* run_base;   //   [run_base[gU/G], run_base[(g+1)U/G]) (the
+                              //   last one to the count): runs balanced in
+                              //   bytes when a unit is a fixed-size region
+                              //   (the WAL's 32 KiB blocks); nullptr = equal
+                              //   block counts per workgroup
 };
 
 // Arguments of the uniform-layout kernel (crc32c_uniform.hip): nblocks

@@ -455,7 +455,7 @@ hipError_t launch_sst_tables(const uint8_t* file, const uint64_t* toff, const ui
   a.mode = kModeSstTable;
   a.nblocks = capacity;
   a.count = &reports[0].total_;
-  a.long_split = 1;  // large data/filter blocks: one workgroup each
+  a.long_split = kLongBytes;  // large data/filter blocks: one workgroup each
   a.sst_reports = reports;
   a.sst_ntables = ntables;
   return launch_crc32c_general(a, groups, stream);

@@ -31,6 +31,9 @@ CASES = {
     "8192_aligned": (8192, 8192, 8192, 0),
     "2048_aligned": (32768, 2048, 2048, 0),
     "4096_aligned_65k": (65536, 4096, 4096, 0),
+    # (n, max length, 0, seed): lengths uniform in [0, max), packed back to back
+    "rand2000_62k": (62000, 2000, 0, 7),
+    "rand8000_16k": (16384, 8000, 0, 8),
 }
 
 
@@ -53,8 +56,13 @@ def main():
     res = {}
     for name in args.cases.split(","):
         n, length, stride, first = CASES[name]
-        offs = (first + stride * np.arange(n, dtype=np.uint64)).astype(np.uint64)
-        lens = np.full(n, length, dtype=np.uint32)
+        if stride == 0:
+            lens = np.random.default_rng(first).integers(0, length, n).astype(np.uint32)
+            offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64))]).astype(np.uint64)
+            length = float(lens.mean())
+        else:
+            offs = (first + stride * np.arange(n, dtype=np.uint64)).astype(np.uint64)
+            lens = np.full(n, length, dtype=np.uint32)
         d_off = torch.from_numpy(offs.astype(np.int64)).to(dev)
         d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
         out = torch.empty(n, dtype=torch.int32, device=dev)
