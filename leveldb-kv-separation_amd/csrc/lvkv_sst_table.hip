@@ -228,19 +228,22 @@ __device__ void find_filter(const uint8_t* m, uint64_t msize, uint64_t file_size
   const uint32_t nr = ld_le32(m + msize - 4);
   if (nr > (msize - 4) / 4) return;
   const uint8_t* limit = m + (msize - (1 + static_cast<uint64_t>(nr)) * 4);
-  constexpr uint32_t kKeyCap = 64;
-  uint8_t key[kKeyCap];
+  // Only the first 7 bytes of each key matter for the test: they are kept in
+  // one register (byte i of key7), not a key buffer (private arrays live in
+  // scratch memory, one memory round trip per access).
+  constexpr uint64_t kFilterPrefix = 0x2e7265746c6966ull;  // "filter." little-endian
+  uint64_t key7 = 0;
   uint32_t klen = 0;
   const uint8_t* p = m;
   while (p < limit) {
     uint32_t sh, ns, vl;
     const uint8_t* q = decode_entry(p, limit, &sh, &ns, &vl);
     if (q == nullptr || sh > klen) return;
-    // key = key[0, sh) + delta; only the first 7 bytes matter for the test
-    for (uint32_t i = 0; i < ns && sh + i < kKeyCap; ++i) key[sh + i] = q[i];
+    // key = key[0, sh) + delta
+    for (uint32_t i = sh; i < 7 && i < sh + ns; ++i)
+      key7 = (key7 & ~(0xffull << (8 * i))) | (static_cast<uint64_t>(q[i - sh]) << (8 * i));
     klen = sh + ns;
-    const bool is_filter = klen >= 7 && key[0] == 'f' && key[1] == 'i' && key[2] == 'l' &&
-                           key[3] == 't' && key[4] == 'e' && key[5] == 'r' && key[6] == '.';
+    const bool is_filter = klen >= 7 && (key7 & 0xffffffffffffffull) == kFilterPrefix;
     if (is_filter) {
       uint64_t fo, fsz;
       if (!decode_handle(q + ns, q + ns + vl, &fo, &fsz, nullptr)) return;
