@@ -34,6 +34,8 @@ CASES = {
     # (n, max length, 0, seed): lengths uniform in [0, max), packed back to back
     "rand2000_62k": (62000, 2000, 0, 7),
     "rand8000_16k": (16384, 8000, 0, 8),
+    "4271_end_unaligned_65k": (65536, 4271, 4272, 0),
+    "rand8000_65k": (65536, 8000, 0, 9),
 }
 
 
