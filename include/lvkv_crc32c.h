@@ -34,6 +34,9 @@ extern "C" {
 /* Store crc32c::Mask(crc) instead of crc (util/crc32c.h:29-32): the value
  * TableBuilder::WriteRawBlock / log::Writer put on disk. */
 #define LVKV_FLAG_MASK 1u
+/* Engine submits only: this dispatch waits for every earlier dispatch of the
+ * engine to complete (AQL barrier bit). Without it, dispatches may overlap. */
+#define LVKV_FLAG_ORDERED 2u
 
 /* ---- per-call, host CPU: the drop-in for the reference's own symbols ---- */
 
@@ -72,6 +75,34 @@ int lvkv_crc32c_batch_device(const void* d_base, const uint64_t* d_offsets,
 int lvkv_crc32c_uniform_device(const void* d_base, uint64_t stride,
                                uint32_t length, uint32_t init, uint32_t* d_out,
                                size_t nblocks, uint32_t flags, void* stream);
+
+/* ---- the AQL engine: batches dispatched into a per-device hardware queue --
+ * Same kernels and results as the calls above, without the HIP launch path:
+ * a submit writes AQL dispatch packets into the engine's own queue (well
+ * under a microsecond of host time, against 2.7-7 us for a hipLaunchKernel)
+ * and consecutive dispatches may overlap on the device (no barrier bit
+ * unless LVKV_FLAG_ORDERED). This is the checksum-service form of the batch
+ * loop that compaction (table_builder.cc:199-203) and recovery
+ * (log_reader.cc:243-257) would run.
+ * Engine dispatches are NOT ordered with HIP streams: synchronise the stream
+ * that produced the input before submitting; results (and outputs reused by
+ * a later submit) are safe after lvkv_engine_wait. One engine per device;
+ * calls on one engine are serialised internally (thread-safe). */
+typedef struct lvkv_engine lvkv_engine;
+/* device = HIP device ordinal. */
+int lvkv_engine_create(int device, lvkv_engine** out);
+/* Waits for outstanding work, then frees the queue. NULL is a no-op. */
+void lvkv_engine_destroy(lvkv_engine* engine);
+/* lvkv_crc32c_uniform_device's contract, asynchronous on the engine, for
+ * blocks of 4..4348 bytes (16 rows of 256 B) whose ends are 4-byte aligned
+ * ((d_base + length) % 4 == 0, stride % 4 == 0); any nblocks (batches
+ * beyond one dispatch's capacity become several dispatches). Other shapes:
+ * LVKV_ERR_INVALID (use lvkv_crc32c_uniform_device). */
+int lvkv_engine_crc32c_uniform(lvkv_engine* engine, const void* d_base, uint64_t stride,
+                               uint32_t length, uint32_t init, uint32_t* d_out,
+                               size_t nblocks, uint32_t flags);
+/* Blocks until every dispatch submitted so far has completed. */
+int lvkv_engine_wait(lvkv_engine* engine);
 
 /* Batched leveldb::ReadBlock checksum test (table/format.cc:92-99): block i
  * is the BlockHandle {d_offsets[i], d_sizes[i]} of an SST image at d_file;
@@ -123,6 +154,8 @@ int lvkv_log_fill_headers_device(void* d_file, const uint64_t* d_hdr_offsets, ui
 #define LVKV_SST_INDEX_CORRUPT 7   /* restart array or an entry unusable (table/block.cc:25-75) */
 #define LVKV_SST_CAPACITY 8        /* more blocks than the caller's arrays hold (ndata says
                                       how many data blocks the index lists) */
+/* Longest FilterPolicy::Name() the verify calls accept. */
+#define LVKV_SST_MAX_POLICY_NAME 64
 /* Per-block status (d_status). */
 #define LVKV_BLOCK_OK 0
 #define LVKV_BLOCK_CHECKSUM 1      /* "block checksum mismatch" (table/format.cc:96) */
@@ -130,13 +163,21 @@ int lvkv_log_fill_headers_device(void* d_file, const uint64_t* d_hdr_offsets, ui
 #define LVKV_BLOCK_BAD_TYPE 3      /* "bad block type": type byte not 0/1/2 (:157) */
 #define LVKV_BLOCK_BAD_HANDLE 4    /* index entry value is not a BlockHandle (:28) */
 #define LVKV_BLOCK_BAD_ENTRY 5     /* "bad entry in block" for the index entry (block.cc:236) */
+#define LVKV_BLOCK_COMPRESSED 6    /* CRC good, type 1/2 (snappy/zstd): the as-built reference has
+                                      no codec (HAVE_SNAPPY=0, HAVE_ZSTD=0) and returns "corrupted
+                                      snappy|zstd compressed block length" (format.cc:120-141,
+                                      port/port_stdcxx.h:108-118) */
+#define LVKV_BLOCK_NOT_READ 7      /* index/metaindex: the footer did not decode, never read */
 
 /* Written by lvkv_sst_verify_table(s)_device into device memory. */
 typedef struct lvkv_sst_report {
   int32_t status;          /* LVKV_SST_* */
-  uint32_t nblocks;        /* entries in the per-block arrays: ndata + has_filter */
-  uint32_t ndata;          /* data blocks the index lists */
-  uint32_t has_filter;     /* 1: entry ndata is the filter block ("filter." in the metaindex) */
+  uint32_t nblocks;        /* entries written to the per-block arrays: ndata + has_filter
+                              (0 with LVKV_SST_CAPACITY) */
+  uint32_t ndata;          /* data blocks the index lists (0 when its restart array is
+                              unusable, LVKV_SST_INDEX_CORRUPT) */
+  uint32_t has_filter;     /* 1: the last entry is the filter block, found under the exact
+                              key "filter." + filter_policy (Table::ReadMeta) */
   uint32_t nbad;           /* entries with status != LVKV_BLOCK_OK */
   uint32_t first_bad;      /* lowest such entry (relative to `first`), or 0xffffffff */
   uint32_t index_crc;      /* computed CRC (contents + type byte) of the index block */
@@ -148,47 +189,52 @@ typedef struct lvkv_sst_report {
   uint32_t first;          /* this table's first entry in the shared per-block arrays */
   uint64_t index_offset, index_size, meta_offset, meta_size;  /* footer handles */
   /* library-internal */
-  uint64_t filter_off_;
-  uint32_t filter_size_;
-  uint8_t scratch_status_[2];
-  uint8_t filter_status_;
-  uint8_t reserved1_;
-  uint32_t scratch_crc_[2];
+  uint64_t link_;          /* multi-table placement: (call generation << 32) | entries */
   uint32_t total_;         /* tables[0] only: entries verified over all tables */
   uint32_t reserved2_;
 } lvkv_sst_report;
 
 /* Verifies a whole SSTable image already in device memory, as Table::Open
- * (table/table.cc:38-79) + Table::ReadMeta (:81-105) + ReadBlock on every
- * block (table/format.cc:69-160) would with verify_checksums: footer and
- * magic, index and metaindex checksums, then every data block the index lists
- * and the filter block, all on the device (footer kernel -> verify of index
- * and metaindex -> parallel index parse, one entry per restart point as
- * table_builder.cc:35 writes it -> one batched verify -> merge). Per-block
- * outputs (arrays of `capacity` entries, device memory), in index order, then
- * the filter block: d_offsets/d_sizes = the BlockHandle (0/0 for an entry
- * that is not a usable handle), d_actual = computed CRC of contents + type
- * byte, d_status = LVKV_BLOCK_*. Asynchronous on `stream` and graph-capturable
- * (no host synchronisation; counts live in *d_report). Returns LVKV_OK when
- * the work was enqueued; the table's verdict is d_report->status. */
+ * (table/table.cc:38-79) with paranoid_checks + Table::ReadMeta (:81-124) +
+ * ReadBlock on every block (table/format.cc:69-160) would with
+ * verify_checksums: footer and magic, index and metaindex checksums and type
+ * bytes, then every data block the index lists and the filter block, all on
+ * the device in two launches (a per-table workgroup for the footer, index and
+ * metaindex CRCs, the filter lookup and the index parse, one entry per
+ * restart point as table_builder.cc:35 writes it; then one batched verify
+ * with the merge). filter_policy = FilterPolicy::Name() of the reader's
+ * Options (e.g. "leveldb.BuiltinBloomFilter2" for NewBloomFilterPolicy,
+ * util/bloom.cc): the filter block is the metaindex entry whose key is
+ * exactly "filter." + filter_policy (table.cc:100-102); NULL = no policy
+ * (Options::filter_policy == nullptr: no filter block, table.cc:82-84). Per-block outputs
+ * (arrays of `capacity` entries, device memory), in index order, then the
+ * filter block: d_offsets/d_sizes = the BlockHandle (0/0 for an entry that is
+ * not a readable handle), d_actual = computed CRC of contents + type byte (0
+ * when not computed), d_status = LVKV_BLOCK_*. index_status / meta_status are
+ * ReadBlock's verdicts on those two blocks whenever the footer decoded
+ * (LVKV_BLOCK_NOT_READ otherwise). Asynchronous on `stream` and
+ * graph-capturable (no host synchronisation; counts live in *d_report).
+ * Returns LVKV_OK when the work was enqueued (LVKV_ERR_INVALID for a policy
+ * name longer than LVKV_SST_MAX_POLICY_NAME); the table's verdict is
+ * d_report->status. */
 int lvkv_sst_verify_table_device(const void* d_file, uint64_t file_size,
                                  uint64_t* d_offsets, uint32_t* d_sizes,
                                  uint32_t* d_actual, uint8_t* d_status, size_t capacity,
-                                 lvkv_sst_report* d_report, void* stream);
+                                 const char* filter_policy, lvkv_sst_report* d_report,
+                                 void* stream);
 
 /* Many SSTables at once: compaction inputs (paranoid checks), a repair scan.
  * Table t is d_file[d_table_off[t], + d_table_size[t]) (device arrays). The
- * same four launches as one table serve all of them: footers, index and
- * metaindex CRCs (one workgroup each), index heads, a scan that packs every
- * table's entries into the shared per-block arrays (table t from
- * d_reports[t].first on), the entry parse, one batched verify and the merge.
- * d_offsets are offsets into d_file (table offset + BlockHandle offset). A
- * table whose entries do not fit in `capacity` gets LVKV_SST_CAPACITY (with
- * ndata set); so do the tables after it. Asynchronous; graph-capturable. */
+ * same two launches as one table serve all of them (one workgroup per
+ * table); table t's entries go to the shared per-block arrays from
+ * d_reports[t].first on, in table order. d_offsets are offsets into d_file
+ * (table offset + BlockHandle offset). A table whose entries do not fit in
+ * `capacity` gets LVKV_SST_CAPACITY (with ndata set); so do the tables after
+ * it. Asynchronous; graph-capturable. */
 int lvkv_sst_verify_tables_device(const void* d_file, const uint64_t* d_table_off,
                                   const uint64_t* d_table_size, size_t ntables,
                                   uint64_t* d_offsets, uint32_t* d_sizes, uint32_t* d_actual,
-                                  uint8_t* d_status, size_t capacity,
+                                  uint8_t* d_status, size_t capacity, const char* filter_policy,
                                   lvkv_sst_report* d_reports, void* stream);
 
 /* ---- WAL / MANIFEST verify, device-resident ----- */

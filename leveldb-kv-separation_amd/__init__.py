@@ -73,9 +73,11 @@ def _load() -> ctypes.CDLL:
     L.lvkv_crc32c_uniform_device.restype = i32
     L.lvkv_sst_verify_device.argtypes = [vp, vp, vp, vp, vp, sz, vp]
     L.lvkv_sst_verify_device.restype = i32
-    L.lvkv_sst_verify_table_device.argtypes = [vp, u64, vp, vp, vp, vp, sz, vp, vp]
+    L.lvkv_sst_verify_table_device.argtypes = [vp, u64, vp, vp, vp, vp, sz, ctypes.c_char_p,
+                                               vp, vp]
     L.lvkv_sst_verify_table_device.restype = i32
-    L.lvkv_sst_verify_tables_device.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, sz, vp, vp]
+    L.lvkv_sst_verify_tables_device.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, sz,
+                                                ctypes.c_char_p, vp, vp]
     L.lvkv_sst_verify_tables_device.restype = i32
     L.lvkv_sst_fill_trailers_device.argtypes = [vp, vp, vp, vp, sz, vp]
     L.lvkv_sst_fill_trailers_device.restype = i32
@@ -266,10 +268,8 @@ class SstReport(ctypes.Structure):
                 ("reserved0_", ctypes.c_uint8 * 2), ("first", ctypes.c_uint32),
                 ("index_offset", ctypes.c_uint64), ("index_size", ctypes.c_uint64),
                 ("meta_offset", ctypes.c_uint64), ("meta_size", ctypes.c_uint64),
-                ("filter_off_", ctypes.c_uint64), ("filter_size_", ctypes.c_uint32),
-                ("scratch_status_", ctypes.c_uint8 * 2), ("filter_status_", ctypes.c_uint8),
-                ("reserved1_", ctypes.c_uint8), ("scratch_crc_", ctypes.c_uint32 * 2),
-                ("total_", ctypes.c_uint32), ("reserved2_", ctypes.c_uint32)]
+                ("link_", ctypes.c_uint64), ("total_", ctypes.c_uint32),
+                ("reserved2_", ctypes.c_uint32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_
@@ -282,16 +282,26 @@ SST_STATUS = {0: "OK", 1: "file is too short to be an sstable",
               6: "index block type not readable here", 7: "bad index block contents",
               8: "capacity too small"}
 BLOCK_STATUS = {0: "OK", 1: "block checksum mismatch", 2: "truncated block read",
-                3: "bad block type", 4: "bad block handle", 5: "bad entry in block"}
+                3: "bad block type", 4: "bad block handle", 5: "bad entry in block",
+                6: "compressed block (no codec as built)", 7: "not read"}
+# FilterPolicy::Name() of leveldb::NewBloomFilterPolicy (util/bloom.cc)
+BLOOM_POLICY = "leveldb.BuiltinBloomFilter2"
 
 
-def sst_verify_table(file_buf, *, capacity: Optional[int] = None, stream=None):
+def _policy(filter_policy):
+    return None if filter_policy is None else filter_policy.encode()
+
+
+def sst_verify_table(file_buf, *, capacity: Optional[int] = None,
+                     filter_policy: Optional[str] = BLOOM_POLICY, stream=None):
     """Whole-SSTable verify on the device (lvkv_sst_verify_table_device):
     footer, index, metaindex, filter and every data block of the SST image
-    in `file_buf` (uint8 CUDA tensor). Returns (report dict, offsets int64,
-    sizes int32, actual int32, status uint8) — the per-block tensors cut to
-    report['nblocks'] entries (data blocks in index order, then the filter).
-    With capacity=None a first guess is retried once at the index's size."""
+    in `file_buf` (uint8 CUDA tensor). filter_policy: the reader's
+    FilterPolicy::Name() (None: no policy, no filter block). Returns (report
+    dict, offsets int64, sizes int32, actual int32, status uint8) — the
+    per-block tensors cut to report['nblocks'] entries (data blocks in index
+    order, then the filter). With capacity=None a first guess is retried once
+    at the index's size."""
     torch = _torch()
     dev = file_buf.device
     size = file_buf.numel()
@@ -306,7 +316,7 @@ def sst_verify_table(file_buf, *, capacity: Optional[int] = None, stream=None):
             rc = _lib.lvkv_sst_verify_table_device(
                 _dev_ptr(file_buf, "file_buf", (torch.uint8, torch.int8)), size,
                 _dev_ptr(off, "offsets"), _dev_ptr(sizes, "sizes"), _dev_ptr(actual, "actual"),
-                _dev_ptr(status, "status"), cap, _dev_ptr(rep, "report"),
+                _dev_ptr(status, "status"), cap, _policy(filter_policy), _dev_ptr(rep, "report"),
                 _stream_handle(stream, dev))
         _check("lvkv_sst_verify_table_device", rc)
         r = SstReport.from_buffer_copy(bytes(rep.cpu().numpy()))
@@ -318,9 +328,10 @@ def sst_verify_table(file_buf, *, capacity: Optional[int] = None, stream=None):
     return r.as_dict(), off[:n], sizes[:n], actual[:n], status[:n]
 
 
-def sst_verify_tables(file_buf, table_offsets, table_sizes, *, capacity=None, stream=None):
+def sst_verify_tables(file_buf, table_offsets, table_sizes, *, capacity=None,
+                      filter_policy: Optional[str] = BLOOM_POLICY, stream=None):
     """Many SST images in one device buffer (lvkv_sst_verify_tables_device):
-    four launches for all of them. Returns one (report dict, offsets, sizes,
+    two launches for all of them. Returns one (report dict, offsets, sizes,
     actual, status) per table as sst_verify_table would for that image alone,
     except that offsets are into file_buf. capacity (shared by all tables)
     defaults to file_buf.numel() // 2048 + 64 per table; a table that does
@@ -341,14 +352,14 @@ def sst_verify_tables(file_buf, table_offsets, table_sizes, *, capacity=None, st
         rc = _lib.lvkv_sst_verify_tables_device(
             _dev_ptr(file_buf, "file_buf", (torch.uint8, torch.int8)), _dev_ptr(toff, "toff"),
             _dev_ptr(tsz, "tsize"), T, _dev_ptr(o, "offsets"), _dev_ptr(sz, "sizes"),
-            _dev_ptr(act, "actual"), _dev_ptr(st, "status"), cap, _dev_ptr(reps, "reports"),
-            _stream_handle(stream, dev))
+            _dev_ptr(act, "actual"), _dev_ptr(st, "status"), cap, _policy(filter_policy),
+            _dev_ptr(reps, "reports"), _stream_handle(stream, dev))
     _check("lvkv_sst_verify_tables_device", rc)
     host = bytes(reps.cpu().numpy())
     out = []
     for t in range(T):
         r = SstReport.from_buffer_copy(host[t * rsz:(t + 1) * rsz])
-        f, n = r.first, (r.nblocks if r.status == 0 else 0)
+        f, n = r.first, r.nblocks
         out.append((r.as_dict(), o[f:f + n], sz[f:f + n], act[f:f + n], st[f:f + n]))
     return out
 

@@ -31,9 +31,12 @@ HOST_SOURCES = ["lvkv_tables.cpp", "lvkv_cpu_crc32c.cpp", "leveldb_crc32c_shim.c
 # HIP sources: kernels and the runtime-facing C-ABI.
 HIP_SOURCES = ["crc32c_kernel.hip", "crc32c_uniform.hip", "crc32c_compact.hip",
                "crc32c_ragged.hip", "lvkv_sst_table.hip", "lvkv_log_blocks.hip",
-               "lvkv_capi.cpp"]
+               "lvkv_capi.cpp", "lvkv_engine.cpp"]
+# Kernels of the AQL engine: compiled alone into a gfx950 code object that is
+# embedded in the library (.incbin) and loaded through the HSA loader.
+ENGINE_KERNELS = "lvkv_engine_kernels.hip"
 HEADERS = ["lvkv_kernel_args.h", "lvkv_tables.h", "crc32c_device_common.h",
-           "crc32c_uniform_common.h", "crc32c_compact_common.h"]
+           "crc32c_uniform_common.h", "crc32c_compact_common.h", "crc32c_burst.h"]
 
 
 def _run(cmd: list[str], verbose: bool) -> None:
@@ -50,7 +53,7 @@ def _newer(target: Path, deps: list[Path]) -> bool:
 
 
 def build_lib(verbose: bool = False, force: bool = False) -> Path:
-    deps = [CSRC / s for s in HOST_SOURCES + HIP_SOURCES + HEADERS]
+    deps = [CSRC / s for s in HOST_SOURCES + HIP_SOURCES + HEADERS + [ENGINE_KERNELS]]
     deps += sorted(INCLUDE.glob("*.h")) + [Path(__file__)]
     if not force and _newer(LIB, deps):
         return LIB
@@ -65,11 +68,24 @@ def build_lib(verbose: bool = False, force: bool = False) -> Path:
         obj = BUILD / (Path(src).stem + ".hip.o")
         cmds.append([HIPCC, f"--offload-arch={ARCH}", *common, "-c", CSRC / src, "-o", obj])
         objs.append(obj)
+    co = BUILD / "lvkv_engine.co"
+    cmds.append([HIPCC, f"--offload-arch={ARCH}", *common, "--cuda-device-only",
+                 "--no-gpu-bundle-output", "-c", CSRC / ENGINE_KERNELS, "-o", co])
     # translation units are independent: compile them concurrently
     with ThreadPoolExecutor(max_workers=min(len(cmds), os.cpu_count() or 1, 8)) as ex:
         list(ex.map(lambda c: _run(c, verbose), cmds))
+    asm = BUILD / "lvkv_engine_co.S"
+    asm.write_text(
+        "\t.section .rodata\n\t.balign 4096\n\t.globl lvkv_engine_co\n"
+        "\t.type lvkv_engine_co, @object\nlvkv_engine_co:\n"
+        f"\t.incbin \"{co}\"\n\t.globl lvkv_engine_co_end\nlvkv_engine_co_end:\n"
+        "\t.section .note.GNU-stack,\"\",@progbits\n")
+    co_obj = BUILD / "lvkv_engine_co.o"
+    _run(["gcc", "-c", asm, "-o", co_obj], verbose)
+    objs.append(co_obj)
     tmp = LIB.with_suffix(".so.tmp")
-    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp, "-lpthread"], verbose)
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp, "-lpthread",
+          "-L/opt/rocm/lib", "-lhsa-runtime64"], verbose)
     os.replace(tmp, LIB)
     return LIB
 

@@ -156,12 +156,15 @@ __device__ __forceinline__ void rag_store(const KernelArgs& a, uint32_t b, const
   if (a.mode == kModeSstTable) {
     // ReadBlock's order (format.cc:92-97, :104-158): the index parse status
     // first, then the checksum, then the type byte
-    a.out_crc[b] = crc;
     uint8_t st = a.out_status[b];
+    a.out_crc[b] = st == LVKV_BLOCK_OK ? crc : 0u;  // no CRC of an unreadable block
     if (st == LVKV_BLOCK_OK) {
+      const uint8_t type = *reinterpret_cast<const uint8_t*>(g.ptr() + g.len - 1);
       if (crc != g.expected)
         st = LVKV_BLOCK_CHECKSUM;
-      else if (*reinterpret_cast<const uint8_t*>(g.ptr() + g.len - 1) > 2)
+      else if (type == 1 || type == 2)  // snappy / zstd: absent in the as-built
+        st = LVKV_BLOCK_COMPRESSED;     // reference (port_stdcxx.h:108-118)
+      else if (type > 2)
         st = LVKV_BLOCK_BAD_TYPE;
       if (st != LVKV_BLOCK_OK) a.out_status[b] = st;
     }

@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -42,8 +43,8 @@ hipError_t launch_crc32c_compact(const UniformArgs& args, int cfg, int num_group
 hipError_t launch_sst_tables(const uint8_t* file, const uint64_t* toff, const uint64_t* tsize,
                              uint64_t single_size, uint32_t ntables, uint64_t* d_off,
                              uint32_t* d_size, uint32_t* d_actual, uint8_t* d_status,
-                             uint32_t capacity, lvkv_sst_report* reports,
-                             const KernelArgs& verify, const uint32_t* zpow,
+                             uint32_t capacity, lvkv_sst_report* reports, const FilterKey& fk,
+                             uint32_t gen, const KernelArgs& verify, const uint32_t* zpow,
                              const uint32_t* lane_cols, int groups, hipStream_t stream);
 hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_off,
                              uint32_t* actual, uint8_t* rec_status, uint32_t capacity,
@@ -163,6 +164,16 @@ DeviceCtx* current_ctx(int* rc) {
   return c.status == LVKV_OK ? &c : nullptr;
 }
 
+}  // namespace
+
+// The current device's tables (lvkv_engine.cpp shares them).
+uint32_t* device_tables(int* rc) {
+  DeviceCtx* c = current_ctx(rc);
+  return c != nullptr ? c->d_tables : nullptr;
+}
+
+namespace {
+
 UniformArgs uniform_args(const DeviceCtx& c, const KernelArgs& b) {
   UniformArgs u;
   memset(&u, 0, sizeof(u));
@@ -172,6 +183,7 @@ UniformArgs uniform_args(const DeviceCtx& c, const KernelArgs& b) {
   u.lane_tab = c.d_tables + kRowTabDwords;
   u.lane_cols = c.d_tables + kRowTabDwords + kLaneTabDwords;
   u.stamps = b.stamps;
+  u.zpow = c.d_tables + kZPowOffset;
   u.length = b.length;
   u.init = b.init;
   u.nblocks = b.nblocks;
@@ -242,6 +254,29 @@ int run_batch(KernelArgs a, size_t nblocks, hipStream_t stream) {
     done += n;
   }
   return LVKV_OK;
+}
+
+// "filter." + policy name (table.cc:100-101); false if the name is too long.
+bool filter_key(const char* policy, FilterKey* fk) {
+  memset(fk, 0, sizeof(*fk));
+  if (policy == nullptr) return true;  // no filter policy: no filter block
+  const size_t n = strlen(policy);
+  if (n > LVKV_SST_MAX_POLICY_NAME) return false;
+  memcpy(fk->key, "filter.", 7);
+  memcpy(fk->key + 7, policy, n);
+  fk->len = static_cast<uint32_t>(7 + n);
+  return true;
+}
+
+// Per-call tag of the multi-table placement words (never 0: fresh report
+// memory is often zeroed).
+uint32_t next_sst_generation() {
+  static std::atomic<uint32_t> g{0};
+  uint32_t v;
+  do {
+    v = g.fetch_add(1, std::memory_order_relaxed) + 1;
+  } while (v == 0);
+  return v;
 }
 
 KernelArgs blank_args() {
@@ -417,9 +452,11 @@ int lvkv_sst_verify_device(const void* d_file, const uint64_t* d_offsets,
 int lvkv_sst_verify_table_device(const void* d_file, uint64_t file_size,
                                  uint64_t* d_offsets, uint32_t* d_sizes,
                                  uint32_t* d_actual, uint8_t* d_status, size_t capacity,
-                                 lvkv_sst_report* d_report, void* stream) {
+                                 const char* filter_policy, lvkv_sst_report* d_report,
+                                 void* stream) {
+  FilterKey fk;
   if (!d_file || !d_offsets || !d_sizes || !d_actual || !d_status || !d_report ||
-      capacity == 0 || capacity > kMaxBlocksPerLaunch)
+      capacity == 0 || capacity > kMaxBlocksPerLaunch || !filter_key(filter_policy, &fk))
     return LVKV_ERR_INVALID;
   int rc = LVKV_OK;
   DeviceCtx* c = current_ctx(&rc);
@@ -430,7 +467,7 @@ int lvkv_sst_verify_table_device(const void* d_file, uint64_t file_size,
   a.mode = kModeSstVerify;
   const hipError_t e = launch_sst_tables(
       static_cast<const uint8_t*>(d_file), nullptr, nullptr, file_size, 1, d_offsets, d_sizes,
-      d_actual, d_status, static_cast<uint32_t>(capacity), d_report, a,
+      d_actual, d_status, static_cast<uint32_t>(capacity), d_report, fk, next_sst_generation(), a,
       c->d_tables + kZPowOffset, c->d_tables + kRowTabDwords + kLaneTabDwords, c->groups,
       static_cast<hipStream_t>(stream));
   return e == hipSuccess ? LVKV_OK : hip_fail(e);
@@ -439,12 +476,13 @@ int lvkv_sst_verify_table_device(const void* d_file, uint64_t file_size,
 int lvkv_sst_verify_tables_device(const void* d_file, const uint64_t* d_table_off,
                                   const uint64_t* d_table_size, size_t ntables,
                                   uint64_t* d_offsets, uint32_t* d_sizes, uint32_t* d_actual,
-                                  uint8_t* d_status, size_t capacity,
+                                  uint8_t* d_status, size_t capacity, const char* filter_policy,
                                   lvkv_sst_report* d_reports, void* stream) {
   if (ntables == 0) return LVKV_OK;
+  FilterKey fk;
   if (!d_file || !d_table_off || !d_table_size || !d_offsets || !d_sizes || !d_actual ||
       !d_status || !d_reports || capacity == 0 || capacity > kMaxBlocksPerLaunch ||
-      ntables > (size_t{1} << 20))
+      ntables > (size_t{1} << 20) || !filter_key(filter_policy, &fk))
     return LVKV_ERR_INVALID;
   int rc = LVKV_OK;
   DeviceCtx* c = current_ctx(&rc);
@@ -456,7 +494,8 @@ int lvkv_sst_verify_tables_device(const void* d_file, const uint64_t* d_table_of
   const hipError_t e = launch_sst_tables(
       static_cast<const uint8_t*>(d_file), d_table_off, d_table_size, 0,
       static_cast<uint32_t>(ntables), d_offsets, d_sizes, d_actual, d_status,
-      static_cast<uint32_t>(capacity), d_reports, a, c->d_tables + kZPowOffset,
+      static_cast<uint32_t>(capacity), d_reports, fk, next_sst_generation(), a,
+      c->d_tables + kZPowOffset,
       c->d_tables + kRowTabDwords + kLaneTabDwords, c->groups, static_cast<hipStream_t>(stream));
   return e == hipSuccess ? LVKV_OK : hip_fail(e);
 }

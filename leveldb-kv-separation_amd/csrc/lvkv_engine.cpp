@@ -1,0 +1,579 @@
+// The AQL engine: a per-device hardware queue that the batch kernels are
+// dispatched into directly (include/lvkv_crc32c.h, lvkv_engine_*).
+//
+// Why: a hipLaunchKernel costs 2.7-7 us of host time on this stack (measured,
+// tools/probe), about as long as the 10k x 4 KiB kernel itself (7-9 us), so a
+// checksum service that launches one batch per call through HIP is paced by
+// the host, and HIP on gfx9 offers no launch that may overlap the previous
+// kernel of its stream (hipExtAnyOrderLaunch is unsupported there). The
+// engine writes 64-byte AQL kernel-dispatch packets into its own user-mode
+// queue (HSA runtime) and rings the doorbell: well under a microsecond per
+// batch, and packets are issued without the barrier bit, so the packet
+// processor starts dispatching batch i+1's workgroups while batch i's are
+// still running (independent batches, distinct output arrays).
+//
+// The kernels come from a gfx950 code object embedded in this library
+// (lvkv_engine_kernels.hip, assembled in by lvkv_engine_co.S) and loaded with
+// the HSA loader. They read no hidden kernel arguments, so the kernarg
+// segment is exactly UniformArgs.
+//
+// Ordering: engine dispatches are not ordered with HIP streams. Inputs must be
+// complete before a submit (synchronize the producing stream), results are
+// complete after lvkv_engine_wait (system-scope release at every kernel end).
+// Kernarg slots and completion signals form a ring of kSlots; a submit that
+// would reuse a slot first waits for the dispatch that last used it.
+#include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+
+#include "lvkv_crc32c.h"
+#include "lvkv_kernel_args.h"
+#include "lvkv_tables.h"
+
+extern "C" const unsigned char lvkv_engine_co[];
+extern "C" const unsigned char lvkv_engine_co_end[];
+
+namespace lvkv {
+
+uint32_t* device_tables(int* rc);  // lvkv_capi.cpp: per-device tables (d_tables)
+
+namespace {
+
+constexpr uint32_t kSlots = 1024;    // kernarg slots (one per dispatch in flight)
+constexpr uint32_t kSigSlots = 64;   // per-dispatch signals (option 5 only)
+constexpr uint32_t kSlotBytes = 256;
+constexpr uint32_t kQueuePackets = 1024;
+constexpr int kMaxQueues = 4;  // hardware queues per engine (dispatch i -> queue i % nq)
+
+struct EngineKernel {
+  uint64_t object = 0;
+  uint32_t kernarg_size = 0, group_size = 0, private_size = 0;
+  uint32_t waves = 8, chains = 3, per_cu = 2;  // shape: workgroups per CU per dispatch
+};
+
+// The engine's kernels (lvkv_engine_kernels.hip): name, shape, and the
+// timestamp build of the same schedule (probes).
+struct KernelSpec {
+  const char* name;
+  const char* stamps;
+  uint32_t waves, chains, per_cu;
+};
+constexpr KernelSpec kSpecs[] = {
+    {"lvkv_engine_uniform_burst.kd", "lvkv_engine_uniform_burst_stamps.kd", 8, 3, 2},
+    {"lvkv_engine_uniform_burst_rows.kd", "lvkv_engine_uniform_burst_stamps.kd", 8, 3, 2},
+    {"lvkv_engine_uniform_half.kd", "lvkv_engine_uniform_half_stamps.kd", 8, 5, 1},
+    {"lvkv_engine_uniform_half_late.kd", "lvkv_engine_uniform_half_late_stamps.kd", 8, 5, 1},
+    {"lvkv_engine_uniform_burst_late.kd", "lvkv_engine_uniform_burst_stamps.kd", 8, 3, 2},
+};
+constexpr int kNumSpecs = static_cast<int>(sizeof(kSpecs) / sizeof(kSpecs[0]));
+
+struct AgentMatch {
+  uint32_t domain, bdfid;
+  hsa_agent_t agent;
+  bool found;
+};
+
+hsa_status_t match_agent(hsa_agent_t agent, void* data) {
+  AgentMatch* m = static_cast<AgentMatch*>(data);
+  hsa_device_type_t type;
+  if (hsa_agent_get_info(agent, HSA_AGENT_INFO_DEVICE, &type) != HSA_STATUS_SUCCESS ||
+      type != HSA_DEVICE_TYPE_GPU)
+    return HSA_STATUS_SUCCESS;
+  uint32_t bdf = 0, dom = 0;
+  if (hsa_agent_get_info(agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_BDFID), &bdf) !=
+          HSA_STATUS_SUCCESS ||
+      hsa_agent_get_info(agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DOMAIN), &dom) !=
+          HSA_STATUS_SUCCESS)
+    return HSA_STATUS_SUCCESS;
+  if (bdf == m->bdfid && dom == m->domain) {
+    m->agent = agent;
+    m->found = true;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t find_kernarg_region(hsa_region_t region, void* data) {
+  hsa_region_segment_t seg;
+  if (hsa_region_get_info(region, HSA_REGION_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS ||
+      seg != HSA_REGION_SEGMENT_GLOBAL)
+    return HSA_STATUS_SUCCESS;
+  uint32_t flags = 0;
+  if (hsa_region_get_info(region, HSA_REGION_INFO_GLOBAL_FLAGS, &flags) != HSA_STATUS_SUCCESS)
+    return HSA_STATUS_SUCCESS;
+  if (flags & HSA_REGION_GLOBAL_FLAG_KERNARG) {
+    *static_cast<hsa_region_t*>(data) = region;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+struct PoolFind {
+  hsa_amd_memory_pool_t pool;
+  bool found;
+};
+
+// The device's coarse-grained VRAM pool (kernargs live there when the host
+// can write it through the PCIe BAR, as HIP's own device kernargs do).
+hsa_status_t find_vram_pool(hsa_amd_memory_pool_t pool, void* data) {
+  hsa_amd_segment_t seg;
+  uint32_t flags = 0;
+  bool alloc = false;
+  if (hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) !=
+          HSA_STATUS_SUCCESS ||
+      seg != HSA_AMD_SEGMENT_GLOBAL)
+    return HSA_STATUS_SUCCESS;
+  if (hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags) !=
+          HSA_STATUS_SUCCESS ||
+      !(flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED))
+    return HSA_STATUS_SUCCESS;
+  if (hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED,
+                                   &alloc) != HSA_STATUS_SUCCESS ||
+      !alloc)
+    return HSA_STATUS_SUCCESS;
+  PoolFind* f = static_cast<PoolFind*>(data);
+  f->pool = pool;
+  f->found = true;
+  return HSA_STATUS_INFO_BREAK;
+}
+
+hsa_status_t find_cpu(hsa_agent_t agent, void* data) {
+  hsa_device_type_t type;
+  if (hsa_agent_get_info(agent, HSA_AGENT_INFO_DEVICE, &type) == HSA_STATUS_SUCCESS &&
+      type == HSA_DEVICE_TYPE_CPU) {
+    *static_cast<hsa_agent_t*>(data) = agent;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+std::once_flag g_hsa_once;
+hsa_status_t g_hsa_status = HSA_STATUS_ERROR_NOT_INITIALIZED;
+
+}  // namespace
+
+struct Engine {
+  int device = -1;
+  hsa_agent_t agent{};
+  hsa_queue_t* queues[kMaxQueues] = {};
+  int nq = 2;           // queues in use
+  int cur = 0;          // queue of the packet being written
+  hsa_executable_t exe{};
+  hsa_code_object_reader_t reader{};
+  bool exe_ok = false, reader_ok = false;
+  EngineKernel kern[kNumSpecs], kern_stamps[kNumSpecs];
+  uint64_t* stamps = nullptr;  // probes: 8 u64 per wave, one area per dispatch
+  uint64_t stamp_next = 0, stamp_areas = 0;
+  uint8_t* kernarg = nullptr;      // system-memory ring (kernarg region)
+  uint8_t* kernarg_dev = nullptr;  // VRAM ring written through the BAR
+  uint32_t* hdp_flush = nullptr;   // HDP_MEM_FLUSH_CNTL: makes BAR writes visible
+  int use_dev_kernarg = 0;
+  int acquire_scope = HSA_FENCE_SCOPE_AGENT, release_scope = HSA_FENCE_SCOPE_SYSTEM;
+  hsa_signal_t sig[kSigSlots];  // per-dispatch completion (signal_mode 1)
+  uint32_t nsig = 0;
+  hsa_signal_t fence_sig{};      // completion of the barrier-AND fence packets (one per queue)
+  bool fence_ok = false;
+  int signal_mode = 0;           // 0: fences only; 1: a signal per dispatch
+  int hdp_readback = 1;
+  uint64_t next = 0;    // dispatches submitted
+  uint64_t fenced = 0;  // every dispatch before this one is known complete
+  int cus = 0;
+  int variant = 0;
+  uint32_t* d_tables = nullptr;
+  uint32_t zcol[32];
+  std::mutex mu;
+  volatile int queue_error = 0;
+};
+
+namespace {
+
+void queue_error_cb(hsa_status_t status, hsa_queue_t*, void* data) {
+  static_cast<Engine*>(data)->queue_error = static_cast<int>(status);
+}
+
+int load_kernel(Engine& e, const char* name, EngineKernel* k) {
+  hsa_executable_symbol_t sym;
+  if (hsa_executable_get_symbol_by_name(e.exe, name, &e.agent, &sym) != HSA_STATUS_SUCCESS)
+    return LVKV_ERR_HIP;
+  if (hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &k->object) !=
+          HSA_STATUS_SUCCESS ||
+      hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE,
+                                     &k->kernarg_size) != HSA_STATUS_SUCCESS ||
+      hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE,
+                                     &k->group_size) != HSA_STATUS_SUCCESS ||
+      hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE,
+                                     &k->private_size) != HSA_STATUS_SUCCESS)
+    return LVKV_ERR_HIP;
+  // The kernarg segment must be exactly the argument struct: no hidden
+  // arguments the engine would have to fill.
+  if (k->kernarg_size != sizeof(UniformArgs) || k->kernarg_size > kSlotBytes)
+    return LVKV_ERR_HIP;
+  return LVKV_OK;
+}
+
+void destroy(Engine* e) {
+  for (hsa_queue_t* q : e->queues)
+    if (q) hsa_queue_destroy(q);
+  for (uint32_t i = 0; i < e->nsig; ++i) hsa_signal_destroy(e->sig[i]);
+  if (e->fence_ok) hsa_signal_destroy(e->fence_sig);
+  if (e->kernarg) hsa_memory_free(e->kernarg);
+  if (e->kernarg_dev) hsa_amd_memory_pool_free(e->kernarg_dev);
+  if (e->exe_ok) hsa_executable_destroy(e->exe);
+  if (e->reader_ok) hsa_code_object_reader_destroy(e->reader);
+  delete e;
+}
+
+int create(int device, Engine** out) {
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return LVKV_ERR_NO_DEVICE;
+  if (device < 0 || device >= ndev) return LVKV_ERR_INVALID;
+  std::call_once(g_hsa_once, [] { g_hsa_status = hsa_init(); });
+  if (g_hsa_status != HSA_STATUS_SUCCESS) return LVKV_ERR_NO_DEVICE;
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) return LVKV_ERR_HIP;
+  unsigned dom = 0, b = 0, d = 0, f = 0;
+  if (sscanf(bus, "%x:%x:%x.%x", &dom, &b, &d, &f) != 4) return LVKV_ERR_HIP;
+  AgentMatch m{dom, (b << 8) | (d << 3) | f, {}, false};
+  hsa_iterate_agents(match_agent, &m);
+  if (!m.found) return LVKV_ERR_NO_DEVICE;
+
+  // The per-device tables of the HIP path (lane columns, zpow) double as the
+  // engine's: allocate them on that device.
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess) return LVKV_ERR_HIP;
+  if (prev != device && hipSetDevice(device) != hipSuccess) return LVKV_ERR_HIP;
+  int rc = LVKV_OK;
+  uint32_t* tables = device_tables(&rc);
+  int ncu = 0;
+  if (rc == LVKV_OK &&
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    rc = LVKV_ERR_HIP;
+  if (prev != device) (void)hipSetDevice(prev);
+  if (rc != LVKV_OK) return rc;
+
+  Engine* e = new Engine();
+  e->device = device;
+  e->agent = m.agent;
+  e->d_tables = tables;
+  e->cus = ncu;
+  const Gf2Op z = gf2_zero_advance(kRowBytes);
+  memcpy(e->zcol, z.col, sizeof(e->zcol));
+
+  const size_t co_size = static_cast<size_t>(lvkv_engine_co_end - lvkv_engine_co);
+  bool ok =
+      hsa_code_object_reader_create_from_memory(lvkv_engine_co, co_size, &e->reader) ==
+      HSA_STATUS_SUCCESS;
+  e->reader_ok = ok;
+  ok = ok && hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT,
+                                       nullptr, &e->exe) == HSA_STATUS_SUCCESS;
+  e->exe_ok = ok;
+  ok = ok && hsa_executable_load_agent_code_object(e->exe, e->agent, e->reader, nullptr,
+                                                   nullptr) == HSA_STATUS_SUCCESS;
+  ok = ok && hsa_executable_freeze(e->exe, nullptr) == HSA_STATUS_SUCCESS;
+  for (int i = 0; ok && i < kNumSpecs; ++i) {
+    ok = load_kernel(*e, kSpecs[i].name, &e->kern[i]) == LVKV_OK &&
+         load_kernel(*e, kSpecs[i].stamps, &e->kern_stamps[i]) == LVKV_OK;
+    for (EngineKernel* k : {&e->kern[i], &e->kern_stamps[i]}) {
+      k->waves = kSpecs[i].waves;
+      k->chains = kSpecs[i].chains;
+      k->per_cu = kSpecs[i].per_cu;
+    }
+  }
+  hsa_region_t karg{};
+  karg.handle = 0;
+  ok = ok && hsa_agent_iterate_regions(e->agent, find_kernarg_region, &karg) !=
+                 HSA_STATUS_ERROR;
+  ok = ok && karg.handle != 0;
+  ok = ok && hsa_memory_allocate(karg, kSlots * kSlotBytes,
+                                 reinterpret_cast<void**>(&e->kernarg)) == HSA_STATUS_SUCCESS;
+  // VRAM kernargs: only where the host may map them (large BAR) and the HDP
+  // flush register is exposed; otherwise the system-memory ring is used.
+  if (ok) {
+    PoolFind pf{{}, false};
+    hsa_agent_t cpu{};
+    hsa_amd_hdp_flush_t hdp{nullptr, nullptr};
+    hsa_amd_agent_iterate_memory_pools(e->agent, find_vram_pool, &pf);
+    hsa_iterate_agents(find_cpu, &cpu);
+    void* p = nullptr;
+    if (pf.found && cpu.handle != 0 &&
+        hsa_agent_get_info(e->agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_HDP_FLUSH),
+                           &hdp) == HSA_STATUS_SUCCESS &&
+        hdp.HDP_MEM_FLUSH_CNTL != nullptr &&
+        hsa_amd_memory_pool_allocate(pf.pool, kSlots * kSlotBytes, 0, &p) == HSA_STATUS_SUCCESS) {
+      if (hsa_amd_agents_allow_access(1, &cpu, nullptr, p) == HSA_STATUS_SUCCESS) {
+        e->kernarg_dev = static_cast<uint8_t*>(p);
+        e->hdp_flush = hdp.HDP_MEM_FLUSH_CNTL;
+        e->use_dev_kernarg = 1;
+      } else {
+        hsa_amd_memory_pool_free(p);
+      }
+    }
+  }
+  for (uint32_t i = 0; ok && i < kSigSlots; ++i) {
+    ok = hsa_signal_create(0, 0, nullptr, &e->sig[i]) == HSA_STATUS_SUCCESS;
+    if (ok) e->nsig = i + 1;
+  }
+  ok = ok && hsa_signal_create(0, 0, nullptr, &e->fence_sig) == HSA_STATUS_SUCCESS;
+  e->fence_ok = ok;
+  for (int i = 0; ok && i < kMaxQueues; ++i)
+    ok = hsa_queue_create(e->agent, kQueuePackets, HSA_QUEUE_TYPE_MULTI, queue_error_cb, e,
+                          UINT32_MAX, UINT32_MAX, &e->queues[i]) == HSA_STATUS_SUCCESS;
+  if (!ok) {
+    destroy(e);
+    return LVKV_ERR_HIP;
+  }
+  *out = e;
+  return LVKV_OK;
+}
+
+// Next free packet of queue e.cur (single producer: the caller holds e.mu).
+void* packet_slot(Engine& e, uint64_t* idx) {
+  hsa_queue_t* q = e.queues[e.cur];
+  *idx = hsa_queue_add_write_index_screlease(q, 1);
+  while (*idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {
+  }
+  return static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address) + (*idx & (q->size - 1));
+}
+
+void publish(Engine& e, void* p, uint16_t header, uint16_t setup, uint64_t idx) {
+  __atomic_store_n(static_cast<uint32_t*>(p), header | (static_cast<uint32_t>(setup) << 16),
+                   __ATOMIC_RELEASE);
+  hsa_signal_store_screlease(e.queues[e.cur]->doorbell_signal,
+                             static_cast<hsa_signal_value_t>(idx));
+}
+
+// A barrier-AND packet with the barrier bit on every queue in use: each
+// completes after every earlier packet of its queue has completed, and its
+// system-scope release makes their results visible to the host. Caller holds
+// e.mu; returns the dispatch count covered. The caller then waits for
+// fence_sig < 1 (each packet decrements it once).
+void submit_fence_one(Engine& e);
+
+uint64_t submit_fence(Engine& e) {
+  hsa_signal_store_relaxed(e.fence_sig, e.nq);
+  const int keep = e.cur;
+  for (int q = 0; q < e.nq; ++q) {
+    e.cur = q;
+    submit_fence_one(e);
+  }
+  e.cur = keep;
+  return e.next;
+}
+
+void submit_fence_one(Engine& e) {
+  uint64_t idx;
+  hsa_barrier_and_packet_t* p = static_cast<hsa_barrier_and_packet_t*>(packet_slot(e, &idx));
+  p->reserved0 = 0;
+  p->reserved1 = 0;
+  for (int i = 0; i < 5; ++i) p->dep_signal[i].handle = 0;
+  p->reserved2 = 0;
+  p->completion_signal = e.fence_sig;
+  const uint16_t header =
+      static_cast<uint16_t>((HSA_PACKET_TYPE_BARRIER_AND << HSA_PACKET_HEADER_TYPE) |
+                            (1 << HSA_PACKET_HEADER_BARRIER) |
+                            (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                            (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+  publish(e, p, header, 0, idx);
+}
+
+void wait_fence(Engine& e) {
+  hsa_signal_wait_scacquire(e.fence_sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+                            HSA_WAIT_STATE_ACTIVE);
+}
+
+// One kernel-dispatch packet; the caller holds e.mu.
+int dispatch(Engine& e, const EngineKernel& k, const UniformArgs& args, uint32_t groups,
+             uint32_t wg, bool barrier) {
+  if (e.queue_error) return LVKV_ERR_HIP;
+  const uint64_t n = e.next;
+  e.cur = static_cast<int>(n % static_cast<uint64_t>(e.nq));
+  // Kernarg slot n % kSlots was last used by dispatch n - kSlots: fence if
+  // that one is not known complete.
+  if (n - e.fenced >= kSlots) {
+    e.fenced = submit_fence(e);
+    wait_fence(e);
+  }
+  hsa_signal_t done{};
+  if (e.signal_mode) {
+    const uint32_t s = static_cast<uint32_t>(n % kSigSlots);
+    if (n >= kSigSlots)
+      hsa_signal_wait_scacquire(e.sig[s], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+                                HSA_WAIT_STATE_ACTIVE);
+    hsa_signal_store_relaxed(e.sig[s], 1);
+    done = e.sig[s];
+  }
+  const uint32_t slot = static_cast<uint32_t>(n % kSlots);
+  uint8_t* ka = (e.use_dev_kernarg ? e.kernarg_dev : e.kernarg) +
+                static_cast<size_t>(slot) * kSlotBytes;
+  memcpy(ka, &args, sizeof(args));
+  if (e.use_dev_kernarg) {
+    // BAR writes are write-combined and may sit in the HDP write cache: fence
+    // them, flush the HDP (and read the register back) before the packet.
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    __builtin_ia32_sfence();
+    *reinterpret_cast<volatile uint32_t*>(e.hdp_flush) = 1u;
+    if (e.hdp_readback) (void)*reinterpret_cast<volatile uint32_t*>(e.hdp_flush);
+  }
+  uint64_t idx;
+  hsa_kernel_dispatch_packet_t* p = static_cast<hsa_kernel_dispatch_packet_t*>(packet_slot(e, &idx));
+  p->workgroup_size_x = static_cast<uint16_t>(wg);
+  p->workgroup_size_y = 1;
+  p->workgroup_size_z = 1;
+  p->reserved0 = 0;
+  p->grid_size_x = groups * wg;
+  p->grid_size_y = 1;
+  p->grid_size_z = 1;
+  p->private_segment_size = k.private_size;
+  p->group_segment_size = k.group_size;
+  p->kernel_object = k.object;
+  p->kernarg_address = ka;
+  p->reserved2 = 0;
+  p->completion_signal = done;
+  // Acquire at agent scope (invalidates the scalar cache the kernargs are
+  // read through); release at the configured scope (the fence packet of
+  // lvkv_engine_wait releases at system scope in any case).
+  const uint16_t header =
+      static_cast<uint16_t>((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                            ((barrier ? 1 : 0) << HSA_PACKET_HEADER_BARRIER) |
+                            (e.acquire_scope << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                            (e.release_scope << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+  publish(e, p, header, 1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS, idx);
+  e.next = n + 1;
+  return LVKV_OK;
+}
+
+}  // namespace
+}  // namespace lvkv
+
+using namespace lvkv;
+
+extern "C" {
+
+int lvkv_engine_create(int device, lvkv_engine** out) {
+  if (out == nullptr) return LVKV_ERR_INVALID;
+  Engine* e = nullptr;
+  const int rc = create(device, &e);
+  *out = reinterpret_cast<lvkv_engine*>(e);
+  return rc;
+}
+
+void lvkv_engine_destroy(lvkv_engine* eng) {
+  if (eng == nullptr) return;
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  (void)lvkv_engine_wait(eng);
+  destroy(e);
+}
+
+int lvkv_engine_crc32c_uniform(lvkv_engine* eng, const void* d_base, uint64_t stride,
+                               uint32_t length, uint32_t init, uint32_t* d_out, size_t nblocks,
+                               uint32_t flags) {
+  if (eng == nullptr) return LVKV_ERR_INVALID;
+  if (nblocks == 0) return LVKV_OK;
+  if (!d_base || !d_out || length < 4 || length > kRowsPerChunk * kRowBytes || stride % 4 != 0 ||
+      (reinterpret_cast<uintptr_t>(d_base) + length) % 4 != 0)
+    return LVKV_ERR_INVALID;
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  std::lock_guard<std::mutex> lk(e->mu);
+  const EngineKernel& k = e->stamps ? e->kern_stamps[e->variant] : e->kern[e->variant];
+  const uint64_t groups = static_cast<uint64_t>(e->cus) * k.per_cu;
+  const uint64_t cap = groups * k.waves * k.chains;
+  // Batches beyond one dispatch's capacity go out as several dispatches of
+  // equal size (all without the barrier bit, except the first if ordered).
+  const uint64_t nd = (nblocks + cap - 1) / cap;
+  const uint64_t per = nblocks / nd, extra = nblocks % nd;
+  uint64_t done = 0;
+  for (uint64_t i = 0; i < nd; ++i) {
+    const uint64_t n = per + (i < extra ? 1 : 0);
+    UniformArgs a;
+    memset(&a, 0, sizeof(a));
+    a.base = static_cast<const uint8_t*>(d_base) + done * stride;
+    a.stride = stride;
+    a.out = d_out + done;
+    a.lane_tab = e->d_tables + kRowTabDwords;
+    a.lane_cols = e->d_tables + kRowTabDwords + kLaneTabDwords;
+    a.zpow = e->d_tables + kZPowOffset;
+    a.length = length;
+    a.init = init;
+    a.nblocks = static_cast<uint32_t>(n);
+    a.mask = (flags & LVKV_FLAG_MASK) ? 1u : 0u;
+    // at least 3 blocks per workgroup (as the HIP path)
+    a.ngroups = static_cast<uint32_t>(std::min<uint64_t>(groups, (n + 2) / 3));
+    memcpy(a.zcol, e->zcol, sizeof(a.zcol));
+    if (e->stamps) {
+      const uint64_t per = groups * k.waves * 8;
+      a.stamps = e->stamps + (e->stamp_next++ % e->stamp_areas) * per;
+    }
+    const int rc =
+        dispatch(*e, k, a, a.ngroups, 64 * k.waves, (flags & LVKV_FLAG_ORDERED) && i == 0);
+    if (rc != LVKV_OK) return rc;
+    done += n;
+  }
+  return LVKV_OK;
+}
+
+int lvkv_engine_wait(lvkv_engine* eng) {
+  if (eng == nullptr) return LVKV_ERR_INVALID;
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (e->fenced != e->next) {
+    const uint64_t covered = submit_fence(*e);
+    wait_fence(*e);
+    e->fenced = covered;
+  }
+  return e->queue_error ? LVKV_ERR_HIP : LVKV_OK;
+}
+
+int lvkv_engine_set_stamps(lvkv_engine* eng, uint64_t* d_stamps, uint64_t areas) {
+  if (eng == nullptr || (d_stamps != nullptr && areas == 0)) return LVKV_ERR_INVALID;
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  (void)lvkv_engine_wait(eng);
+  std::lock_guard<std::mutex> lk(e->mu);
+  e->stamps = d_stamps;
+  e->stamp_areas = areas;
+  e->stamp_next = 0;
+  return LVKV_OK;
+}
+
+int lvkv_engine_set_option(lvkv_engine* eng, int option, int value) {
+  if (eng == nullptr) return LVKV_ERR_INVALID;
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  (void)lvkv_engine_wait(eng);
+  std::lock_guard<std::mutex> lk(e->mu);
+  switch (option) {
+    case 0:
+      if (value < 0 || value >= kNumSpecs) return LVKV_ERR_INVALID;
+      e->variant = value;
+      return LVKV_OK;
+    case 1:
+      if (value && e->kernarg_dev == nullptr) return LVKV_ERR_INVALID;
+      e->use_dev_kernarg = value ? 1 : 0;
+      return LVKV_OK;
+    case 2:
+    case 3:
+      if (value < HSA_FENCE_SCOPE_NONE || value > HSA_FENCE_SCOPE_SYSTEM) return LVKV_ERR_INVALID;
+      (option == 2 ? e->acquire_scope : e->release_scope) = value;
+      return LVKV_OK;
+    case 4:
+      return e->use_dev_kernarg;
+    case 5:
+      e->signal_mode = value ? 1 : 0;
+      return LVKV_OK;
+    case 6:
+      e->hdp_readback = value ? 1 : 0;
+      return LVKV_OK;
+    case 7:
+      if (value < 1 || value > kMaxQueues) return LVKV_ERR_INVALID;
+      e->nq = value;
+      return LVKV_OK;
+  }
+  return LVKV_ERR_INVALID;
+}
+
+}  // extern "C"

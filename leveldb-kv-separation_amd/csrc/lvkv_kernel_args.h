@@ -18,6 +18,8 @@
 
 #include <stdint.h>
 
+#include "lvkv_crc32c.h"
+
 namespace lvkv {
 
 constexpr int kWaveLanes = 64;
@@ -93,6 +95,14 @@ struct KernelArgs {
                               //   block counts per workgroup
 };
 
+// "filter." + FilterPolicy::Name() (table/table.cc:100-101), the metaindex
+// key the whole-SSTable verify looks for; len 0: no filter policy.
+constexpr uint32_t kMaxFilterKey = 7 + LVKV_SST_MAX_POLICY_NAME;
+struct FilterKey {
+  uint32_t len;
+  uint8_t key[kMaxFilterKey + 1];
+};
+
 // Arguments of the uniform-layout kernel (crc32c_uniform.hip): nblocks
 // blocks of `length` bytes at base + i*stride, every block END 4-byte aligned.
 struct UniformArgs {
@@ -103,10 +113,12 @@ struct UniformArgs {
   const uint32_t* lane_cols;  // kLaneColDwords (compact kernel generates the
                               // lane tables from these)
   uint64_t* stamps;           // probe builds only
+  const uint32_t* zpow;       // kZPowDwords (Z_{2^j} byte tables)
   uint32_t length;            // >= 4
   uint32_t init;
   uint32_t nblocks;
   uint32_t mask;
+  uint32_t ngroups;           // workgroups of the launch (engine dispatches)
   uint32_t zcol[32];          // zcol[k] = Z_256(1 << k): the row tables are
                               // generated in-kernel from these columns
 };

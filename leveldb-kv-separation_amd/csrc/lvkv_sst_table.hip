@@ -1,35 +1,50 @@
 // Whole-SSTable verify on the device, for one table or
-// many at once: the footer, index and metaindex walk of Table::Open /
-// Table::ReadMeta (table/table.cc:38-105) and ReadBlock's checks
-// (table/format.cc:69-160) for every block, as four launches on one stream
-// whatever the number of tables, with no host round trip:
+// many at once, as TWO launches on one stream whatever the number of tables,
+// with no host round trip:
 //
-//   1. sst_open_kernel           two 1024-thread workgroups per table: the
-//                                footer (format.cc:43-67: size, magic, the
-//                                two BlockHandles, range checks), then the
-//                                index resp. metaindex CRC, 16 KiB segments
-//                                over the waves (workgroup_crc)
-//   2. sst_head_kernel           one wave per table: index checksum verdict,
-//                                type byte, restart array (block.cc:25-39),
-//                                the "filter." handle in the metaindex
-//                                (table.cc:95-104), entry count; the last
-//                                wave packs the tables' entries into the
-//                                shared arrays (first, capacity)
-//   3. sst_entry_kernel          one lane per entry of every table: the index
-//                                is written with block_restart_interval = 1
-//                                (table_builder.cc:35, :90), so restart point
-//                                i IS entry i and the entries decode in
-//                                parallel (DecodeEntry, block.cc:55-75;
-//                                BlockHandle varints, format.cc:24-30)
-//   4. crc32c_ragged_kernel      SST-table mode over all entries (count read
-//                                on the device): the CRC, then stored trailer
-//                                vs computed CRC, type byte and parse status
-//                                -> LVKV_BLOCK_*, per-table nbad / first_bad
-//                                (format.cc:92-97, :104-158)
+//   1. sst_table_kernel     one 1024-thread workgroup per table does what
+//                           Table::Open + Table::ReadMeta + the index walk do
+//                           (table/table.cc:38-124, table/format.cc:24-160,
+//                           table/block.cc:25-75), in LDS where it can:
+//                             * the footer (format.cc:43-67): size, magic, the
+//                               two BlockHandles, the short-read test;
+//                             * the index and metaindex CRCs (contents + type
+//                               byte against the stored trailer), 1 KiB
+//                               segments over the 16 waves (workgroup_crc);
+//                             * the verdicts in ReadBlock's order (short read,
+//                               checksum, type byte), Block::Block's restart
+//                               array test;
+//                             * ReadMeta's exact Seek("filter." + policy name)
+//                               over the metaindex staged in LDS;
+//                             * its place in the shared per-block arrays: the
+//                               entry count of every earlier table (published
+//                               by their workgroups, agent-scope 8-byte
+//                               atomics, tagged with the call's generation so
+//                               no clearing pass is needed);
+//                             * every index entry (the index staged in LDS
+//                               when it fits): the index is written with
+//                               block_restart_interval = 1 (table_builder.cc:35,
+//                               :90), so restart point i IS entry i and the
+//                               1024 threads decode entries in parallel
+//                               (DecodeEntry, block.cc:55-75; BlockHandle
+//                               varints, format.cc:24-30).
+//   2. crc32c_ragged_kernel SST-table mode over all entries (count read on the
+//                           device): the CRC, then stored trailer vs computed
+//                           CRC, type byte and parse status -> LVKV_BLOCK_*,
+//                           per-table nbad / first_bad (format.cc:92-158).
 //
-// Bounds: every byte the kernels touch is inside its table image: handles
-// are range-checked before they reach the CRC kernels (a bad one becomes 0/0
-// with a non-zero status), varints are decoded against explicit limits.
+// Bounds: every byte the kernels touch is inside its table image: handles are
+// range-checked (in an order that cannot overflow) before anything is read
+// through them; a bad one becomes 0/0 with a non-zero status; varints are
+// decoded against explicit limits.
+//
+// BlockHandle sizes near 2^64: ReadBlock computes n + kBlockTrailerSize in
+// size_t (format.cc:77-80), so n = 2^64 - 1 reads 4 bytes, passes the
+// short-read test and compares Unmask(those 4 bytes) with the CRC of zero
+// bytes (0): "block checksum mismatch" (pinned by tests/golden/damage_sst.json
+// footer_*_size_max). This path gives the same verdict. n in [2^64-5, 2^64-2]
+// makes the reference read before its buffer (undefined); this path reports
+// "truncated block read" there.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -39,12 +54,16 @@
 #include "lvkv_kernel_args.h"
 
 namespace lvkv {
+
 namespace {
 
 constexpr uint64_t kTableMagic = 0xdb4775248b80fb57ull;  // table/format.h:76
 constexpr uint64_t kFooterLen = 48;  // table/format.h:53 (2 * 20 + 8)
 constexpr uint64_t kTrailer = 5;     // table/format.h:79
-constexpr uint32_t kThreads = 256;
+constexpr int kW = 16;               // waves per table workgroup
+constexpr uint32_t kThreads = 64 * kW;
+constexpr uint32_t kMetaStage = 2048;                // metaindex staged in LDS up to this
+constexpr uint32_t kIndexStage = kCompactLdsBytes;   // index staged in the (spent) image
 
 struct Table {  // one image of the batch
   const uint8_t* img;
@@ -52,7 +71,6 @@ struct Table {  // one image of the batch
   uint64_t size;
 };
 
-// Table t: from the descriptor arrays, or the single-table call's scalars.
 __device__ __forceinline__ Table table_of(const uint8_t* file, const uint64_t* toff,
                                           const uint64_t* tsize, uint64_t single_size,
                                           uint32_t t) {
@@ -97,10 +115,33 @@ __device__ bool decode_handle(const uint8_t* p, const uint8_t* limit, uint64_t* 
   return true;
 }
 
-// ReadBlock's short-read test (format.cc:78-87) plus what the CRC kernels
-// need: contents + type byte + 4-byte trailer inside the image, n + 1 < 4 GiB.
-__device__ __forceinline__ bool handle_in_file(uint64_t off, uint64_t size, uint64_t file_size) {
-  return off <= file_size && size + kTrailer <= file_size - off && size + 1 <= 0xffffffffull;
+// ReadBlock's read of size + kBlockTrailerSize bytes at off (format.cc:76-87)
+// against an image of file_size bytes, without overflow: kFitOk when block
+// and trailer are inside the image (and n + 1 < 4 GiB, the CRC kernels'
+// length type), kFitWrap for n = 2^64 - 1 with 4 bytes readable (see the
+// header comment), else kFitShort ("truncated block read").
+enum Fit : uint32_t { kFitOk, kFitShort, kFitWrap };
+
+__device__ __forceinline__ Fit handle_fit(uint64_t off, uint64_t size, uint64_t file_size) {
+  if (off > file_size) return kFitShort;
+  const uint64_t avail = file_size - off;
+  if (size == ~uint64_t{0}) return avail >= 4 ? kFitWrap : kFitShort;
+  if (size > 0xfffffffeull || avail < kTrailer || avail - kTrailer < size) return kFitShort;
+  return kFitOk;
+}
+
+// LVKV_BLOCK_* of a block that is not kFitOk.
+__device__ __forceinline__ uint8_t unfit_status(const uint8_t* img, Fit f, uint64_t off) {
+  if (f == kFitWrap && crc_unmask(ld_le32(img + off)) != 0u) return LVKV_BLOCK_CHECKSUM;
+  return LVKV_BLOCK_TRUNCATED;  // also kFitWrap whose dword unmasks to 0 (see header)
+}
+
+// ReadBlock's verdict for a kFitOk block from its CRC test and type byte.
+__device__ __forceinline__ uint8_t read_status(bool crc_ok, uint8_t type) {
+  if (!crc_ok) return LVKV_BLOCK_CHECKSUM;
+  if (type == 1 || type == 2) return LVKV_BLOCK_COMPRESSED;  // no codec as built
+  if (type > 2) return LVKV_BLOCK_BAD_TYPE;
+  return LVKV_BLOCK_OK;
 }
 
 // DecodeEntry (table/block.cc:55-75): pointer to the key delta or nullptr.
@@ -123,330 +164,332 @@ __device__ const uint8_t* decode_entry(const uint8_t* p, const uint8_t* limit, u
   return p;
 }
 
-// Footer (format.cc:43-67): the two BlockHandles and the magic, from the 48
-// footer bytes `f` (nullptr: file shorter than a footer).
-struct Footer {
+// Everything the table's workgroup shares, in LDS.
+struct Head {
   int32_t status;
   uint64_t mo, ms, io, is;
-  bool index_ok, meta_ok;  // handle inside the file (handle_in_file)
+  uint32_t ifit, mfit;
+  uint8_t index_status, meta_status, itype, mtype;
+  uint32_t nr;          // index restart count = data blocks
+  uint32_t has_filter;
+  uint64_t fo, fs;      // filter handle
+  uint8_t filter_status;
+  uint32_t nb;          // entries this table contributes
+  uint32_t first;
+  uint32_t icrc, mcrc;
 };
 
-__device__ Footer parse_footer(const uint8_t* f, uint64_t size) {
-  Footer r;
-  r.status = LVKV_SST_OK;
-  r.mo = r.ms = r.io = r.is = 0;
-  r.index_ok = r.meta_ok = false;
+// Footer::DecodeFrom (format.cc:43-67) on the 48 staged footer bytes.
+__device__ void parse_footer(Head& h, const uint8_t* f, uint64_t size) {
+  h.status = LVKV_SST_OK;
+  h.mo = h.ms = h.io = h.is = 0;
+  h.ifit = h.mfit = kFitShort;
+  h.index_status = h.meta_status = LVKV_BLOCK_NOT_READ;
+  h.itype = h.mtype = 0;
+  h.nr = 0;
+  h.has_filter = 0;
+  h.fo = h.fs = 0;
+  h.filter_status = LVKV_BLOCK_OK;
+  h.nb = h.first = 0;
+  h.icrc = h.mcrc = 0;
   if (size < kFooterLen) {  // table/table.cc:40-42
-    r.status = LVKV_SST_TOO_SHORT;
-    return r;
+    h.status = LVKV_SST_TOO_SHORT;
+    return;
   }
   const uint64_t magic = static_cast<uint64_t>(ld_le32(f + 40)) |
                          (static_cast<uint64_t>(ld_le32(f + 44)) << 32);
   if (magic != kTableMagic) {  // format.cc:48-55
-    r.status = LVKV_SST_BAD_MAGIC;
-    return r;
+    h.status = LVKV_SST_BAD_MAGIC;
+    return;
   }
   const uint8_t* p = nullptr;
-  if (!decode_handle(f, f + kFooterLen, &r.mo, &r.ms, &p) ||
-      !decode_handle(p, f + kFooterLen, &r.io, &r.is, nullptr)) {  // format.cc:58-61
-    r.status = LVKV_SST_BAD_HANDLE;
-    return r;
+  if (!decode_handle(f, f + kFooterLen, &h.mo, &h.ms, &p) ||
+      !decode_handle(p, f + kFooterLen, &h.io, &h.is, nullptr)) {  // format.cc:58-61
+    h.status = LVKV_SST_BAD_HANDLE;
+    return;
   }
-  r.index_ok = handle_in_file(r.io, r.is, size);
-  r.meta_ok = handle_in_file(r.mo, r.ms, size);
-  if (!r.index_ok) r.status = LVKV_SST_INDEX_TRUNCATED;
-  return r;
+  h.ifit = handle_fit(h.io, h.is, size);
+  h.mfit = handle_fit(h.mo, h.ms, size);
 }
 
-// Launch 1, sst_open_kernel: workgroup 2t + w parses table t's footer (its
-// 48 bytes staged in LDS by 48 lanes, then one lane) and checksums the index
-// (w = 0) or the metaindex (w = 1), contents + type byte, against the stored
-// trailer (format.cc:92-97): 16 KiB segments over the 16 waves
-// (workgroup_crc). Workgroup 2t writes the report; 2t + 1 only its scratch
-// fields.
-__global__ void __launch_bounds__(1024, 1)
-    sst_open_kernel(const uint8_t* file, const uint64_t* toff, const uint64_t* tsize,
-                    uint64_t single_size, lvkv_sst_report* reports, const uint32_t* zpow,
-                    const uint32_t* lane_cols) {
-  constexpr int W = 16;
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kCompactLdsBytes / 4 + W];
-  __shared__ uint8_t foot[kFooterLen];
-  __shared__ Footer fs;
-  const uint32_t t = blockIdx.x >> 1, which = blockIdx.x & 1u;
-  const uint32_t tid = threadIdx.x;
-  const Table tb = table_of(file, toff, tsize, single_size, t);
-  if (tid < kFooterLen && tb.size >= kFooterLen) foot[tid] = tb.img[tb.size - kFooterLen + tid];
-  __syncthreads();
-  lvkv_sst_report* r = reports + t;
-  if (tid == 0) {
-    fs = parse_footer(foot, tb.size);
-    r->scratch_crc_[which] = 0;
-    r->scratch_status_[which] = 0;
-    if (which == 0) {
-      r->status = fs.status;
-      r->nblocks = r->ndata = r->has_filter = r->nbad = 0;
-      r->first_bad = 0xffffffffu;
-      r->index_crc = r->meta_crc = 0;
-      r->index_status = fs.status == LVKV_SST_INDEX_TRUNCATED ? LVKV_BLOCK_TRUNCATED : LVKV_BLOCK_OK;
-      r->meta_status = fs.meta_ok ? LVKV_BLOCK_OK : LVKV_BLOCK_TRUNCATED;
-      r->first = 0;
-      r->index_offset = fs.io;
-      r->index_size = fs.is;
-      r->meta_offset = fs.mo;
-      r->meta_size = fs.ms;
-      r->filter_off_ = 0;
-      r->filter_size_ = 0;
-      r->filter_status_ = LVKV_BLOCK_OK;
-      r->total_ = 0;
-      r->reserved2_ = 0;  // tables[0]: sst_head_kernel's arrival counter
-    }
-  }
-  __syncthreads();
-  if (fs.status != LVKV_SST_OK || (which == 1 && !fs.meta_ok)) return;  // workgroup-uniform
-  const uint32_t lane = lane_id();
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  build_compact_image<W>(lds, zpow, lane_cols, tid, wave, lane);
-  const uint64_t off = which ? fs.mo : fs.io;
-  const uint64_t len = (which ? fs.ms : fs.is) + 1;
-  const uint64_t start = reinterpret_cast<uint64_t>(tb.img) + off;
-  const uint32_t crc = workgroup_crc<W>(lds, lds + kCompactLdsBytes / 4, start, start + len, 0u,
-                                        lane_keys(lane), tid, wave, lane, compact_lane_base(lane),
-                                        zpow);
-  if (tid == 0) {
-    r->scratch_crc_[which] = crc;
-    r->scratch_status_[which] = crc != crc_unmask(ld_le32(tb.img + off + len)) ? 1 : 0;
-  }
-}
-
-// Table::ReadMeta's lookup (table.cc:95-104) over the metaindex bytes m[0,
-// msize] (contents + type byte): the first key with the "filter." prefix (the
-// reference matches "filter." + the policy name, which this path does not
-// know; a table carries one filter).
-__device__ void find_filter(const uint8_t* m, uint64_t msize, uint64_t file_size,
-                            lvkv_sst_report* r) {
-  if (m[msize] != 0 || msize < 4) return;  // compressed or no restart array
+// Table::ReadMeta's Seek("filter." + name) and exact key test (table.cc:95-102)
+// over the staged metaindex m[0, msize) (kNoCompression, CRC verified): a
+// linear walk keeping the length of the common prefix of the current key and
+// the target, so no key buffer is needed. Sets the filter handle on a match.
+__device__ void find_filter(Head& h, const uint8_t* m, uint64_t msize, const FilterKey& fk,
+                            const Table& tb) {
+  h.has_filter = 0;
+  if (fk.len == 0 || msize < 4) return;
   const uint32_t nr = ld_le32(m + msize - 4);
   if (nr > (msize - 4) / 4) return;
   const uint8_t* limit = m + (msize - (1 + static_cast<uint64_t>(nr)) * 4);
-  // Only the first 7 bytes of each key matter for the test: they are kept in
-  // one register (byte i of key7), not a key buffer (private arrays live in
-  // scratch memory, one memory round trip per access).
-  constexpr uint64_t kFilterPrefix = 0x2e7265746c6966ull;  // "filter." little-endian
-  uint64_t key7 = 0;
-  uint32_t klen = 0;
+  uint32_t lcp = 0, klen = 0;
   const uint8_t* p = m;
   while (p < limit) {
     uint32_t sh, ns, vl;
     const uint8_t* q = decode_entry(p, limit, &sh, &ns, &vl);
-    if (q == nullptr || sh > klen) return;
-    // key = key[0, sh) + delta
-    for (uint32_t i = sh; i < 7 && i < sh + ns; ++i)
-      key7 = (key7 & ~(0xffull << (8 * i))) | (static_cast<uint64_t>(q[i - sh]) << (8 * i));
+    if (q == nullptr || sh > klen) return;  // Block::Iter: "bad entry in block"
+    uint32_t l = min(sh, lcp);
+    if (l == sh)
+      for (uint32_t i = 0; i < ns && sh + i < fk.len && q[i] == fk.key[sh + i]; ++i) l = sh + i + 1;
+    lcp = l;
     klen = sh + ns;
-    const bool is_filter = klen >= 7 && (key7 & 0xffffffffffffffull) == kFilterPrefix;
-    if (is_filter) {
+    if (klen == fk.len && lcp == fk.len) {
       uint64_t fo, fsz;
-      if (!decode_handle(q + ns, q + ns + vl, &fo, &fsz, nullptr)) return;
-      const bool ok = handle_in_file(fo, fsz, file_size);
-      r->filter_off_ = ok ? fo : 0;
-      r->filter_size_ = ok ? static_cast<uint32_t>(fsz) : 0;
-      r->filter_status_ = ok ? LVKV_BLOCK_OK : LVKV_BLOCK_TRUNCATED;
-      r->has_filter = 1;
+      if (!decode_handle(q + ns, q + ns + vl, &fo, &fsz, nullptr)) return;  // ReadFilter: ignored
+      const Fit f = handle_fit(fo, fsz, tb.size);
+      h.fo = f == kFitOk ? fo : 0;
+      h.fs = f == kFitOk ? fsz : 0;
+      h.filter_status = f == kFitOk ? LVKV_BLOCK_OK : unfit_status(tb.img, f, fo);
+      h.has_filter = 1;
       return;
     }
     p = q + ns + vl;
   }
 }
 
-// Index verdict, restart array (Block::Block, block.cc:25-39), the filter
-// handle; `meta` = the metaindex bytes (an LDS copy or the image itself).
-__device__ void table_head(const Table& tb, lvkv_sst_report* r, const uint8_t* meta) {
-  r->index_crc = r->scratch_crc_[0];
-  if (r->meta_status == LVKV_BLOCK_OK) {
-    r->meta_crc = r->scratch_crc_[1];
-    if (r->scratch_status_[1] != 0)
-      r->meta_status = LVKV_BLOCK_CHECKSUM;
-    else if (meta[r->meta_size] > 2)
-      r->meta_status = LVKV_BLOCK_BAD_TYPE;
+// Wave 0 of table t's workgroup: first = sum of the entry counts published by
+// tables 0..t-1 (spin until each carries this call's generation). Table
+// workgroups are dispatched in order, so every table waited on is resident or
+// done. The last table also derives the launch's entry total: entries up to
+// the first table that does not fit in `capacity`.
+__device__ uint32_t place_table(lvkv_sst_report* reports, uint32_t t, uint32_t ntables,
+                                uint32_t gen, uint32_t nb, uint32_t capacity, uint32_t lane,
+                                uint32_t* total) {
+  const uint64_t mine = (static_cast<uint64_t>(gen) << 32) | nb;
+  if (lane == 0)
+    __hip_atomic_store(&reports[t].link_, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t run = 0;  // inclusive prefix so far (u64: no wrap)
+  uint64_t cut = ~uint64_t{0};
+  const uint32_t upto = (t == ntables - 1) ? ntables : t;
+  for (uint32_t b = 0; b < upto; b += 64) {
+    const uint32_t j = b + lane;
+    uint64_t v = 0;
+    if (j < upto) {
+      uint64_t x;
+      do {
+        x = __hip_atomic_load(&reports[j].link_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } while (static_cast<uint32_t>(x >> 32) != gen);
+      v = x & 0xffffffffull;
+    }
+    // inclusive prefix over the 64 lanes
+    uint64_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t o = __shfl_up(static_cast<unsigned long long>(inc), d, 64);
+      if (lane >= static_cast<uint32_t>(d)) inc += o;
+    }
+    const uint64_t p = run + inc;
+    // first table (in order) whose end passes the capacity: the total stops
+    // at its start
+    const uint64_t start = p - v;
+    const bool over = j < upto && v != 0 && p > capacity;
+    const uint64_t mask = __ballot(over);
+    if (mask != 0 && cut == ~uint64_t{0}) {
+      const uint32_t src = static_cast<uint32_t>(__builtin_ctzll(mask));
+      cut = __shfl(static_cast<unsigned long long>(start), src, 64);
+    }
+    run = __shfl(static_cast<unsigned long long>(p), 63, 64);
   }
-  if (r->scratch_status_[0] != 0) {  // ReadBlock on the index (format.cc:92-97)
-    r->index_status = LVKV_BLOCK_CHECKSUM;
-    r->status = LVKV_SST_INDEX_CHECKSUM;
-    return;
+  if (t == ntables - 1) {
+    *total = static_cast<uint32_t>(min<uint64_t>(run, min<uint64_t>(cut, capacity)));
+    // `run` included this table: its own start is run - nb
+    return static_cast<uint32_t>(min<uint64_t>(run - nb, capacity));
   }
-  const uint8_t* idx = tb.img + r->index_offset;
-  const uint64_t isize = r->index_size;
-  const uint8_t itype = idx[isize];
-  const uint32_t nr = isize >= 4 ? ld_le32(idx + isize - 4) : 0xffffffffu;
-  if (itype != 0) {  // kNoCompression only: snappy/zstd are not on this path
-    if (itype > 2) r->index_status = LVKV_BLOCK_BAD_TYPE;
-    r->status = LVKV_SST_INDEX_TYPE;
-    return;
-  }
-  if (isize < 4 || nr > (isize - 4) / 4) {
-    r->status = LVKV_SST_INDEX_CORRUPT;
-    return;
-  }
-  r->ndata = nr;
-  if (r->meta_status == LVKV_BLOCK_OK) find_filter(meta, r->meta_size, tb.size, r);
-  r->nblocks = nr + r->has_filter;
+  return static_cast<uint32_t>(min<uint64_t>(run, capacity));
 }
 
-// Launch 2, sst_head_kernel: one wave per table. The metaindex (typically
-// tens of bytes) is staged in LDS by the 64 lanes so that lane 0's serial
-// parse reads LDS, not HBM. The last wave to finish (arrival counter in
-// tables[0], agent-scope fences) then packs the tables' entries: first =
-// exclusive prefix of nblocks over the tables still OK; a table that would
-// end past `capacity` gets LVKV_SST_CAPACITY, and so does every later table.
-constexpr uint32_t kMetaStage = 2048;
-
-__global__ void __launch_bounds__(64)
-    sst_head_kernel(const uint8_t* file, const uint64_t* toff, const uint64_t* tsize,
-                    uint64_t single_size, uint32_t ntables, uint32_t capacity,
-                    lvkv_sst_report* reports) {
+// Launch 1: table t = blockIdx.x.
+__global__ void __launch_bounds__(kThreads, 1)
+    sst_table_kernel(const uint8_t* file, const uint64_t* toff, const uint64_t* tsize,
+                     uint64_t single_size, uint32_t ntables, uint32_t capacity, uint32_t gen,
+                     FilterKey fk, lvkv_sst_report* reports, uint64_t* out_off,
+                     uint32_t* out_size, uint8_t* out_status, const uint32_t* zpow,
+                     const uint32_t* lane_cols) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kCompactLdsBytes / 4 + kW];
+  __shared__ uint8_t foot[kFooterLen];
   __shared__ uint8_t mbuf[kMetaStage];
-  __shared__ uint32_t part[64];
-  __shared__ uint32_t last, overflow_at;
-  const uint32_t t = blockIdx.x, lane = threadIdx.x;
-  lvkv_sst_report* r = reports + t;
-  if (r->status == LVKV_SST_OK) {
-    const Table tb = table_of(file, toff, tsize, single_size, t);
-    const bool stage = r->meta_status == LVKV_BLOCK_OK && r->meta_size + 1 <= kMetaStage;
-    if (stage) {
-      const uint8_t* m = tb.img + r->meta_offset;
-      for (uint32_t i = lane; i <= r->meta_size; i += 64) mbuf[i] = m[i];
-    }
-    __syncthreads();
-    if (lane == 0) table_head(tb, r, stage ? mbuf : tb.img + r->meta_offset);
-  }
-  if (lane == 0) {
-    __threadfence();
-    last = atomicAdd(&reports[0].reserved2_, 1u) == ntables - 1 ? 1u : 0u;
-    overflow_at = 0xffffffffu;
-  }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  // the scan, 64 lanes over contiguous chunks of tables
-  volatile lvkv_sst_report* vr = reports;
-  const uint32_t per = (ntables + 63) / 64;
-  const uint32_t lo = min(ntables, lane * per), hi = min(ntables, lo + per);
-  uint32_t sum = 0;
-  for (uint32_t i = lo; i < hi; ++i) sum += vr[i].status == LVKV_SST_OK ? vr[i].nblocks : 0u;
-  part[lane] = sum;
-  __syncthreads();
-  for (uint32_t d = 1; d < 64; d <<= 1) {  // Hillis-Steele, inclusive
-    const uint32_t v = lane >= d ? part[lane - d] : 0u;
-    __syncthreads();
-    part[lane] += v;
-    __syncthreads();
-  }
-  uint64_t run = part[lane] - sum;
-  for (uint32_t i = lo; i < hi; ++i) {
-    const uint32_t nb = vr[i].status == LVKV_SST_OK ? vr[i].nblocks : 0u;
-    vr[i].first = static_cast<uint32_t>(min<uint64_t>(run, capacity));
-    if (run + nb > capacity) {
-      if (nb) vr[i].status = LVKV_SST_CAPACITY;
-      atomicMin(&overflow_at, static_cast<uint32_t>(min<uint64_t>(run, capacity)));
-    }
-    run += nb;
-  }
-  __syncthreads();
-  if (lane == 63) {
-    vr[0].total_ = min(part[63], overflow_at);
-    vr[0].reserved2_ = 0;
-  }
-}
-
-// Table of entry e: the last table whose first <= e (binary search; tables
-// hold contiguous, increasing ranges).
-__device__ __forceinline__ uint32_t table_of_entry(const lvkv_sst_report* reports,
-                                                   uint32_t ntables, uint32_t e) {
-  uint32_t lo = 0, hi = ntables;  // answer in [lo, hi)
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (reports[mid].first <= e) lo = mid; else hi = mid;
-  }
-  return lo;
-}
-
-// Launch 3, sst_entry_kernel: one lane per entry of every table. Entry i of
-// the index starts at restart point i and, with interval 1, ends at the next
-// one (or at the restart array).
-__global__ void __launch_bounds__(kThreads)
-    sst_entry_kernel(const uint8_t* file, const uint64_t* toff, const uint64_t* tsize,
-                     uint64_t single_size, uint32_t ntables, const lvkv_sst_report* reports,
-                     uint64_t* out_off, uint32_t* out_size, uint8_t* out_status) {
-  const uint32_t e = blockIdx.x * kThreads + threadIdx.x;
-  if (e >= reports[0].total_) return;
-  const uint32_t t = table_of_entry(reports, ntables, e);
-  const lvkv_sst_report* r = reports + t;
-  const uint32_t i = e - r->first;
+  __shared__ Head h;
+  const uint32_t t = blockIdx.x;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const Table tb = table_of(file, toff, tsize, single_size, t);
-  uint8_t st = LVKV_BLOCK_BAD_ENTRY;
-  uint64_t off = 0, size = 0;
-  // (entries below total_ all belong to OK tables, see the scan; the test
-  // only keeps the CRC kernel on an empty range should that ever not hold)
-  if (r->status != LVKV_SST_OK || i >= r->nblocks) {
-  } else if (i == r->ndata) {  // the filter block
-    st = r->filter_status_;
-    off = r->filter_off_;
-    size = r->filter_size_;
-  } else {
-    const uint8_t* idx = tb.img + r->index_offset;
-    const uint64_t nr = r->ndata;
-    const uint64_t ro = r->index_size - (1 + nr) * 4;
-    const uint32_t rs = ld_le32(idx + ro + 4ull * i);
-    const uint64_t end = i + 1 < nr ? ld_le32(idx + ro + 4ull * (i + 1)) : ro;
-    if (rs < ro && end <= ro) {
-      uint32_t sh, ns, vl;
-      const uint8_t* q = decode_entry(idx + rs, idx + ro, &sh, &ns, &vl);
-      if (q != nullptr && sh == 0 && q + ns + vl == idx + end) {
-        uint64_t ho, hs;
-        if (!decode_handle(q + ns, q + ns + vl, &ho, &hs, nullptr)) {
-          st = LVKV_BLOCK_BAD_HANDLE;
-        } else if (!handle_in_file(ho, hs, tb.size)) {
-          st = LVKV_BLOCK_TRUNCATED;
-        } else {
-          st = LVKV_BLOCK_OK;
-          off = ho;
-          size = hs;
+  lvkv_sst_report* r = reports + t;
+
+  // 1. Footer bytes (48 lanes) while the workgroup builds its LDS image.
+  if (tid < kFooterLen && tb.size >= kFooterLen) foot[tid] = tb.img[tb.size - kFooterLen + tid];
+  build_compact_image<kW>(lds, zpow, lane_cols, tid, wave, lane);  // ends with a barrier
+  if (tid == 0) parse_footer(h, foot, tb.size);
+  __syncthreads();
+  const bool footer_ok = h.status == LVKV_SST_OK;  // workgroup-uniform from here on
+
+  // 2. Index and metaindex: contents + type byte, CRC against the trailer.
+  const LaneKeys keys = lane_keys(lane);
+  const uint32_t lane_base = compact_lane_base(lane);
+  for (int which = 0; which < 2; ++which) {
+    const uint64_t off = which ? h.mo : h.io, sz = which ? h.ms : h.is;
+    if (!footer_ok || (which ? h.mfit : h.ifit) != kFitOk) continue;
+    const uint64_t start = reinterpret_cast<uint64_t>(tb.img) + off;
+    const uint32_t crc = workgroup_crc<kW, 1024>(lds, lds + kCompactLdsBytes / 4, start,
+                                                 start + sz + 1, 0u, keys, tid, wave, lane,
+                                                 lane_base, zpow);
+    if (tid == 0) (which ? h.mcrc : h.icrc) = crc;
+  }
+
+  // 3. Verdicts (ReadBlock's order), restart array; stage the metaindex.
+  if (tid == 0 && footer_ok) {
+    h.icrc = h.ifit == kFitOk ? h.icrc : 0u;
+    h.mcrc = h.mfit == kFitOk ? h.mcrc : 0u;
+    if (h.ifit != kFitOk) {
+      h.index_status = unfit_status(tb.img, static_cast<Fit>(h.ifit), h.io);
+    } else {
+      h.itype = tb.img[h.io + h.is];
+      h.index_status =
+          read_status(h.icrc == crc_unmask(ld_le32(tb.img + h.io + h.is + 1)), h.itype);
+    }
+    if (h.mfit != kFitOk) {
+      h.meta_status = unfit_status(tb.img, static_cast<Fit>(h.mfit), h.mo);
+    } else {
+      h.mtype = tb.img[h.mo + h.ms];
+      h.meta_status =
+          read_status(h.mcrc == crc_unmask(ld_le32(tb.img + h.mo + h.ms + 1)), h.mtype);
+    }
+    switch (h.index_status) {
+      case LVKV_BLOCK_OK: break;
+      case LVKV_BLOCK_TRUNCATED: h.status = LVKV_SST_INDEX_TRUNCATED; break;
+      case LVKV_BLOCK_CHECKSUM: h.status = LVKV_SST_INDEX_CHECKSUM; break;
+      default: h.status = LVKV_SST_INDEX_TYPE; break;  // compressed / bad type
+    }
+    h.nr = 0;
+    if (h.status == LVKV_SST_OK) {
+      const uint32_t nr = h.is >= 4 ? ld_le32(tb.img + h.io + h.is - 4) : 0xffffffffu;
+      if (h.is < 4 || nr > (h.is - 4) / 4)  // Block::Block (block.cc:28-37)
+        h.status = LVKV_SST_INDEX_CORRUPT;
+      else
+        h.nr = nr;
+    }
+    h.has_filter = 0;
+    h.fo = h.fs = 0;
+    h.filter_status = LVKV_BLOCK_OK;
+  }
+  __syncthreads();
+  // Table::Open succeeded iff the index block was read (Block::Block's
+  // restart test only makes the index iterator fail, table.cc:62-75); then
+  // ReadMeta runs (:76).
+  const bool index_read = footer_ok && h.index_status == LVKV_BLOCK_OK;
+  const bool index_usable = h.status == LVKV_SST_OK;
+  const bool stage_meta = index_read && h.meta_status == LVKV_BLOCK_OK && h.ms < kMetaStage;
+  if (stage_meta)
+    for (uint32_t i = tid; i < h.ms; i += kThreads) mbuf[i] = tb.img[h.mo + i];
+  const bool stage_index = index_usable && h.is <= kIndexStage;
+  uint8_t* ibuf = reinterpret_cast<uint8_t*>(lds);  // the CRC image is spent
+  if (stage_index)
+    for (uint32_t i = tid; i < h.is; i += kThreads) ibuf[i] = tb.img[h.io + i];
+  __syncthreads();
+  if (tid == 0) {
+    if (index_read && h.meta_status == LVKV_BLOCK_OK)
+      find_filter(h, stage_meta ? mbuf : tb.img + h.mo, h.ms, fk, tb);
+    // entries: the data blocks the index lists (none when its restart array
+    // is unusable), then the filter block
+    h.nb = (index_usable ? h.nr : 0u) + h.has_filter;
+  }
+  __syncthreads();
+
+  // 4. Place this table's entries in the shared arrays.
+  if (wave == 0) {
+    uint32_t total = 0, first = 0;
+    if (ntables == 1) {
+      total = h.nb <= capacity ? h.nb : 0u;
+    } else {
+      first = place_table(reports, t, ntables, gen, h.nb, capacity, lane, &total);
+    }
+    if (lane == 0) {
+      h.first = first;
+      const bool over = static_cast<uint64_t>(first) + h.nb > capacity;
+      if (over) h.status = LVKV_SST_CAPACITY;
+      r->status = h.status;
+      r->ndata = index_usable || over ? h.nr : 0u;
+      r->has_filter = h.has_filter;
+      r->nblocks = over ? 0u : h.nb;  // entries written to the shared arrays
+      r->nbad = 0;
+      r->first_bad = 0xffffffffu;
+      r->index_crc = footer_ok ? h.icrc : 0u;
+      r->meta_crc = footer_ok ? h.mcrc : 0u;
+      r->index_status = h.index_status;
+      r->meta_status = h.meta_status;
+      r->first = first;
+      r->index_offset = h.io;
+      r->index_size = h.is;
+      r->meta_offset = h.mo;
+      r->meta_size = h.ms;
+      if (t == ntables - 1) reports[0].total_ = total;
+    }
+  }
+  __syncthreads();
+  if (h.status == LVKV_SST_CAPACITY || h.nb == 0) return;
+
+  // 5. Every entry: index entries 0..nr-1, then the filter block.
+  const uint8_t* idx = stage_index ? ibuf : tb.img + h.io;
+  const uint64_t nr = index_usable ? h.nr : 0u;
+  const uint64_t ro = h.is - (1 + nr) * 4;
+  for (uint32_t i = tid; i < h.nb; i += kThreads) {
+    uint8_t st = LVKV_BLOCK_BAD_ENTRY;
+    uint64_t off = 0, size = 0;
+    if (i == nr) {  // the filter block
+      st = h.filter_status;
+      off = h.fo;
+      size = h.fs;
+    } else {
+      const uint32_t rs = ld_le32(idx + ro + 4ull * i);
+      const uint64_t end = i + 1 < nr ? ld_le32(idx + ro + 4ull * (i + 1)) : ro;
+      if (rs < ro && end <= ro) {
+        uint32_t sh, ns, vl;
+        const uint8_t* q = decode_entry(idx + rs, idx + ro, &sh, &ns, &vl);
+        if (q != nullptr && sh == 0 && q + ns + vl == idx + end) {
+          uint64_t ho, hs;
+          if (!decode_handle(q + ns, q + ns + vl, &ho, &hs, nullptr)) {
+            st = LVKV_BLOCK_BAD_HANDLE;
+          } else {
+            const Fit f = handle_fit(ho, hs, tb.size);
+            if (f == kFitOk) {
+              st = LVKV_BLOCK_OK;
+              off = ho;
+              size = hs;
+            } else {
+              st = unfit_status(tb.img, f, ho);
+            }
+          }
         }
       }
     }
+    if (st != LVKV_BLOCK_OK) off = size = 0;
+    const uint32_t e = h.first + i;
+    out_off[e] = tb.base + off;  // into d_file
+    out_size[e] = static_cast<uint32_t>(size);
+    out_status[e] = st;
   }
-  if (st != LVKV_BLOCK_OK) off = size = 0;
-  out_off[e] = tb.base + off;  // into d_file
-  out_size[e] = static_cast<uint32_t>(size);
-  out_status[e] = st;
 }
 
 }  // namespace
 
 hipError_t launch_crc32c_general(const KernelArgs& a, int cus, hipStream_t stream);
 
-// The four launches for `ntables` images (toff/tsize device arrays, or
+// The two launches for `ntables` images (toff/tsize device arrays, or
 // nullptr and `single_size` for one image at d_file); `verify` carries the
 // KernelArgs template (tables) the caller filled.
 hipError_t launch_sst_tables(const uint8_t* file, const uint64_t* toff, const uint64_t* tsize,
                              uint64_t single_size, uint32_t ntables, uint64_t* d_off,
                              uint32_t* d_size, uint32_t* d_actual, uint8_t* d_status,
-                             uint32_t capacity, lvkv_sst_report* reports,
-                             const KernelArgs& verify, const uint32_t* zpow,
+                             uint32_t capacity, lvkv_sst_report* reports, const FilterKey& fk,
+                             uint32_t gen, const KernelArgs& verify, const uint32_t* zpow,
                              const uint32_t* lane_cols, int groups, hipStream_t stream) {
-  hipLaunchKernelGGL(sst_open_kernel, dim3(2 * ntables), dim3(1024), 0, stream, file, toff, tsize,
-                     single_size, reports, zpow, lane_cols);
+  hipLaunchKernelGGL(sst_table_kernel, dim3(ntables), dim3(kThreads), 0, stream, file, toff,
+                     tsize, single_size, ntables, capacity, gen, fk, reports, d_off, d_size,
+                     d_status, zpow, lane_cols);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(sst_head_kernel, dim3(ntables), dim3(64), 0, stream, file, toff, tsize,
-                     single_size, ntables, capacity, reports);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  const uint32_t egrid = (capacity + kThreads - 1) / kThreads;
-  hipLaunchKernelGGL(sst_entry_kernel, dim3(egrid), dim3(kThreads), 0, stream, file, toff, tsize,
-                     single_size, ntables, reports, d_off, d_size, d_status);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-
-  // 4. every data and filter block of every table: CRC, then the merge into
+  // 2. every data and filter block of every table: CRC, then the merge into
   //    LVKV_BLOCK_* and the per-table totals in the kernel's store
   KernelArgs a = verify;
   a.base = file;

@@ -122,3 +122,141 @@ def block_verdicts(img: bytes) -> BlockVerdicts:
         v.block_status.append(status)
         v.block_drop.append(drop)
     return v
+
+
+# ---- the logical layer: log::Reader::ReadRecord (db/log_reader.cc:55-176) ----
+# Physical events, in file order, as ReadPhysicalRecord hands them over:
+#   ("rec", header_offset, length, type)   a record whose checksum passed
+#   ("bad", drop_bytes, reason)            kBadRecord; reason None = silent
+#                                          (the zero-type zero-length skip)
+#   ("eof",)                               kEof
+K_FULL, K_FIRST, K_MIDDLE, K_LAST = 1, 2, 3, 4
+
+
+def physical_events(img: bytes):
+    """The events the sequential walk above produces (ReadPhysicalRecord
+    with checksum = true from offset 0)."""
+    ev = []
+    pos, eof = 0, False
+    buf_start, buf_end = 0, 0
+    while True:
+        if buf_end - buf_start < K_HEADER:
+            if not eof:
+                buf_start = pos
+                buf_end = min(len(img), pos + K_BLOCK)
+                pos = buf_end
+                if buf_end - buf_start < K_BLOCK:
+                    eof = True
+                continue
+            ev.append(("eof",))
+            return ev
+        h = buf_start
+        length = img[h + 4] | (img[h + 5] << 8)
+        rtype = img[h + 6]
+        if K_HEADER + length > buf_end - buf_start:
+            drop = buf_end - buf_start
+            buf_start = buf_end
+            if not eof:
+                ev.append(("bad", drop, "bad record length"))
+                continue
+            ev.append(("eof",))
+            return ev
+        if rtype == 0 and length == 0:
+            buf_start = buf_end
+            ev.append(("bad", 0, None))
+            continue
+        expected = oracle.unmask(struct.unpack_from("<I", img, h)[0])
+        if oracle.value(img[h + 6: h + 7 + length]) != expected:
+            drop = buf_end - buf_start
+            buf_start = buf_end
+            ev.append(("bad", drop, "checksum mismatch"))
+            continue
+        buf_start += K_HEADER + length
+        ev.append(("rec", h, length, rtype))
+
+
+def assemble(img: bytes, events):
+    """ReadRecord over the physical events: the logical records it returns
+    as (LastRecordOffset, length, CRC32C of the contents) and every
+    Reporter::Corruption(bytes, reason) in order (physical and logical)."""
+    records, reports = [], []
+    it = iter(events)
+    while True:
+        in_frag, scratch, prospective = False, b"", 0
+        done = False
+        for e in it:
+            if e[0] == "eof":
+                return records, reports
+            if e[0] == "bad":
+                if e[2] is not None:
+                    reports.append((e[1], e[2]))
+                if in_frag:
+                    reports.append((len(scratch), "error in middle of record"))
+                    in_frag, scratch = False, b""
+                continue
+            _, h, length, rtype = e
+            frag = img[h + K_HEADER: h + K_HEADER + length]
+            if rtype == K_FULL:
+                if in_frag and scratch:
+                    reports.append((len(scratch), "partial record without end(1)"))
+                records.append((h, len(frag), oracle.value(frag)))
+                done = True
+                break
+            if rtype == K_FIRST:
+                if in_frag and scratch:
+                    reports.append((len(scratch), "partial record without end(2)"))
+                prospective, scratch, in_frag = h, frag, True
+            elif rtype == K_MIDDLE:
+                if not in_frag:
+                    reports.append((len(frag), "missing start of fragmented record(1)"))
+                else:
+                    scratch += frag
+            elif rtype == K_LAST:
+                if not in_frag:
+                    reports.append((len(frag), "missing start of fragmented record(2)"))
+                else:
+                    scratch += frag
+                    records.append((prospective, len(scratch), oracle.value(scratch)))
+                    done = True
+                    break
+            else:
+                reports.append((len(frag) + (len(scratch) if in_frag else 0),
+                                f"unknown record type {rtype}"))
+                in_frag, scratch = False, b""
+        if not done:
+            return records, reports
+
+
+def read_records(img: bytes):
+    """log::Reader(checksum = true, initial_offset = 0) over the whole image."""
+    return assemble(img, physical_events(img))
+
+
+def events_from_blocks(img: bytes, hdrs, rec_status, block_status, block_drop):
+    """The same physical events rebuilt from the per-block / per-record
+    verdicts of the block form (and of lvkv_log_verify_blocks_device): a
+    block's records up to its first mismatch, then its error, block by block;
+    kEof after the last block (or at a truncated end)."""
+    ev = []
+    nblocks = (len(img) + K_BLOCK - 1) // K_BLOCK
+    j = 0
+    for b in range(nblocks):
+        start, end = b * K_BLOCK, min(len(img), (b + 1) * K_BLOCK)
+        while j < len(hdrs) and hdrs[j] < end:
+            h = hdrs[j]
+            if rec_status[j] == REC_OK:
+                length = img[h + 4] | (img[h + 5] << 8)
+                ev.append(("rec", h, length, img[h + 6]))
+            j += 1
+        st = block_status[b]
+        if st == BLK_CHECKSUM:
+            ev.append(("bad", int(block_drop[b]), "checksum mismatch"))
+        elif st == BLK_BAD_LENGTH:
+            ev.append(("bad", int(block_drop[b]), "bad record length"))
+        elif st == BLK_ZERO:
+            ev.append(("bad", 0, None))
+        elif st == BLK_EOF:
+            ev.append(("eof",))
+            return ev
+    ev.append(("eof",))
+    return ev

@@ -11,7 +11,13 @@ Restates, from the reference snapshot:
     kBlockTrailerSize table/format.h:79);
   * Block::Block's restart-array sanity and DecodeEntry (table/block.cc:25-75),
     walked entry by entry like Block::Iter::ParseNextKey (:252-280);
-  * Table::ReadMeta's "filter." lookup in the metaindex (table/table.cc:82-105).
+  * Table::ReadMeta's exact Seek("filter." + policy name) in the metaindex
+    and ReadFilter (table/table.cc:81-124);
+  * ReadBlock's size_t arithmetic for handles near 2^64 (format.cc:77-87).
+
+Pinned by tests/golden/damage_sst.json: verdicts the reference's own
+Table::Open / ReadBlock / Block::Iter / ReadMeta steps gave on damaged copies
+of the reference-written table (oracle/gen_damage.cc).
 
 Only tests/ import this module. Status codes are the ones
 include/lvkv_crc32c.h defines for the device path.
@@ -34,6 +40,9 @@ SST_INDEX_TRUNCATED, SST_INDEX_CHECKSUM, SST_INDEX_TYPE = 4, 5, 6
 SST_INDEX_CORRUPT, SST_CAPACITY = 7, 8
 # per-block status (LVKV_BLOCK_*)
 BLK_OK, BLK_CHECKSUM, BLK_TRUNCATED, BLK_BAD_TYPE, BLK_BAD_HANDLE, BLK_BAD_ENTRY = 0, 1, 2, 3, 4, 5
+BLK_COMPRESSED, BLK_NOT_READ = 6, 7
+BLOOM_POLICY = "leveldb.BuiltinBloomFilter2"   # util/bloom.cc BloomFilterPolicy::Name()
+U64_MAX = (1 << 64) - 1
 
 
 def get_varint(buf: bytes, pos: int, limit: int, max_shift: int) -> Tuple[Optional[int], int]:
@@ -63,15 +72,27 @@ def decode_handle(buf: bytes, pos: int, limit: int):
 
 
 def block_status(img: bytes, off: int, size: int) -> Tuple[int, int]:
-    """ReadBlock with verify_checksums (table/format.cc:78-100, :104-158):
-    (status, crc of contents + type byte)."""
-    if off > len(img) or size + K_TRAILER > len(img) - off or size + 1 > 0xFFFFFFFF:
+    """ReadBlock with verify_checksums (table/format.cc:69-158) as built
+    (no snappy/zstd): (status, crc of contents + type byte; 0 if none).
+
+    n + kBlockTrailerSize is size_t arithmetic (:77-80): n = 2^64-1 reads
+    4 bytes, passes the length test and compares Unmask of them with the CRC
+    of zero bytes (0). n in [2^64-5, 2^64-2] reads before the reference's
+    buffer (undefined): reported as a short read, as the device does."""
+    avail = len(img) - off if off <= len(img) else -1
+    if size == U64_MAX and avail >= 4:
+        stored = oracle.unmask(struct.unpack_from("<I", img, off)[0])
+        return (BLK_CHECKSUM if stored != 0 else BLK_TRUNCATED), 0
+    if avail < 0 or size > 0xFFFFFFFE or avail < K_TRAILER or avail - K_TRAILER < size:
         return BLK_TRUNCATED, 0
     actual = oracle.value(img[off: off + size + 1])
     stored = oracle.unmask(struct.unpack_from("<I", img, off + size + 1)[0])
     if actual != stored:
         return BLK_CHECKSUM, actual
-    if img[off + size] > 2:  # kNoCompression, kSnappyCompression, kZstdCompression
+    t = img[off + size]
+    if t in (1, 2):   # kSnappyCompression / kZstdCompression: no codec as built
+        return BLK_COMPRESSED, actual
+    if t > 2:
         return BLK_BAD_TYPE, actual
     return BLK_OK, actual
 
@@ -116,8 +137,8 @@ class TableReport:
     has_filter: int = 0
     index: Tuple[int, int] = (0, 0)
     meta: Tuple[int, int] = (0, 0)
-    index_status: int = 0
-    meta_status: int = 0
+    index_status: int = BLK_NOT_READ
+    meta_status: int = BLK_NOT_READ
     index_crc: int = 0
     meta_crc: int = 0
     handles: List[Tuple[int, int]] = field(default_factory=list)  # data..., filter
@@ -133,7 +154,37 @@ class TableReport:
         return sum(1 for s in self.status_per_block if s)
 
 
-def verify_table(img: bytes, capacity: int = 1 << 30) -> TableReport:
+def _entry(r: TableReport, img: bytes, h) -> None:
+    st, crc = block_status(img, *h)
+    r.handles.append(h if st in (BLK_OK, BLK_CHECKSUM, BLK_BAD_TYPE, BLK_COMPRESSED)
+                     and h[1] != U64_MAX else (0, 0))
+    r.status_per_block.append(st)
+    r.crc_per_block.append(crc if r.handles[-1] != (0, 0) or st == BLK_OK else None)
+
+
+def find_filter(img: bytes, moff: int, msize: int, key: bytes):
+    """Table::ReadMeta's Seek(key) + exact test (table.cc:95-102) on a
+    well-formed, CRC-verified metaindex: the value of the entry whose key is
+    exactly `key`, else None."""
+    mra = restart_array(img, moff, msize)
+    if mra is None:
+        return None
+    mro = mra[0]
+    p, k = moff, b""
+    while p < moff + mro:
+        e = decode_entry(img, p, moff + mro)
+        if e is None or e[0] > len(k):
+            return None
+        sh, ns, vl, q = e
+        k = k[:sh] + img[q: q + ns]
+        if k == key:
+            return q + ns, q + ns + vl
+        p = q + ns + vl
+    return None
+
+
+def verify_table(img: bytes, capacity: int = 1 << 30,
+                 filter_policy: Optional[str] = BLOOM_POLICY) -> TableReport:
     r = TableReport()
     if len(img) < K_FOOTER_LEN:                           # table/table.cc:40-42
         r.status = SST_TOO_SHORT
@@ -157,61 +208,43 @@ def verify_table(img: bytes, capacity: int = 1 << 30) -> TableReport:
     if r.index_status == BLK_CHECKSUM:
         r.status = SST_INDEX_CHECKSUM
         return r
-    ioff, isize = index
-    if img[ioff + isize] != 0:  # compressed (snappy/zstd absent here) or bad type
+    if r.index_status != BLK_OK:   # compressed (no codec as built) or bad type
         r.status = SST_INDEX_TYPE
         return r
+    ioff, isize = index
     ra = restart_array(img, ioff, isize)
     if ra is None:
-        r.status = SST_INDEX_CORRUPT
-        return r
-    ro, restarts = ra
-    r.ndata = len(restarts)
-    if r.ndata + 1 > capacity:
+        r.status = SST_INDEX_CORRUPT   # Table::Open is OK; the index iterator fails
+    else:
+        ro, restarts = ra
+        r.ndata = len(restarts)
+        # The index is written with block_restart_interval = 1
+        # (table/table_builder.cc:35, :90): one entry per restart point, shared 0.
+        for i, rs in enumerate(restarts):
+            end = restarts[i + 1] if i + 1 < len(restarts) else ro
+            e = decode_entry(img, ioff + rs, ioff + ro) if rs < ro and end <= ro else None
+            if e is None or e[0] != 0 or e[3] + e[1] + e[2] != ioff + end:
+                r.handles.append((0, 0))
+                r.status_per_block.append(BLK_BAD_ENTRY)
+                r.crc_per_block.append(None)
+                continue
+            _, ns, vl, q = e
+            h, _ = decode_handle(img, q + ns, q + ns + vl)
+            if h is None:
+                r.handles.append((0, 0))
+                r.status_per_block.append(BLK_BAD_HANDLE)
+                r.crc_per_block.append(None)
+                continue
+            _entry(r, img, h)
+    # Table::ReadMeta + ReadFilter (table.cc:81-124): Open succeeded
+    if filter_policy is not None and r.meta_status == BLK_OK:
+        moff, msize = meta
+        v = find_filter(img, moff, msize, b"filter." + filter_policy.encode())
+        if v is not None:
+            h, _ = decode_handle(img, v[0], v[1])
+            if h is not None:
+                _entry(r, img, h)
+                r.has_filter = 1
+    if r.nblocks > capacity:
         r.status = SST_CAPACITY
-        return r
-    # The index is written with block_restart_interval = 1
-    # (table/table_builder.cc:35, :90): one entry per restart point, shared 0.
-    for i, rs in enumerate(restarts):
-        end = restarts[i + 1] if i + 1 < len(restarts) else ro
-        e = decode_entry(img, ioff + rs, ioff + ro) if rs < ro else None
-        if e is None or e[0] != 0 or e[3] + e[1] + e[2] != ioff + end:
-            r.handles.append((0, 0))
-            r.status_per_block.append(BLK_BAD_ENTRY)
-            r.crc_per_block.append(None)
-            continue
-        _, ns, vl, q = e
-        h, _ = decode_handle(img, q + ns, q + ns + vl)
-        if h is None:
-            r.handles.append((0, 0))
-            r.status_per_block.append(BLK_BAD_HANDLE)
-            r.crc_per_block.append(None)
-            continue
-        st, crc = block_status(img, *h)
-        r.handles.append(h if st != BLK_TRUNCATED else (0, 0))
-        r.status_per_block.append(st)
-        r.crc_per_block.append(crc if st != BLK_TRUNCATED else None)
-    # Table::ReadMeta: the filter handle under a "filter." key (table.cc:95-104)
-    moff, msize = meta
-    if r.meta_status == BLK_OK and img[moff + msize] == 0:
-        mra = restart_array(img, moff, msize)
-        if mra is not None:
-            mro = mra[0]
-            p, key = moff, b""
-            while p < moff + mro:
-                e = decode_entry(img, p, moff + mro)
-                if e is None or e[0] > len(key):
-                    break
-                sh, ns, vl, q = e
-                key = key[:sh] + img[q: q + ns]
-                if key.startswith(b"filter."):
-                    h, _ = decode_handle(img, q + ns, q + ns + vl)
-                    if h is not None:
-                        st, crc = block_status(img, *h)
-                        r.handles.append(h if st != BLK_TRUNCATED else (0, 0))
-                        r.status_per_block.append(st)
-                        r.crc_per_block.append(crc if st != BLK_TRUNCATED else None)
-                        r.has_filter = 1
-                    break
-                p = q + ns + vl
     return r

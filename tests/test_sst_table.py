@@ -96,8 +96,7 @@ def test_report_struct_layout_matches_header(tmp_path, lvkv):
           printf("size %zu\\n", sizeof(lvkv_sst_report));
           F(status) F(nblocks) F(ndata) F(has_filter) F(nbad) F(first_bad) F(index_crc)
           F(meta_crc) F(index_status) F(meta_status) F(first) F(index_offset) F(index_size)
-          F(meta_offset) F(meta_size) F(filter_off_) F(filter_size_) F(scratch_status_)
-          F(filter_status_) F(scratch_crc_) F(total_)
+          F(meta_offset) F(meta_size) F(link_) F(total_)
           return 0;
         }"""))
     exe = tmp_path / "layout"
@@ -125,25 +124,27 @@ def _assert_matches_oracle(lvkv, img: bytes, gpu, capacity=None, got=None, base=
     want = st.verify_table(img)
     rep, off, size, actual, status = got if got is not None else _device_verify(
         lvkv, img, gpu, capacity)
-    # handles come back as offsets into the device buffer, bad entries as
-    # (table start, 0)
+    # handles come back as offsets into the device buffer, unreadable entries
+    # as (table start, 0)
     off = np.array([int(x) - base for x in off], dtype=np.int64)
     assert rep["status"] == want.status
-    if want.status not in (st.SST_OK,):
+    assert rep["index_status"] == want.index_status and rep["meta_status"] == want.meta_status
+    if want.status in (st.SST_TOO_SHORT, st.SST_BAD_MAGIC, st.SST_BAD_HANDLE):
+        assert rep["nblocks"] == 0
+        return rep, want
+    assert (rep["index_offset"], rep["index_size"]) == want.index
+    assert (rep["meta_offset"], rep["meta_size"]) == want.meta
+    assert rep["index_crc"] == want.index_crc
+    assert rep["meta_crc"] == want.meta_crc
+    if want.status == st.SST_CAPACITY:
+        assert rep["nblocks"] == 0 and rep["ndata"] == want.ndata
         return rep, want
     assert rep["ndata"] == want.ndata and rep["has_filter"] == want.has_filter
     assert rep["nblocks"] == want.nblocks
-    assert (rep["index_offset"], rep["index_size"]) == want.index
-    assert (rep["meta_offset"], rep["meta_size"]) == want.meta
-    assert rep["index_status"] == want.index_status and rep["meta_status"] == want.meta_status
-    assert rep["index_crc"] == want.index_crc
-    if want.meta_status in (st.BLK_OK, st.BLK_CHECKSUM):
-        assert rep["meta_crc"] == want.meta_crc
     assert [tuple(int(x) for x in h) for h in zip(off, size)] == want.handles
     assert list(status) == want.status_per_block
     for i, c in enumerate(want.crc_per_block):
-        if c is not None:
-            assert int(actual[i]) == c, i
+        assert int(actual[i]) == (c if c is not None else 0), i
     assert rep["nbad"] == want.nbad
     bad = [i for i, s in enumerate(want.status_per_block) if s]
     assert rep["first_bad"] == (bad[0] if bad else 0xFFFFFFFF)
