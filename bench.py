@@ -1,50 +1,65 @@
 """Benchmark: device-resident batched CRC32C (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config headline|wal32k|blocks1m|host]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config NAME]
 
-One step = one launch of the batch kernel over one batch of blocks already
-resident in HBM (the headline batch: 10,000 x 4096 B). Consecutive steps read
-different windows of a >= 1 GiB rotation so every launch is cold in the
-256 MiB Infinity Cache. Steps are independent batches: step i is issued on
-stream i % S (--streams, default 2), so one batch's kernel can start on the
-CUs the previous batch's kernel has released (a checksum service with two
-batches in flight); --streams 1 serialises them. N > 1: one process per GPU
-(torchrun), every rank checksums its own 10k-block batch (independent slices,
-weak scaling, no collective on the data path); time = max over ranks of the
-barrier-bracketed K steps. Rank 0 prints ONE JSON line.
+Configs (BASELINE.json "configs"; the default line is the headline):
+  headline        10,000 x 4 KiB blocks per GPU per step (the metric's
+                  workload); the line also carries `split`, config 5 measured
+                  in the same run.
+  blocks1m_split  config 5: ONE batch of 1M x 4 KiB blocks split across the
+                  ranks (shard.shard_range), aggregate GiB/s.
+  blocks1m        config 4: 1M x 4 KiB blocks per GPU per step.
+  wal32k          config 3: 16,384 x 32 KiB WAL blocks, CRC over [6, 32768)
+                  (HIP launch path: the engine's kernel holds blocks <= 4 KiB).
 
-value = whole-job GiB/s of the K steps (all streams, barrier + synchronize
-on both sides). roofline.achieved = algorithmic bytes per launch (nblocks x
-(block + 4 B CRC out)) / the kernel's own average launch
-duration, measured by a HIP event pair around K launches issued back to back
-on ONE stream (so it agrees with a rocprofv3 kernel trace of --streams 1);
-roofline.pipelined prices the same bytes on the S-stream launch period.
-cpu_baseline = the reference's own util/crc32c.cc (compiled in place into
-oracle/_ref) timed on this host.
+One step = one batch submitted to the AQL engine (lvkv_engine_crc32c_uniform,
+include/lvkv_crc32c.h) over blocks already resident in HBM. Consecutive steps
+read different windows of a >= 1.25 GiB rotation, so every batch is cold in
+the 256 MiB Infinity Cache; consecutive batches overlap on the device (the
+engine's queues), as in a checksum service with batches in flight.
+
+Timed region (every config, every rank; `timed_region`): time-based warm-up
+(>= --warmup-ms and >= W steps), barrier, synchronize, t0, K steps, engine
+wait, synchronize, t1, barrier; elapsed = max over ranks of t1 - t0 (common
+start to last completion). value = all ranks' bytes / elapsed.
+
+roofline: algorithmic bytes per launch (nblocks x (block + 4 B CRC out),
+SURVEY.md §8(d)) / the launch's duration, from the packet processor's
+start/end timestamps of each dispatch (HSA profiling, the engine's HIP-event
+counterpart): `achieved` prices a launch running alone (ordered dispatches,
+the same kernel a rocprofv3 kernel trace of `--isolated` times); `pipelined`
+prices the device span of K overlapped launches / K.
+cpu_baseline: the reference's util/crc32c.cc (compiled in place into
+oracle/_ref) on this host.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 from pathlib import Path
 
 import numpy as np
-import torch
 
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 GIB = float(1 << 30)
+BLOCK = 4096
+SPLIT_TOTAL = 1_000_000
+METRIC = "device-resident CRC32C GiB/s over 10k×4KiB blocks; % of MI355X HBM peak"
 
 CONFIGS = {
     # name: (nblocks, block_bytes, stride, crc_offset_in_block, description)
-    "headline": (10_000, 4096, 4096, 0, "10k x 4 KiB blocks (BASELINE headline)"),
+    "headline": (10_000, 4096, 4096, 0, "10k x 4 KiB blocks per GPU per step (BASELINE headline)"),
+    "blocks1m": (1_000_000, 4096, 4096, 0, "1M x 4 KiB blocks per GPU per step (config 4)"),
+    "blocks1m_split": (SPLIT_TOTAL, 4096, 4096, 0,
+                       "1M x 4 KiB blocks split across the ranks (config 5)"),
     "wal32k": (16_384, 32762, 32768, 6, "16384 x 32 KiB WAL blocks, CRC over [6, 32768) (config 3)"),
-    "blocks1m": (1_000_000, 4096, 4096, 0, "1M x 4 KiB blocks (config 4)"),
 }
 
 
@@ -57,6 +72,197 @@ def dist_env():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     return world, rank, local
+
+
+def _load_shard():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "lvkv_shard", REPO / "leveldb-kv-separation_amd" / "shard.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+# --------------------------------------------------------------------------
+# the timed region (shared by every config and by tests/test_dist.py)
+
+
+class Comm:
+    """Barrier and max-over-ranks on the process group (RCCL on the GPU box,
+    gloo in the CPU tests); no-ops at world 1."""
+
+    def __init__(self, world: int, device=None):
+        self.world = world
+        self.device = device
+
+    def barrier(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    def max(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([x], dtype=torch.float64, device=self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+
+def timed_region(runner, comm: Comm, steps: int, warmup: int, warmup_s: float,
+                 first: int = 0):
+    """Warm-up (>= warmup steps and >= warmup_s seconds), then K steps timed
+    from a common start (barrier + sync) to this rank's last completion
+    (finish + sync); returns (max over ranks in seconds, next step index).
+    `runner` has step(i), finish() and sync(). Step indices continue from `first` so the
+    timed steps read windows the warm-up did not just leave in the cache."""
+    i = first
+    t_end = time.perf_counter() + warmup_s
+    n = 0
+    while n < warmup or time.perf_counter() < t_end:
+        runner.step(i)
+        i += 1
+        n += 1
+        if n % 16 == 0:
+            runner.finish()
+    runner.finish()
+    runner.sync()
+    comm.barrier()
+    runner.sync()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        runner.step(i + k)
+    runner.finish()
+    runner.sync()
+    elapsed = time.perf_counter() - t0
+    comm.barrier()
+    return comm.max(elapsed), i + steps
+
+
+def split_measure(make_runner, comm: Comm, rank: int, world: int, steps: int, warmup: int,
+                  warmup_s: float, total: int = SPLIT_TOTAL, block: int = BLOCK):
+    """Config 5: one batch of `total` blocks split into contiguous slices, one
+    per rank (shard.shard_range, no collective on the data path); every step
+    checksums the rank's whole slice. Returns the runner and the aggregate
+    record (GiB/s of the whole batch over the max-over-ranks time)."""
+    shard = _load_shard()
+    start, count = shard.shard_range(total, rank, world)
+    runner = make_runner(start, count)
+    elapsed, _ = timed_region(runner, comm, steps, warmup, warmup_s)
+    value = total * block * steps / elapsed / GIB
+    rec = {"workload": CONFIGS["blocks1m_split"][4], "total_blocks": total,
+           "block_bytes": block, "ranks": world, "slice_blocks_rank0": shard.shard_range(total, 0, world)[1],
+           "steps": steps, "ms_per_step": round(elapsed / steps * 1e3, 5),
+           "value": round(value, 4), "unit": "GiB/s",
+           "pct_hbm_peak_per_gpu": round(100.0 * value * GIB / 1e9 / HBM_PEAK_GBS / world, 2),
+           "timing": "common start barrier to the last rank's completion (max over ranks)"}
+    return runner, rec
+
+
+# --------------------------------------------------------------------------
+# GPU runners
+
+
+class EngineRunner:
+    """Steps through the AQL engine over rotating HBM windows."""
+
+    def __init__(self, lvkv, eng, buf, nb, L, stride, crc_off, nrot, window, outs):
+        import torch
+        self.torch = torch
+        self.eng = eng
+        self.submit = eng.submit_ptr
+        self.h = eng.handle
+        self.nb, self.L, self.stride = nb, L, stride
+        self.bases = [buf.data_ptr() + w * window + crc_off for w in range(nrot)]
+        self.outs = [o.data_ptr() for o in outs]
+        self.nrot = nrot
+        self.flags = 0
+
+    def step(self, i):
+        rc = self.submit(self.h, self.bases[i % self.nrot], self.stride, self.L, 0,
+                         self.outs[i % len(self.outs)], self.nb, self.flags)
+        if rc != 0:
+            raise SystemExit(f"bench: lvkv_engine_crc32c_uniform failed ({rc})")
+
+    def finish(self):
+        self.eng.wait()
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+
+class HipRunner:
+    """Steps through the HIP launch path (lvkv_crc32c_uniform_device) on two
+    streams (blocks beyond the engine's 4 KiB kernel)."""
+
+    def __init__(self, lvkv, buf, nb, L, stride, crc_off, nrot, window, outs, dev):
+        import torch
+        self.torch = torch
+        self.fn = lvkv.lib.lvkv_crc32c_uniform_device
+        self.nb, self.L, self.stride = nb, L, stride
+        self.bases = [buf.data_ptr() + w * window + crc_off for w in range(nrot)]
+        self.outs = [o.data_ptr() for o in outs]
+        self.nrot = nrot
+        self.main = torch.cuda.current_stream(dev)
+        self.side = torch.cuda.Stream(dev)
+        self.hs = [self.main.cuda_stream, self.side.cuda_stream]
+        self.forked = False
+
+    def step(self, i):
+        if not self.forked:
+            self.side.wait_stream(self.main)
+            self.forked = True
+        rc = self.fn(self.bases[i % self.nrot], self.stride, self.L, 0,
+                     self.outs[i % len(self.outs)], self.nb, 0, self.hs[i % 2])
+        if rc != 0:
+            raise SystemExit(f"bench: lvkv_crc32c_uniform_device failed ({rc})")
+
+    def finish(self):
+        if self.forked:
+            self.main.wait_stream(self.side)
+            self.forked = False
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+
+def make_buffers(torch, dev, rank, nb, stride, rotate_bytes, extra=64):
+    window = nb * stride
+    nrot = max(1, int(np.ceil(rotate_bytes / window)))
+    gen = torch.Generator(device=dev).manual_seed(0x1EDC6F41 + 17 * rank)
+    buf = torch.randint(0, 256, (nrot * window + extra,), dtype=torch.uint8, device=dev,
+                        generator=gen)
+    return buf, nrot, window
+
+
+def parity_check(buf, outs0, nb, L, stride, crc_off, rank, what):
+    """Spot check outside the timed region against the oracle (checker)."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    import oracle
+    check_n = min(nb, 2000)
+    host = buf[crc_off: crc_off + (check_n - 1) * stride + L].cpu().numpy()
+    want = oracle.uniform(host, check_n, L, stride, threads=8)
+    got = outs0[:check_n].cpu().numpy().view(np.uint32)
+    if not np.array_equal(got, want):
+        raise SystemExit(f"bench: parity check FAILED on rank {rank} ({what})")
+
+
+def profile_launches(runner, eng, n, ordered, first):
+    """Packet-processor start/end of n dispatches (HSA profiling)."""
+    runner.flags = 2 if ordered else 0  # LVKV_FLAG_ORDERED
+    eng.profile(True)
+    for k in range(n):
+        runner.step(first + k)
+    eng.wait()
+    spans = eng.profile_read(4096)
+    eng.profile(False)
+    runner.flags = 0
+    return spans
+
+
+# --------------------------------------------------------------------------
+# CPU baseline (rank 0, N = 1)
 
 
 def cpu_baseline(seconds: float = 8.0):
@@ -75,6 +281,7 @@ def cpu_baseline(seconds: float = 8.0):
     else:
         fn = lambda: oracle.uniform(data, nb, L, threads=1)  # noqa: E731
         kind = "port"
+
     def best_of(f, secs):
         f()
         best, t_end, passes = float("inf"), time.perf_counter() + secs, 0
@@ -122,175 +329,171 @@ def load_pmc_traffic():
     return None
 
 
+# --------------------------------------------------------------------------
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--warmup-ms", type=float, default=150.0,
+                    help="warm-up lasts at least this long, whatever --warmup says")
     ap.add_argument("--config", default="headline", choices=sorted(CONFIGS))
     ap.add_argument("--rotate-bytes", type=float, default=1.25 * GIB)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-split", action="store_true", help="skip config 5 in the headline line")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
-    ap.add_argument("--streams", type=int, default=2,
-                    help="independent batches in flight: step i runs on stream i %% S")
+    ap.add_argument("--isolated", type=int, default=0,
+                    help="only run N ordered (one-at-a-time) launches and exit: the "
+                         "command a rocprofv3 kernel trace of the roofline kernel wraps")
     args = ap.parse_args()
 
+    import torch
     world, rank, local = dist_env()
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    comm = Comm(world, dev)
 
     import __graft_entry__ as g
     lvkv = g.load_package()
+    warm_s = args.warmup_ms / 1e3
+
+    if args.config == "blocks1m_split":
+        eng = lvkv.Engine(local)
+        runner, rec = split_measure(
+            lambda s, c: _split_runner(torch, lvkv, eng, dev, rank, s, c), comm, rank, world,
+            args.steps, args.warmup, warm_s)
+        if rank == 0:
+            line = _line_base(args, world, rec["value"], rec["ms_per_step"] / 1e3,
+                              {"workload": rec["workload"], "total_blocks": SPLIT_TOTAL,
+                               "block_bytes": BLOCK,
+                               "parallelism": f"{world} contiguous slices (no collective)"})
+            line["split"] = rec
+            print(json.dumps(line), flush=True)
+        _end(world)
+        return
 
     nb, L, stride, crc_off, desc = CONFIGS[args.config]
-    batch_bytes = nb * stride
-    nrot = max(1, int(np.ceil(args.rotate_bytes / batch_bytes)))
-    gen = torch.Generator(device=dev).manual_seed(0x1EDC6F41 + 17 * rank)
-    buf = torch.randint(0, 256, (nrot * batch_bytes + 64,), dtype=torch.uint8,
-                        device=dev, generator=gen)
-    nstreams = max(1, args.streams)
-    outs = [torch.empty(nb, dtype=torch.int32, device=dev) for _ in range(2 * nstreams)]
-    stream = torch.cuda.current_stream(dev)
-    side = [torch.cuda.Stream(dev) for _ in range(nstreams - 1)]
-    hstreams = [stream.cuda_stream] + [s.cuda_stream for s in side]
+    use_engine = L <= 4096 and stride % 4 == 0
+    buf, nrot, window = make_buffers(torch, dev, rank, nb, stride, args.rotate_bytes)
+    outs = [torch.empty(nb, dtype=torch.int32, device=dev) for _ in range(4)]
+    eng = lvkv.Engine(local) if use_engine else None
+    if use_engine:
+        runner = EngineRunner(lvkv, eng, buf, nb, L, stride, crc_off, nrot, window, outs)
+    else:
+        runner = HipRunner(lvkv, buf, nb, L, stride, crc_off, nrot, window, outs, dev)
+    runner.step(0)
+    runner.finish()
+    runner.sync()
+    parity_check(buf, outs[0], nb, L, stride, crc_off, rank, args.config)
 
-    # Steps call the C-ABI entry point directly (lvkv_crc32c_uniform_device,
-    # include/lvkv_crc32c.h) with pre-computed device pointers, so the host
-    # issues launches faster than the GPU retires them.
-    c_uniform = lvkv.lib.lvkv_crc32c_uniform_device
-    bases = [buf.data_ptr() + w * batch_bytes + crc_off for w in range(nrot)]
-    out_ptrs = [o.data_ptr() for o in outs]
-    hstream = stream.cuda_stream
+    if args.isolated:
+        if not use_engine:
+            raise SystemExit("bench: --isolated times the engine kernel")
+        runner.flags = 2
+        for k in range(args.isolated):
+            runner.step(1 + k)
+        eng.wait()
+        return
 
-    def launch(i):
-        rc = c_uniform(bases[i % nrot], stride, L, 0, out_ptrs[i % len(out_ptrs)], nb, 0,
-                       hstreams[i % nstreams])
-        if rc != 0:
-            raise SystemExit(f"bench: lvkv_crc32c_uniform_device failed ({rc})")
-
-    # correctness spot check (outside the timed region) against the oracle
-    sys.path.insert(0, str(REPO / "oracle"))
-    import oracle
-    launch(0)
-    torch.cuda.synchronize()
-    check_n = min(nb, 2000)
-    host = buf[crc_off: crc_off + (check_n - 1) * stride + L].cpu().numpy()
-    want = oracle.uniform(host, check_n, L, stride, threads=8)
-    got = outs[0][:check_n].cpu().numpy().view(np.uint32)
-    if not np.array_equal(got, want):
-        raise SystemExit(f"bench: parity check FAILED on rank {rank}")
-
-    # The kernel's own launch duration (roofline): K launches issued back to
-    # back on ONE stream, before any side stream is used (a process whose
-    # side streams have run measured ~10 % longer single-stream launches).
-    for i in range(args.warmup):
-        c_uniform(bases[(i + 1) % nrot], stride, L, 0, out_ptrs[i & 1], nb, 0, hstream)
-    k0 = torch.cuda.Event(enable_timing=True)
-    k1 = torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    k0.record(stream)
-    for i in range(args.steps):
-        c_uniform(bases[(i + 5) % nrot], stride, L, 0, out_ptrs[i & 1], nb, 0, hstream)
-    k1.record(stream)
-    torch.cuda.synchronize()
-    kern_ms = k0.elapsed_time(k1) / args.steps
-
-    # Labelled secondary figure: the same batch re-read while resident in the
-    # 256 MiB MALL (not the headline; the headline rotates >= 1.25 GiB).
-    warm_us = None
-    if args.config == "headline":
-        torch.cuda.synchronize()
-        w0 = torch.cuda.Event(enable_timing=True)
-        w1 = torch.cuda.Event(enable_timing=True)
-        for _ in range(5):
-            c_uniform(bases[0], stride, L, 0, out_ptrs[0], nb, 0, hstream)
-        w0.record(stream)
-        for _ in range(100):
-            c_uniform(bases[0], stride, L, 0, out_ptrs[0], nb, 0, hstream)
-        w1.record(stream)
-        torch.cuda.synchronize()
-        warm_us = w0.elapsed_time(w1) * 10.0
-
-    for i in range(args.warmup):
-        launch(i + 1)
-    torch.cuda.synchronize()
-
-    # timed region: K back-to-back steps over S streams, barrier + sync on
-    # both sides; an event pair on the default stream (the side streams fork
-    # from and join into it) gives the device-side launch period.
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for s in side:
-        s.wait_stream(stream)
-    for i in range(args.steps):
-        launch(i + 3)
-    for s in side:
-        stream.wait_stream(s)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
-    period_ms = ev0.elapsed_time(ev1) / args.steps
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
-
+    elapsed, nxt = timed_region(runner, comm, args.steps, args.warmup, warm_s, first=1)
     ms_per_step = elapsed / args.steps * 1e3
-    data_bytes = nb * L
-    value = world * data_bytes * args.steps / elapsed / GIB
+    value = world * nb * L * args.steps / elapsed / GIB
     algo_bytes = nb * (L + 4)
-    achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-    achieved_pipe = algo_bytes / (period_ms * 1e-3) / 1e9
+
+    roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": None, "traffic": None, "algo_bytes_per_launch": algo_bytes}
+    if use_engine:
+        # one launch alone (ordered: the engine drains, then the whole-chip kernel)
+        iso = profile_launches(runner, eng, 64, True, nxt)
+        d = [b - a for a, b in iso]
+        kern_us = statistics.mean(d)
+        achieved = algo_bytes / (kern_us * 1e-6) / 1e9
+        # K overlapped launches: device span (first start -> last end) / K
+        runner.step(nxt + 64)
+        eng.wait()
+        pipe = profile_launches(runner, eng, args.steps, False, nxt + 65)
+        span = (max(b for _, b in pipe) - min(a for a, _ in pipe)) / len(pipe)
+        w, c, gr = eng.shape()
+        roof.update({
+            "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": load_pmc_traffic() if args.config == "headline" else None,
+            "kernel": "lvkv_ek_uniform_pair (ordered launch, 2 workgroups x 8 waves per CU)",
+            "kernel_us_avg": round(kern_us, 3), "kernel_us_median": round(statistics.median(d), 3),
+            "kernel_us_min": round(min(d), 3), "launches": len(d),
+            "timing": "HSA packet-processor start/end per dispatch (engine profiling)",
+            "pipelined": {"kernel": f"lvkv_ek_uniform ({w} waves x {c} chains, {gr} workgroups, "
+                                    f"{eng.queues()} queues)",
+                          "launches": len(pipe), "period_us": round(span, 3),
+                          "achieved": round(algo_bytes / (span * 1e-6) / 1e9, 1),
+                          "frac": round(algo_bytes / (span * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                          "launch_us_avg": round(statistics.mean(b - a for a, b in pipe), 3)}})
+    else:
+        roof.update({"kernel": "HIP launch path (two streams)", "achieved":
+                     round(algo_bytes / (ms_per_step * 1e-3) / 1e9, 1)})
+        roof["frac"] = round(roof["achieved"] / HBM_PEAK_GBS, 4)
+        roof["timing"] = "host wall of the timed region / K (no per-launch device timing)"
+
+    split = None
+    if args.config == "headline" and not args.no_split:
+        del buf, outs
+        torch.cuda.empty_cache()
+        split_runner, split = split_measure(
+            lambda s, c: _split_runner(torch, lvkv, eng, dev, rank, s, c), comm, rank, world,
+            min(args.steps, 20), 2, warm_s)
+        del split_runner
+        torch.cuda.empty_cache()
 
     if rank == 0:
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.cpu_seconds)
-        traffic = load_pmc_traffic() if args.config == "headline" else None
-        line = {
-            "metric": "device-resident CRC32C GiB/s over 10k×4KiB blocks; % of MI355X HBM peak",
-            "value": round(value, 2),
-            "unit": "GiB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 5),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32",
-            "data": "synthetic (uniform random bytes, device-generated), resident in HBM",
-            "pct_hbm_peak": round(100.0 * value * GIB / 1e9 / HBM_PEAK_GBS, 2),
-            "config": {"workload": desc, "nblocks_per_gpu": nb, "block_bytes": L,
-                       "stride": stride, "rotation_buffers": nrot,
-                       "rotation_bytes": nrot * batch_bytes,
-                       "streams": nstreams,
-                       "parallelism": f"{world} independent block slices (no collective)"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic,
-                         "kernel_us_avg": round(kern_ms * 1e3, 3),
-                         "pipelined": {"streams": nstreams,
-                                       "period_us": round(period_ms * 1e3, 3),
-                                       "achieved": round(achieved_pipe, 1),
-                                       "frac": round(achieved_pipe / HBM_PEAK_GBS, 4)},
-                         "warm_mall_us_avg": None if warm_us is None else round(warm_us, 3),
-                         "algo_bytes_per_launch": algo_bytes},
-            "cpu_baseline": cpu,
-        }
+        line = _line_base(args, world, value, ms_per_step / 1e3, {
+            "workload": desc, "nblocks_per_gpu": nb, "block_bytes": L, "stride": stride,
+            "rotation_buffers": nrot, "rotation_bytes": nrot * window,
+            "path": "AQL engine, batches overlapped" if use_engine else "HIP launch, 2 streams",
+            "parallelism": f"{world} independent block batches (no collective)"})
+        line["pct_hbm_peak"] = round(100.0 * value * GIB / 1e9 / HBM_PEAK_GBS / world, 2)
+        line["roofline"] = roof
+        line["split"] = split
+        line["cpu_baseline"] = (cpu_baseline(args.cpu_seconds)
+                                if world == 1 and not args.no_cpu_baseline else None)
         print(json.dumps(line), flush=True)
+    _end(world)
+
+
+def _split_runner(torch, lvkv, eng, dev, rank, start, count):
+    """This rank's slice [start, start + count) of the config-5 batch,
+    resident in its HBM, checksummed through the engine."""
+    gen = torch.Generator(device=dev).manual_seed(0x5EED + start)
+    buf = torch.randint(0, 256, (max(count, 1) * BLOCK,), dtype=torch.uint8, device=dev,
+                        generator=gen)
+    outs = [torch.empty(max(count, 1), dtype=torch.int32, device=dev) for _ in range(2)]
+    r = EngineRunner(lvkv, eng, buf, count, BLOCK, BLOCK, 0, 1, 0, outs)
+    r.step(0)
+    r.finish()
+    r.sync()
+    if count:
+        parity_check(buf, outs[0], count, BLOCK, BLOCK, 0, rank, "split")
+    r.buf = buf
+    return r
+
+
+def _line_base(args, world, value, sec_per_step, config):
+    return {"metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(sec_per_step * 1e3, 5), "higher_is_better": True,
+            "scaling": "weak" if args.config != "blocks1m_split" else "strong",
+            "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (uniform random bytes, device-generated), resident in HBM",
+            "warmup_ms_min": args.warmup_ms, "config": config}
+
+
+def _end(world):
     if world > 1:
-        torch.distributed.destroy_process_group()
+        import torch.distributed as dist
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

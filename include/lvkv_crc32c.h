@@ -34,8 +34,10 @@ extern "C" {
 /* Store crc32c::Mask(crc) instead of crc (util/crc32c.h:29-32): the value
  * TableBuilder::WriteRawBlock / log::Writer put on disk. */
 #define LVKV_FLAG_MASK 1u
-/* Engine submits only: this dispatch waits for every earlier dispatch of the
- * engine to complete (AQL barrier bit). Without it, dispatches may overlap. */
+/* Engine submits only: the batch runs alone — it starts after every earlier
+ * dispatch of the engine has completed (host drain of the other queues + AQL
+ * barrier bit) and uses the kernel shaped for the whole chip. Without it,
+ * consecutive batches overlap, each on half of every CU. */
 #define LVKV_FLAG_ORDERED 2u
 
 /* ---- per-call, host CPU: the drop-in for the reference's own symbols ---- */
@@ -101,8 +103,22 @@ void lvkv_engine_destroy(lvkv_engine* engine);
 int lvkv_engine_crc32c_uniform(lvkv_engine* engine, const void* d_base, uint64_t stride,
                                uint32_t length, uint32_t init, uint32_t* d_out,
                                size_t nblocks, uint32_t flags);
-/* Blocks until every dispatch submitted so far has completed. */
+/* Blocks until every dispatch submitted so far has completed (a barrier
+ * packet on every queue, system-scope release, host spin-wait). */
 int lvkv_engine_wait(lvkv_engine* engine);
+/* Hardware queues the dispatches rotate over (1..4; default 3); 0 queries. */
+int lvkv_engine_queues(lvkv_engine* engine, int nqueues);
+/* Kernel shape: waves and chains per workgroup, workgroups per dispatch. */
+int lvkv_engine_shape(lvkv_engine* engine, uint32_t* waves, uint32_t* chains,
+                      uint32_t* groups);
+/* Per-dispatch timing (the engine's HIP-event counterpart): with profiling on,
+ * every dispatch carries a completion signal and the packet processor's start
+ * and end times of it are logged (HSA system clock, us); _read copies those
+ * of the most recent dispatches (up to n, in submission order), returns how
+ * many and clears the log. */
+int lvkv_engine_profile(lvkv_engine* engine, int enable);
+long lvkv_engine_profile_read(lvkv_engine* engine, double* start_us, double* end_us,
+                              size_t n);
 
 /* Batched leveldb::ReadBlock checksum test (table/format.cc:92-99): block i
  * is the BlockHandle {d_offsets[i], d_sizes[i]} of an SST image at d_file;

@@ -44,20 +44,16 @@ void lvkv_debug_set_stamps(uint64_t* d_stamps);
 int lvkv_debug_read_bw(const void* d_data, uint64_t bytes, uint32_t* d_scratch,
                        int groups, void* stream);
 
-/* Engine knobs (tools/probe A/B timing); waits for outstanding work first.
- * option 0: kernel variant (0 = row tables generated from the Z_256 columns,
- *           1 = copied from HBM); 1: kernargs in VRAM through the BAR (1) or
- *           in system memory (0); 2 / 3: acquire / release fence scope
- *           (1 = agent, 2 = system); 4: returns whether VRAM kernargs are on;
- *           5: a completion signal on every dispatch (1) or fence packets
- *           only (0); 6: read the HDP flush register back after a flush;
- *           7: hardware queues the dispatches rotate over (1..4). */
+/* Engine probes (tools/probe). Each waits for outstanding work first. */
 struct lvkv_engine;
-int lvkv_engine_set_option(struct lvkv_engine* engine, int option, int value);
-/* Probes: dispatch the timestamp build of the engine kernel; dispatch k
- * writes 8 u64 per wave (s_memrealtime, 100 MHz; slots 0 start, 1 loads
- * issued, 2 image built, 3 walk done, 4 stored) into area k % areas of
- * d_stamps (areas x CUs x 2 x 8 waves x 8 u64). NULL turns it off. */
+/* Kernels of overlapped and of ordered dispatches: 0 = 8 waves x 5 chains,
+ * one workgroup per CU per dispatch (overlapped default); 1 = 8 x 3, two
+ * workgroups per CU (ordered default). */
+int lvkv_engine_set_variant(struct lvkv_engine* engine, int variant, int ordered_variant);
+/* Dispatch the timestamp build of the current kernel: dispatch k writes 8 u64
+ * per wave (s_memrealtime, 100 MHz; slots 0 start, 1 loads issued, 2 image
+ * built, 3 walk done, 4 stored) into area k % areas of d_stamps (areas x
+ * groups x waves x 8 u64, lvkv_engine_shape). NULL turns it off. */
 int lvkv_engine_set_stamps(struct lvkv_engine* engine, uint64_t* d_stamps, uint64_t areas);
 
 #ifdef __cplusplus

@@ -21,7 +21,7 @@ from typing import Optional, Tuple
 __all__ = [
     "Extend", "Value", "Mask", "Unmask", "kMaskDelta",
     "crc32c_batch", "crc32c_uniform", "sst_verify", "log_verify",
-    "crc32c_batch_host", "LvkvError", "lib", "LIB_PATH", "device_groups",
+    "crc32c_batch_host", "LvkvError", "lib", "LIB_PATH", "device_groups", "Engine",
 ]
 
 LIB_PATH = Path(__file__).resolve().parent / "liblvkv_crc32c.so"
@@ -29,6 +29,7 @@ kMaskDelta = 0xA282EAD8  # util/crc32c.h:22
 
 LVKV_OK = 0
 LVKV_FLAG_MASK = 1
+LVKV_FLAG_ORDERED = 2
 
 
 class LvkvError(RuntimeError):
@@ -89,6 +90,24 @@ def _load() -> ctypes.CDLL:
     L.lvkv_log_verify_device.restype = i32
     L.lvkv_crc32c_batch_host.argtypes = [vp, vp, vp, vp, u32, vp, sz, u32]
     L.lvkv_crc32c_batch_host.restype = i32
+    L.lvkv_engine_create.argtypes = [i32, ctypes.POINTER(vp)]
+    L.lvkv_engine_create.restype = i32
+    L.lvkv_engine_destroy.argtypes = [vp]
+    L.lvkv_engine_destroy.restype = None
+    L.lvkv_engine_crc32c_uniform.argtypes = [vp, vp, u64, u32, u32, vp, sz, u32]
+    L.lvkv_engine_crc32c_uniform.restype = i32
+    L.lvkv_engine_wait.argtypes = [vp]
+    L.lvkv_engine_wait.restype = i32
+    L.lvkv_engine_queues.argtypes = [vp, i32]
+    L.lvkv_engine_queues.restype = i32
+    L.lvkv_engine_shape.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32),
+                                    ctypes.POINTER(u32)]
+    L.lvkv_engine_shape.restype = i32
+    L.lvkv_engine_profile.argtypes = [vp, i32]
+    L.lvkv_engine_profile.restype = i32
+    L.lvkv_engine_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(ctypes.c_double), sz]
+    L.lvkv_engine_profile_read.restype = ctypes.c_long
     L.lvkv_strerror.argtypes = [i32]
     L.lvkv_strerror.restype = ctypes.c_char_p
     L.lvkv_last_hip_error.argtypes = []
@@ -485,3 +504,81 @@ def crc32c_batch_host(data, offsets, lengths, *, init: int = 0, inits=None,
         ctypes.c_void_p(out.ctypes.data), n, LVKV_FLAG_MASK if mask else 0)
     _check("lvkv_crc32c_batch_host", rc)
     return out
+
+
+# --------------------------------------------------------------------------
+# the AQL engine (lvkv_engine_*): batches dispatched into hardware queues
+
+
+class Engine:
+    """Per-device batch engine (include/lvkv_crc32c.h, lvkv_engine_*): a
+    submit writes AQL dispatch packets into the engine's own hardware queues
+    (no HIP launch), consecutive batches overlap on the device, ``wait()``
+    fences every queue. Inputs must be complete before a submit (synchronize
+    the stream that produced them); results are valid after ``wait()``.
+
+    Same results as ``crc32c_uniform`` for blocks of 4..4348 bytes whose
+    ends are 4-byte aligned."""
+
+    def __init__(self, device=None):
+        torch = _torch()
+        dev = torch.device("cuda", torch.cuda.current_device() if device is None else
+                           (device.index if isinstance(device, torch.device) else int(device)))
+        h = ctypes.c_void_p()
+        _check("lvkv_engine_create", _lib.lvkv_engine_create(dev.index, ctypes.byref(h)))
+        self.device = dev
+        self.handle = h
+        # the raw entry, for callers that pass pointers themselves (bench.py)
+        self.submit_ptr = _lib.lvkv_engine_crc32c_uniform
+
+    def crc32c_uniform(self, buf, nblocks: int, length: int, stride: Optional[int] = None, *,
+                       init: int = 0, mask: bool = False, ordered: bool = False, out=None):
+        torch = _torch()
+        stride = length if stride is None else stride
+        if nblocks and (nblocks - 1) * stride + length > buf.numel():
+            raise ValueError("blocks exceed the buffer")
+        out = _u32_out(torch, nblocks, buf.device, out)
+        flags = (LVKV_FLAG_MASK if mask else 0) | (LVKV_FLAG_ORDERED if ordered else 0)
+        # the engine does not follow HIP streams: the inputs must be complete
+        torch.cuda.current_stream(buf.device).synchronize()
+        rc = _lib.lvkv_engine_crc32c_uniform(
+            self.handle, _dev_ptr(buf, "buf", (torch.uint8, torch.int8)), stride, length,
+            init & 0xFFFFFFFF, _dev_ptr(out, "out", (torch.int32,), nblocks), nblocks, flags)
+        _check("lvkv_engine_crc32c_uniform", rc)
+        return out
+
+    def wait(self) -> None:
+        _check("lvkv_engine_wait", _lib.lvkv_engine_wait(self.handle))
+
+    def queues(self, n: int = 0) -> int:
+        r = int(_lib.lvkv_engine_queues(self.handle, n))
+        _check("lvkv_engine_queues", r if r < 0 else 0)
+        return r
+
+    def shape(self):
+        w, c, g = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        _check("lvkv_engine_shape", _lib.lvkv_engine_shape(self.handle, ctypes.byref(w),
+                                                            ctypes.byref(c), ctypes.byref(g)))
+        return w.value, c.value, g.value
+
+    def profile(self, enable: bool) -> None:
+        _check("lvkv_engine_profile", _lib.lvkv_engine_profile(self.handle, int(enable)))
+
+    def profile_read(self, n: int = 4096):
+        """[(start_us, end_us)] of the most recent profiled dispatches, in
+        submission order (HSA system clock)."""
+        t0, t1 = (ctypes.c_double * n)(), (ctypes.c_double * n)()
+        k = int(_lib.lvkv_engine_profile_read(self.handle, t0, t1, n))
+        _check("lvkv_engine_profile_read", k if k < 0 else 0)
+        return list(zip(t0[:k], t1[:k]))
+
+    def close(self) -> None:
+        if self.handle:
+            _lib.lvkv_engine_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass

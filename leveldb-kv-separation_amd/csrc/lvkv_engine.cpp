@@ -1,27 +1,37 @@
-// The AQL engine: a per-device hardware queue that the batch kernels are
-// dispatched into directly (include/lvkv_crc32c.h, lvkv_engine_*).
+// The AQL engine: batches dispatched straight into per-device hardware queues
+// (include/lvkv_crc32c.h, lvkv_engine_*).
 //
-// Why: a hipLaunchKernel costs 2.7-7 us of host time on this stack (measured,
-// tools/probe), about as long as the 10k x 4 KiB kernel itself (7-9 us), so a
-// checksum service that launches one batch per call through HIP is paced by
-// the host, and HIP on gfx9 offers no launch that may overlap the previous
-// kernel of its stream (hipExtAnyOrderLaunch is unsupported there). The
-// engine writes 64-byte AQL kernel-dispatch packets into its own user-mode
-// queue (HSA runtime) and rings the doorbell: well under a microsecond per
-// batch, and packets are issued without the barrier bit, so the packet
-// processor starts dispatching batch i+1's workgroups while batch i's are
-// still running (independent batches, distinct output arrays).
+// Why (measured, tools/probe):
+//   * a hipLaunchKernel costs 2.7-7 us of host time on this stack, as long as
+//     the 10k x 4 KiB kernel itself (~7-9 us), so one-batch-per-call through
+//     HIP is paced by the host; a submit here writes one 64-byte AQL packet
+//     and its kernarg slot: ~1 us from Python;
+//   * one AQL queue runs its dispatches one after another even without the
+//     barrier bit (the next starts when the previous ends, timestamps in
+//     profiles/), so the engine rotates dispatches over several hardware
+//     queues: dispatch i goes to queue i % nq, and consecutive batches run
+//     side by side;
+//   * the production kernel takes one workgroup per CU (8 waves x 5 chains,
+//     64 KiB LDS, half of a CU's waves), so the next dispatch's workgroups
+//     are resident beside the running ones instead of waiting for them.
 //
 // The kernels come from a gfx950 code object embedded in this library
 // (lvkv_engine_kernels.hip, assembled in by lvkv_engine_co.S) and loaded with
 // the HSA loader. They read no hidden kernel arguments, so the kernarg
 // segment is exactly UniformArgs.
 //
-// Ordering: engine dispatches are not ordered with HIP streams. Inputs must be
-// complete before a submit (synchronize the producing stream), results are
-// complete after lvkv_engine_wait (system-scope release at every kernel end).
-// Kernarg slots and completion signals form a ring of kSlots; a submit that
-// would reuse a slot first waits for the dispatch that last used it.
+// Memory model (gfx950: one L2 per XCD, not coherent with each other):
+//   * kernargs live in VRAM, written through the PCIe BAR, then an HDP flush
+//     (the path HIP's device kernargs take); a ring of kSlots slots, and a
+//     slot is reused only after a fence covering its previous dispatch;
+//   * the first dispatch of every submit acquires at agent scope (inputs other
+//     agents wrote and released are seen); the rest of a submit's dispatches
+//     acquire nothing; no dispatch releases;
+//   * lvkv_engine_wait (and the slot-reuse fence) puts a barrier-AND packet on
+//     every queue in use, acquire and release at system scope: results are
+//     visible to the host, to HIP streams and to copy engines after it.
+// Engine dispatches are not ordered with HIP streams: synchronise the stream
+// that produced the input before submitting.
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
@@ -45,31 +55,31 @@ uint32_t* device_tables(int* rc);  // lvkv_capi.cpp: per-device tables (d_tables
 
 namespace {
 
-constexpr uint32_t kSlots = 1024;    // kernarg slots (one per dispatch in flight)
-constexpr uint32_t kSigSlots = 64;   // per-dispatch signals (option 5 only)
+constexpr uint32_t kSlots = 1024;       // kernarg slots (dispatches between fences)
 constexpr uint32_t kSlotBytes = 256;
 constexpr uint32_t kQueuePackets = 1024;
-constexpr int kMaxQueues = 4;  // hardware queues per engine (dispatch i -> queue i % nq)
+constexpr int kQueues = 4;              // hardware queues per engine
+constexpr int kDefaultQueues = 3;       // in use by default (measured best)
+constexpr uint32_t kProfSlots = 64;     // completion signals while profiling
+constexpr uint32_t kProfLog = 4096;     // dispatch durations kept
 
 struct EngineKernel {
   uint64_t object = 0;
   uint32_t kernarg_size = 0, group_size = 0, private_size = 0;
-  uint32_t waves = 8, chains = 3, per_cu = 2;  // shape: workgroups per CU per dispatch
+  uint32_t waves = 8, chains = 5, per_cu = 1;  // shape; per_cu = workgroups per CU
 };
 
-// The engine's kernels (lvkv_engine_kernels.hip): name, shape, and the
-// timestamp build of the same schedule (probes).
+// The engine's kernels (lvkv_engine_kernels.hip): symbol, timestamp build,
+// shape. [0] is the production schedule.
 struct KernelSpec {
   const char* name;
   const char* stamps;
   uint32_t waves, chains, per_cu;
 };
 constexpr KernelSpec kSpecs[] = {
-    {"lvkv_engine_uniform_burst.kd", "lvkv_engine_uniform_burst_stamps.kd", 8, 3, 2},
-    {"lvkv_engine_uniform_burst_rows.kd", "lvkv_engine_uniform_burst_stamps.kd", 8, 3, 2},
-    {"lvkv_engine_uniform_half.kd", "lvkv_engine_uniform_half_stamps.kd", 8, 5, 1},
-    {"lvkv_engine_uniform_half_late.kd", "lvkv_engine_uniform_half_late_stamps.kd", 8, 5, 1},
-    {"lvkv_engine_uniform_burst_late.kd", "lvkv_engine_uniform_burst_stamps.kd", 8, 3, 2},
+    {"lvkv_ek_uniform.kd", "lvkv_ek_uniform_stamps.kd", 8, 5, 1},
+    {"lvkv_ek_uniform_pair.kd", "lvkv_ek_uniform_pair_stamps.kd", 8, 3,
+     2},
 };
 constexpr int kNumSpecs = static_cast<int>(sizeof(kSpecs) / sizeof(kSpecs[0]));
 
@@ -99,28 +109,12 @@ hsa_status_t match_agent(hsa_agent_t agent, void* data) {
   return HSA_STATUS_SUCCESS;
 }
 
-hsa_status_t find_kernarg_region(hsa_region_t region, void* data) {
-  hsa_region_segment_t seg;
-  if (hsa_region_get_info(region, HSA_REGION_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS ||
-      seg != HSA_REGION_SEGMENT_GLOBAL)
-    return HSA_STATUS_SUCCESS;
-  uint32_t flags = 0;
-  if (hsa_region_get_info(region, HSA_REGION_INFO_GLOBAL_FLAGS, &flags) != HSA_STATUS_SUCCESS)
-    return HSA_STATUS_SUCCESS;
-  if (flags & HSA_REGION_GLOBAL_FLAG_KERNARG) {
-    *static_cast<hsa_region_t*>(data) = region;
-    return HSA_STATUS_INFO_BREAK;
-  }
-  return HSA_STATUS_SUCCESS;
-}
-
 struct PoolFind {
   hsa_amd_memory_pool_t pool;
   bool found;
 };
 
-// The device's coarse-grained VRAM pool (kernargs live there when the host
-// can write it through the PCIe BAR, as HIP's own device kernargs do).
+// The device's coarse-grained VRAM pool.
 hsa_status_t find_vram_pool(hsa_amd_memory_pool_t pool, void* data) {
   hsa_amd_segment_t seg;
   uint32_t flags = 0;
@@ -153,6 +147,22 @@ hsa_status_t find_cpu(hsa_agent_t agent, void* data) {
   return HSA_STATUS_SUCCESS;
 }
 
+// Fallback kernarg memory (system memory) when the BAR path is unavailable.
+hsa_status_t find_kernarg_region(hsa_region_t region, void* data) {
+  hsa_region_segment_t seg;
+  if (hsa_region_get_info(region, HSA_REGION_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS ||
+      seg != HSA_REGION_SEGMENT_GLOBAL)
+    return HSA_STATUS_SUCCESS;
+  uint32_t flags = 0;
+  if (hsa_region_get_info(region, HSA_REGION_INFO_GLOBAL_FLAGS, &flags) != HSA_STATUS_SUCCESS)
+    return HSA_STATUS_SUCCESS;
+  if (flags & HSA_REGION_GLOBAL_FLAG_KERNARG) {
+    *static_cast<hsa_region_t*>(data) = region;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
 std::once_flag g_hsa_once;
 hsa_status_t g_hsa_status = HSA_STATUS_ERROR_NOT_INITIALIZED;
 
@@ -160,31 +170,35 @@ hsa_status_t g_hsa_status = HSA_STATUS_ERROR_NOT_INITIALIZED;
 
 struct Engine {
   int device = -1;
+  int cus = 0;
   hsa_agent_t agent{};
-  hsa_queue_t* queues[kMaxQueues] = {};
-  int nq = 2;           // queues in use
-  int cur = 0;          // queue of the packet being written
+  hsa_queue_t* queues[kQueues] = {};
+  int nq = kDefaultQueues;
+  int cur = 0;  // queue of the packet being written
   hsa_executable_t exe{};
   hsa_code_object_reader_t reader{};
   bool exe_ok = false, reader_ok = false;
   EngineKernel kern[kNumSpecs], kern_stamps[kNumSpecs];
-  uint64_t* stamps = nullptr;  // probes: 8 u64 per wave, one area per dispatch
-  uint64_t stamp_next = 0, stamp_areas = 0;
-  uint8_t* kernarg = nullptr;      // system-memory ring (kernarg region)
-  uint8_t* kernarg_dev = nullptr;  // VRAM ring written through the BAR
-  uint32_t* hdp_flush = nullptr;   // HDP_MEM_FLUSH_CNTL: makes BAR writes visible
-  int use_dev_kernarg = 0;
-  int acquire_scope = HSA_FENCE_SCOPE_AGENT, release_scope = HSA_FENCE_SCOPE_SYSTEM;
-  hsa_signal_t sig[kSigSlots];  // per-dispatch completion (signal_mode 1)
-  uint32_t nsig = 0;
-  hsa_signal_t fence_sig{};      // completion of the barrier-AND fence packets (one per queue)
+  int variant = 0;          // kernel of overlapped dispatches
+  int ordered_variant = 1;  // kernel of ordered dispatches (the whole chip)
+  uint8_t* kernarg = nullptr;     // kSlots x kSlotBytes
+  bool kernarg_vram = false;      // BAR-written VRAM (else system memory)
+  uint32_t* hdp_flush = nullptr;  // HDP_MEM_FLUSH_CNTL
+  hsa_signal_t fence_sig{};       // barrier-AND fences, one decrement per queue
   bool fence_ok = false;
-  int signal_mode = 0;           // 0: fences only; 1: a signal per dispatch
-  int hdp_readback = 1;
   uint64_t next = 0;    // dispatches submitted
-  uint64_t fenced = 0;  // every dispatch before this one is known complete
-  int cus = 0;
-  int variant = 0;
+  uint64_t fenced = 0;  // every dispatch before this index is known complete
+  // probes
+  uint64_t* stamps = nullptr;  // 8 u64 per wave, one area per dispatch
+  uint64_t stamp_next = 0, stamp_areas = 0;
+  bool profiling = false;
+  hsa_signal_t prof_sig[kProfSlots];
+  uint32_t nprof_sig = 0;
+  bool prof_pending[kProfSlots] = {};
+  double tick_us = 0;
+  double prof_start[kProfLog];  // us, HSA system clock
+  double prof_end[kProfLog];
+  uint64_t prof_count = 0;
   uint32_t* d_tables = nullptr;
   uint32_t zcol[32];
   std::mutex mu;
@@ -220,13 +234,48 @@ int load_kernel(Engine& e, const char* name, EngineKernel* k) {
 void destroy(Engine* e) {
   for (hsa_queue_t* q : e->queues)
     if (q) hsa_queue_destroy(q);
-  for (uint32_t i = 0; i < e->nsig; ++i) hsa_signal_destroy(e->sig[i]);
+  for (uint32_t i = 0; i < e->nprof_sig; ++i) hsa_signal_destroy(e->prof_sig[i]);
   if (e->fence_ok) hsa_signal_destroy(e->fence_sig);
-  if (e->kernarg) hsa_memory_free(e->kernarg);
-  if (e->kernarg_dev) hsa_amd_memory_pool_free(e->kernarg_dev);
+  if (e->kernarg) {
+    if (e->kernarg_vram)
+      hsa_amd_memory_pool_free(e->kernarg);
+    else
+      hsa_memory_free(e->kernarg);
+  }
   if (e->exe_ok) hsa_executable_destroy(e->exe);
   if (e->reader_ok) hsa_code_object_reader_destroy(e->reader);
   delete e;
+}
+
+// Kernarg ring: VRAM through the BAR when the host may map it and the HDP
+// flush register is exposed, else the agent's system-memory kernarg region.
+bool alloc_kernargs(Engine& e) {
+  PoolFind pf{{}, false};
+  hsa_agent_t cpu{};
+  hsa_amd_hdp_flush_t hdp{nullptr, nullptr};
+  hsa_amd_agent_iterate_memory_pools(e.agent, find_vram_pool, &pf);
+  hsa_iterate_agents(find_cpu, &cpu);
+  void* p = nullptr;
+  if (pf.found && cpu.handle != 0 &&
+      hsa_agent_get_info(e.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_HDP_FLUSH),
+                         &hdp) == HSA_STATUS_SUCCESS &&
+      hdp.HDP_MEM_FLUSH_CNTL != nullptr &&
+      hsa_amd_memory_pool_allocate(pf.pool, kSlots * kSlotBytes, 0, &p) == HSA_STATUS_SUCCESS) {
+    if (hsa_amd_agents_allow_access(1, &cpu, nullptr, p) == HSA_STATUS_SUCCESS) {
+      e.kernarg = static_cast<uint8_t*>(p);
+      e.kernarg_vram = true;
+      e.hdp_flush = hdp.HDP_MEM_FLUSH_CNTL;
+      return true;
+    }
+    hsa_amd_memory_pool_free(p);
+  }
+  hsa_region_t karg{};
+  karg.handle = 0;
+  if (hsa_agent_iterate_regions(e.agent, find_kernarg_region, &karg) == HSA_STATUS_ERROR ||
+      karg.handle == 0)
+    return false;
+  return hsa_memory_allocate(karg, kSlots * kSlotBytes, reinterpret_cast<void**>(&e.kernarg)) ==
+         HSA_STATUS_SUCCESS;
 }
 
 int create(int device, Engine** out) {
@@ -244,8 +293,8 @@ int create(int device, Engine** out) {
   hsa_iterate_agents(match_agent, &m);
   if (!m.found) return LVKV_ERR_NO_DEVICE;
 
-  // The per-device tables of the HIP path (lane columns, zpow) double as the
-  // engine's: allocate them on that device.
+  // The per-device tables of the HIP path (lane columns, zpow) serve the
+  // engine too: allocate them on that device.
   int prev = -1;
   if (hipGetDevice(&prev) != hipSuccess) return LVKV_ERR_HIP;
   if (prev != device && hipSetDevice(device) != hipSuccess) return LVKV_ERR_HIP;
@@ -265,6 +314,9 @@ int create(int device, Engine** out) {
   e->cus = ncu;
   const Gf2Op z = gf2_zero_advance(kRowBytes);
   memcpy(e->zcol, z.col, sizeof(e->zcol));
+  uint64_t freq = 0;
+  hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &freq);
+  e->tick_us = freq ? 1e6 / static_cast<double>(freq) : 0.0;
 
   const size_t co_size = static_cast<size_t>(lvkv_engine_co_end - lvkv_engine_co);
   bool ok =
@@ -286,45 +338,21 @@ int create(int device, Engine** out) {
       k->per_cu = kSpecs[i].per_cu;
     }
   }
-  hsa_region_t karg{};
-  karg.handle = 0;
-  ok = ok && hsa_agent_iterate_regions(e->agent, find_kernarg_region, &karg) !=
-                 HSA_STATUS_ERROR;
-  ok = ok && karg.handle != 0;
-  ok = ok && hsa_memory_allocate(karg, kSlots * kSlotBytes,
-                                 reinterpret_cast<void**>(&e->kernarg)) == HSA_STATUS_SUCCESS;
-  // VRAM kernargs: only where the host may map them (large BAR) and the HDP
-  // flush register is exposed; otherwise the system-memory ring is used.
-  if (ok) {
-    PoolFind pf{{}, false};
-    hsa_agent_t cpu{};
-    hsa_amd_hdp_flush_t hdp{nullptr, nullptr};
-    hsa_amd_agent_iterate_memory_pools(e->agent, find_vram_pool, &pf);
-    hsa_iterate_agents(find_cpu, &cpu);
-    void* p = nullptr;
-    if (pf.found && cpu.handle != 0 &&
-        hsa_agent_get_info(e->agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_HDP_FLUSH),
-                           &hdp) == HSA_STATUS_SUCCESS &&
-        hdp.HDP_MEM_FLUSH_CNTL != nullptr &&
-        hsa_amd_memory_pool_allocate(pf.pool, kSlots * kSlotBytes, 0, &p) == HSA_STATUS_SUCCESS) {
-      if (hsa_amd_agents_allow_access(1, &cpu, nullptr, p) == HSA_STATUS_SUCCESS) {
-        e->kernarg_dev = static_cast<uint8_t*>(p);
-        e->hdp_flush = hdp.HDP_MEM_FLUSH_CNTL;
-        e->use_dev_kernarg = 1;
-      } else {
-        hsa_amd_memory_pool_free(p);
-      }
-    }
-  }
-  for (uint32_t i = 0; ok && i < kSigSlots; ++i) {
-    ok = hsa_signal_create(0, 0, nullptr, &e->sig[i]) == HSA_STATUS_SUCCESS;
-    if (ok) e->nsig = i + 1;
-  }
+  ok = ok && alloc_kernargs(*e);
   ok = ok && hsa_signal_create(0, 0, nullptr, &e->fence_sig) == HSA_STATUS_SUCCESS;
   e->fence_ok = ok;
-  for (int i = 0; ok && i < kMaxQueues; ++i)
+  for (uint32_t i = 0; ok && i < kProfSlots; ++i) {
+    ok = hsa_signal_create(0, 0, nullptr, &e->prof_sig[i]) == HSA_STATUS_SUCCESS;
+    if (ok) e->nprof_sig = i + 1;
+  }
+  for (int i = 0; ok && i < kQueues; ++i)
     ok = hsa_queue_create(e->agent, kQueuePackets, HSA_QUEUE_TYPE_MULTI, queue_error_cb, e,
-                          UINT32_MAX, UINT32_MAX, &e->queues[i]) == HSA_STATUS_SUCCESS;
+                          UINT32_MAX, UINT32_MAX, &e->queues[i]) == HSA_STATUS_SUCCESS &&
+         // Timestamps are written only for packets that carry a completion
+         // signal (profiled dispatches); the queue property is set before
+         // the first packet because the packet processor may not see a later
+         // change.
+         hsa_amd_profiling_set_profiler_enabled(e->queues[i], 1) == HSA_STATUS_SUCCESS;
   if (!ok) {
     destroy(e);
     return LVKV_ERR_HIP;
@@ -333,7 +361,7 @@ int create(int device, Engine** out) {
   return LVKV_OK;
 }
 
-// Next free packet of queue e.cur (single producer: the caller holds e.mu).
+// Next free packet of queue e.cur (the caller holds e.mu).
 void* packet_slot(Engine& e, uint64_t* idx) {
   hsa_queue_t* q = e.queues[e.cur];
   *idx = hsa_queue_add_write_index_screlease(q, 1);
@@ -349,85 +377,86 @@ void publish(Engine& e, void* p, uint16_t header, uint16_t setup, uint64_t idx) 
                              static_cast<hsa_signal_value_t>(idx));
 }
 
-// A barrier-AND packet with the barrier bit on every queue in use: each
-// completes after every earlier packet of its queue has completed, and its
-// system-scope release makes their results visible to the host. Caller holds
-// e.mu; returns the dispatch count covered. The caller then waits for
-// fence_sig < 1 (each packet decrements it once).
-void submit_fence_one(Engine& e);
+// Reads the finished profiled dispatch of signal slot s into the log.
+void collect_profile(Engine& e, uint32_t s) {
+  if (!e.prof_pending[s]) return;
+  hsa_signal_wait_scacquire(e.prof_sig[s], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+                            HSA_WAIT_STATE_ACTIVE);
+  hsa_amd_profiling_dispatch_time_t t{};
+  const hsa_status_t st = hsa_amd_profiling_get_dispatch_time(e.agent, e.prof_sig[s], &t);
+  if (st == HSA_STATUS_SUCCESS) {
+    const uint64_t i = e.prof_count++ % kProfLog;
+    e.prof_start[i] = static_cast<double>(t.start) * e.tick_us;
+    e.prof_end[i] = static_cast<double>(t.end) * e.tick_us;
+  }
+  e.prof_pending[s] = false;
+}
 
-uint64_t submit_fence(Engine& e) {
+// A barrier-AND packet with the barrier bit on every queue in use: each
+// completes after every earlier packet of its queue, acquires and releases
+// at system scope; then wait for all of them. Caller holds e.mu.
+void fence(Engine& e) {
   hsa_signal_store_relaxed(e.fence_sig, e.nq);
   const int keep = e.cur;
   for (int q = 0; q < e.nq; ++q) {
     e.cur = q;
-    submit_fence_one(e);
+    uint64_t idx;
+    hsa_barrier_and_packet_t* p = static_cast<hsa_barrier_and_packet_t*>(packet_slot(e, &idx));
+    p->reserved0 = 0;
+    p->reserved1 = 0;
+    for (int i = 0; i < 5; ++i) p->dep_signal[i].handle = 0;
+    p->reserved2 = 0;
+    p->completion_signal = e.fence_sig;
+    const uint16_t header =
+        static_cast<uint16_t>((HSA_PACKET_TYPE_BARRIER_AND << HSA_PACKET_HEADER_TYPE) |
+                              (1 << HSA_PACKET_HEADER_BARRIER) |
+                              (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                              (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+    publish(e, p, header, 0, idx);
   }
   e.cur = keep;
-  return e.next;
-}
-
-void submit_fence_one(Engine& e) {
-  uint64_t idx;
-  hsa_barrier_and_packet_t* p = static_cast<hsa_barrier_and_packet_t*>(packet_slot(e, &idx));
-  p->reserved0 = 0;
-  p->reserved1 = 0;
-  for (int i = 0; i < 5; ++i) p->dep_signal[i].handle = 0;
-  p->reserved2 = 0;
-  p->completion_signal = e.fence_sig;
-  const uint16_t header =
-      static_cast<uint16_t>((HSA_PACKET_TYPE_BARRIER_AND << HSA_PACKET_HEADER_TYPE) |
-                            (1 << HSA_PACKET_HEADER_BARRIER) |
-                            (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                            (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
-  publish(e, p, header, 0, idx);
-}
-
-void wait_fence(Engine& e) {
   hsa_signal_wait_scacquire(e.fence_sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
                             HSA_WAIT_STATE_ACTIVE);
+  e.fenced = e.next;
+  // oldest first: dispatch n used slot n % kProfSlots
+  for (uint32_t i = 0; i < kProfSlots; ++i)
+    collect_profile(e, static_cast<uint32_t>((e.next + i) % kProfSlots));
 }
 
 // One kernel-dispatch packet; the caller holds e.mu.
-int dispatch(Engine& e, const EngineKernel& k, const UniformArgs& args, uint32_t groups,
-             uint32_t wg, bool barrier) {
+int dispatch(Engine& e, const EngineKernel& k, const UniformArgs& args, bool acquire,
+             bool barrier) {
   if (e.queue_error) return LVKV_ERR_HIP;
   const uint64_t n = e.next;
+  // Kernarg slot n % kSlots was last used by dispatch n - kSlots.
+  if (n - e.fenced >= kSlots) fence(e);
   e.cur = static_cast<int>(n % static_cast<uint64_t>(e.nq));
-  // Kernarg slot n % kSlots was last used by dispatch n - kSlots: fence if
-  // that one is not known complete.
-  if (n - e.fenced >= kSlots) {
-    e.fenced = submit_fence(e);
-    wait_fence(e);
-  }
   hsa_signal_t done{};
-  if (e.signal_mode) {
-    const uint32_t s = static_cast<uint32_t>(n % kSigSlots);
-    if (n >= kSigSlots)
-      hsa_signal_wait_scacquire(e.sig[s], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
-                                HSA_WAIT_STATE_ACTIVE);
-    hsa_signal_store_relaxed(e.sig[s], 1);
-    done = e.sig[s];
+  if (e.profiling) {
+    const uint32_t s = static_cast<uint32_t>(n % kProfSlots);
+    collect_profile(e, s);
+    hsa_signal_store_relaxed(e.prof_sig[s], 1);
+    e.prof_pending[s] = true;
+    done = e.prof_sig[s];
   }
-  const uint32_t slot = static_cast<uint32_t>(n % kSlots);
-  uint8_t* ka = (e.use_dev_kernarg ? e.kernarg_dev : e.kernarg) +
-                static_cast<size_t>(slot) * kSlotBytes;
+  uint8_t* ka = e.kernarg + static_cast<size_t>(n % kSlots) * kSlotBytes;
   memcpy(ka, &args, sizeof(args));
-  if (e.use_dev_kernarg) {
+  if (e.kernarg_vram) {
     // BAR writes are write-combined and may sit in the HDP write cache: fence
-    // them, flush the HDP (and read the register back) before the packet.
-    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    // them, flush the HDP and read the register back (the read completes
+    // only behind the posted writes) before the packet can be seen.
     __builtin_ia32_sfence();
     *reinterpret_cast<volatile uint32_t*>(e.hdp_flush) = 1u;
-    if (e.hdp_readback) (void)*reinterpret_cast<volatile uint32_t*>(e.hdp_flush);
+    (void)*reinterpret_cast<volatile uint32_t*>(e.hdp_flush);
   }
   uint64_t idx;
   hsa_kernel_dispatch_packet_t* p = static_cast<hsa_kernel_dispatch_packet_t*>(packet_slot(e, &idx));
+  const uint32_t wg = 64u * k.waves;
   p->workgroup_size_x = static_cast<uint16_t>(wg);
   p->workgroup_size_y = 1;
   p->workgroup_size_z = 1;
   p->reserved0 = 0;
-  p->grid_size_x = groups * wg;
+  p->grid_size_x = args.ngroups * wg;
   p->grid_size_y = 1;
   p->grid_size_z = 1;
   p->private_segment_size = k.private_size;
@@ -436,14 +465,12 @@ int dispatch(Engine& e, const EngineKernel& k, const UniformArgs& args, uint32_t
   p->kernarg_address = ka;
   p->reserved2 = 0;
   p->completion_signal = done;
-  // Acquire at agent scope (invalidates the scalar cache the kernargs are
-  // read through); release at the configured scope (the fence packet of
-  // lvkv_engine_wait releases at system scope in any case).
-  const uint16_t header =
-      static_cast<uint16_t>((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
-                            ((barrier ? 1 : 0) << HSA_PACKET_HEADER_BARRIER) |
-                            (e.acquire_scope << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                            (e.release_scope << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+  const uint16_t header = static_cast<uint16_t>(
+      (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+      ((barrier ? 1 : 0) << HSA_PACKET_HEADER_BARRIER) |
+      ((acquire ? HSA_FENCE_SCOPE_AGENT : HSA_FENCE_SCOPE_NONE)
+       << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+      (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
   publish(e, p, header, 1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS, idx);
   e.next = n + 1;
   return LVKV_OK;
@@ -466,9 +493,8 @@ int lvkv_engine_create(int device, lvkv_engine** out) {
 
 void lvkv_engine_destroy(lvkv_engine* eng) {
   if (eng == nullptr) return;
-  Engine* e = reinterpret_cast<Engine*>(eng);
   (void)lvkv_engine_wait(eng);
-  destroy(e);
+  destroy(reinterpret_cast<Engine*>(eng));
 }
 
 int lvkv_engine_crc32c_uniform(lvkv_engine* eng, const void* d_base, uint64_t stride,
@@ -477,15 +503,21 @@ int lvkv_engine_crc32c_uniform(lvkv_engine* eng, const void* d_base, uint64_t st
   if (eng == nullptr) return LVKV_ERR_INVALID;
   if (nblocks == 0) return LVKV_OK;
   if (!d_base || !d_out || length < 4 || length > kRowsPerChunk * kRowBytes || stride % 4 != 0 ||
-      (reinterpret_cast<uintptr_t>(d_base) + length) % 4 != 0)
+      (reinterpret_cast<uintptr_t>(d_base) + length) % 4 != 0 || nblocks > (size_t{1} << 40))
     return LVKV_ERR_INVALID;
   Engine* e = reinterpret_cast<Engine*>(eng);
   std::lock_guard<std::mutex> lk(e->mu);
-  const EngineKernel& k = e->stamps ? e->kern_stamps[e->variant] : e->kern[e->variant];
+  const bool ordered = (flags & LVKV_FLAG_ORDERED) != 0;
+  // An ordered batch runs alone: the other queues drain first (the barrier
+  // bit orders a packet only within its own queue), and it gets the kernel
+  // shaped for the whole chip.
+  if (ordered && e->nq > 1 && e->fenced != e->next) fence(*e);
+  const int v = ordered ? e->ordered_variant : e->variant;
+  const EngineKernel& k = e->stamps ? e->kern_stamps[v] : e->kern[v];
   const uint64_t groups = static_cast<uint64_t>(e->cus) * k.per_cu;
   const uint64_t cap = groups * k.waves * k.chains;
-  // Batches beyond one dispatch's capacity go out as several dispatches of
-  // equal size (all without the barrier bit, except the first if ordered).
+  // A batch beyond one dispatch's capacity goes out as several dispatches of
+  // equal size, rotating over the queues like separate batches.
   const uint64_t nd = (nblocks + cap - 1) / cap;
   const uint64_t per = nblocks / nd, extra = nblocks % nd;
   uint64_t done = 0;
@@ -507,11 +539,11 @@ int lvkv_engine_crc32c_uniform(lvkv_engine* eng, const void* d_base, uint64_t st
     a.ngroups = static_cast<uint32_t>(std::min<uint64_t>(groups, (n + 2) / 3));
     memcpy(a.zcol, e->zcol, sizeof(a.zcol));
     if (e->stamps) {
-      const uint64_t per = groups * k.waves * 8;
-      a.stamps = e->stamps + (e->stamp_next++ % e->stamp_areas) * per;
+      const uint64_t area = groups * k.waves * 8;
+      a.stamps = e->stamps + (e->stamp_next++ % e->stamp_areas) * area;
     }
-    const int rc =
-        dispatch(*e, k, a, a.ngroups, 64 * k.waves, (flags & LVKV_FLAG_ORDERED) && i == 0);
+    const int rc = dispatch(*e, k, a, /*acquire=*/i == 0,
+                            /*barrier=*/ordered);
     if (rc != LVKV_OK) return rc;
     done += n;
   }
@@ -522,58 +554,79 @@ int lvkv_engine_wait(lvkv_engine* eng) {
   if (eng == nullptr) return LVKV_ERR_INVALID;
   Engine* e = reinterpret_cast<Engine*>(eng);
   std::lock_guard<std::mutex> lk(e->mu);
-  if (e->fenced != e->next) {
-    const uint64_t covered = submit_fence(*e);
-    wait_fence(*e);
-    e->fenced = covered;
-  }
+  if (e->fenced != e->next) fence(*e);
   return e->queue_error ? LVKV_ERR_HIP : LVKV_OK;
+}
+
+int lvkv_engine_queues(lvkv_engine* eng, int nq) {
+  if (eng == nullptr || nq < 0 || nq > kQueues) return LVKV_ERR_INVALID;
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (nq == 0) return e->nq;
+  if (e->fenced != e->next) fence(*e);
+  e->nq = nq;
+  return nq;
+}
+
+int lvkv_engine_profile(lvkv_engine* eng, int enable) {
+  if (eng == nullptr) return LVKV_ERR_INVALID;
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (e->fenced != e->next) fence(*e);
+  e->profiling = enable != 0;
+  e->prof_count = 0;
+  return LVKV_OK;
+}
+
+long lvkv_engine_profile_read(lvkv_engine* eng, double* start_us, double* end_us, size_t n) {
+  if (eng == nullptr || ((start_us == nullptr || end_us == nullptr) && n != 0))
+    return LVKV_ERR_INVALID;
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (e->fenced != e->next) fence(*e);
+  const uint64_t have = std::min<uint64_t>(e->prof_count, kProfLog);
+  const uint64_t take = std::min<uint64_t>(have, n);
+  for (uint64_t i = 0; i < take; ++i) {
+    const uint64_t j = (e->prof_count - take + i) % kProfLog;
+    start_us[i] = e->prof_start[j];
+    end_us[i] = e->prof_end[j];
+  }
+  e->prof_count = 0;
+  return static_cast<long>(take);
 }
 
 int lvkv_engine_set_stamps(lvkv_engine* eng, uint64_t* d_stamps, uint64_t areas) {
   if (eng == nullptr || (d_stamps != nullptr && areas == 0)) return LVKV_ERR_INVALID;
   Engine* e = reinterpret_cast<Engine*>(eng);
-  (void)lvkv_engine_wait(eng);
   std::lock_guard<std::mutex> lk(e->mu);
+  if (e->fenced != e->next) fence(*e);
   e->stamps = d_stamps;
   e->stamp_areas = areas;
   e->stamp_next = 0;
   return LVKV_OK;
 }
 
-int lvkv_engine_set_option(lvkv_engine* eng, int option, int value) {
+int lvkv_engine_set_variant(lvkv_engine* eng, int variant, int ordered_variant) {
+  if (eng == nullptr || variant < 0 || variant >= kNumSpecs || ordered_variant < 0 ||
+      ordered_variant >= kNumSpecs)
+    return LVKV_ERR_INVALID;
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (e->fenced != e->next) fence(*e);
+  e->variant = variant;
+  e->ordered_variant = ordered_variant;
+  return LVKV_OK;
+}
+
+int lvkv_engine_shape(lvkv_engine* eng, uint32_t* waves, uint32_t* chains, uint32_t* groups) {
   if (eng == nullptr) return LVKV_ERR_INVALID;
   Engine* e = reinterpret_cast<Engine*>(eng);
-  (void)lvkv_engine_wait(eng);
   std::lock_guard<std::mutex> lk(e->mu);
-  switch (option) {
-    case 0:
-      if (value < 0 || value >= kNumSpecs) return LVKV_ERR_INVALID;
-      e->variant = value;
-      return LVKV_OK;
-    case 1:
-      if (value && e->kernarg_dev == nullptr) return LVKV_ERR_INVALID;
-      e->use_dev_kernarg = value ? 1 : 0;
-      return LVKV_OK;
-    case 2:
-    case 3:
-      if (value < HSA_FENCE_SCOPE_NONE || value > HSA_FENCE_SCOPE_SYSTEM) return LVKV_ERR_INVALID;
-      (option == 2 ? e->acquire_scope : e->release_scope) = value;
-      return LVKV_OK;
-    case 4:
-      return e->use_dev_kernarg;
-    case 5:
-      e->signal_mode = value ? 1 : 0;
-      return LVKV_OK;
-    case 6:
-      e->hdp_readback = value ? 1 : 0;
-      return LVKV_OK;
-    case 7:
-      if (value < 1 || value > kMaxQueues) return LVKV_ERR_INVALID;
-      e->nq = value;
-      return LVKV_OK;
-  }
-  return LVKV_ERR_INVALID;
+  const EngineKernel& k = e->kern[e->variant];
+  if (waves) *waves = k.waves;
+  if (chains) *chains = k.chains;
+  if (groups) *groups = static_cast<uint32_t>(e->cus) * k.per_cu;
+  return LVKV_OK;
 }
 
 }  // extern "C"

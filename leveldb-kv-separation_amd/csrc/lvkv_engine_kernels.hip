@@ -1,69 +1,49 @@
 // Kernels dispatched by the AQL engine (lvkv_engine.cpp). Compiled on their
-// own into a gfx950 code object (--genco) that is embedded in
-// liblvkv_crc32c.so and loaded through the HSA loader, so the engine can
-// write dispatch packets straight into its own hardware queue. The entry
-// points are extern "C" (stable symbol names) and read no hidden kernel
-// arguments: the workgroup count comes from UniformArgs::ngroups.
+// own into a gfx950 code object (--cuda-device-only, unbundled) that is
+// embedded in liblvkv_crc32c.so and loaded through the HSA loader, so the
+// engine can write dispatch packets straight into its own hardware queues.
+// The entry points are extern "C" (stable symbol names) and read no hidden
+// kernel arguments: the workgroup count comes from UniformArgs::ngroups.
+//
+// Arithmetic and schedule: crc32c_burst.h (util/crc32c.cc:276-377 restated
+// as an end-aligned Horner walk over 256-byte rows).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "crc32c_burst.h"
 #include "lvkv_kernel_args.h"
 
-// Uniform batches of blocks <= 16 rows (4 KiB + 252 B), <= 24 blocks per
-// workgroup of 8 waves, two workgroups per CU (crc32c_burst.h).
-extern "C" __global__ void __launch_bounds__(512, 2)
-    lvkv_engine_uniform_burst(lvkv::UniformArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::kCompactLdsBytes / 4];
-  lvkv::burst_kernel_body<0, 8, 3>(a, lds, a.ngroups);
+namespace {
+constexpr int kLds = lvkv::kCompactLdsBytes / 4;
 }
 
-// The same with the row tables copied from the Z_256 set of zpow (HBM/L2)
-// instead of generated from the columns.
+// Production: one 512-thread workgroup per CU per dispatch, 8 waves x 5
+// chains (40 blocks of <= 16 rows). It holds half of a CU's waves and 64 KiB
+// of its LDS, so the next dispatch (another queue) runs beside it. Chain 0's
+// row loads go out before the LDS image is built, the other chains' after.
 extern "C" __global__ void __launch_bounds__(512, 2)
-    lvkv_engine_uniform_burst_rows(lvkv::UniformArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::kCompactLdsBytes / 4];
-  lvkv::burst_kernel_body<lvkv::kBurstRowsHbm, 8, 3>(a, lds, a.ngroups);
-}
-
-// One workgroup per CU per dispatch (8 waves x 5 chains = 40 blocks): a
-// dispatch takes half of each CU's LDS and waves, so the next dispatch's
-// workgroups are resident beside it and the two overlap (the engine issues
-// dispatches without the barrier bit).
-extern "C" __global__ void __launch_bounds__(512, 2)
-    lvkv_engine_uniform_half(lvkv::UniformArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::kCompactLdsBytes / 4];
-  lvkv::burst_kernel_body<0, 8, 5>(a, lds, a.ngroups);
-}
-
-// The same, chain 0's loads before the LDS image, the others after it.
-extern "C" __global__ void __launch_bounds__(512, 2)
-    lvkv_engine_uniform_half_late(lvkv::UniformArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::kCompactLdsBytes / 4];
+    lvkv_ek_uniform(lvkv::UniformArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLds];
   lvkv::burst_kernel_body<lvkv::kBurstLate, 8, 5>(a, lds, a.ngroups);
 }
 
-// 8 x 3, chain 0 first (the HIP path's compact schedule).
+// Two workgroups per CU per dispatch, 8 waves x 3 chains, every row load
+// issued before the image (A/B shape, lvkv_engine_set_variant 1).
 extern "C" __global__ void __launch_bounds__(512, 2)
-    lvkv_engine_uniform_burst_late(lvkv::UniformArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::kCompactLdsBytes / 4];
-  lvkv::burst_kernel_body<lvkv::kBurstLate, 8, 3>(a, lds, a.ngroups);
+    lvkv_ek_uniform_pair(lvkv::UniformArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLds];
+  lvkv::burst_kernel_body<0, 8, 3>(a, lds, a.ngroups);
 }
 
-// Timing builds: per-wave s_memrealtime stamps into UniformArgs::stamps
-// (tools/probe; selected by lvkv_engine_set_stamps).
+// Timestamp builds of the two (per-wave s_memrealtime into
+// UniformArgs::stamps; lvkv_engine_set_stamps, tools/probe/timeline.py).
 extern "C" __global__ void __launch_bounds__(512, 2)
-    lvkv_engine_uniform_burst_stamps(lvkv::UniformArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::kCompactLdsBytes / 4];
+    lvkv_ek_uniform_stamps(lvkv::UniformArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLds];
+  lvkv::burst_kernel_body<lvkv::kBurstLate | lvkv::kBurstStamps, 8, 5>(a, lds, a.ngroups);
+}
+extern "C" __global__ void __launch_bounds__(512, 2)
+    lvkv_ek_uniform_pair_stamps(lvkv::UniformArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLds];
   lvkv::burst_kernel_body<lvkv::kBurstStamps, 8, 3>(a, lds, a.ngroups);
-}
-extern "C" __global__ void __launch_bounds__(512, 2)
-    lvkv_engine_uniform_half_stamps(lvkv::UniformArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::kCompactLdsBytes / 4];
-  lvkv::burst_kernel_body<lvkv::kBurstStamps, 8, 5>(a, lds, a.ngroups);
-}
-extern "C" __global__ void __launch_bounds__(512, 2)
-    lvkv_engine_uniform_half_late_stamps(lvkv::UniformArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::kCompactLdsBytes / 4];
-  lvkv::burst_kernel_body<lvkv::kBurstStamps | lvkv::kBurstLate, 8, 5>(a, lds, a.ngroups);
 }

@@ -1,8 +1,12 @@
 """Multi-process plumbing of the N>1 path on CPU (gloo, world_size 2).
 
 The device work per rank is the same batch call as at N=1 (covered by the GPU
-tests); here we check the slicing (every block exactly once, remainder on the
-first ranks) and the result gather, with two real processes.
+tests). Here two real processes run bench.py's own config-5 code
+(bench.split_measure -> shard.shard_range -> bench.timed_region ->
+bench.Comm) with a CPU runner in place of the engine: every block is
+checksummed exactly once, the gathered slices equal the oracle over the whole
+batch, and the reported time is the slowest rank's (common start barrier to
+the last completion).
 """
 from __future__ import annotations
 
@@ -49,36 +53,77 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, q):
+def _worker(rank, world, port, total, slow_rank, q):
+    import sys
+    import time
+
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, str(REPO))
+    sys.path.insert(0, str(REPO / "oracle"))
+    import bench
+    import oracle
+
+    block = 4096
+    data = oracle.splitmix_bytes(0xC0FFEE, total * block)
+
+    class CpuSliceRunner:
+        """bench.EngineRunner's interface over this rank's slice, on the CPU."""
+
+        def __init__(self, start, count):
+            self.view = data[start * block:(start + count) * block]
+            self.count = count
+            self.crc = None
+            self.steps = 0
+
+        def step(self, i):
+            self.crc = oracle.uniform(self.view, self.count, block, threads=1)
+            self.steps += 1
+            if rank == slow_rank:
+                time.sleep(0.02)
+
+        def finish(self):
+            pass
+
+        def sync(self):
+            pass
+
+    comm = bench.Comm(world)
+    runner, rec = bench.split_measure(CpuSliceRunner, comm, rank, world, steps=3, warmup=1,
+                                      warmup_s=0.0, total=total, block=block)
     shard = _load_shard()
-    start, count = shard.shard_range(n, rank, world)
-    # Stand-in per-rank result: a value derived from the block index only.
-    local = (torch.arange(start, start + count, dtype=torch.int64) * 2654435761) % (1 << 31)
-    full = shard.gather_slices(local.to(torch.int32), n)
-    t = torch.tensor([float(rank + 1)])
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)  # the bench's max-over-ranks timing
+    local = torch.from_numpy(runner.crc.view(np.int32).copy())
+    full = shard.gather_slices(local, total)
     if rank == 0:
-        q.put((full.numpy().tolist(), float(t.item())))
+        q.put((full.numpy().view(np.uint32).tolist(), rec, runner.count))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [11, 4096])
-def test_gloo_world2_gather(n):
+@pytest.mark.parametrize("total,slow_rank", [(11, 1), (64, 0), (97, 1)])
+def test_gloo_world2_split_bench(total, slow_rank):
+    import sys
+    sys.path.insert(0, str(REPO / "oracle"))
+    import oracle
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, total, slow_rank, q))
+             for r in range(2)]
     for p in procs:
         p.start()
-    full, tmax = q.get(timeout=120)
+    full, rec, count0 = q.get(timeout=180)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    want = ((np.arange(n, dtype=np.int64) * 2654435761) % (1 << 31)).astype(np.int32)
-    assert np.array_equal(np.array(full, np.int32), want)
-    assert tmax == 2.0
+    data = oracle.splitmix_bytes(0xC0FFEE, total * 4096)
+    want = oracle.uniform(data, total, 4096, threads=1)
+    assert full == [int(x) for x in want]
+    assert count0 == (total + 1) // 2
+    assert rec["total_blocks"] == total and rec["ranks"] == 2 and rec["steps"] == 3
+    # max over ranks: the slow rank's 3 x 20 ms is the reported time on rank 0
+    assert rec["ms_per_step"] >= 20.0
+    assert rec["value"] == pytest.approx(total * 4096 / (rec["ms_per_step"] * 1e-3) / 2**30,
+                                         rel=1e-3, abs=1e-3)

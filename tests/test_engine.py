@@ -1,0 +1,107 @@
+"""The AQL engine (lvkv_engine_*, include/lvkv_crc32c.h) against the oracle
+and the HIP launch path: same contract as lvkv_crc32c_uniform_device for
+blocks of 4..4096 bytes, over batches of one and of several dispatches,
+overlapped and ordered, with init/mask, and its profiling log."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng(lvkv, gpu):
+    e = lvkv.Engine(gpu)
+    yield e
+    e.close()
+
+
+def _data(torch, gpu, n, seed):
+    g = torch.Generator(device=gpu).manual_seed(seed)
+    return torch.randint(0, 256, (n,), dtype=torch.uint8, device=gpu, generator=g)
+
+
+@pytest.mark.parametrize("nblocks,length,stride", [
+    (1, 4096, 4096), (2, 4096, 4096), (3, 4096, 4096), (10_000, 4096, 4096),
+    (10_241, 4096, 4096), (25_000, 4096, 4096), (777, 4, 4), (500, 100, 104),
+    (4000, 1024, 1024), (333, 2048, 4096), (100, 260, 260), (64, 3996, 4000)])
+def test_engine_matches_oracle(lvkv, oracle, eng, gpu, nblocks, length, stride):
+    import torch
+    buf = _data(torch, gpu, (nblocks - 1) * stride + length, nblocks * 7 + length)
+    got = eng.crc32c_uniform(buf, nblocks, length, stride)
+    eng.wait()
+    want = oracle.uniform(buf.cpu().numpy(), nblocks, length, stride, threads=8)
+    assert np.array_equal(got.cpu().numpy().view(np.uint32), want)
+    hip = lvkv.crc32c_uniform(buf, nblocks, length, stride)
+    torch.cuda.synchronize()
+    assert torch.equal(hip, got)
+
+
+def test_engine_init_mask_ordered(lvkv, oracle, eng, gpu):
+    import torch
+    nb, L = 3000, 4096
+    buf = _data(torch, gpu, nb * L, 5)
+    host = buf.cpu().numpy()
+    a = eng.crc32c_uniform(buf, nb, L, init=0xDEADBEEF, mask=True)
+    b = eng.crc32c_uniform(buf, nb, L, ordered=True)
+    eng.wait()
+    want = oracle.uniform(host, nb, L, threads=8)
+    assert np.array_equal(b.cpu().numpy().view(np.uint32), want)
+    hip = lvkv.crc32c_uniform(buf, nb, L, init=0xDEADBEEF, mask=True)
+    torch.cuda.synchronize()
+    assert torch.equal(a, hip)
+
+
+def test_engine_many_batches_in_flight(oracle, eng, gpu):
+    """More dispatches than kernarg slots between waits: the engine fences
+    itself; every batch's result is intact."""
+    import torch
+    nb, L, K = 64, 4096, 1500
+    buf = _data(torch, gpu, 8 * nb * L, 11)
+    outs = torch.zeros(K, nb, dtype=torch.int32, device=gpu)
+    for k in range(K):
+        eng.crc32c_uniform(buf[(k % 8) * nb * L:], nb, L, out=outs[k])
+    eng.wait()
+    host = buf.cpu().numpy()
+    want = [oracle.uniform(host[w * nb * L:(w + 1) * nb * L], nb, L, threads=8) for w in range(8)]
+    got = outs.cpu().numpy().view(np.uint32)
+    for k in range(K):
+        assert np.array_equal(got[k], want[k % 8]), k
+
+
+def test_engine_queues_and_profile(oracle, eng, gpu):
+    import torch
+    nb, L = 10_000, 4096
+    buf = _data(torch, gpu, nb * L, 3)
+    want = oracle.uniform(buf.cpu().numpy(), nb, L, threads=8)
+    assert eng.queues() == 3
+    for nq in (1, 2, 4, 3):
+        assert eng.queues(nq) == nq
+        out = eng.crc32c_uniform(buf, nb, L)
+        eng.wait()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+    eng.profile(True)
+    for _ in range(5):
+        eng.crc32c_uniform(buf, nb, L, ordered=True)
+    eng.wait()
+    spans = eng.profile_read()
+    eng.profile(False)
+    assert len(spans) == 5
+    for (a, b), (c, _) in zip(spans, spans[1:]):
+        assert 0.5 < b - a < 1000.0   # us
+        assert c >= b - 1e-3          # ordered: one after the other
+    assert eng.profile_read() == []
+
+
+def test_engine_rejects_bad_shapes(lvkv, eng, gpu):
+    import torch
+    buf = _data(torch, gpu, 1 << 16, 1)
+    with pytest.raises(lvkv.LvkvError):
+        eng.crc32c_uniform(buf, 2, 8192)      # beyond the kernel's 16 rows
+    with pytest.raises(lvkv.LvkvError):
+        eng.crc32c_uniform(buf, 2, 3)         # < 4 bytes
+    with pytest.raises(lvkv.LvkvError):
+        eng.crc32c_uniform(buf[1:], 2, 8, 8)  # end not 4-byte aligned
+    out = eng.crc32c_uniform(buf, 0, 4096)
+    assert out.numel() == 0

@@ -29,7 +29,7 @@ L.lvkv_engine_crc32c_uniform.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint3
                                          ctypes.c_uint32, vp, ctypes.c_size_t, ctypes.c_uint32]
 L.lvkv_engine_wait.argtypes = [vp]
 L.lvkv_engine_destroy.argtypes = [vp]
-L.lvkv_engine_set_option.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+L.lvkv_engine_set_variant.argtypes = [vp, ctypes.c_int, ctypes.c_int]
 
 
 def arg(name, default):
@@ -55,22 +55,13 @@ def main():
     rc = L.lvkv_engine_create(0, ctypes.byref(eng))
     assert rc == 0, f"engine create {rc}"
     res = {}
-    print("VRAM kernargs available:", L.lvkv_engine_set_option(eng, 4, 0), flush=True)
-    combos = [(v, 1, a, r, 0, q) for v in (0, 3, 4) for a, r in ((1, 1), (0, 0))
-              for q in (1, 2, 3)]
+    combos = [(v, q) for v in (0, 1) for q in (1, 2, 3, 4)]
     if "--one" in sys.argv:
-        combos = combos[1:2]
-    for variant, devk, acq, rel, sigm, nq in combos:
-        rb = 0
-        assert L.lvkv_engine_set_option(eng, 7, nq) == 0
-        if L.lvkv_engine_set_option(eng, 1, devk) != 0:
-            continue
-        assert L.lvkv_engine_set_option(eng, 0, variant) == 0
-        assert L.lvkv_engine_set_option(eng, 2, acq) == 0
-        assert L.lvkv_engine_set_option(eng, 3, rel) == 0
-        assert L.lvkv_engine_set_option(eng, 5, sigm) == 0
-        assert L.lvkv_engine_set_option(eng, 6, rb) == 0
-        tag = f"v{variant}_acq{acq}_rel{rel}_nq{nq}"
+        combos = [(0, 3)]
+    for variant, nq in combos:
+        assert L.lvkv_engine_queues(eng, nq) == nq
+        assert L.lvkv_engine_set_variant(eng, variant, variant) == 0
+        tag = f"v{variant}_nq{nq}"
         rc = L.lvkv_engine_crc32c_uniform(eng, vp(buf.data_ptr()), Lb, Lb, 0,
                                           vp(outs[0].data_ptr()), nb, 0)
         assert rc == 0, rc
@@ -108,6 +99,19 @@ def main():
                 us = statistics.median(ts)
                 row[f"{name}_{n}_us"] = round(us, 3)
                 row[f"{name}_{n}_pct"] = round(100 * nb * Lb / (us * 1e-6) / 8e12, 2)
+        # device time of isolated dispatches (HSA profiling, one queue, ordered)
+        L.lvkv_engine_queues(eng, 1)
+        L.lvkv_engine_profile(eng, 1)
+        submit(64, 2)
+        L.lvkv_engine_wait(eng)
+        t0s, t1s = (ctypes.c_double * 64)(), (ctypes.c_double * 64)()
+        k = L.lvkv_engine_profile_read(eng, t0s, t1s, 64)
+        dts = [b - a for a, b in zip(t0s[:k], t1s[:k])]
+        L.lvkv_engine_profile(eng, 0)
+        L.lvkv_engine_queues(eng, nq)
+        dt = statistics.median(dts[:k])
+        row["single_dispatch_us"] = round(dt, 3)
+        row["single_dispatch_pct"] = round(100 * nb * Lb / (dt * 1e-6) / 8e12, 2)
         # submit cost alone (host)
         t0 = time.perf_counter()
         submit(64, 0)

@@ -29,7 +29,6 @@ L.lvkv_engine_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
 L.lvkv_engine_crc32c_uniform.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint32,
                                          ctypes.c_uint32, vp, ctypes.c_size_t, ctypes.c_uint32]
 L.lvkv_engine_wait.argtypes = [vp]
-L.lvkv_engine_set_option.argtypes = [vp, ctypes.c_int, ctypes.c_int]
 
 
 def main():
@@ -43,10 +42,6 @@ def main():
     optr = [o.data_ptr() for o in outs]
     eng = vp()
     assert L.lvkv_engine_create(0, ctypes.byref(eng)) == 0
-    acq = int(next((a.split("=")[1] for a in sys.argv if a.startswith("--acq=")), 1))
-    rel = int(next((a.split("=")[1] for a in sys.argv if a.startswith("--rel=")), 1))
-    L.lvkv_engine_set_option(eng, 2, acq)
-    L.lvkv_engine_set_option(eng, 3, rel)
     sub = L.lvkv_engine_crc32c_uniform
     uni = L.lvkv_crc32c_uniform_device
     side = torch.cuda.Stream()

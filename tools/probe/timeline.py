@@ -1,6 +1,6 @@
 """Device timeline of a 20-step engine region (GPU box). Not part of the product.
 
-    python tools/probe/timeline.py [--acq=A] [--rel=R]
+    python tools/probe/timeline.py [--variant=V] [--nq=Q] [--K=K]
 
 The bench-style region (sync, t0, 20 engine submits, wait, sync, t1) with the
 timestamp build of the engine kernel: per dispatch the first wave start and
@@ -28,7 +28,7 @@ L.lvkv_engine_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
 L.lvkv_engine_crc32c_uniform.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint32,
                                          ctypes.c_uint32, vp, ctypes.c_size_t, ctypes.c_uint32]
 L.lvkv_engine_wait.argtypes = [vp]
-L.lvkv_engine_set_option.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+L.lvkv_engine_set_variant.argtypes = [vp, ctypes.c_int, ctypes.c_int]
 L.lvkv_engine_set_stamps.argtypes = [vp, vp, ctypes.c_uint64]
 
 
@@ -50,13 +50,12 @@ def main():
     optr = [o.data_ptr() for o in outs]
     eng = vp()
     assert L.lvkv_engine_create(0, ctypes.byref(eng)) == 0
-    L.lvkv_engine_set_option(eng, 2, arg("acq", 1))
-    L.lvkv_engine_set_option(eng, 3, arg("rel", 1))
     variant = arg("variant", 0)
-    assert L.lvkv_engine_set_option(eng, 7, arg("nq", 1)) == 0
-    assert L.lvkv_engine_set_option(eng, 0, variant) == 0
-    groups = lvkv.device_groups() * (1 if variant in (2, 3) else 2)
-    waves = groups * 8
+    assert L.lvkv_engine_queues(eng, arg("nq", 3)) == arg("nq", 3)
+    assert L.lvkv_engine_set_variant(eng, variant, variant) == 0
+    w, c, gr = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+    L.lvkv_engine_shape(eng, ctypes.byref(w), ctypes.byref(c), ctypes.byref(gr))
+    waves = gr.value * w.value
     stamps = torch.zeros(K * waves * 8, dtype=torch.int64, device=dev)
     sub = L.lvkv_engine_crc32c_uniform
     res = {}
@@ -105,7 +104,7 @@ def main():
         print("  wave start spread in kernel 10 (p0/p50/p100 us from its first):",
               best["spread"])
     (REPO / "gpurun_out").mkdir(exist_ok=True)
-    (REPO / "gpurun_out" / f"timeline_v{variant}_nq{arg('nq', 1)}.json").write_text(json.dumps(res, indent=1))
+    (REPO / "gpurun_out" / f"timeline_v{variant}_nq{arg('nq', 3)}.json").write_text(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":
