@@ -50,6 +50,13 @@ struct lvkv_engine;
  * one workgroup per CU per dispatch (overlapped default); 1 = 8 x 3, two
  * workgroups per CU (ordered default). */
 int lvkv_engine_set_variant(struct lvkv_engine* engine, int variant, int ordered_variant);
+/* Ordered (overlapped = 0) or overlapped dispatches run `kernel` (a
+ * UniformArgs kernel of the given shape, symbol name with ".kd") from a
+ * separate gfx950 code object in memory (tools/probe/build.sh) instead of the
+ * engine's own; NULL restores them. */
+int lvkv_engine_load_probe(struct lvkv_engine* engine, const void* code_object, size_t size,
+                           const char* kernel, uint32_t waves, uint32_t chains, uint32_t per_cu,
+                           int overlapped);
 /* Dispatch the timestamp build of the current kernel: dispatch k writes 8 u64
  * per wave (s_memrealtime, 100 MHz; slots 0 start, 1 loads issued, 2 image
  * built, 3 walk done, 4 stored) into area k % areas of d_stamps (areas x

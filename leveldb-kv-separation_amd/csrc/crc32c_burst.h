@@ -42,6 +42,8 @@ enum : int {
   kBurstStamps = 64,   // per-wave s_memrealtime stamps (UniformArgs::stamps)
   kBurstSplit2 = 128,  // full blocks walked as 2 independent 8-row groups
   kBurstSplit4 = 256,  // ... as 4 independent 4-row groups
+  kBurstPipe1 = 512,   // chain-pipelined: walk chain c, then issue chain c + 1
+  kBurstPipe2 = 1024,  // ... two chains ahead: walk c, then issue c + 2
 };
 
 namespace {
@@ -143,6 +145,63 @@ __device__ __forceinline__ void burst_body(const UniformArgs& a, const UniGeo& g
     if (lane == 0 && live)
 #pragma unroll
       for (int c = 0; c < NV; ++c) a.out[blk[c]] = x;
+    return;
+  }
+
+  if (F & (kBurstPipe1 | kBurstPipe2)) {
+    // Chain pipeline: the first D chains' rows go out before the image; then
+    // each chain is walked, reduced and stored as soon as its rows land, and
+    // the chain D ahead is issued after it, so a wave's row loads never sit
+    // between it and the walk of data that has already arrived.
+    constexpr int D = (F & kBurstPipe2) ? 2 : 1;
+    LaneTabGen<W> lg;
+    lg.load(a.lane_cols, wave, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    load_rows(0, D < NV ? D : NV);
+    __builtin_amdgcn_sched_barrier(0);
+    burst_stamp<F>(a, gw, 1);
+    burst_fill_rows<W>(lds, a, tid);
+    burst_stamp<F>(a, gw, 3);
+    lg.store(lds, wave, lane);
+    burst_stamp<F>(a, gw, 5);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    burst_stamp<F>(a, gw, 2);
+    const LaneKeys keys = lane_keys(lane);
+    const uint32_t lane_base = compact_lane_base(lane);
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      fix_first_chunk(w[c], g);
+      uint32_t crc;
+      if (G > 1) {
+        // G independent R-row groups (ILP within the chain), Horner-combined
+        uint32_t sg[G];
+#pragma unroll
+        for (int k = 0; k < G; ++k) sg[k] = w[c][k * R];
+#pragma unroll
+        for (int t = 1; t < R; ++t)
+#pragma unroll
+          for (int k = 0; k < G; ++k) sg[k] = row_step_c(lds, sg[k], w[c][k * R + t], keys);
+        constexpr uint32_t kJ = (R == 8) ? 11u : (R == 4) ? 10u : 0u;  // log2(R * 256)
+        uint32_t v = wave_xor_dpp(lane_end_shift_c(lds, sg[0], lane_base));
+#pragma unroll
+        for (int k = 1; k < G; ++k)
+          v = zpow_uniform(a.zpow, kJ, v) ^ wave_xor_dpp(lane_end_shift_c(lds, sg[k], lane_base));
+        crc = v ^ 0xffffffffu;
+      } else {
+        uint32_t st = w[c][0];
+#pragma unroll
+        for (int j = 1; j < kRowsPerChunk; ++j)
+          if (FULL || static_cast<uint32_t>(j) < g.rows) st = row_step_c(lds, st, w[c][j], keys);
+        crc = wave_xor_dpp(lane_end_shift_c(lds, st, lane_base)) ^ 0xffffffffu;
+      }
+      if (lane == 0 && live) a.out[blk[c]] = a.mask ? crc_mask(crc) : crc;
+      if (c < 2) burst_stamp<F>(a, gw, 6 + c);
+      __builtin_amdgcn_sched_barrier(0);
+      if (c + D < NV) load_rows(c + D, c + D + 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    burst_stamp<F>(a, gw, 4);
     return;
   }
 

@@ -179,6 +179,12 @@ struct Engine {
   hsa_code_object_reader_t reader{};
   bool exe_ok = false, reader_ok = false;
   EngineKernel kern[kNumSpecs], kern_stamps[kNumSpecs];
+  // a probe kernel loaded from a separate code object (tools/probe only)
+  hsa_executable_t probe_exe{};
+  hsa_code_object_reader_t probe_reader{};
+  bool probe_exe_ok = false, probe_reader_ok = false, probe_on = false;
+  bool probe_overlapped = false;  // the probe replaces overlapped (else ordered) dispatches' kernel
+  EngineKernel probe;
   int variant = 0;          // kernel of overlapped dispatches
   int ordered_variant = 1;  // kernel of ordered dispatches (the whole chip)
   uint8_t* kernarg = nullptr;     // kSlots x kSlotBytes
@@ -211,9 +217,15 @@ void queue_error_cb(hsa_status_t status, hsa_queue_t*, void* data) {
   static_cast<Engine*>(data)->queue_error = static_cast<int>(status);
 }
 
-int load_kernel(Engine& e, const char* name, EngineKernel* k) {
+void drop_probe(Engine& e) {
+  if (e.probe_exe_ok) hsa_executable_destroy(e.probe_exe);
+  if (e.probe_reader_ok) hsa_code_object_reader_destroy(e.probe_reader);
+  e.probe_exe_ok = e.probe_reader_ok = e.probe_on = false;
+}
+
+int load_kernel(Engine& e, hsa_executable_t exe, const char* name, EngineKernel* k) {
   hsa_executable_symbol_t sym;
-  if (hsa_executable_get_symbol_by_name(e.exe, name, &e.agent, &sym) != HSA_STATUS_SUCCESS)
+  if (hsa_executable_get_symbol_by_name(exe, name, &e.agent, &sym) != HSA_STATUS_SUCCESS)
     return LVKV_ERR_HIP;
   if (hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &k->object) !=
           HSA_STATUS_SUCCESS ||
@@ -242,6 +254,7 @@ void destroy(Engine* e) {
     else
       hsa_memory_free(e->kernarg);
   }
+  drop_probe(*e);
   if (e->exe_ok) hsa_executable_destroy(e->exe);
   if (e->reader_ok) hsa_code_object_reader_destroy(e->reader);
   delete e;
@@ -330,8 +343,8 @@ int create(int device, Engine** out) {
                                                    nullptr) == HSA_STATUS_SUCCESS;
   ok = ok && hsa_executable_freeze(e->exe, nullptr) == HSA_STATUS_SUCCESS;
   for (int i = 0; ok && i < kNumSpecs; ++i) {
-    ok = load_kernel(*e, kSpecs[i].name, &e->kern[i]) == LVKV_OK &&
-         load_kernel(*e, kSpecs[i].stamps, &e->kern_stamps[i]) == LVKV_OK;
+    ok = load_kernel(*e, e->exe, kSpecs[i].name, &e->kern[i]) == LVKV_OK &&
+         load_kernel(*e, e->exe, kSpecs[i].stamps, &e->kern_stamps[i]) == LVKV_OK;
     for (EngineKernel* k : {&e->kern[i], &e->kern_stamps[i]}) {
       k->waves = kSpecs[i].waves;
       k->chains = kSpecs[i].chains;
@@ -513,7 +526,9 @@ int lvkv_engine_crc32c_uniform(lvkv_engine* eng, const void* d_base, uint64_t st
   // shaped for the whole chip.
   if (ordered && e->nq > 1 && e->fenced != e->next) fence(*e);
   const int v = ordered ? e->ordered_variant : e->variant;
-  const EngineKernel& k = e->stamps ? e->kern_stamps[v] : e->kern[v];
+  const EngineKernel& k = (e->probe_on && ordered != e->probe_overlapped) ? e->probe
+                          : e->stamps                ? e->kern_stamps[v]
+                                                     : e->kern[v];
   const uint64_t groups = static_cast<uint64_t>(e->cus) * k.per_cu;
   const uint64_t cap = groups * k.waves * k.chains;
   // A batch beyond one dispatch's capacity goes out as several dispatches of
@@ -615,6 +630,39 @@ int lvkv_engine_set_variant(lvkv_engine* eng, int variant, int ordered_variant) 
   if (e->fenced != e->next) fence(*e);
   e->variant = variant;
   e->ordered_variant = ordered_variant;
+  return LVKV_OK;
+}
+
+int lvkv_engine_load_probe(lvkv_engine* eng, const void* code_object, size_t size,
+                           const char* kernel, uint32_t waves, uint32_t chains, uint32_t per_cu,
+                           int overlapped) {
+  if (eng == nullptr) return LVKV_ERR_INVALID;
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (e->fenced != e->next) fence(*e);
+  drop_probe(*e);
+  if (code_object == nullptr) return LVKV_OK;
+  if (kernel == nullptr || waves == 0 || waves > 16 || chains == 0 || per_cu == 0)
+    return LVKV_ERR_INVALID;
+  bool ok = hsa_code_object_reader_create_from_memory(code_object, size, &e->probe_reader) ==
+            HSA_STATUS_SUCCESS;
+  e->probe_reader_ok = ok;
+  ok = ok && hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT,
+                                       nullptr, &e->probe_exe) == HSA_STATUS_SUCCESS;
+  e->probe_exe_ok = ok;
+  ok = ok && hsa_executable_load_agent_code_object(e->probe_exe, e->agent, e->probe_reader,
+                                                   nullptr, nullptr) == HSA_STATUS_SUCCESS;
+  ok = ok && hsa_executable_freeze(e->probe_exe, nullptr) == HSA_STATUS_SUCCESS;
+  ok = ok && load_kernel(*e, e->probe_exe, kernel, &e->probe) == LVKV_OK;
+  if (!ok) {
+    drop_probe(*e);
+    return LVKV_ERR_HIP;
+  }
+  e->probe.waves = waves;
+  e->probe.chains = chains;
+  e->probe.per_cu = per_cu;
+  e->probe_overlapped = overlapped != 0;
+  e->probe_on = true;
   return LVKV_OK;
 }
 

@@ -8,3 +8,6 @@ PKG="$R/leveldb-kv-separation_amd"
   -I "$R/include" -I "$PKG/csrc" "$HERE/probe.hip" "$PKG/csrc/lvkv_tables.cpp" \
   -L "$PKG" -llvkv_crc32c -Wl,-rpath,'$ORIGIN/../../leveldb-kv-separation_amd' \
   -o "$HERE/libprobe.so"
+# Engine probe kernels: an unbundled gfx950 code object for lvkv_engine_load_probe.
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 --cuda-device-only --no-gpu-bundle-output \
+  -I "$R/include" -I "$PKG/csrc" -c "$HERE/engine_probe_kernels.hip" -o "$HERE/engine_probe_kernels.co"
