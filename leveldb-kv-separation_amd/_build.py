@@ -18,6 +18,10 @@ CSRC = PKG / "csrc"
 INCLUDE = REPO / "include"
 BUILD = REPO / "build" / "lvkv"
 LIB = PKG / "liblvkv_crc32c.so"
+# The probe build: the same sources with -DLVKV_PROBE_BUILD (schedule
+# variants, timestamp builds, read-bandwidth kernel; tools/probe/lvkv_probe.h).
+PROBE_BUILD = REPO / "build" / "lvkv_probe"
+PROBE_LIB = REPO / "tools" / "probe" / "liblvkv_probe.so"
 ORACLE_DIR = REPO / "oracle"
 ORACLE_LIB = ORACLE_DIR / "liboracle_crc32c.so"
 REF_LIB = ORACLE_DIR / "_ref" / "libref_crc32c.so"
@@ -52,42 +56,49 @@ def _newer(target: Path, deps: list[Path]) -> bool:
     return all(d.stat().st_mtime <= t for d in deps)
 
 
-def build_lib(verbose: bool = False, force: bool = False) -> Path:
+def build_lib(verbose: bool = False, force: bool = False, probe: bool = False) -> Path:
+    lib = PROBE_LIB if probe else LIB
+    build = PROBE_BUILD if probe else BUILD
     deps = [CSRC / s for s in HOST_SOURCES + HIP_SOURCES + HEADERS + [ENGINE_KERNELS]]
     deps += sorted(INCLUDE.glob("*.h")) + [Path(__file__)]
-    if not force and _newer(LIB, deps):
-        return LIB
-    BUILD.mkdir(parents=True, exist_ok=True)
+    if not force and _newer(lib, deps):
+        return lib
+    build.mkdir(parents=True, exist_ok=True)
     objs, cmds = [], []
     common = ["-O3", "-fPIC", "-std=c++17", "-Wall", "-I", INCLUDE, "-I", CSRC]
+    if probe:
+        common.append("-DLVKV_PROBE_BUILD")
     for src in HOST_SOURCES:
-        obj = BUILD / (Path(src).stem + ".o")
+        obj = build / (Path(src).stem + ".o")
         cmds.append(["g++", *common, "-c", CSRC / src, "-o", obj])
         objs.append(obj)
     for src in HIP_SOURCES:
-        obj = BUILD / (Path(src).stem + ".hip.o")
+        obj = build / (Path(src).stem + ".hip.o")
         cmds.append([HIPCC, f"--offload-arch={ARCH}", *common, "-c", CSRC / src, "-o", obj])
         objs.append(obj)
-    co = BUILD / "lvkv_engine.co"
+    co = build / "lvkv_engine.co"
     cmds.append([HIPCC, f"--offload-arch={ARCH}", *common, "--cuda-device-only",
                  "--no-gpu-bundle-output", "-c", CSRC / ENGINE_KERNELS, "-o", co])
     # translation units are independent: compile them concurrently
     with ThreadPoolExecutor(max_workers=min(len(cmds), os.cpu_count() or 1, 8)) as ex:
         list(ex.map(lambda c: _run(c, verbose), cmds))
-    asm = BUILD / "lvkv_engine_co.S"
+    asm = build / "lvkv_engine_co.S"
     asm.write_text(
         "\t.section .rodata\n\t.balign 4096\n\t.globl lvkv_engine_co\n"
         "\t.type lvkv_engine_co, @object\nlvkv_engine_co:\n"
         f"\t.incbin \"{co}\"\n\t.globl lvkv_engine_co_end\nlvkv_engine_co_end:\n"
         "\t.section .note.GNU-stack,\"\",@progbits\n")
-    co_obj = BUILD / "lvkv_engine_co.o"
+    co_obj = build / "lvkv_engine_co.o"
     _run(["gcc", "-c", asm, "-o", co_obj], verbose)
     objs.append(co_obj)
-    tmp = LIB.with_suffix(".so.tmp")
+    tmp = lib.with_suffix(".so.tmp")
+    # the probe library binds its own symbols (it may be loaded next to the
+    # product library in one process)
+    extra = ["-Wl,-Bsymbolic"] if probe else []
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp, "-lpthread",
-          "-L/opt/rocm/lib", "-lhsa-runtime64"], verbose)
-    os.replace(tmp, LIB)
-    return LIB
+          "-L/opt/rocm/lib", "-lhsa-runtime64", *extra], verbose)
+    os.replace(tmp, lib)
+    return lib
 
 
 def build_oracle(verbose: bool = False) -> Path:
@@ -101,6 +112,7 @@ def build_oracle(verbose: bool = False) -> Path:
 
 def build_all(verbose: bool = False, force: bool = False) -> None:
     build_lib(verbose=verbose, force=force)
+    build_lib(verbose=verbose, force=force, probe=True)
     build_oracle(verbose=verbose)
 
 

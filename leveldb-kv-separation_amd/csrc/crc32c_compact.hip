@@ -319,6 +319,8 @@ hipError_t launch_crc32c_compact(const UniformArgs& args, int cfg, int num_group
     hipLaunchKernelGGL((crc32c_compact_kernel<p, w, nch, occ>), dim3(num_groups), \
                        dim3(64 * w), 0, stream, args);                          \
     break;
+    LVKV_CMP_CASE(9, kCmpGenLane, 8, 3, 2)  // production (kCompactProductionCfg)
+#ifdef LVKV_PROBE_BUILD
     LVKV_CMP_CASE(0, 0, 16, 3, 1)
     LVKV_CMP_CASE(1, 0, 8, 3, 2)
     LVKV_CMP_CASE(2, 0, 16, 2, 2)
@@ -326,7 +328,7 @@ hipError_t launch_crc32c_compact(const UniformArgs& args, int cfg, int num_group
     LVKV_CMP_CASE(5, kCmpBare, 8, 3, 2)
     LVKV_CMP_CASE(6, kCmpBare, 16, 2, 2)
     LVKV_CMP_CASE(8, kCmpGenLane, 16, 3, 1)
-    LVKV_CMP_CASE(9, kCmpGenLane, 8, 3, 2)
+#endif
 #undef LVKV_CMP_CASE
     default:
       return hipErrorInvalidValue;

@@ -586,6 +586,7 @@ __global__ void __launch_bounds__(kGroupThreads, 1)
   stamp<V>(a, gw, 7);
 }
 
+#ifdef LVKV_PROBE_BUILD
 // Read-bandwidth ceiling: every byte read once with 16 B per lane, grid
 // stride; nothing is stored unless the xor of the data hits a magic value, so
 // the loads cannot be dropped. Used to state the measured HBM ceiling next to
@@ -624,6 +625,8 @@ __global__ void __launch_bounds__(256)
   if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9E3779B9u) out[0] = acc.x;
 }
 
+#endif  // LVKV_PROBE_BUILD
+
 // Host-side launchers (compiled in this TU so the kernel symbols stay local).
 hipError_t launch_crc32c_batch(const KernelArgs& args, bool uniform_aligned,
                                int num_groups, hipStream_t stream) {
@@ -637,6 +640,7 @@ hipError_t launch_crc32c_batch(const KernelArgs& args, bool uniform_aligned,
   return hipGetLastError();
 }
 
+#ifdef LVKV_PROBE_BUILD
 hipError_t launch_crc32c_probe(const KernelArgs& args, int variant,
                                int num_groups, hipStream_t stream) {
   switch (variant) {
@@ -680,5 +684,7 @@ hipError_t launch_read_bw(const void* p, uint64_t bytes, uint32_t* out,
   }
   return hipGetLastError();
 }
+
+#endif  // LVKV_PROBE_BUILD
 
 }  // namespace lvkv

@@ -473,13 +473,6 @@ hipError_t launch_crc32c_ragged(const KernelArgs& a, const uint32_t* zpow,
 hipError_t launch_crc32c_batch(const KernelArgs& args, bool uniform_aligned, int num_groups,
                                hipStream_t stream);
 
-// Which kernel walks general-layout batches (per-block offsets): a ragged
-// cfg (>= 0), or -1 for crc32c_kernel.hip's persistent kernel. Set only by
-// lvkv_debug_set_general_kernel (A/B timing).
-int g_general_kernel = 0;
-// The shape for WAL records (type + payload, mostly well under 2 KiB).
-int g_log_kernel = 8;
-
 hipError_t launch_crc32c_long(const KernelArgs& args, const uint32_t* zpow,
                               const uint32_t* lane_cols, int num_groups, hipStream_t stream);
 
@@ -491,7 +484,10 @@ hipError_t launch_crc32c_general(const KernelArgs& a, int cus, hipStream_t strea
   if (n == 0) return hipSuccess;
   // (kModeSstTable exists in this kernel only)
   const bool log = a.mode == kModeLogVerify || a.mode == kModeLogFill;
-  int cfg = log && g_general_kernel >= 0 ? g_log_kernel : g_general_kernel;
+  // a.general_cfg: a ragged cfg (>= 0) or -1 for crc32c_kernel.hip's
+  // persistent kernel; a.log_cfg: the shape for WAL records (the device
+  // context's choices, lvkv_capi.cpp)
+  int cfg = log && a.general_cfg >= 0 ? a.log_cfg : a.general_cfg;
   if (a.mode == kModeSstTable && cfg < 0) cfg = 0;
   if (cfg < 0) {  // the persistent kernel and, for long blocks, a second launch
     KernelArgs b = a;

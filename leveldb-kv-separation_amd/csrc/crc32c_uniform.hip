@@ -590,10 +590,12 @@ hipError_t launch_crc32c_uniform_small(const UniformArgs& args, int variant,
                        dim3(kGroupThreads), 0, stream, args);                \
     break;
 #define LVKV_UNI_SMALL_PAIR(v) LVKV_UNI_SMALL_CASE(v) LVKV_UNI_SMALL_CASE(v + 64)
+    LVKV_UNI_SMALL_CASE(12)   // production: lane tables first, chain A before the fill
+#ifdef LVKV_PROBE_BUILD
+    LVKV_UNI_SMALL_CASE(76)   // 12 with stamps
     LVKV_UNI_SMALL_PAIR(0)    // all loads, then the fill
     LVKV_UNI_SMALL_PAIR(4)    // + lane tables first
     LVKV_UNI_SMALL_PAIR(8)    // chain A before the fill
-    LVKV_UNI_SMALL_PAIR(12)   // production: 4 | 8
     LVKV_UNI_SMALL_PAIR(16)   // one barrier after chains B/C
     LVKV_UNI_SMALL_PAIR(128)  // fill first
     LVKV_UNI_SMALL_PAIR(132)
@@ -603,6 +605,7 @@ hipError_t launch_crc32c_uniform_small(const UniformArgs& args, int variant,
     LVKV_UNI_SMALL_PAIR(44)   //   without the row-table fill,
     LVKV_UNI_SMALL_PAIR(15)   //   loads and walk both off
     LVKV_UNI_SMALL_PAIR(4096)  // memory side only
+#endif
 #undef LVKV_UNI_SMALL_PAIR
 #undef LVKV_UNI_SMALL_CASE
     default:
@@ -619,7 +622,8 @@ hipError_t launch_crc32c_uniform(const UniformArgs& args, int variant,
     hipLaunchKernelGGL(crc32c_uniform_kernel<v>, dim3(num_groups),           \
                        dim3(kGroupThreads), 0, stream, args);                \
     break;
-    LVKV_UNI_CASE(0)
+    LVKV_UNI_CASE(0)  // production
+#ifdef LVKV_PROBE_BUILD
     LVKV_UNI_CASE(1)
     LVKV_UNI_CASE(2)
     LVKV_UNI_CASE(3)
@@ -635,7 +639,10 @@ hipError_t launch_crc32c_uniform(const UniformArgs& args, int variant,
     LVKV_UNI_CASE(193)
     LVKV_UNI_CASE(194)
     LVKV_UNI_CASE(195)
+#endif
 #undef LVKV_UNI_CASE
+    default:
+      return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }

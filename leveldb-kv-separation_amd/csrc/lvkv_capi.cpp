@@ -24,12 +24,12 @@ namespace lvkv {
 hipError_t launch_crc32c_batch(const KernelArgs& args, bool uniform_aligned,
                                int num_groups, hipStream_t stream);
 hipError_t launch_crc32c_general(const KernelArgs& a, int cus, hipStream_t stream);
-extern int g_general_kernel;
-extern int g_log_kernel;
+#ifdef LVKV_PROBE_BUILD
 hipError_t launch_crc32c_probe(const KernelArgs& args, int variant,
                                int num_groups, hipStream_t stream);
 hipError_t launch_read_bw(const void* p, uint64_t bytes, uint32_t* out,
                           int num_groups, hipStream_t stream);
+#endif
 hipError_t launch_crc32c_uniform(const UniformArgs& args, int variant,
                                  int num_groups, hipStream_t stream);
 // Lane tables loaded first and written with the row tables (no end barrier),
@@ -93,6 +93,10 @@ struct DeviceCtx {
   int groups = 0;  // one workgroup per CU
   uint32_t* d_tables = nullptr;
   uint32_t zcol[32];  // columns of Z_256 (uniform kernel's row tables)
+  // kernels of general-layout batches and of WAL records
+  // (launch_crc32c_general; lvkv_debug_set_general_kernel/_log_kernel)
+  std::atomic<int> general_cfg{0};  // ragged cfg 0: 8 waves x 2 chains x 24 rows
+  std::atomic<int> log_cfg{8};      // one workgroup per round of 32 small records
   std::mutex host_mu;  // serialises lvkv_crc32c_batch_host per device
   bool stages_ready = false;
   Stage stage[2];
@@ -199,6 +203,8 @@ int run_batch(KernelArgs a, size_t nblocks, hipStream_t stream) {
   if (c == nullptr) return rc;
   a.row_tab = c->d_tables;
   a.lane_tab = c->d_tables + kRowTabDwords;
+  a.general_cfg = c->general_cfg.load(std::memory_order_relaxed);
+  a.log_cfg = c->log_cfg.load(std::memory_order_relaxed);
   for (size_t done = 0; done < nblocks;) {
     const size_t n = std::min(nblocks - done, kMaxBlocksPerLaunch);
     KernelArgs b = a;
@@ -282,6 +288,16 @@ uint32_t next_sst_generation() {
 KernelArgs blank_args() {
   KernelArgs a;
   memset(&a, 0, sizeof(a));
+  return a;
+}
+
+// Zeroed arguments with the device context's tables and kernel choices.
+KernelArgs ctx_args(const DeviceCtx& c) {
+  KernelArgs a = blank_args();
+  a.row_tab = c.d_tables;
+  a.lane_tab = c.d_tables + kRowTabDwords;
+  a.general_cfg = c.general_cfg.load(std::memory_order_relaxed);
+  a.log_cfg = c.log_cfg.load(std::memory_order_relaxed);
   return a;
 }
 
@@ -461,9 +477,7 @@ int lvkv_sst_verify_table_device(const void* d_file, uint64_t file_size,
   int rc = LVKV_OK;
   DeviceCtx* c = current_ctx(&rc);
   if (c == nullptr) return rc;
-  KernelArgs a = blank_args();
-  a.row_tab = c->d_tables;
-  a.lane_tab = c->d_tables + kRowTabDwords;
+  KernelArgs a = ctx_args(*c);
   a.mode = kModeSstVerify;
   const hipError_t e = launch_sst_tables(
       static_cast<const uint8_t*>(d_file), nullptr, nullptr, file_size, 1, d_offsets, d_sizes,
@@ -487,9 +501,7 @@ int lvkv_sst_verify_tables_device(const void* d_file, const uint64_t* d_table_of
   int rc = LVKV_OK;
   DeviceCtx* c = current_ctx(&rc);
   if (c == nullptr) return rc;
-  KernelArgs a = blank_args();
-  a.row_tab = c->d_tables;
-  a.lane_tab = c->d_tables + kRowTabDwords;
+  KernelArgs a = ctx_args(*c);
   a.mode = kModeSstVerify;
   const hipError_t e = launch_sst_tables(
       static_cast<const uint8_t*>(d_file), d_table_off, d_table_size, 0,
@@ -512,9 +524,7 @@ int lvkv_log_verify_blocks_device(const void* d_file, uint64_t file_size,
   int rc = LVKV_OK;
   DeviceCtx* c = current_ctx(&rc);
   if (c == nullptr) return rc;
-  KernelArgs a = blank_args();
-  a.row_tab = c->d_tables;
-  a.lane_tab = c->d_tables + kRowTabDwords;
+  KernelArgs a = ctx_args(*c);
   a.mode = kModeLogVerify;
   const hipError_t e = launch_log_blocks(
       static_cast<const uint8_t*>(d_file), file_size, d_hdr_offsets, d_actual, d_rec_status,
@@ -579,6 +589,17 @@ int lvkv_crc32c_batch_host(const void* h_base, const uint64_t* offsets,
     biggest = std::max<size_t>(biggest, lengths[i]);
   rc = ensure_stages(*c, biggest + 8);
   if (rc != LVKV_OK) return rc;
+  // Every return leaves both stages idle: on an error the stage still in
+  // flight is waited for and dropped, so no later call copies its results.
+  struct StageGuard {
+    DeviceCtx* c;
+    ~StageGuard() {
+      for (Stage& s : c->stage) {
+        if (s.busy) (void)hipStreamSynchronize(s.stream);
+        s.busy = false;
+      }
+    }
+  } guard{c};
   const uint8_t* src = static_cast<const uint8_t*>(h_base);
 
   size_t next = 0;
@@ -655,6 +676,8 @@ int lvkv_last_hip_error(void) { return t_last_hip_error; }
 
 const char* lvkv_cpu_impl(void) { return cpu_crc32c_impl_name(); }
 
+#ifdef LVKV_PROBE_BUILD
+// Probe entry points (tools/probe/liblvkv_probe.so only).
 static uint64_t* g_debug_stamps = nullptr;
 
 void lvkv_debug_set_stamps(uint64_t* d_stamps) { g_debug_stamps = d_stamps; }
@@ -724,18 +747,26 @@ int lvkv_debug_read_bw(const void* d_data, uint64_t bytes, uint32_t* d_scratch,
   return e == hipSuccess ? LVKV_OK : hip_fail(e);
 }
 
+#endif  // LVKV_PROBE_BUILD
+
 // -1: crc32c_kernel.hip's persistent kernel for general-layout batches;
 // 0..31: crc32c_ragged.hip cfgs (launch_crc32c_ragged). Timing only.
 int lvkv_debug_set_general_kernel(int k) {
   if (k < -1 || k > 31) return LVKV_ERR_INVALID;
-  g_general_kernel = k;
+  int rc = LVKV_OK;
+  DeviceCtx* c = current_ctx(&rc);
+  if (c == nullptr) return rc;
+  c->general_cfg.store(k, std::memory_order_relaxed);
   return LVKV_OK;
 }
 
 // The ragged cfg used for WAL records (8, 16, 24: small-record shapes).
 int lvkv_debug_set_log_kernel(int k) {
   if (k < 0 || k > 31) return LVKV_ERR_INVALID;
-  g_log_kernel = k;
+  int rc = LVKV_OK;
+  DeviceCtx* c = current_ctx(&rc);
+  if (c == nullptr) return rc;
+  c->log_cfg.store(k, std::memory_order_relaxed);
   return LVKV_OK;
 }
 

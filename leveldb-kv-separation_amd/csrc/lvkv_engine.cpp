@@ -185,6 +185,12 @@ struct Engine {
   bool probe_exe_ok = false, probe_reader_ok = false, probe_on = false;
   bool probe_overlapped = false;  // the probe replaces overlapped (else ordered) dispatches' kernel
   EngineKernel probe;
+  // fence scopes: a submission's first dispatch acquires at `dispatch_acq`;
+  // the wait's barrier packets acquire/release at fence_acq/fence_rel
+  // (system: the inputs may have been written by a copy engine, which the
+  // L2 does not see)
+  int dispatch_acq = HSA_FENCE_SCOPE_SYSTEM;
+  int fence_acq = HSA_FENCE_SCOPE_SYSTEM, fence_rel = HSA_FENCE_SCOPE_SYSTEM;
   int variant = 0;          // kernel of overlapped dispatches
   int ordered_variant = 1;  // kernel of ordered dispatches (the whole chip)
   uint8_t* kernarg = nullptr;     // kSlots x kSlotBytes
@@ -192,6 +198,7 @@ struct Engine {
   uint32_t* hdp_flush = nullptr;  // HDP_MEM_FLUSH_CNTL
   hsa_signal_t fence_sig{};       // barrier-AND fences, one decrement per queue
   bool fence_ok = false;
+
   uint64_t next = 0;    // dispatches submitted
   uint64_t fenced = 0;  // every dispatch before this index is known complete
   // probes
@@ -423,8 +430,8 @@ void fence(Engine& e) {
     const uint16_t header =
         static_cast<uint16_t>((HSA_PACKET_TYPE_BARRIER_AND << HSA_PACKET_HEADER_TYPE) |
                               (1 << HSA_PACKET_HEADER_BARRIER) |
-                              (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                              (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+                              (e.fence_acq << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                              (e.fence_rel << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
     publish(e, p, header, 0, idx);
   }
   e.cur = keep;
@@ -481,9 +488,10 @@ int dispatch(Engine& e, const EngineKernel& k, const UniformArgs& args, bool acq
   const uint16_t header = static_cast<uint16_t>(
       (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
       ((barrier ? 1 : 0) << HSA_PACKET_HEADER_BARRIER) |
-      ((acquire ? HSA_FENCE_SCOPE_AGENT : HSA_FENCE_SCOPE_NONE)
+      ((acquire ? e.dispatch_acq : HSA_FENCE_SCOPE_NONE)
        << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-      (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+      (HSA_FENCE_SCOPE_NONE
+       << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
   publish(e, p, header, 1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS, idx);
   e.next = n + 1;
   return LVKV_OK;
@@ -663,6 +671,20 @@ int lvkv_engine_load_probe(lvkv_engine* eng, const void* code_object, size_t siz
   e->probe.per_cu = per_cu;
   e->probe_overlapped = overlapped != 0;
   e->probe_on = true;
+  return LVKV_OK;
+}
+
+int lvkv_engine_set_scopes(lvkv_engine* eng, int dispatch_acquire, int fence_acquire,
+                           int fence_release) {
+  if (eng == nullptr) return LVKV_ERR_INVALID;
+  for (int v : {dispatch_acquire, fence_acquire, fence_release})
+    if (v < HSA_FENCE_SCOPE_NONE || v > HSA_FENCE_SCOPE_SYSTEM) return LVKV_ERR_INVALID;
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (e->fenced != e->next) fence(*e);
+  e->dispatch_acq = dispatch_acquire;
+  e->fence_acq = fence_acquire;
+  e->fence_rel = fence_release;
   return LVKV_OK;
 }
 

@@ -93,6 +93,10 @@ struct KernelArgs {
                               //   bytes when a unit is a fixed-size region
                               //   (the WAL's 32 KiB blocks); nullptr = equal
                               //   block counts per workgroup
+  int32_t general_cfg;        // host side: kernel of general-layout batches
+  int32_t log_cfg;            //   and of WAL records (launch_crc32c_general);
+                              //   the device context's choice, never read
+                              //   by a kernel
 };
 
 // "filter." + FilterPolicy::Name() (table/table.cc:100-101), the metaindex

@@ -12,6 +12,8 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
+from conftest import REPO
+
 pytestmark = pytest.mark.gpu
 
 
@@ -242,7 +244,8 @@ def test_every_uniform_variant(lvkv, oracle, gpu, length, nblocks, groups):
     # and grid; all must match the oracle bit for bit.
     import ctypes
     import torch
-    L = lvkv.lib
+    # the alternative schedules are compiled into the probe build only
+    L = ctypes.CDLL(str(REPO / "tools" / "probe" / "liblvkv_probe.so"))
     L.lvkv_debug_uniform_variant.argtypes = [
         ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
         ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]

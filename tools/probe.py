@@ -20,7 +20,8 @@ sys.path.insert(0, str(REPO))
 import __graft_entry__ as g  # noqa: E402
 
 lvkv = g.load_package()
-L = lvkv.lib
+# schedule variants and the read-bandwidth kernel: the probe build
+L = ctypes.CDLL(str(Path(__file__).resolve().parent / "probe" / "liblvkv_probe.so"))
 vp = ctypes.c_void_p
 L.lvkv_debug_uniform_variant.argtypes = [ctypes.c_int, ctypes.c_int, vp, ctypes.c_uint64,
                                          ctypes.c_uint32, vp, ctypes.c_size_t, vp]
