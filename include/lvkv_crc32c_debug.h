@@ -19,6 +19,10 @@ extern "C" {
  * Either pointer may be NULL. */
 void lvkv_debug_tables(uint32_t* row_tab, uint32_t* lane_tab);
 
+/* The portable slicing-by-8 per-call path (lvkv_cpu_crc32c.cpp), whatever
+ * implementation the per-call entry points picked on this CPU. */
+uint32_t lvkv_debug_extend_portable(uint32_t crc, const uint8_t* data, size_t n);
+
 /* The kernel-variant, timestamp and read-bandwidth probes live in the probe
  * build of the library (tools/probe/liblvkv_probe.so, tools/probe/lvkv_probe.h),
  * not in liblvkv_crc32c.so. */

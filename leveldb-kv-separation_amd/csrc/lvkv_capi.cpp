@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <unordered_map>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -25,6 +26,8 @@ hipError_t launch_crc32c_batch(const KernelArgs& args, bool uniform_aligned,
                                int num_groups, hipStream_t stream);
 hipError_t launch_crc32c_general(const KernelArgs& a, int cus, hipStream_t stream);
 #ifdef LVKV_PROBE_BUILD
+extern uint64_t* g_log_stamps;
+extern uint32_t g_log_knobs;
 hipError_t launch_crc32c_probe(const KernelArgs& args, int variant,
                                int num_groups, hipStream_t stream);
 hipError_t launch_read_bw(const void* p, uint64_t bytes, uint32_t* out,
@@ -49,7 +52,9 @@ hipError_t launch_sst_tables(const uint8_t* file, const uint64_t* toff, const ui
 hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_off,
                              uint32_t* actual, uint8_t* rec_status, uint32_t capacity,
                              uint8_t* block_status, uint32_t* block_drop, lvkv_log_report* r,
-                             const KernelArgs& verify, int groups, hipStream_t stream);
+                             const uint32_t* zpow, const uint32_t* lane_cols, int cus,
+                             void* scratch, hipStream_t stream);
+size_t log_scratch_bytes(uint64_t size);
 hipError_t launch_crc32c_long(const KernelArgs& args, const uint32_t* zpow,
                               const uint32_t* lane_cols, int num_groups, hipStream_t stream);
 int compact_capacity(int cfg);
@@ -98,6 +103,10 @@ struct DeviceCtx {
   std::atomic<int> general_cfg{0};  // ragged cfg 0: 8 waves x 2 chains x 24 rows
   std::atomic<int> log_cfg{8};      // one workgroup per round of 32 small records
   std::mutex host_mu;  // serialises lvkv_crc32c_batch_host per device
+  // WAL verify scratch, one buffer per stream (calls on one stream are
+  // ordered, so a buffer is never used by two calls at once)
+  std::mutex scratch_mu;
+  std::unordered_map<hipStream_t, std::pair<void*, size_t>> log_scratch;
   bool stages_ready = false;
   Stage stage[2];
 };
@@ -299,6 +308,30 @@ KernelArgs ctx_args(const DeviceCtx& c) {
   a.general_cfg = c.general_cfg.load(std::memory_order_relaxed);
   a.log_cfg = c.log_cfg.load(std::memory_order_relaxed);
   return a;
+}
+
+// The WAL verify scratch of `stream`, grown (stream-ordered) when too small;
+// a fresh buffer's completion counter is zeroed on the stream.
+hipError_t log_scratch_for(DeviceCtx& c, hipStream_t stream, size_t bytes, void** out) {
+  std::lock_guard<std::mutex> lk(c.scratch_mu);
+  auto& slot = c.log_scratch[stream];
+  if (slot.first != nullptr && slot.second >= bytes) {
+    *out = slot.first;
+    return hipSuccess;
+  }
+  hipError_t e = hipSuccess;
+  if (slot.first != nullptr && (e = hipFreeAsync(slot.first, stream)) != hipSuccess) return e;
+  slot = {nullptr, 0};
+  const size_t cap = std::max<size_t>(bytes, size_t{1} << 16);
+  void* p = nullptr;
+  if ((e = hipMallocAsync(&p, cap, stream)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(p, 0, 16, stream)) != hipSuccess) {
+    (void)hipFreeAsync(p, stream);
+    return e;
+  }
+  slot = {p, cap};
+  *out = p;
+  return hipSuccess;
 }
 
 // ---- host-resident pipeline ------------------------------------------
@@ -524,12 +557,14 @@ int lvkv_log_verify_blocks_device(const void* d_file, uint64_t file_size,
   int rc = LVKV_OK;
   DeviceCtx* c = current_ctx(&rc);
   if (c == nullptr) return rc;
-  KernelArgs a = ctx_args(*c);
-  a.mode = kModeLogVerify;
-  const hipError_t e = launch_log_blocks(
-      static_cast<const uint8_t*>(d_file), file_size, d_hdr_offsets, d_actual, d_rec_status,
-      static_cast<uint32_t>(capacity), d_block_status, d_block_drop, d_report, a, c->groups,
-      static_cast<hipStream_t>(stream));
+  const hipStream_t hs = static_cast<hipStream_t>(stream);
+  void* scratch = nullptr;
+  hipError_t e = log_scratch_for(*c, hs, log_scratch_bytes(file_size), &scratch);
+  if (e == hipSuccess)
+    e = launch_log_blocks(static_cast<const uint8_t*>(d_file), file_size, d_hdr_offsets,
+                          d_actual, d_rec_status, static_cast<uint32_t>(capacity),
+                          d_block_status, d_block_drop, d_report, c->d_tables + kZPowOffset,
+                          c->d_tables + kRowTabDwords + kLaneTabDwords, c->groups, scratch, hs);
   return e == hipSuccess ? LVKV_OK : hip_fail(e);
 }
 
@@ -678,6 +713,8 @@ const char* lvkv_cpu_impl(void) { return cpu_crc32c_impl_name(); }
 
 #ifdef LVKV_PROBE_BUILD
 // Probe entry points (tools/probe/liblvkv_probe.so only).
+void lvkv_debug_log_stamps(uint64_t* d_stamps) { g_log_stamps = d_stamps; }
+void lvkv_debug_log_knobs(uint32_t knobs) { g_log_knobs = knobs; }
 static uint64_t* g_debug_stamps = nullptr;
 
 void lvkv_debug_set_stamps(uint64_t* d_stamps) { g_debug_stamps = d_stamps; }

@@ -116,3 +116,10 @@ const char* cpu_crc32c_impl_name() {
 }
 
 }  // namespace lvkv
+
+// Test hook (include/lvkv_crc32c_debug.h): the portable slicing-by-8 path,
+// whichever implementation the process picked.
+extern "C" __attribute__((visibility("default"))) uint32_t lvkv_debug_extend_portable(
+    uint32_t crc, const uint8_t* data, size_t n) {
+  return lvkv::cpu_crc32c_extend_portable(crc, data, n);
+}

@@ -299,6 +299,50 @@ __device__ uint32_t place_table(lvkv_sst_report* reports, uint32_t t, uint32_t n
   return static_cast<uint32_t>(min<uint64_t>(run, capacity));
 }
 
+// Index entry i (restart point i, block_restart_interval = 1) -> its data
+// block handle and status in the shared arrays at first + i. The entry bytes
+// are read from `w` (a copy of index bytes [wlo, whi)) when they lie inside
+// it, else from the index `idx` itself; `ro` is the restart array's offset.
+__device__ void emit_entry(const uint8_t* idx, uint64_t ro, uint64_t nr, uint32_t i,
+                           const uint8_t* w, uint64_t wlo, uint64_t whi, const Table& tb,
+                           uint32_t first, uint64_t* out_off, uint32_t* out_size,
+                           uint8_t* out_status) {
+  uint8_t st = LVKV_BLOCK_BAD_ENTRY;
+  uint64_t off = 0, size = 0;
+  const uint32_t rs = ld_le32(idx + ro + 4ull * i);
+  const uint64_t end = i + 1 < nr ? ld_le32(idx + ro + 4ull * (i + 1)) : ro;
+  if (rs < ro && end <= ro) {
+    // DecodeEntry's limit is the restart array (block.cc:55-75, :181-195)
+    // (pointers formed only inside their buffer: no out-of-range base)
+    const bool in = rs >= wlo && end <= whi && rs <= end;
+    const uint8_t* p = in ? w + (rs - wlo) : idx + rs;
+    const uint8_t* pe = in ? w + (end - wlo) : idx + end;
+    const uint8_t* limit = in ? w + (whi - wlo) : idx + ro;
+    uint32_t sh, ns, vl;
+    const uint8_t* q = decode_entry(p, limit, &sh, &ns, &vl);
+    if (q != nullptr && sh == 0 && q + ns + vl == pe) {
+      uint64_t ho, hs;
+      if (!decode_handle(q + ns, q + ns + vl, &ho, &hs, nullptr)) {
+        st = LVKV_BLOCK_BAD_HANDLE;
+      } else {
+        const Fit f = handle_fit(ho, hs, tb.size);
+        if (f == kFitOk) {
+          st = LVKV_BLOCK_OK;
+          off = ho;
+          size = hs;
+        } else {
+          st = unfit_status(tb.img, f, ho);
+        }
+      }
+    }
+  }
+  if (st != LVKV_BLOCK_OK) off = size = 0;
+  const uint32_t e = first + i;
+  out_off[e] = tb.base + off;  // into d_file
+  out_size[e] = static_cast<uint32_t>(size);
+  out_status[e] = st;
+}
+
 // Launch 1: table t = blockIdx.x.
 __global__ void __launch_bounds__(kThreads, 1)
     sst_table_kernel(const uint8_t* file, const uint64_t* toff, const uint64_t* tsize,
@@ -430,44 +474,55 @@ __global__ void __launch_bounds__(kThreads, 1)
   if (h.status == LVKV_SST_CAPACITY || h.nb == 0) return;
 
   // 5. Every entry: index entries 0..nr-1, then the filter block.
-  const uint8_t* idx = stage_index ? ibuf : tb.img + h.io;
   const uint64_t nr = index_usable ? h.nr : 0u;
-  const uint64_t ro = h.is - (1 + nr) * 4;
-  for (uint32_t i = tid; i < h.nb; i += kThreads) {
-    uint8_t st = LVKV_BLOCK_BAD_ENTRY;
-    uint64_t off = 0, size = 0;
-    if (i == nr) {  // the filter block
-      st = h.filter_status;
-      off = h.fo;
-      size = h.fs;
-    } else {
-      const uint32_t rs = ld_le32(idx + ro + 4ull * i);
-      const uint64_t end = i + 1 < nr ? ld_le32(idx + ro + 4ull * (i + 1)) : ro;
-      if (rs < ro && end <= ro) {
-        uint32_t sh, ns, vl;
-        const uint8_t* q = decode_entry(idx + rs, idx + ro, &sh, &ns, &vl);
-        if (q != nullptr && sh == 0 && q + ns + vl == idx + end) {
-          uint64_t ho, hs;
-          if (!decode_handle(q + ns, q + ns + vl, &ho, &hs, nullptr)) {
-            st = LVKV_BLOCK_BAD_HANDLE;
-          } else {
-            const Fit f = handle_fit(ho, hs, tb.size);
-            if (f == kFitOk) {
-              st = LVKV_BLOCK_OK;
-              off = ho;
-              size = hs;
-            } else {
-              st = unfit_status(tb.img, f, ho);
-            }
-          }
-        }
-      }
-    }
-    if (st != LVKV_BLOCK_OK) off = size = 0;
-    const uint32_t e = h.first + i;
-    out_off[e] = tb.base + off;  // into d_file
-    out_size[e] = static_cast<uint32_t>(size);
+  if (tid == 0 && h.has_filter) {
+    const uint32_t e = h.first + static_cast<uint32_t>(nr);
+    const uint8_t st = h.filter_status;
+    out_off[e] = tb.base + (st == LVKV_BLOCK_OK ? h.fo : 0);
+    out_size[e] = static_cast<uint32_t>(st == LVKV_BLOCK_OK ? h.fs : 0);
     out_status[e] = st;
+  }
+  if (nr == 0) return;
+  const uint64_t ro = h.is - (1 + nr) * 4;
+  if (stage_index) {
+    for (uint32_t i = tid; i < nr; i += kThreads)
+      emit_entry(ibuf, ro, nr, i, ibuf, 0, ro, tb, h.first, out_off, out_size, out_status);
+    return;
+  }
+  // An index larger than LDS: windows of up to kThreads consecutive entries,
+  // the window's bytes staged in LDS (one coalesced pass) and the entries
+  // decoded from there; an entry that does not fit its window is decoded
+  // from the image.
+  const uint8_t* idx = tb.img + h.io;
+  uint32_t* wnd = reinterpret_cast<uint32_t*>(lds);
+  __shared__ uint64_t win_lo, win_hi;
+  for (uint64_t i0 = 0; i0 < nr; i0 += kThreads) {
+    const uint64_t i1 = min<uint64_t>(nr, i0 + kThreads);
+    if (tid == 0) {
+      // restart offsets are ascending in a well-formed block; a window that
+      // is not (or is too long) is decoded from the image
+      const uint64_t lo = ld_le32(idx + ro + 4 * i0);
+      const uint64_t hi = i1 < nr ? ld_le32(idx + ro + 4 * i1) : ro;
+      const bool ok = lo <= hi && hi <= ro && hi - lo <= kIndexStage - 16;
+      win_lo = ok ? (lo & ~uint64_t{3}) : 0;
+      win_hi = ok ? hi : 0;
+    }
+    __syncthreads();
+    const uint64_t lo = win_lo, hi = win_hi;
+    const uint64_t ndw = (hi - lo + 3) / 4;
+    for (uint64_t k = tid; k < ndw; k += kThreads) {
+      const uint64_t b = lo + 4 * k;
+      wnd[k] = (b + 4 <= ro) ? ld_le32(idx + b)
+                             : (static_cast<uint32_t>(idx[b]) |
+                                (b + 1 < ro ? static_cast<uint32_t>(idx[b + 1]) << 8 : 0u) |
+                                (b + 2 < ro ? static_cast<uint32_t>(idx[b + 2]) << 16 : 0u));
+    }
+    __syncthreads();
+    const uint64_t i = i0 + tid;
+    if (i < i1)
+      emit_entry(idx, ro, nr, static_cast<uint32_t>(i), reinterpret_cast<const uint8_t*>(wnd), lo,
+                 hi, tb, h.first, out_off, out_size, out_status);
+    __syncthreads();
   }
 }
 

@@ -78,11 +78,25 @@ def test_google_abi_and_cpp_symbol(lvkv):
     assert f(0, b"TestCRCBuffer", 13) == 0xDCBC59FA
 
 
-def test_portable_and_hw_paths_agree(lvkv):
-    # Both per-call implementations exist; whichever was picked must agree
-    # with the other on random data (the portable one is reachable through
-    # a CPU without SSE4.2 only, so compare via the Google ABI + oracle).
+def test_portable_and_hw_paths_agree(lvkv, oracle, golden):
+    # Both per-call implementations: the one picked for this CPU (the public
+    # entry points) and the portable slicing-by-8 (debug export), against the
+    # reference KATs and the oracle on every length 0..300 and alignment.
     assert lvkv.cpu_impl() in ("sse4.2", "portable-slice8")
+    f = lvkv.lib.lvkv_debug_extend_portable
+    f.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]
+    f.restype = ctypes.c_uint32
+    for v in golden("kat.json")["vectors"]:
+        data = bytes.fromhex(v["hex"])
+        assert f(v["init"], data, len(data)) == v["crc"], v["name"]
+    rng = np.random.default_rng(8)
+    buf = rng.integers(0, 256, 70000, dtype=np.uint8).tobytes()
+    for n in list(range(0, 300)) + [4095, 4096, 4097, 32762, 65536]:
+        for a in (0, 1, 3, 5):
+            init = int(rng.integers(0, 2**32))
+            want = oracle.extend(init, buf[a:a + n])
+            assert f(init, buf[a:], n) == want
+            assert lvkv.Extend(init, buf[a:a + n]) == want
 
 
 def test_no_device_is_an_error_not_a_fallback(lvkv):

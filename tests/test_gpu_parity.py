@@ -333,3 +333,34 @@ def test_general_layout_kernels(lvkv, oracle, gpu, kernel):
         assert np.array_equal(_u32(got), want)
     finally:
         L_.lvkv_debug_set_general_kernel(0)
+
+
+@pytest.mark.gpu
+def test_kat_vectors_through_the_batch_kernels(lvkv, gpu, golden):
+    # tests/golden/kat.json (util/crc32c_test.cc's known answers) as one
+    # batch: every vector a block with its own init, at every start
+    # alignment, through the general-layout kernel; masked values too.
+    import torch
+    vecs = golden("kat.json")["vectors"]
+    blob, offs, lens, inits, want, wmask = bytearray(), [], [], [], [], []
+    for a in range(4):
+        for v in vecs:
+            data = bytes.fromhex(v["hex"])
+            blob += b"\0" * ((a - len(blob)) % 8)
+            offs.append(len(blob))
+            blob += data
+            lens.append(len(data))
+            inits.append(v["init"])
+            want.append(v["crc"])
+            wmask.append(v["masked"])
+    data = np.frombuffer(bytes(blob) + b"\0" * 64, dtype=np.uint8)
+    d = _to_dev(torch, data, gpu)
+    o = _to_dev(torch, np.array(offs, np.int64), gpu)
+    n = _to_dev(torch, np.array(lens, np.uint32).view(np.int32), gpu)
+    i = _to_dev(torch, np.array(inits, np.uint32).view(np.int32), gpu)
+    got = lvkv.crc32c_batch(d, o, n, inits=i)
+    torch.cuda.synchronize()
+    assert _u32(got).tolist() == want
+    got_m = lvkv.crc32c_batch(d, o, n, inits=i, mask=True)
+    torch.cuda.synchronize()
+    assert _u32(got_m).tolist() == wmask

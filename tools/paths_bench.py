@@ -98,7 +98,8 @@ def main():
         def call():
             rc = L.lvkv_sst_verify_table_device(vp(buf.data_ptr()), len(img), vp(o2.data_ptr()),
                                                 vp(s2.data_ptr()), vp(a2.data_ptr()),
-                                                vp(st2.data_ptr()), cap, vp(rp.data_ptr()), h)
+                                                vp(st2.data_ptr()), cap, lvkv.BLOOM_POLICY.encode(),
+                                                vp(rp.data_ptr()), h)
             assert rc == 0
         us = timed(call, args.reps)
         handles = want.handles + [want.meta, want.index]
@@ -163,7 +164,7 @@ def main():
         rc = L.lvkv_sst_verify_tables_device(
             vp(buf.data_ptr()), vp(d_toff.data_ptr()), vp(d_tsz.data_ptr()), 32,
             vp(o3.data_ptr()), vp(s3.data_ptr()), vp(a3.data_ptr()), vp(st3.data_ptr()), tot,
-            vp(rp3.data_ptr()), h)
+            lvkv.BLOOM_POLICY.encode(), vp(rp3.data_ptr()), h)
         assert rc == 0
 
     def single():
@@ -172,13 +173,14 @@ def main():
             rc = L.lvkv_sst_verify_table_device(
                 vp(buf.data_ptr() + offs[t]), sizes_t[t], vp(o3.data_ptr() + 8 * f),
                 vp(s3.data_ptr() + 4 * f), vp(a3.data_ptr() + 4 * f), vp(st3.data_ptr() + f),
-                600, vp(rp3.data_ptr() + t * ctypes.sizeof(lvkv.SstReport)), h)
+                600, lvkv.BLOOM_POLICY.encode(),
+                vp(rp3.data_ptr() + t * ctypes.sizeof(lvkv.SstReport)), h)
             assert rc == 0
     nbytes = sum(sizes_t)
     us_m = timed(multi, max(5, args.reps // 5))
     us_s = timed(single, max(5, args.reps // 5))
     report("sst_verify_tables_32x2MiB", nbytes, us_m, None,
-           f"one multi-table call (4 launches); 32 single-table calls: {us_s:.1f} us")
+           f"one multi-table call (2 launches); 32 single-table calls: {us_s:.1f} us")
 
     for nrec in (2000, 60000):
         img = log_synth.build_log(nrec, seed=nrec, max_len=2000, big_every=997)

@@ -39,6 +39,14 @@ void lvkv_debug_set_stamps(uint64_t* d_stamps);
 int lvkv_debug_read_bw(const void* d_data, uint64_t bytes, uint32_t* d_scratch,
                        int groups, void* stream);
 
+/* WAL verify kernel phase stamps: 8 u64 (s_memrealtime) per workgroup and
+ * iteration (16 iterations kept), slots 0 start, 1 placed, 2 next walked,
+ * 3 wave 2's records done, 4 all records, 5 long records, 6 merged. */
+void lvkv_debug_log_stamps(uint64_t* d_stamps);
+/* WAL verify kernel ablations (timing only, results wrong): 1 no record CRCs,
+ * 4 no placement look-back. */
+void lvkv_debug_log_knobs(uint32_t knobs);
+
 #ifdef __cplusplus
 }
 #endif
