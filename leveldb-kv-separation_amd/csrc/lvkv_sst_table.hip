@@ -375,9 +375,15 @@ __global__ void __launch_bounds__(kThreads, 1)
     const uint64_t off = which ? h.mo : h.io, sz = which ? h.ms : h.is;
     if (!footer_ok || (which ? h.mfit : h.ifit) != kFitOk) continue;
     const uint64_t start = reinterpret_cast<uint64_t>(tb.img) + off;
-    const uint32_t crc = workgroup_crc<kW, 1024>(lds, lds + kCompactLdsBytes / 4, start,
-                                                 start + sz + 1, 0u, keys, tid, wave, lane,
-                                                 lane_base, zpow);
+    // 1 KiB segments spread a small block over all 16 waves (one memory round
+    // trip); a large one (the index of a big table) in 32 KiB segments, whose
+    // 4 KiB chunks each wave streams with the next one in flight
+    const uint32_t crc =
+        sz + 1 > 64 * 1024
+            ? workgroup_crc<kW, 32 * 1024>(lds, lds + kCompactLdsBytes / 4, start, start + sz + 1,
+                                          0u, keys, tid, wave, lane, lane_base, zpow)
+            : workgroup_crc<kW, 1024>(lds, lds + kCompactLdsBytes / 4, start, start + sz + 1, 0u,
+                                      keys, tid, wave, lane, lane_base, zpow);
     if (tid == 0) (which ? h.mcrc : h.icrc) = crc;
   }
 

@@ -211,7 +211,7 @@ def main():
         cpu = cpu_rate(ref, np.frombuffer(img, dtype=np.uint8), [x + 6 for x in v.hdrs],
                        lens) if ref else None
         report(f"log_verify_blocks_{nrec}rec", len(img), us, cpu,
-               f"{nb} blocks, {cap} records: walk + scan + emit + verify + merge")
+               f"{nb} blocks, {cap} records: one launch: stage, walk, place, checksum, merge")
 
         def fill():
             rc = L.lvkv_log_fill_headers_device(vp(buf.data_ptr()), vp(hdr.data_ptr()), None,
