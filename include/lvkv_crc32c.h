@@ -39,6 +39,12 @@ extern "C" {
  * barrier bit) and uses the kernel shaped for the whole chip. Without it,
  * consecutive batches overlap, each on half of every CU. */
 #define LVKV_FLAG_ORDERED 2u
+/* Engine submits only: the batch's first dispatch acquires at system scope
+ * (invalidates the L2) instead of agent scope. Needed when the input was
+ * written by a copy engine or the host since the device last read that
+ * memory (hipMemcpy into a reused buffer); inputs written by kernels on this
+ * device do not need it. Costs about 2.5 us per submission. */
+#define LVKV_FLAG_SYSTEM_ACQUIRE 4u
 
 /* ---- per-call, host CPU: the drop-in for the reference's own symbols ---- */
 

@@ -41,7 +41,7 @@ int lvkv_engine_load_probe(struct lvkv_engine* engine, const void* code_object, 
                            const char* kernel, uint32_t waves, uint32_t chains, uint32_t per_cu,
                            int overlapped);
 /* Memory-fence scopes (0 none, 1 agent, 2 system) of a submission's first
- * dispatch (acquire; default system) and of the wait's barrier packets
+ * dispatch (acquire; default agent) and of the wait's barrier packets
  * (acquire, release; default system, system). Timing probes only. */
 int lvkv_engine_set_scopes(struct lvkv_engine* engine, int dispatch_acquire, int fence_acquire,
                            int fence_release);

@@ -30,6 +30,7 @@ kMaskDelta = 0xA282EAD8  # util/crc32c.h:22
 LVKV_OK = 0
 LVKV_FLAG_MASK = 1
 LVKV_FLAG_ORDERED = 2
+LVKV_FLAG_SYSTEM_ACQUIRE = 4
 
 
 class LvkvError(RuntimeError):
@@ -532,13 +533,17 @@ class Engine:
         self.submit_ptr = _lib.lvkv_engine_crc32c_uniform
 
     def crc32c_uniform(self, buf, nblocks: int, length: int, stride: Optional[int] = None, *,
-                       init: int = 0, mask: bool = False, ordered: bool = False, out=None):
+                       init: int = 0, mask: bool = False, ordered: bool = False,
+                       fresh: bool = True, out=None):
+        """fresh: the input may have been written by a copy engine or the host
+        (LVKV_FLAG_SYSTEM_ACQUIRE); False when a kernel on this device wrote it."""
         torch = _torch()
         stride = length if stride is None else stride
         if nblocks and (nblocks - 1) * stride + length > buf.numel():
             raise ValueError("blocks exceed the buffer")
         out = _u32_out(torch, nblocks, buf.device, out)
-        flags = (LVKV_FLAG_MASK if mask else 0) | (LVKV_FLAG_ORDERED if ordered else 0)
+        flags = ((LVKV_FLAG_MASK if mask else 0) | (LVKV_FLAG_ORDERED if ordered else 0) |
+                 (LVKV_FLAG_SYSTEM_ACQUIRE if fresh else 0))
         # the engine does not follow HIP streams: the inputs must be complete
         torch.cuda.current_stream(buf.device).synchronize()
         rc = _lib.lvkv_engine_crc32c_uniform(

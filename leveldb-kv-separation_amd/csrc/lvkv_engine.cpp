@@ -187,9 +187,8 @@ struct Engine {
   EngineKernel probe;
   // fence scopes: a submission's first dispatch acquires at `dispatch_acq`;
   // the wait's barrier packets acquire/release at fence_acq/fence_rel
-  // (system: the inputs may have been written by a copy engine, which the
-  // L2 does not see)
-  int dispatch_acq = HSA_FENCE_SCOPE_SYSTEM;
+  // (LVKV_FLAG_SYSTEM_ACQUIRE raises it to system scope for one submission)
+  int dispatch_acq = HSA_FENCE_SCOPE_AGENT;
   int fence_acq = HSA_FENCE_SCOPE_SYSTEM, fence_rel = HSA_FENCE_SCOPE_SYSTEM;
   int variant = 0;          // kernel of overlapped dispatches
   int ordered_variant = 1;  // kernel of ordered dispatches (the whole chip)
@@ -445,7 +444,7 @@ void fence(Engine& e) {
 
 // One kernel-dispatch packet; the caller holds e.mu.
 int dispatch(Engine& e, const EngineKernel& k, const UniformArgs& args, bool acquire,
-             bool barrier) {
+             bool barrier, bool system_acquire) {
   if (e.queue_error) return LVKV_ERR_HIP;
   const uint64_t n = e.next;
   // Kernarg slot n % kSlots was last used by dispatch n - kSlots.
@@ -488,7 +487,8 @@ int dispatch(Engine& e, const EngineKernel& k, const UniformArgs& args, bool acq
   const uint16_t header = static_cast<uint16_t>(
       (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
       ((barrier ? 1 : 0) << HSA_PACKET_HEADER_BARRIER) |
-      ((acquire ? e.dispatch_acq : HSA_FENCE_SCOPE_NONE)
+      ((acquire ? (system_acquire ? HSA_FENCE_SCOPE_SYSTEM : e.dispatch_acq)
+                 : HSA_FENCE_SCOPE_NONE)
        << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
       (HSA_FENCE_SCOPE_NONE
        << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
@@ -565,8 +565,8 @@ int lvkv_engine_crc32c_uniform(lvkv_engine* eng, const void* d_base, uint64_t st
       const uint64_t area = groups * k.waves * 8;
       a.stamps = e->stamps + (e->stamp_next++ % e->stamp_areas) * area;
     }
-    const int rc = dispatch(*e, k, a, /*acquire=*/i == 0,
-                            /*barrier=*/ordered);
+    const int rc = dispatch(*e, k, a, /*acquire=*/i == 0, /*barrier=*/ordered,
+                            (flags & LVKV_FLAG_SYSTEM_ACQUIRE) != 0);
     if (rc != LVKV_OK) return rc;
     done += n;
   }

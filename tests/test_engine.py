@@ -105,3 +105,22 @@ def test_engine_rejects_bad_shapes(lvkv, eng, gpu):
         eng.crc32c_uniform(buf[1:], 2, 8, 8)  # end not 4-byte aligned
     out = eng.crc32c_uniform(buf, 0, 4096)
     assert out.numel() == 0
+
+
+def test_engine_reads_a_reused_buffer_after_a_host_copy(oracle, eng, gpu):
+    """A buffer the device has read, overwritten by a host-to-device copy,
+    checksummed again with LVKV_FLAG_SYSTEM_ACQUIRE (the wrapper's default):
+    the new bytes, not lines left in the L2."""
+    import torch
+    nb, L = 2000, 4096
+    buf = _data(torch, gpu, nb * L, 21)
+    first = eng.crc32c_uniform(buf, nb, L, fresh=False)
+    eng.wait()
+    host = np.random.default_rng(5).integers(0, 256, nb * L, dtype=np.uint8)
+    buf.copy_(torch.from_numpy(host))
+    torch.cuda.synchronize()
+    again = eng.crc32c_uniform(buf, nb, L)  # fresh=True
+    eng.wait()
+    assert np.array_equal(again.cpu().numpy().view(np.uint32),
+                          oracle.uniform(host, nb, L, threads=8))
+    assert not torch.equal(first, again)
