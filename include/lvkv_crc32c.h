@@ -109,8 +109,9 @@ void lvkv_engine_destroy(lvkv_engine* engine);
 int lvkv_engine_crc32c_uniform(lvkv_engine* engine, const void* d_base, uint64_t stride,
                                uint32_t length, uint32_t init, uint32_t* d_out,
                                size_t nblocks, uint32_t flags);
-/* Blocks until every dispatch submitted so far has completed (a barrier
- * packet on every queue, system-scope release, host spin-wait). */
+/* Blocks until every dispatch submitted so far has completed and its results
+ * are visible to the host and other devices (a barrier packet on every queue,
+ * system-scope release, host spin-wait). */
 int lvkv_engine_wait(lvkv_engine* engine);
 /* Hardware queues the dispatches rotate over (1..4; default 3); 0 queries. */
 int lvkv_engine_queues(lvkv_engine* engine, int nqueues);

@@ -42,9 +42,11 @@ int lvkv_engine_load_probe(struct lvkv_engine* engine, const void* code_object, 
                            int overlapped);
 /* Memory-fence scopes (0 none, 1 agent, 2 system) of a submission's first
  * dispatch (acquire; default agent) and of the wait's barrier packets
- * (acquire, release; default system, system). Timing probes only. */
+ * (acquire, release; default none, system). Timing probes only. */
 int lvkv_engine_set_scopes(struct lvkv_engine* engine, int dispatch_acquire, int fence_acquire,
                            int fence_release);
+/* Hardware queue priority of the engine's queues (0 low, 1 normal, 2 high). */
+int lvkv_engine_set_priority(struct lvkv_engine* engine, int priority);
 /* Dispatch the timestamp build of the current kernel: dispatch k writes 8 u64
  * per wave (s_memrealtime, 100 MHz; slots 0 start, 1 loads issued, 2 image
  * built, 3 walk done, 4 stored) into area k % areas of d_stamps (areas x

@@ -189,7 +189,9 @@ struct Engine {
   // the wait's barrier packets acquire/release at fence_acq/fence_rel
   // (LVKV_FLAG_SYSTEM_ACQUIRE raises it to system scope for one submission)
   int dispatch_acq = HSA_FENCE_SCOPE_AGENT;
-  int fence_acq = HSA_FENCE_SCOPE_SYSTEM, fence_rel = HSA_FENCE_SCOPE_SYSTEM;
+  // (the fence acquires nothing: every later submission does its own
+  // acquire; measured 2 us sooner than a system-scope acquire)
+  int fence_acq = HSA_FENCE_SCOPE_NONE, fence_rel = HSA_FENCE_SCOPE_SYSTEM;
   int variant = 0;          // kernel of overlapped dispatches
   int ordered_variant = 1;  // kernel of ordered dispatches (the whole chip)
   uint8_t* kernarg = nullptr;     // kSlots x kSlotBytes
@@ -412,8 +414,9 @@ void collect_profile(Engine& e, uint32_t s) {
 }
 
 // A barrier-AND packet with the barrier bit on every queue in use: each
-// completes after every earlier packet of its queue, acquires and releases
-// at system scope; then wait for all of them. Caller holds e.mu.
+// completes after every earlier packet of its queue and releases at system
+// scope (the results visible to the host and to copy engines); then wait for
+// all of them. Caller holds e.mu.
 void fence(Engine& e) {
   hsa_signal_store_relaxed(e.fence_sig, e.nq);
   const int keep = e.cur;
@@ -685,6 +688,18 @@ int lvkv_engine_set_scopes(lvkv_engine* eng, int dispatch_acquire, int fence_acq
   e->dispatch_acq = dispatch_acquire;
   e->fence_acq = fence_acquire;
   e->fence_rel = fence_release;
+  return LVKV_OK;
+}
+
+int lvkv_engine_set_priority(lvkv_engine* eng, int priority) {
+  if (eng == nullptr || priority < 0 || priority > 2) return LVKV_ERR_INVALID;
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (e->fenced != e->next) fence(*e);
+  for (hsa_queue_t* q : e->queues)
+    if (hsa_amd_queue_set_priority(q, static_cast<hsa_amd_queue_priority_t>(priority)) !=
+        HSA_STATUS_SUCCESS)
+      return LVKV_ERR_HIP;
   return LVKV_OK;
 }
 

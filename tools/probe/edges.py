@@ -57,7 +57,9 @@ def main():
                                                  ctypes.c_int]
     scopes = [tuple(int(x) for x in a.split("=", 1)[1].split(","))
               for a in sys.argv if a.startswith("--scopes=")] or [(2, 2, 2)]
+    lvkv.lib.lvkv_engine_set_priority.argtypes = [ctypes.c_void_p, ctypes.c_int]
     for sc in scopes:
+        assert lvkv.lib.lvkv_engine_set_priority(h, sc[3] if len(sc) > 3 else 1) == 0
         assert lvkv.lib.lvkv_engine_set_scopes(h, *sc[:3]) == 0
         res[f"scopes_{sc}"] = run_set(eng, step, sc)
     (REPO / "gpurun_out").mkdir(exist_ok=True)
