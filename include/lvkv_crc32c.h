@@ -214,7 +214,7 @@ typedef struct lvkv_sst_report {
   /* library-internal */
   uint64_t link_;          /* multi-table placement: (call generation << 32) | entries */
   uint32_t total_;         /* tables[0] only: entries verified over all tables */
-  uint32_t reserved2_;
+  uint32_t done_;           /* fused form: the call's tag once this table's entries are out */
 } lvkv_sst_report;
 
 /* Verifies a whole SSTable image already in device memory, as Table::Open
@@ -299,6 +299,59 @@ int lvkv_log_verify_blocks_device(const void* d_file, uint64_t file_size,
                                   uint8_t* d_rec_status, size_t capacity,
                                   uint8_t* d_block_status, uint32_t* d_block_drop,
                                   lvkv_log_report* d_report, void* stream);
+
+/* ---- WAL / MANIFEST logical records (log::Reader::ReadRecord) --------- */
+/* Reporter::Corruption reasons, physical and logical (lvkv_log_corruption). */
+#define LVKV_LOGR_CHECKSUM 1       /* "checksum mismatch" (db/log_reader.cc:243-255) */
+#define LVKV_LOGR_BAD_LENGTH 2     /* "bad record length" (:221-232) */
+#define LVKV_LOGR_PARTIAL_1 3      /* "partial record without end(1)" (:86-98) */
+#define LVKV_LOGR_PARTIAL_2 4      /* "partial record without end(2)" (:100-112) */
+#define LVKV_LOGR_MISSING_1 5      /* "missing start of fragmented record(1)" (:114-121) */
+#define LVKV_LOGR_MISSING_2 6      /* "missing start of fragmented record(2)" (:123-134) */
+#define LVKV_LOGR_MIDDLE 7         /* "error in middle of record" (:145-151) */
+#define LVKV_LOGR_UNKNOWN_TYPE 8   /* "unknown record type %u" (:153-162), type in .type */
+
+typedef struct lvkv_log_record {
+  uint64_t offset;   /* LastRecordOffset(): header offset of its first fragment */
+  uint64_t length;   /* bytes of the record: its fragments' payloads, in order */
+  uint32_t first;    /* its first fragment, an index into d_hdr_offsets */
+  uint32_t nfrags;   /* its fragments are d_hdr_offsets[first .. first + nfrags) */
+} lvkv_log_record;
+
+typedef struct lvkv_log_corruption {
+  uint64_t bytes;    /* Reporter::Corruption's bytes argument */
+  uint32_t reason;   /* LVKV_LOGR_* */
+  uint32_t type;     /* LVKV_LOGR_UNKNOWN_TYPE: the header's type byte; else 0 */
+} lvkv_log_corruption;
+
+typedef struct lvkv_log_read_report {
+  int32_t status;    /* LVKV_OK, or LVKV_LOG_CAPACITY: the physical records did not fit
+                        `capacity` (nothing assembled), or the records / reports exceed
+                        their capacities (the counts stay exact, the arrays hold the first) */
+  uint32_t nrecords; /* logical records ReadRecord returns, in order */
+  uint32_t nreports; /* Reporter::Corruption calls, in order */
+  uint32_t stopped;  /* 1: a header whose type byte is kEof (5) ended ReadRecord early */
+  uint64_t bytes;    /* total bytes of the returned records */
+} lvkv_log_read_report;
+
+/* log::Reader(reporter, checksum = true, initial_offset = 0) over a whole
+ * log image in device memory: ReadRecord until it returns false
+ * (db/log_reader.cc:55-176 over ReadPhysicalRecord :189-271). Runs
+ * lvkv_log_verify_blocks_device (same physical outputs, same meaning) and then
+ * the logical layer on the device: FULL records, FIRST MIDDLE* LAST
+ * assembly, and every Reporter::Corruption call in the reader's order (the
+ * physical "checksum mismatch" / "bad record length" drops, "partial record
+ * without end", "missing start of fragmented record", "error in middle of
+ * record", "unknown record type"). d_records[i] locates logical record i
+ * (its fragments are consecutive physical records); d_reports[i] is the
+ * i-th Reporter call. Two launches on `stream`, no host synchronisation;
+ * totals in *d_read. */
+int lvkv_log_read_device(const void* d_file, uint64_t file_size, uint64_t* d_hdr_offsets,
+                         uint32_t* d_actual, uint8_t* d_rec_status, size_t capacity,
+                         uint8_t* d_block_status, uint32_t* d_block_drop,
+                         lvkv_log_report* d_report, lvkv_log_record* d_records,
+                         size_t record_capacity, lvkv_log_corruption* d_reports,
+                         size_t report_capacity, lvkv_log_read_report* d_read, void* stream);
 
 /* ---- batched, host-resident (end-to-end incl. PCIe) ------------------- */
 /* Blocks live in host memory (pageable or pinned). The library packs them

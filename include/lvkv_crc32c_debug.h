@@ -23,6 +23,14 @@ void lvkv_debug_tables(uint32_t* row_tab, uint32_t* lane_tab);
  * implementation the per-call entry points picked on this CPU. */
 uint32_t lvkv_debug_extend_portable(uint32_t crc, const uint8_t* data, size_t n);
 
+/* Kernel choices of the current device (per device, not process globals;
+ * timing and A/B tests): general-layout batches (-1 crc32c_kernel.hip's
+ * persistent kernel, 0..31 ragged cfgs), WAL records (ragged cfg), and the
+ * whole-SSTable verify form (0 by size, 1 one fused launch, 2 two launches). */
+int lvkv_debug_set_general_kernel(int cfg);
+int lvkv_debug_set_log_kernel(int cfg);
+int lvkv_debug_set_sst_form(int form);
+
 /* The kernel-variant, timestamp and read-bandwidth probes live in the probe
  * build of the library (tools/probe/liblvkv_probe.so, tools/probe/lvkv_probe.h),
  * not in liblvkv_crc32c.so. */

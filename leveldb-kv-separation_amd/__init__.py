@@ -87,6 +87,10 @@ def _load() -> ctypes.CDLL:
     L.lvkv_log_fill_headers_device.restype = i32
     L.lvkv_log_verify_blocks_device.argtypes = [vp, u64, vp, vp, vp, sz, vp, vp, vp, vp]
     L.lvkv_log_verify_blocks_device.restype = i32
+    L.lvkv_log_read_device.argtypes = [vp, u64, vp, vp, vp, sz, vp, vp, vp, vp, sz, vp, sz, vp, vp]
+    L.lvkv_log_read_device.restype = i32
+    L.lvkv_debug_set_sst_form.argtypes = [i32]
+    L.lvkv_debug_set_sst_form.restype = i32
     L.lvkv_log_verify_device.argtypes = [vp, vp, vp, vp, sz, vp]
     L.lvkv_log_verify_device.restype = i32
     L.lvkv_crc32c_batch_host.argtypes = [vp, vp, vp, vp, u32, vp, sz, u32]
@@ -289,7 +293,7 @@ class SstReport(ctypes.Structure):
                 ("index_offset", ctypes.c_uint64), ("index_size", ctypes.c_uint64),
                 ("meta_offset", ctypes.c_uint64), ("meta_size", ctypes.c_uint64),
                 ("link_", ctypes.c_uint64), ("total_", ctypes.c_uint32),
-                ("reserved2_", ctypes.c_uint32)]
+                ("done_", ctypes.c_uint32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_
@@ -478,6 +482,79 @@ def log_verify_blocks(file_buf, *, capacity: Optional[int] = None, stream=None):
         break
     n = r.nrecords if r.status == 0 else 0
     return r.as_dict(), hdr[:n], actual[:n], rst[:n], bst[:nblocks], bdrop[:nblocks]
+
+
+class LogReadReport(ctypes.Structure):
+    """lvkv_log_read_report (include/lvkv_crc32c.h)."""
+    _fields_ = [("status", ctypes.c_int32), ("nrecords", ctypes.c_uint32),
+                ("nreports", ctypes.c_uint32), ("stopped", ctypes.c_uint32),
+                ("bytes", ctypes.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# Reporter::Corruption reasons (LVKV_LOGR_*) as the reference words them
+# (db/log_reader.cc); an unknown type carries its number.
+LOG_REASONS = {1: "checksum mismatch", 2: "bad record length",
+               3: "partial record without end(1)", 4: "partial record without end(2)",
+               5: "missing start of fragmented record(1)",
+               6: "missing start of fragmented record(2)", 7: "error in middle of record",
+               8: "unknown record type {}"}
+
+
+def log_read(file_buf, *, capacity: Optional[int] = None, record_capacity: Optional[int] = None,
+             report_capacity: Optional[int] = None, stream=None):
+    """log::Reader(reporter, checksum=True, initial_offset=0) over the log image
+    in `file_buf` (uint8 CUDA tensor), all on the device
+    (lvkv_log_read_device): ReadRecord until it returns false.
+
+    Returns (read report dict, records, reports, physical):
+      records  list of (LastRecordOffset, length, first fragment, fragments)
+      reports  list of (bytes, reason text) — every Reporter::Corruption call
+      physical the log_verify_blocks tuple of the same call
+    Capacities default to sizes that always fit; a LVKV_LOG_CAPACITY result
+    from smaller ones is returned as is."""
+    import numpy as np
+    torch = _torch()
+    dev = file_buf.device
+    size = file_buf.numel()
+    nblocks = (size + 32767) // 32768
+    cap = capacity if capacity is not None else max(64, size // 7 + nblocks)
+    rcap = record_capacity if record_capacity is not None else cap
+    pcap = report_capacity if report_capacity is not None else cap + nblocks
+    hdr = torch.empty(cap, dtype=torch.int64, device=dev)
+    actual = torch.empty(cap, dtype=torch.int32, device=dev)
+    rst = torch.empty(cap, dtype=torch.uint8, device=dev)
+    bst = torch.empty(max(1, nblocks), dtype=torch.uint8, device=dev)
+    bdrop = torch.empty(max(1, nblocks), dtype=torch.int32, device=dev)
+    rep = torch.zeros(ctypes.sizeof(LogReport), dtype=torch.uint8, device=dev)
+    recs = torch.zeros(max(1, rcap) * 24, dtype=torch.uint8, device=dev)
+    reps = torch.zeros(max(1, pcap) * 16, dtype=torch.uint8, device=dev)
+    rd = torch.zeros(ctypes.sizeof(LogReadReport), dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        rc = _lib.lvkv_log_read_device(
+            _dev_ptr(file_buf, "file_buf", (torch.uint8, torch.int8)), size,
+            _dev_ptr(hdr, "hdr"), _dev_ptr(actual, "actual"), _dev_ptr(rst, "rec_status"), cap,
+            _dev_ptr(bst, "block_status"), _dev_ptr(bdrop, "block_drop"), _dev_ptr(rep, "report"),
+            _dev_ptr(recs, "records"), rcap, _dev_ptr(reps, "reports"), pcap,
+            _dev_ptr(rd, "read"), _stream_handle(stream, dev))
+    _check("lvkv_log_read_device", rc)
+    r = LogReport.from_buffer_copy(bytes(rep.cpu().numpy()))
+    o = LogReadReport.from_buffer_copy(bytes(rd.cpu().numpy()))
+    nrec = min(o.nrecords, rcap)
+    nrep = min(o.nreports, pcap)
+    rv = recs.cpu().numpy()[: nrec * 24].view(np.uint64).reshape(-1, 3)
+    records = [(int(x[0]), int(x[1]), int(x[2]) & 0xFFFFFFFF, int(x[2]) >> 32) for x in rv]
+    pv = reps.cpu().numpy()[: nrep * 16].view(np.uint64).reshape(-1, 2)
+    reports = []
+    for x in pv:
+        reason, typ = int(x[1]) & 0xFFFFFFFF, int(x[1]) >> 32
+        text = LOG_REASONS.get(reason, "?")
+        reports.append((int(x[0]), text.format(typ) if reason == 8 else text))
+    n = r.nrecords if r.status == 0 else 0
+    physical = (r.as_dict(), hdr[:n], actual[:n], rst[:n], bst[:nblocks], bdrop[:nblocks])
+    return o.as_dict(), records, reports, physical
 
 
 def crc32c_batch_host(data, offsets, lengths, *, init: int = 0, inits=None,

@@ -35,12 +35,13 @@ HOST_SOURCES = ["lvkv_tables.cpp", "lvkv_cpu_crc32c.cpp", "leveldb_crc32c_shim.c
 # HIP sources: kernels and the runtime-facing C-ABI.
 HIP_SOURCES = ["crc32c_kernel.hip", "crc32c_uniform.hip", "crc32c_compact.hip",
                "crc32c_ragged.hip", "lvkv_sst_table.hip", "lvkv_log_blocks.hip",
-               "lvkv_capi.cpp", "lvkv_engine.cpp"]
+               "lvkv_log_assemble.hip", "lvkv_capi.cpp", "lvkv_engine.cpp"]
 # Kernels of the AQL engine: compiled alone into a gfx950 code object that is
 # embedded in the library (.incbin) and loaded through the HSA loader.
 ENGINE_KERNELS = "lvkv_engine_kernels.hip"
 HEADERS = ["lvkv_kernel_args.h", "lvkv_tables.h", "crc32c_device_common.h",
-           "crc32c_uniform_common.h", "crc32c_compact_common.h", "crc32c_burst.h"]
+           "crc32c_uniform_common.h", "crc32c_compact_common.h", "crc32c_burst.h",
+           "crc32c_ragged_body.h", "lvkv_log_events.h"]
 
 
 def _run(cmd: list[str], verbose: bool) -> None:

@@ -287,6 +287,95 @@ __device__ uint32_t workgroup_crc(const uint32_t* lds, uint32_t* acc_slots, uint
   return crc;
 }
 
+// ---- one block over a group of waves, constant shifts in registers ------
+
+// Columns of Z_{c * 2^log2seg} (lvkv_tables.h build_zmul_columns; they
+// follow zpow in the device tables).
+__device__ __forceinline__ const uint32_t* zmul_cols(const uint32_t* zpow, uint32_t log2seg,
+                                                     uint32_t c) {
+  return zpow + kZPowDwords + ((log2seg - kZMulLog0) * kZMulMaxC + c - 1u) * 32u;
+}
+
+// Z(v) for a wave-uniform v and an operator given by its 32 columns: scalar
+// loads of the (never written) columns and 32 conditional xors, no chain of
+// dependent table lookups.
+__device__ __forceinline__ uint32_t apply_cols(const uint32_t* cols, uint32_t v) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int b = 0; b < 32; ++b) r ^= ((v >> b) & 1u) ? sload_u32(cols, static_cast<uint32_t>(b)) : 0u;
+  return r;
+}
+
+// Bitwise register update over the n (< 4) little-endian bytes of `bytes`.
+__device__ __forceinline__ uint32_t crc_bytes_bitwise(uint32_t reg, uint32_t bytes, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) {
+    reg ^= (bytes >> (8u * i)) & 0xffu;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) reg = (reg >> 1) ^ (kCastagnoliReflected & (0u - (reg & 1u)));
+  }
+  return reg;
+}
+
+// Smallest segment (log2, 2^10 .. 2^15 bytes) that gives each of GW waves at
+// most one segment of a `len`-byte block, where that is possible.
+__device__ __forceinline__ uint32_t group_log2seg(uint64_t len, uint32_t GW) {
+  uint32_t l = 10;
+  while (l < 15 && (uint64_t{GW} << l) < len) ++l;
+  return l;
+}
+
+// This wave's share of the register of [start, end) from `init`, for wave gw
+// of a group of GW waves. Segments of 2^log2seg bytes are cut back from
+// e4 = floor4(end): segment j (j = 0 the last) is [max(start, e4 - (j+1)S),
+// e4 - jS). Wave gw takes j = gw, gw + GW, ..., front to back, folding
+// acc <- Z_{GW S}(acc) ^ reg, and finally shifts acc by Z_{gw S} to e4: every
+// shift is a constant operator (apply_cols). The xor of the group's shares is
+// the register at e4; group_crc_finish adds the 0-3 bytes after it.
+__device__ inline uint32_t group_crc_part(const uint32_t* lds, uint64_t start, uint64_t end,
+                                   uint32_t init, uint32_t gw, uint32_t GW, uint32_t log2seg,
+                                   const LaneKeys& keys, uint32_t lane, uint32_t lane_base,
+                                   const uint32_t* zpow) {
+  const uint64_t seg = uint64_t{1} << log2seg;
+  const uint64_t e4 = end & ~uint64_t{3};
+  if (e4 <= start) return 0u;
+  const uint32_t m = static_cast<uint32_t>((e4 - start + seg - 1) >> log2seg);
+  if (gw >= m) return 0u;
+  const uint32_t jmax = gw + ((m - 1u - gw) / GW) * GW;
+  const uint32_t* stride_cols = zmul_cols(zpow, log2seg, GW);
+  uint32_t acc = 0;
+  for (uint32_t j = jmax;; j -= GW) {
+    const uint64_t e = e4 - uint64_t{j} * seg;
+    const bool front = j == m - 1u;
+    const uint64_t s = front ? start : e - seg;
+    const uint32_t reg =
+        segment_register(lds, s, e, front ? init : 0xffffffffu, keys, lane, lane_base);
+    acc = (j == jmax ? 0u : apply_cols(stride_cols, acc)) ^ reg;
+    if (j < GW) break;
+  }
+  return gw ? apply_cols(zmul_cols(zpow, log2seg, gw), acc) : acc;
+}
+
+// CRC of [start, end) from the xor of the group's shares and `tail`, the
+// little-endian bytes from max(start, floor4(end)) to end (fewer than 4).
+__device__ __forceinline__ uint32_t group_crc_finish(uint32_t parts, uint64_t start, uint64_t end,
+                                                     uint32_t init, uint32_t tail) {
+  const uint64_t e4 = end & ~uint64_t{3};
+  const bool none = e4 <= start;  // fewer than 4 bytes up to a boundary
+  const uint32_t reg = none ? init ^ 0xffffffffu : parts;
+  return crc_bytes_bitwise(reg, tail, static_cast<uint32_t>(end - (none ? start : e4))) ^
+         0xffffffffu;
+}
+
+// The little-endian bytes [max(start, floor4(end)), end) (the `tail` above).
+__device__ __forceinline__ uint32_t group_crc_tail(uint64_t start, uint64_t end) {
+  const uint64_t e4 = end & ~uint64_t{3};
+  const uint64_t from = e4 <= start ? start : e4;
+  uint32_t v = 0;
+  for (uint64_t p = from; p < end; ++p)
+    v |= static_cast<uint32_t>(*reinterpret_cast<const uint8_t*>(p)) << (8u * (p - from));
+  return v;
+}
+
 }  // namespace
 }  // namespace lvkv
 

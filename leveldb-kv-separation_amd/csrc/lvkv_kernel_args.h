@@ -39,6 +39,10 @@ constexpr uint32_t kLogLongBytes = 8 * 1024;
 constexpr uint32_t kZPowCount = 48;               // Z_{2^j}, j < 48 (256 TiB)
 constexpr uint32_t kZPowDwords = kZPowCount * 1024;
 constexpr uint32_t kZPowOffset = 1024 + 8 * 16 * 64 + 8 * 64 * 4;  // in d_tables
+// Columns of Z_{c * 2^j}, j in [kZMulLog0, kZMulLog0 + kZMulLogs), c in
+// [1, kZMulMaxC] (lvkv_tables.h), right after zpow in d_tables.
+constexpr uint32_t kZMulLog0 = 8, kZMulLogs = 16, kZMulMaxC = 16;
+constexpr uint32_t kZMulDwords = kZMulLogs * kZMulMaxC * 32;
 constexpr uint32_t kLdsRowRegionBytes = 64 * 1024;
 constexpr uint32_t kLdsLaneTabBase = 128 * 1024;
 constexpr uint32_t kLdsBytes = 160 * 1024;
@@ -93,6 +97,8 @@ struct KernelArgs {
                               //   bytes when a unit is a fixed-size region
                               //   (the WAL's 32 KiB blocks); nullptr = equal
                               //   block counts per workgroup
+  uint32_t fresh_desc;        // 1: offsets/lengths were written by this same
+                              //   launch (vector loads after an acquire)
   int32_t general_cfg;        // host side: kernel of general-layout batches
   int32_t log_cfg;            //   and of WAL records (launch_crc32c_general);
                               //   the device context's choice, never read

@@ -41,6 +41,7 @@
 #include "crc32c_device_common.h"
 #include "lvkv_crc32c.h"
 #include "lvkv_kernel_args.h"
+#include "lvkv_log_events.h"
 
 namespace lvkv {
 namespace {
@@ -127,6 +128,7 @@ struct LogArgs {
   uint64_t* done;  // finished workgroups (zeroed before the launch)
   const uint32_t* zpow;
   const uint32_t* lane_cols;
+  uint32_t* events;  // nullable: the ReadRecord event stream (lvkv_log_events.h)
   uint64_t* stamps;  // probe build only: 8 u64 per (workgroup, iteration)
   uint32_t knobs;    // probe build only: 1 no record CRCs, 2 no walk wait, 4 no placement
 };
@@ -168,20 +170,6 @@ __device__ __forceinline__ LdsRec lds_rec(uint32_t a, uint32_t n, uint32_t rows)
   r.spill = delta ? (0xffffffffu >> (32u - r.sh)) : 0u;
   r.first = a - delta;  // byte address of grid word s0l
   return r;
-}
-
-// Grid word 64 r + lane, branch-free (a word before the record reads
-// address 0 and is masked).
-__device__ __forceinline__ uint32_t lds_grid_word(const uint8_t* buf, const LdsRec& g, uint32_t r,
-                                                  uint32_t lane) {
-  const uint32_t j = 64u * r + lane;
-  const bool in = j >= g.s0l;
-  const uint32_t x = in ? g.first + 4u * (j - g.s0l) : 0u;
-  const uint32_t* d = reinterpret_cast<const uint32_t*>(buf + (x & ~3u));
-  uint32_t w = __builtin_amdgcn_alignbyte(d[1], d[0], x & 3u);
-  w = in ? w : 0u;
-  w = j == g.s0l ? ((w & (0xffffffffu << g.sh)) ^ (0xffffffffu << g.sh)) : w;
-  return j == g.s0l + 1u ? (w ^ g.spill) : w;
 }
 
 // Byte address of grid word 64 r + lane (0 for a word before the record).
@@ -508,6 +496,9 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
               a.hdr_off[gi] = s.start + pp[t];
               a.actual[gi] = crc[t];
               a.rec_status[gi] = ok ? LVKV_REC_OK : LVKV_REC_CHECKSUM;
+              if (a.events != nullptr)
+                a.events[gi + b] = ok ? log_event(kEvRec, blk[pp[t] + 6], nn[t] - 1u)
+                                      : log_event(kEvSkip, 0, 0);
             }
           }
         }
@@ -534,6 +525,8 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
           a.hdr_off[gi] = s.start + p;
           a.actual[gi] = crc;
           a.rec_status[gi] = ok ? LVKV_REC_OK : LVKV_REC_CHECKSUM;
+          if (a.events != nullptr)
+            a.events[gi + b] = ok ? log_event(kEvRec, blk[p + 6], n - 1u) : log_event(kEvSkip, 0, 0);
         }
       }
     }
@@ -551,6 +544,9 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
       }
       a.block_status[b] = status;
       a.block_drop[b] = static_cast<uint32_t>(drop);
+      // the block's event follows its c records: item base + c + b
+      if (a.events != nullptr && base_s + c <= a.capacity)
+        a.events[base_s + c + b] = log_block_event(status, static_cast<uint32_t>(drop));
       a.good[b] = bad != 0xffffffffu ? bad : c;
       bad_s = bad;
     }
@@ -559,7 +555,10 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
     const uint32_t bad = bad_s;
     if (bad != 0xffffffffu)
       for (uint32_t j = bad + 1 + tid; j < c; j += kVThreads)
-        if (base_s + j < a.capacity) a.rec_status[base_s + j] = LVKV_REC_DROPPED;
+        if (base_s + j < a.capacity) {
+          a.rec_status[base_s + j] = LVKV_REC_DROPPED;
+          if (a.events != nullptr) a.events[base_s + j + b] = log_event(kEvSkip, 0, 0);
+        }
     __syncthreads();  // pos[cur], ready, first_bad are reused
     if (tid == 0) log_stamp(a, k, 6);
   }
@@ -645,7 +644,7 @@ hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_o
                              uint32_t* actual, uint8_t* rec_status, uint32_t capacity,
                              uint8_t* block_status, uint32_t* block_drop, lvkv_log_report* r,
                              const uint32_t* zpow, const uint32_t* lane_cols, int cus,
-                             void* scratch, hipStream_t stream) {
+                             void* scratch, uint32_t* events, hipStream_t stream) {
   const uint32_t nblocks = static_cast<uint32_t>((size + kLogBlock - 1) / kLogBlock);
   LogArgs a;
   memset(&a, 0, sizeof(a));
@@ -666,6 +665,7 @@ hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_o
   a.good = reinterpret_cast<uint32_t*>(a.inc + nblocks);
   a.zpow = zpow;
   a.lane_cols = lane_cols;
+  a.events = events;
 #ifdef LVKV_PROBE_BUILD
   a.stamps = g_log_stamps;
   a.knobs = g_log_knobs;

@@ -50,6 +50,7 @@
 
 #include "crc32c_compact_common.h"
 #include "crc32c_device_common.h"
+#include "crc32c_ragged_body.h"
 #include "lvkv_crc32c.h"
 #include "lvkv_kernel_args.h"
 
@@ -60,8 +61,6 @@ namespace {
 constexpr uint64_t kTableMagic = 0xdb4775248b80fb57ull;  // table/format.h:76
 constexpr uint64_t kFooterLen = 48;  // table/format.h:53 (2 * 20 + 8)
 constexpr uint64_t kTrailer = 5;     // table/format.h:79
-constexpr int kW = 16;               // waves per table workgroup
-constexpr uint32_t kThreads = 64 * kW;
 constexpr uint32_t kMetaStage = 2048;                // metaindex staged in LDS up to this
 constexpr uint32_t kIndexStage = kCompactLdsBytes;   // index staged in the (spent) image
 
@@ -343,18 +342,37 @@ __device__ void emit_entry(const uint8_t* idx, uint64_t ro, uint64_t nr, uint32_
   out_status[e] = st;
 }
 
-// Launch 1: table t = blockIdx.x.
-__global__ void __launch_bounds__(kThreads, 1)
-    sst_table_kernel(const uint8_t* file, const uint64_t* toff, const uint64_t* tsize,
-                     uint64_t single_size, uint32_t ntables, uint32_t capacity, uint32_t gen,
-                     FilterKey fk, lvkv_sst_report* reports, uint64_t* out_off,
-                     uint32_t* out_size, uint8_t* out_status, const uint32_t* zpow,
-                     const uint32_t* lane_cols) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kCompactLdsBytes / 4 + kW];
-  __shared__ uint8_t foot[kFooterLen];
-  __shared__ uint8_t mbuf[kMetaStage];
-  __shared__ Head h;
-  const uint32_t t = blockIdx.x;
+// What a table's workgroup keeps in LDS after the 64 KiB CRC image.
+struct SstHeadLds {
+  uint32_t acc[16];  // per-wave CRC shares
+  uint8_t foot[kFooterLen];
+  uint8_t mbuf[kMetaStage];
+  Head h;
+  uint64_t win_lo, win_hi;
+};
+
+// Index bytes prefetched into registers during the CRCs, per thread: an
+// index of up to 64 W * kIndexPf dwords is staged from these, without a
+// memory round trip after its checksum.
+constexpr int kIndexPf = 6;
+
+// Table t's head with W waves (Table::Open + ReadMeta + the index walk):
+// footer; index and metaindex CRCs at once (index on waves [0, wi),
+// metaindex on [wi, W), shifts as constant operators, group_crc_part), with
+// every byte the verdicts need (type bytes, trailers, restart count, the
+// 0-3 bytes after the last 4-byte boundary), the metaindex and a small index
+// loaded before the walks; verdicts in ReadBlock's order; the filter key;
+// the table's place; every entry's handle and status into the shared arrays.
+// `lds`: the compact image followed by SstHeadLds.
+template <int W>
+__device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, const uint64_t* toff,
+                         const uint64_t* tsize, uint64_t single_size, uint32_t t,
+                         uint32_t ntables, uint32_t capacity, uint32_t gen, const FilterKey& fk,
+                         lvkv_sst_report* reports, uint64_t* out_off, uint32_t* out_size,
+                         uint8_t* out_status, const uint32_t* zpow, const uint32_t* lane_cols) {
+  constexpr uint32_t kT = 64 * W;
+  SstHeadLds& L = *reinterpret_cast<SstHeadLds*>(lds + kCompactLdsBytes / 4);
+  Head& h = L.h;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = lane_id();
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -362,48 +380,86 @@ __global__ void __launch_bounds__(kThreads, 1)
   lvkv_sst_report* r = reports + t;
 
   // 1. Footer bytes (48 lanes) while the workgroup builds its LDS image.
-  if (tid < kFooterLen && tb.size >= kFooterLen) foot[tid] = tb.img[tb.size - kFooterLen + tid];
-  build_compact_image<kW>(lds, zpow, lane_cols, tid, wave, lane);  // ends with a barrier
-  if (tid == 0) parse_footer(h, foot, tb.size);
+  if (tid < kFooterLen && tb.size >= kFooterLen) L.foot[tid] = tb.img[tb.size - kFooterLen + tid];
+  build_compact_image<W>(lds, zpow, lane_cols, tid, wave, lane);  // ends with a barrier
+  if (tid == 0) parse_footer(h, L.foot, tb.size);
   __syncthreads();
   const bool footer_ok = h.status == LVKV_SST_OK;  // workgroup-uniform from here on
+  const bool ifit = footer_ok && h.ifit == kFitOk;
+  const bool mfit = footer_ok && h.mfit == kFitOk;
+  const uint64_t istart = reinterpret_cast<uint64_t>(tb.img) + h.io, iend = istart + h.is + 1;
+  const uint64_t mstart = reinterpret_cast<uint64_t>(tb.img) + h.mo, mend = mstart + h.ms + 1;
 
-  // 2. Index and metaindex: contents + type byte, CRC against the trailer.
-  const LaneKeys keys = lane_keys(lane);
-  const uint32_t lane_base = compact_lane_base(lane);
-  for (int which = 0; which < 2; ++which) {
-    const uint64_t off = which ? h.mo : h.io, sz = which ? h.ms : h.is;
-    if (!footer_ok || (which ? h.mfit : h.ifit) != kFitOk) continue;
-    const uint64_t start = reinterpret_cast<uint64_t>(tb.img) + off;
-    // 1 KiB segments spread a small block over all 16 waves (one memory round
-    // trip); a large one (the index of a big table) in 32 KiB segments, whose
-    // 4 KiB chunks each wave streams with the next one in flight
-    const uint32_t crc =
-        sz + 1 > 64 * 1024
-            ? workgroup_crc<kW, 32 * 1024>(lds, lds + kCompactLdsBytes / 4, start, start + sz + 1,
-                                          0u, keys, tid, wave, lane, lane_base, zpow)
-            : workgroup_crc<kW, 1024>(lds, lds + kCompactLdsBytes / 4, start, start + sz + 1, 0u,
-                                      keys, tid, wave, lane, lane_base, zpow);
-    if (tid == 0) (which ? h.mcrc : h.icrc) = crc;
+  // 2. Loads whose values are used after the CRCs, issued before them.
+  uint32_t itype = 0, itrail = 0, inr = 0xffffffffu, itail = 0, mtype = 0, mtrail = 0, mtail = 0;
+  if (tid == 0) {
+    if (ifit) {
+      const uint8_t* e = tb.img + h.io + h.is;
+      itype = e[0];
+      itrail = ld_le32(e + 1);
+      if (h.is >= 4) inr = ld_le32(e - 4);
+      itail = group_crc_tail(istart, iend);
+    }
+    if (mfit) {
+      const uint8_t* e = tb.img + h.mo + h.ms;
+      mtype = e[0];
+      mtrail = ld_le32(e + 1);
+      mtail = group_crc_tail(mstart, mend);
+    }
+  }
+  if (mfit && h.ms < kMetaStage)
+    for (uint32_t i = tid; i < h.ms; i += kT) L.mbuf[i] = tb.img[h.mo + i];
+  // a small index, as the aligned dwords holding it (the dword before it
+  // only when that is inside the image)
+  const uint64_t ia4 = istart & ~uint64_t{3};
+  const uint32_t ind = static_cast<uint32_t>((istart + h.is + 3 - ia4) >> 2);
+  const bool ipf = ifit && ind <= kT * kIndexPf && ia4 >= reinterpret_cast<uint64_t>(tb.img);
+  uint32_t pf[kIndexPf];
+  if (ipf) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(ia4);
+#pragma unroll
+    for (int k = 0; k < kIndexPf; ++k) {
+      const uint32_t i = tid + kT * static_cast<uint32_t>(k);
+      pf[k] = i < ind ? src[i] : 0u;
+    }
   }
 
-  // 3. Verdicts (ReadBlock's order), restart array; stage the metaindex.
+  // 3. Index and metaindex CRCs (contents + type byte) side by side.
+  const LaneKeys keys = lane_keys(lane);
+  const uint32_t lane_base = compact_lane_base(lane);
+  const uint32_t wi = h.ms + 1 > 4096 ? W / 2 : W - 1;  // waves on the index
+  uint32_t part = 0;
+  if (wave < wi) {
+    if (ifit)
+      part = group_crc_part(lds, istart, iend, 0u, wave, wi, group_log2seg(h.is + 1, wi), keys,
+                            lane, lane_base, zpow);
+  } else if (mfit) {
+    part = group_crc_part(lds, mstart, mend, 0u, wave - wi, W - wi,
+                          group_log2seg(h.ms + 1, W - wi), keys, lane, lane_base, zpow);
+  }
+  if (lane == 0) L.acc[wave] = part;
+  __syncthreads();
+
+  // 4. Verdicts (ReadBlock's order), restart array.
   if (tid == 0 && footer_ok) {
-    h.icrc = h.ifit == kFitOk ? h.icrc : 0u;
-    h.mcrc = h.mfit == kFitOk ? h.mcrc : 0u;
-    if (h.ifit != kFitOk) {
+    uint32_t ip = 0, mp = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      if (static_cast<uint32_t>(w) < wi) ip ^= L.acc[w]; else mp ^= L.acc[w];
+    }
+    h.icrc = ifit ? group_crc_finish(ip, istart, iend, 0u, itail) : 0u;
+    h.mcrc = mfit ? group_crc_finish(mp, mstart, mend, 0u, mtail) : 0u;
+    if (!ifit) {
       h.index_status = unfit_status(tb.img, static_cast<Fit>(h.ifit), h.io);
     } else {
-      h.itype = tb.img[h.io + h.is];
-      h.index_status =
-          read_status(h.icrc == crc_unmask(ld_le32(tb.img + h.io + h.is + 1)), h.itype);
+      h.itype = static_cast<uint8_t>(itype);
+      h.index_status = read_status(h.icrc == crc_unmask(itrail), h.itype);
     }
-    if (h.mfit != kFitOk) {
+    if (!mfit) {
       h.meta_status = unfit_status(tb.img, static_cast<Fit>(h.mfit), h.mo);
     } else {
-      h.mtype = tb.img[h.mo + h.ms];
-      h.meta_status =
-          read_status(h.mcrc == crc_unmask(ld_le32(tb.img + h.mo + h.ms + 1)), h.mtype);
+      h.mtype = static_cast<uint8_t>(mtype);
+      h.meta_status = read_status(h.mcrc == crc_unmask(mtrail), h.mtype);
     }
     switch (h.index_status) {
       case LVKV_BLOCK_OK: break;
@@ -413,11 +469,10 @@ __global__ void __launch_bounds__(kThreads, 1)
     }
     h.nr = 0;
     if (h.status == LVKV_SST_OK) {
-      const uint32_t nr = h.is >= 4 ? ld_le32(tb.img + h.io + h.is - 4) : 0xffffffffu;
-      if (h.is < 4 || nr > (h.is - 4) / 4)  // Block::Block (block.cc:28-37)
+      if (h.is < 4 || inr > (h.is - 4) / 4)  // Block::Block (block.cc:28-37)
         h.status = LVKV_SST_INDEX_CORRUPT;
       else
-        h.nr = nr;
+        h.nr = inr;
     }
     h.has_filter = 0;
     h.fo = h.fs = 0;
@@ -430,23 +485,31 @@ __global__ void __launch_bounds__(kThreads, 1)
   const bool index_read = footer_ok && h.index_status == LVKV_BLOCK_OK;
   const bool index_usable = h.status == LVKV_SST_OK;
   const bool stage_meta = index_read && h.meta_status == LVKV_BLOCK_OK && h.ms < kMetaStage;
-  if (stage_meta)
-    for (uint32_t i = tid; i < h.ms; i += kThreads) mbuf[i] = tb.img[h.mo + i];
   const bool stage_index = index_usable && h.is <= kIndexStage;
   uint8_t* ibuf = reinterpret_cast<uint8_t*>(lds);  // the CRC image is spent
-  if (stage_index)
-    for (uint32_t i = tid; i < h.is; i += kThreads) ibuf[i] = tb.img[h.io + i];
+  if (stage_index) {
+    if (ipf) {
+#pragma unroll
+      for (int k = 0; k < kIndexPf; ++k) {
+        const uint32_t i = tid + kT * static_cast<uint32_t>(k);
+        if (i < ind) lds[i] = pf[k];
+      }
+      ibuf += istart & 3u;
+    } else {
+      for (uint32_t i = tid; i < h.is; i += kT) ibuf[i] = tb.img[h.io + i];
+    }
+  }
   __syncthreads();
   if (tid == 0) {
     if (index_read && h.meta_status == LVKV_BLOCK_OK)
-      find_filter(h, stage_meta ? mbuf : tb.img + h.mo, h.ms, fk, tb);
+      find_filter(h, stage_meta ? L.mbuf : tb.img + h.mo, h.ms, fk, tb);
     // entries: the data blocks the index lists (none when its restart array
     // is unusable), then the filter block
     h.nb = (index_usable ? h.nr : 0u) + h.has_filter;
   }
   __syncthreads();
 
-  // 4. Place this table's entries in the shared arrays.
+  // 5. Place this table's entries in the shared arrays.
   if (wave == 0) {
     uint32_t total = 0, first = 0;
     if (ntables == 1) {
@@ -479,7 +542,7 @@ __global__ void __launch_bounds__(kThreads, 1)
   __syncthreads();
   if (h.status == LVKV_SST_CAPACITY || h.nb == 0) return;
 
-  // 5. Every entry: index entries 0..nr-1, then the filter block.
+  // 6. Every entry: index entries 0..nr-1, then the filter block.
   const uint64_t nr = index_usable ? h.nr : 0u;
   if (tid == 0 && h.has_filter) {
     const uint32_t e = h.first + static_cast<uint32_t>(nr);
@@ -491,32 +554,31 @@ __global__ void __launch_bounds__(kThreads, 1)
   if (nr == 0) return;
   const uint64_t ro = h.is - (1 + nr) * 4;
   if (stage_index) {
-    for (uint32_t i = tid; i < nr; i += kThreads)
+    for (uint32_t i = tid; i < nr; i += kT)
       emit_entry(ibuf, ro, nr, i, ibuf, 0, ro, tb, h.first, out_off, out_size, out_status);
     return;
   }
-  // An index larger than LDS: windows of up to kThreads consecutive entries,
-  // the window's bytes staged in LDS (one coalesced pass) and the entries
-  // decoded from there; an entry that does not fit its window is decoded
-  // from the image.
+  // An index larger than LDS: windows of up to kT consecutive entries, the
+  // window's bytes staged in LDS (one coalesced pass) and the entries decoded
+  // from there; an entry that does not fit its window is decoded from the
+  // image.
   const uint8_t* idx = tb.img + h.io;
-  uint32_t* wnd = reinterpret_cast<uint32_t*>(lds);
-  __shared__ uint64_t win_lo, win_hi;
-  for (uint64_t i0 = 0; i0 < nr; i0 += kThreads) {
-    const uint64_t i1 = min<uint64_t>(nr, i0 + kThreads);
+  uint32_t* wnd = lds;
+  for (uint64_t i0 = 0; i0 < nr; i0 += kT) {
+    const uint64_t i1 = min<uint64_t>(nr, i0 + kT);
     if (tid == 0) {
       // restart offsets are ascending in a well-formed block; a window that
       // is not (or is too long) is decoded from the image
       const uint64_t lo = ld_le32(idx + ro + 4 * i0);
       const uint64_t hi = i1 < nr ? ld_le32(idx + ro + 4 * i1) : ro;
       const bool ok = lo <= hi && hi <= ro && hi - lo <= kIndexStage - 16;
-      win_lo = ok ? (lo & ~uint64_t{3}) : 0;
-      win_hi = ok ? hi : 0;
+      L.win_lo = ok ? (lo & ~uint64_t{3}) : 0;
+      L.win_hi = ok ? hi : 0;
     }
     __syncthreads();
-    const uint64_t lo = win_lo, hi = win_hi;
+    const uint64_t lo = L.win_lo, hi = L.win_hi;
     const uint64_t ndw = (hi - lo + 3) / 4;
-    for (uint64_t k = tid; k < ndw; k += kThreads) {
+    for (uint64_t k = tid; k < ndw; k += kT) {
       const uint64_t b = lo + 4 * k;
       wnd[k] = (b + 4 <= ro) ? ld_le32(idx + b)
                              : (static_cast<uint32_t>(idx[b]) |
@@ -532,26 +594,93 @@ __global__ void __launch_bounds__(kThreads, 1)
   }
 }
 
+constexpr int kW = 16;  // waves per head of the two-launch form
+constexpr int kFW = 8;  // waves per workgroup of the fused form
+
+// Two-launch form, launch 1: table t = blockIdx.x, 16 waves (large indexes).
+__global__ void __launch_bounds__(64 * kW, 1)
+    sst_table_kernel(const uint8_t* file, const uint64_t* toff, const uint64_t* tsize,
+                     uint64_t single_size, uint32_t ntables, uint32_t capacity, uint32_t gen,
+                     FilterKey fk, lvkv_sst_report* reports, uint64_t* out_off,
+                     uint32_t* out_size, uint8_t* out_status, const uint32_t* zpow,
+                     const uint32_t* lane_cols) {
+  __shared__ __attribute__((aligned(16)))
+  uint32_t lds[kCompactLdsBytes / 4 + (sizeof(SstHeadLds) + 3) / 4];
+  sst_head<kW>(lds, file, toff, tsize, single_size, blockIdx.x, ntables, capacity, gen, fk,
+               reports, out_off, out_size, out_status, zpow, lane_cols);
+}
+
+constexpr uint32_t kHeadLdsDwords =
+    static_cast<uint32_t>(kCompactLdsBytes / 4 + (sizeof(SstHeadLds) + 3) / 4);
+constexpr uint32_t kFusedLdsDwords =
+    RagLds<kFW>::kDwords > kHeadLdsDwords ? RagLds<kFW>::kDwords : kHeadLdsDwords;
+
+// Fused form, ONE launch: workgroups [0, ntables) are the table heads
+// (sst_head<8>), each publishing its report's done_ word (this call's
+// generation, release at agent scope) when its entries are written; the
+// others build their CRC image, wait for every head (acquire) and run the
+// ragged walk in kModeSstTable over all entries, reading the descriptors
+// with vector loads (KernelArgs::fresh_desc). Heads never wait on a CRC
+// workgroup, and have the lower workgroup ids, so they are dispatched first:
+// every wait ends.
+__global__ void __launch_bounds__(64 * kFW, 2)
+    sst_fused_kernel(KernelArgs a, const uint8_t* file, const uint64_t* toff,
+                     const uint64_t* tsize, uint64_t single_size, uint32_t ntables,
+                     uint32_t capacity, uint32_t gen, FilterKey fk, lvkv_sst_report* reports,
+                     const uint32_t* zpow, const uint32_t* lane_cols) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kFusedLdsDwords];
+  const uint32_t tid = threadIdx.x;
+  if (blockIdx.x < ntables) {
+    sst_head<kFW>(lds, file, toff, tsize, single_size, blockIdx.x, ntables, capacity, gen, fk,
+                  reports, const_cast<uint64_t*>(a.offsets), const_cast<uint32_t*>(a.lengths),
+                  a.out_status, zpow, lane_cols);
+    // every wave's stores are done at the barrier; one agent-scope release
+    // (writes this XCD's L2 back) publishes them with the tag
+    __syncthreads();
+    if (tid == 0)
+      __hip_atomic_store(&reports[blockIdx.x].done_, gen, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  const uint32_t lane = lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (tid == 0) lds[RagLds<kFW>::kFlag] = 0;
+  build_compact_image<kFW>(lds, zpow, lane_cols, tid, wave, lane);  // ends with a barrier
+  // Wait for every head. No acquire fence afterwards (one per workgroup
+  // would invalidate the XCD's L2 hundreds of times): everything the heads
+  // wrote is read with agent-scope atomic loads (desc_u64/_u32, the
+  // kModeSstTable store), which see the released values.
+  if (wave == 0) {
+    for (uint32_t j = lane; j < ntables; j += 64)
+      while (__hip_atomic_load(&reports[j].done_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen)
+        __builtin_amdgcn_s_sleep(8);
+  }
+  __syncthreads();
+  const uint32_t total = min(
+      capacity, __builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                    &reports[0].total_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+  ragged_run<kFW, 2, 24>(a, zpow, lane_cols, lds, blockIdx.x - ntables, gridDim.x - ntables, total,
+                         true);
+}
+
 }  // namespace
 
 hipError_t launch_crc32c_general(const KernelArgs& a, int cus, hipStream_t stream);
 
-// The two launches for `ntables` images (toff/tsize device arrays, or
+// Whole-table verify of `ntables` images (toff/tsize device arrays, or
 // nullptr and `single_size` for one image at d_file); `verify` carries the
-// KernelArgs template (tables) the caller filled.
+// KernelArgs template (tables) the caller filled. `fused`: one launch
+// (sst_fused_kernel, for tables whose index the 8-wave head handles well);
+// else the two-launch form (16-wave heads, then the ragged kernel).
 hipError_t launch_sst_tables(const uint8_t* file, const uint64_t* toff, const uint64_t* tsize,
                              uint64_t single_size, uint32_t ntables, uint64_t* d_off,
                              uint32_t* d_size, uint32_t* d_actual, uint8_t* d_status,
                              uint32_t capacity, lvkv_sst_report* reports, const FilterKey& fk,
                              uint32_t gen, const KernelArgs& verify, const uint32_t* zpow,
-                             const uint32_t* lane_cols, int groups, hipStream_t stream) {
-  hipLaunchKernelGGL(sst_table_kernel, dim3(ntables), dim3(kThreads), 0, stream, file, toff,
-                     tsize, single_size, ntables, capacity, gen, fk, reports, d_off, d_size,
-                     d_status, zpow, lane_cols);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  // 2. every data and filter block of every table: CRC, then the merge into
-  //    LVKV_BLOCK_* and the per-table totals in the kernel's store
+                             const uint32_t* lane_cols, int groups, bool fused,
+                             hipStream_t stream) {
+  // every data and filter block of every table: CRC, then the merge into
+  // LVKV_BLOCK_* and the per-table totals in the kernel's store
   KernelArgs a = verify;
   a.base = file;
   a.offsets = d_off;
@@ -565,6 +694,19 @@ hipError_t launch_sst_tables(const uint8_t* file, const uint64_t* toff, const ui
   a.long_split = kLongBytes;  // large data/filter blocks: one workgroup each
   a.sst_reports = reports;
   a.sst_ntables = ntables;
+  if (fused) {
+    a.fresh_desc = 1;
+    // two workgroups per CU resident; the heads come first
+    const uint32_t grid = max(2u * static_cast<uint32_t>(groups), ntables + static_cast<uint32_t>(groups));
+    hipLaunchKernelGGL(sst_fused_kernel, dim3(grid), dim3(64 * kFW), 0, stream, a, file, toff,
+                       tsize, single_size, ntables, capacity, gen, fk, reports, zpow, lane_cols);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(sst_table_kernel, dim3(ntables), dim3(64 * kW), 0, stream, file, toff,
+                     tsize, single_size, ntables, capacity, gen, fk, reports, d_off, d_size,
+                     d_status, zpow, lane_cols);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
   return launch_crc32c_general(a, groups, stream);
 }
 

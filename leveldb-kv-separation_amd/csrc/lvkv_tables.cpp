@@ -85,6 +85,18 @@ void build_zpow_tables(uint32_t* zpow) {
   }
 }
 
+void build_zmul_columns(uint32_t* zmul) {
+  for (uint32_t j = kZMulLog0; j < kZMulLog0 + kZMulLogs; ++j) {
+    const Gf2Op z = gf2_zero_advance(uint64_t{1} << j);
+    Gf2Op m = z;
+    for (uint32_t c = 1; c <= kZMulMaxC; ++c) {
+      for (uint32_t b = 0; b < 32; ++b)
+        zmul[((j - kZMulLog0) * kZMulMaxC + c - 1) * 32 + b] = m.col[b];
+      m = gf2_compose(z, m);
+    }
+  }
+}
+
 }  // namespace lvkv
 
 extern "C" __attribute__((visibility("default"))) void lvkv_debug_tables(

@@ -33,6 +33,10 @@ void build_lane_columns(uint32_t* lane_cols);
 //   zpow[j*1024 + t*256 + b]        = Z_{2^j}(b << 8t), j < kZPowCount:
 //   Z_n(v) for any n = the product over the set bits j of n
 void build_zpow_tables(uint32_t* zpow);
+//   zmul[((j - kZMulLog0) * kZMulMaxC + c - 1) * 32 + b] = Z_{c * 2^j}(1 << b),
+//   c in [1, kZMulMaxC]: the 32 columns of a constant shift, applied with
+//   register xors instead of dependent table lookups (group_crc)
+void build_zmul_columns(uint32_t* zmul);
 
 
 }  // namespace lvkv

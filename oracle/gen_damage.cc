@@ -571,6 +571,37 @@ void write_wal_cases(const std::string& dir) {
     leveldb::EncodeFixed32(c, leveldb::crc32c::Mask(leveldb::crc32c::Value(img.data() + h + 6, 1 + len)));
     add("unknown_type_crc_fixed", {{h + 6, std::string(1, '\x09')}, {h, std::string(c, 4)}});
   }
+  // Every type byte 0..6 under a fixed CRC at a FULL record and at a FIRST,
+  // MIDDLE and LAST fragment: the physical layer returns them all; the
+  // logical layer (ReadRecord) sees kZeroType as unknown, 5 as kEof (stop)
+  // and 6 as kBadRecord, and the fragment types start, continue or end the
+  // record or report a missing start / partial record.
+  {
+    auto retype = [&](uint64_t h, int t) {
+      std::string img = base;
+      img[h + 6] = static_cast<char>(t);
+      const uint32_t len = static_cast<uint8_t>(img[h + 4]) |
+                           (static_cast<uint32_t>(static_cast<uint8_t>(img[h + 5])) << 8);
+      char c[4];
+      leveldb::EncodeFixed32(c,
+                             leveldb::crc32c::Mask(leveldb::crc32c::Value(img.data() + h + 6, 1 + len)));
+      return std::vector<Patch>{{h + 6, std::string(1, static_cast<char>(t))}, {h, std::string(c, 4)}};
+    };
+    const char* kind[] = {"zero", "full", "first", "middle", "last", "eof", "bad"};
+    std::vector<std::pair<const char*, uint64_t>> at;
+    for (int want : {1, 2, 3, 4}) {
+      for (uint64_t h : hdrs) {
+        if (static_cast<uint8_t>(base[h + 6]) == want) {
+          at.push_back({kind[want], h});
+          break;
+        }
+      }
+    }
+    for (const auto& [orig, h] : at)
+      for (int t = 0; t <= 6; ++t)
+        if (t != static_cast<uint8_t>(base[h + 6]))
+          add(std::string("retype_") + orig + "_to_" + kind[t], retype(h, t));
+  }
   add("truncated_mid_record", {}, hdrs[hdrs.size() - 2] + 20);
   add("truncated_mid_header", {}, hdrs.back() + 3);
   add("truncated_block_edge", {}, 32768 + 5);

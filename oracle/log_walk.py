@@ -131,6 +131,7 @@ def block_verdicts(img: bytes) -> BlockVerdicts:
 #                                          (the zero-type zero-length skip)
 #   ("eof",)                               kEof
 K_FULL, K_FIRST, K_MIDDLE, K_LAST = 1, 2, 3, 4
+K_EOF, K_BAD_RECORD = 5, 6  # log_reader.h: kMaxRecordType + 1, + 2
 
 
 def physical_events(img: bytes):
@@ -196,6 +197,16 @@ def assemble(img: bytes, events):
                 continue
             _, h, length, rtype = e
             frag = img[h + K_HEADER: h + K_HEADER + length]
+            # a header's own type byte 5 / 6 IS kEof / kBadRecord to ReadRecord
+            # (ReadPhysicalRecord returns the byte as is, log_reader.cc:258-262;
+            # switch at :143-161)
+            if rtype == K_EOF:
+                return records, reports
+            if rtype == K_BAD_RECORD:
+                if in_frag:
+                    reports.append((len(scratch), "error in middle of record"))
+                    in_frag, scratch = False, b""
+                continue
             if rtype == K_FULL:
                 if in_frag and scratch:
                     reports.append((len(scratch), "partial record without end(1)"))

@@ -61,3 +61,12 @@ def gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+@pytest.fixture(params=[1, 2], ids=["fused", "two_launch"])
+def sst_form(request, lvkv, gpu):
+    """Whole-SSTable verify form under test: 1 = one fused launch, 2 = the
+    two-launch form (lvkv_debug_set_sst_form); back to by-size afterwards."""
+    assert lvkv.lib.lvkv_debug_set_sst_form(request.param) == 0
+    yield request.param
+    lvkv.lib.lvkv_debug_set_sst_form(0)

@@ -70,7 +70,7 @@ def test_oracle_wal_matches_reference(case):
 # ---------------------------------------------------------------- GPU -----
 
 @pytest.mark.gpu
-def test_device_sst_matches_reference(lvkv, gpu):
+def test_device_sst_matches_reference(lvkv, gpu, sst_form):
     import torch
     for case in SST_CASES:
         img = df.image(case)
@@ -103,3 +103,66 @@ def test_device_wal_matches_reference(lvkv, gpu):
                                    list(rst.cpu().numpy()), list(bst.cpu().numpy()),
                                    list(bdrop.cpu().numpy()))
         assert lw.assemble(img, ev) == df.wal_expected(case), case["name"]
+
+
+def _device_log_records(img, records, hdrs):
+    """(LastRecordOffset, length, CRC32C of the contents) of each device
+    record: its fragments' payloads concatenated (checker: the oracle)."""
+    import oracle
+    out = []
+    for off, length, first, nfrags in records:
+        body = b"".join(img[h + lw.K_HEADER: h + lw.K_HEADER + (img[h + 4] | img[h + 5] << 8)]
+                        for h in hdrs[first: first + nfrags])
+        assert hdrs[first] == off and len(body) == length
+        out.append((off, length, oracle.value(body)))
+    return out
+
+
+@pytest.mark.gpu
+def test_device_log_read_matches_reference(lvkv, gpu):
+    # The logical layer on the device (lvkv_log_read_device): records and
+    # every Reporter call, against the reference's own log::Reader run on
+    # the same damaged images (oracle/gen_damage.cc).
+    import torch
+    for case in WAL_CASES:
+        img = df.image(case, "wal.log")
+        buf = torch.from_numpy(np.frombuffer(img, dtype=np.uint8).copy()).to(gpu)
+        rd, records, reports, phys = lvkv.log_read(buf)
+        torch.cuda.synchronize()
+        assert rd["status"] == 0, case["name"]
+        hdrs = [int(x) for x in phys[1].cpu().numpy()]
+        want_recs, want_reps = df.wal_expected(case)
+        assert _device_log_records(img, records, hdrs) == want_recs, case["name"]
+        assert reports == want_reps, case["name"]
+        assert rd["bytes"] == sum(r[1] for r in want_recs), case["name"]
+        assert rd["stopped"] == int(case["name"].endswith("_to_eof")), case["name"]
+
+
+@pytest.mark.gpu
+def test_device_log_read_large_and_capacity(lvkv, gpu):
+    # A synthetic 20k-record log with fragmented records across blocks and
+    # random damage: device ReadRecord = the oracle's; too-small capacities
+    # are reported with exact counts.
+    import torch
+    import log_synth
+    rng = np.random.default_rng(7)
+    base = log_synth.build_log(20000, seed=11, max_len=2000, big_every=97)
+    for trial in range(6):
+        img = bytearray(base)
+        for _ in range(trial * 3):
+            img[int(rng.integers(0, len(img)))] ^= int(rng.integers(1, 256))
+        if trial % 2:  # retyped headers under fixed CRCs (types 0..7)
+            hdrs0 = lw.block_verdicts(base).hdrs
+            for h in rng.choice(hdrs0, 12, replace=False):
+                img[int(h) + 6] = int(rng.integers(0, 8))
+                log_synth.fix_header_crc(img, int(h))
+        img = bytes(img)
+        buf = torch.from_numpy(np.frombuffer(img, dtype=np.uint8).copy()).to(gpu)
+        rd, records, reports, phys = lvkv.log_read(buf)
+        hdrs = [int(x) for x in phys[1].cpu().numpy()]
+        want_recs, want_reps = lw.read_records(img)
+        assert _device_log_records(img, records, hdrs) == want_recs, trial
+        assert reports == want_reps, trial
+    rd, records, reports, _ = lvkv.log_read(buf, record_capacity=5, report_capacity=1)
+    assert rd["status"] == 1 and rd["nrecords"] == len(want_recs)
+    assert rd["nreports"] == len(want_reps) and len(records) == 5

@@ -96,7 +96,7 @@ def test_report_struct_layout_matches_header(tmp_path, lvkv):
           printf("size %zu\\n", sizeof(lvkv_sst_report));
           F(status) F(nblocks) F(ndata) F(has_filter) F(nbad) F(first_bad) F(index_crc)
           F(meta_crc) F(index_status) F(meta_status) F(first) F(index_offset) F(index_size)
-          F(meta_offset) F(meta_size) F(link_) F(total_)
+          F(meta_offset) F(meta_size) F(link_) F(total_) F(done_)
           return 0;
         }"""))
     exe = tmp_path / "layout"
@@ -152,13 +152,13 @@ def _assert_matches_oracle(lvkv, img: bytes, gpu, capacity=None, got=None, base=
 
 
 @pytest.mark.gpu
-def test_device_table_verify_golden(lvkv, gpu):
+def test_device_table_verify_golden(lvkv, gpu, sst_form):
     rep, want = _assert_matches_oracle(lvkv, _golden_img(), gpu)
     assert rep["status"] == 0 and rep["nbad"] == 0 and rep["ndata"] == 49
 
 
 @pytest.mark.gpu
-def test_device_table_verify_footer_and_index_errors(lvkv, gpu):
+def test_device_table_verify_footer_and_index_errors(lvkv, gpu, sst_form):
     img = _golden_img()
     r0 = st.verify_table(img)
     cases = [img[:40]]
@@ -176,7 +176,7 @@ def test_device_table_verify_footer_and_index_errors(lvkv, gpu):
 
 
 @pytest.mark.gpu
-def test_device_table_verify_detects_every_block_kind(lvkv, gpu):
+def test_device_table_verify_detects_every_block_kind(lvkv, gpu, sst_form):
     img = _golden_img()
     r0 = st.verify_table(img)
     nd = r0.ndata
@@ -190,7 +190,7 @@ def test_device_table_verify_detects_every_block_kind(lvkv, gpu):
 
 
 @pytest.mark.gpu
-def test_device_table_verify_bad_type_and_handles(lvkv, gpu):
+def test_device_table_verify_bad_type_and_handles(lvkv, gpu, sst_form):
     # block 5: type byte 9 under a valid CRC -> "bad block type"; index entry 7
     # points past the file -> "truncated block read"; entry 9's value is not
     # a varint pair -> "bad block handle"; entry 11 has a trailing byte after
@@ -210,7 +210,7 @@ def test_device_table_verify_bad_type_and_handles(lvkv, gpu):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,bs,filt", [(1, 100, False), (257, 1000, True), (5000, 4096, True)])
-def test_device_table_verify_synthetic(lvkv, gpu, n, bs, filt):
+def test_device_table_verify_synthetic(lvkv, gpu, sst_form, n, bs, filt):
     img = sst_synth.build_sst(n, bs, seed=n, with_filter=filt)
     rep, _ = _assert_matches_oracle(lvkv, img, gpu)
     assert rep["ndata"] == n and rep["nbad"] == 0
@@ -250,7 +250,7 @@ def test_device_fill_trailers_rebuilds_the_table(lvkv, gpu, source):
 
 
 @pytest.mark.gpu
-def test_device_table_with_long_blocks(lvkv, gpu):
+def test_device_table_with_long_blocks(lvkv, gpu, sst_form):
     # Data blocks far beyond kLongBytes (one huge value per block, as a table
     # with big values gets): verify, a corrupted long block, and the refill.
     import torch
@@ -275,7 +275,7 @@ def test_device_table_with_long_blocks(lvkv, gpu):
 
 
 @pytest.mark.gpu
-def test_device_multi_table_verify(lvkv, gpu):
+def test_device_multi_table_verify(lvkv, gpu, sst_form):
     # Compaction-input shape: many tables in one buffer, each checked exactly
     # as the single-table call would (lvkv_sst_verify_tables_device).
     import torch

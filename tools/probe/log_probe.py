@@ -92,6 +92,28 @@ def main():
                   f"(max merged {rel[:, 6].max():.2f})", flush=True)
     print(f"log_verify {nrec} records, {len(img)} bytes, {nb} blocks: {us:.1f} us/call, "
           f"{len(img) / us / 1e3:.1f} GB/s", flush=True)
+    if "--read" in sys.argv:
+        # verify + the logical layer (lvkv_log_read_device)
+        recs = torch.zeros(cap * 24, dtype=torch.uint8, device=dev)
+        reps = torch.zeros((cap + nb) * 16, dtype=torch.uint8, device=dev)
+        rd = torch.zeros(64, dtype=torch.uint8, device=dev)
+
+        def read():
+            rc = L.lvkv_log_read_device(vp(buf.data_ptr()), len(img), vp(hdr.data_ptr()),
+                                        vp(act.data_ptr()), vp(rst.data_ptr()), cap,
+                                        vp(bst.data_ptr()), vp(bdr.data_ptr()), vp(rp.data_ptr()),
+                                        vp(recs.data_ptr()), cap, vp(reps.data_ptr()), cap + nb,
+                                        vp(rd.data_ptr()), h)
+            assert rc == 0
+        for _ in range(5):
+            read()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(50):
+            read()
+        torch.cuda.synchronize()
+        us2 = (time.perf_counter() - t0) / 50 * 1e6
+        print(f"log_read {nrec} records: {us2:.1f} us/call (verify + ReadRecord)", flush=True)
 
 
 if __name__ == "__main__":

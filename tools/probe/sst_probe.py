@@ -1,6 +1,6 @@
 """Whole-SSTable verify timing (GPU box). Not part of the product.
 
-    python tools/probe/sst_probe.py [nblocks]
+    python tools/probe/sst_probe.py [nblocks] [--form=0|1|2] [--tables=K]
 
 A synthetic table (tests/sst_synth.py) through lvkv_sst_verify_table_device,
 back to back on one stream; with rocprofv3 around it, the two launches' own
@@ -25,8 +25,56 @@ import sst_synth  # noqa: E402
 lvkv = g.load_package()
 
 
+def opt(name, default):
+    return int(next((x.split("=")[1] for x in sys.argv if x.startswith(f"--{name}=")), default))
+
+
+def multi(nblocks, k):
+    # k copies of one table in one buffer, back-to-back lvkv_sst_verify_tables_device calls
+    img = sst_synth.build_sst(nblocks, 4096, seed=nblocks, ragged=True)
+    dev = torch.device("cuda:0")
+    offs = [i * (len(img) + 13) for i in range(k)]
+    raw = bytearray(offs[-1] + len(img))
+    for o in offs:
+        raw[o: o + len(img)] = img
+    buf = torch.from_numpy(np.frombuffer(bytes(raw), dtype=np.uint8).copy()).to(dev)
+    res = lvkv.sst_verify_tables(buf, offs, [len(img)] * k)
+    assert all(r[0]["status"] == 0 and r[0]["nbad"] == 0 for r in res)
+    cap = k * (res[0][0]["nblocks"] + 1)
+    toff = torch.tensor(offs, dtype=torch.int64, device=dev)
+    tsz = torch.tensor([len(img)] * k, dtype=torch.int64, device=dev)
+    o = torch.empty(cap, dtype=torch.int64, device=dev)
+    sz = torch.empty(cap, dtype=torch.int32, device=dev)
+    ac = torch.empty(cap, dtype=torch.int32, device=dev)
+    st = torch.empty(cap, dtype=torch.uint8, device=dev)
+    rp = torch.zeros(k * ctypes.sizeof(lvkv.SstReport), dtype=torch.uint8, device=dev)
+    vp = ctypes.c_void_p
+    h = vp(torch.cuda.current_stream().cuda_stream)
+    pol = lvkv.BLOOM_POLICY.encode()
+
+    def call():
+        rc = lvkv.lib.lvkv_sst_verify_tables_device(
+            vp(buf.data_ptr()), vp(toff.data_ptr()), vp(tsz.data_ptr()), k, vp(o.data_ptr()),
+            vp(sz.data_ptr()), vp(ac.data_ptr()), vp(st.data_ptr()), cap, pol, vp(rp.data_ptr()), h)
+        assert rc == 0
+    for _ in range(5):
+        call()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(50):
+        call()
+    torch.cuda.synchronize()
+    us = (time.perf_counter() - t0) / 50 * 1e6
+    print(f"sst_verify_tables form {opt('form', 0)}, {k} x {nblocks} blocks, {len(raw)} bytes: "
+          f"{us:.1f} us/call", flush=True)
+
+
 def main():
-    nblocks = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
+    nblocks = int(sys.argv[1]) if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else 16384
+    form = opt("form", 0)
+    assert lvkv.lib.lvkv_debug_set_sst_form(form) == 0
+    if opt("tables", 0):
+        return multi(nblocks, opt("tables", 0))
     img = sst_synth.build_sst(nblocks, 4096, seed=nblocks, ragged=True)
     dev = torch.device("cuda:0")
     buf = torch.from_numpy(np.frombuffer(img, dtype=np.uint8).copy()).to(dev)
@@ -55,7 +103,8 @@ def main():
         call()
     torch.cuda.synchronize()
     us = (time.perf_counter() - t0) / 50 * 1e6
-    print(f"sst_verify {nblocks} blocks, {len(img)} bytes: {us:.1f} us/call", flush=True)
+    print(f"sst_verify form {form}, {nblocks} blocks, {len(img)} bytes: {us:.1f} us/call",
+          flush=True)
 
 
 if __name__ == "__main__":
