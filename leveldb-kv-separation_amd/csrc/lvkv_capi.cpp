@@ -57,10 +57,11 @@ hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_o
                              void* scratch, uint32_t* events, hipStream_t stream);
 size_t log_scratch_bytes(uint64_t size);
 hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
-                               const lvkv_log_report* phys, uint64_t size,
+                               const lvkv_log_report* phys, uint64_t size, uint32_t capacity,
                                lvkv_log_record* recs, uint32_t rec_cap,
                                lvkv_log_corruption* reps, uint32_t rep_cap,
-                               lvkv_log_read_report* out, hipStream_t stream);
+                               lvkv_log_read_report* out, void* scratch, hipStream_t stream);
+size_t log_asm_scratch_bytes(size_t max_items);
 hipError_t launch_crc32c_long(const KernelArgs& args, const uint32_t* zpow,
                               const uint32_t* lane_cols, int num_groups, hipStream_t stream);
 int compact_capacity(int cfg);
@@ -609,13 +610,16 @@ int lvkv_log_read_device(const void* d_file, uint64_t file_size, uint64_t* d_hdr
   DeviceCtx* c = current_ctx(&rc);
   if (c == nullptr) return rc;
   const hipStream_t hs = static_cast<hipStream_t>(stream);
-  // scratch: the verify's counters, then the event stream (one u32 per
-  // candidate record and per block)
+  // scratch: the verify's counters, the event stream (one u32 per candidate
+  // record and per block), then the logical layer's per-chunk state
   const size_t nblocks = static_cast<size_t>((file_size + 32767) / 32768);
   const size_t ev_at = (log_scratch_bytes(file_size) + 15) & ~size_t{15};
+  const size_t asm_at = (ev_at + (capacity + nblocks) * 4 + 15) & ~size_t{15};
   void* scratch = nullptr;
-  hipError_t e = log_scratch_for(*c, hs, ev_at + (capacity + nblocks) * 4, &scratch);
-  uint32_t* events = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(scratch) + ev_at);
+  hipError_t e = log_scratch_for(*c, hs, asm_at + log_asm_scratch_bytes(capacity + nblocks),
+                                 &scratch);
+  uint8_t* sb = static_cast<uint8_t*>(scratch);
+  uint32_t* events = reinterpret_cast<uint32_t*>(sb + ev_at);
   if (e == hipSuccess)
     e = launch_log_blocks(static_cast<const uint8_t*>(d_file), file_size, d_hdr_offsets,
                           d_actual, d_rec_status, static_cast<uint32_t>(capacity),
@@ -623,9 +627,10 @@ int lvkv_log_read_device(const void* d_file, uint64_t file_size, uint64_t* d_hdr
                           c->d_tables + kRowTabDwords + kLaneTabDwords, c->groups, scratch,
                           events, hs);
   if (e == hipSuccess)
-    e = launch_log_assemble(events, d_hdr_offsets, d_report, file_size, d_records,
+    e = launch_log_assemble(events, d_hdr_offsets, d_report, file_size,
+                            static_cast<uint32_t>(capacity), d_records,
                             static_cast<uint32_t>(record_capacity), d_reports,
-                            static_cast<uint32_t>(report_capacity), d_read, hs);
+                            static_cast<uint32_t>(report_capacity), d_read, sb + asm_at, hs);
   return e == hipSuccess ? LVKV_OK : hip_fail(e);
 }
 

@@ -12,14 +12,19 @@
 // through (adding their bytes to an open fragment); otherwise its first
 // other event resets the state the same way whatever came before, so the run
 // ends in a state of its own. That makes runs composable (Summ, compose),
-// and one workgroup does it in three passes over contiguous chunks:
+// and the work is reduce-then-scan over chunks of kChunk items, one chunk
+// per thread, in three launches:
 //
-//   1. each thread summarises its chunk (Summ); a scan of the summaries gives
-//      every chunk the reader's state at its start;
-//   2. each thread replays its chunk from that state, counting records,
-//      reports and bytes; a scan gives output positions;
-//   3. each thread replays it again and writes records and reports; then the
-//      records' LastRecordOffset values are filled in parallel.
+//   1. log_asm_reduce (grid): every chunk's summary and its record / report
+//      counts for each state it may start in (idle; in a fragment with
+//      bytes; in an empty fragment); a workgroup scan of the summaries gives
+//      each chunk's start relative to its workgroup's, and the workgroup's
+//      aggregate (its summary and its counts for each starting state);
+//   2. log_asm_scan (one workgroup): the aggregates scanned: each
+//      workgroup's starting state, first candidate and output positions;
+//   3. log_asm_emit (grid): the same chunk work again, now from the known
+//      starting state, writing records (LastRecordOffset from the verify's
+//      header offsets, loaded beside the events) and reports.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -30,7 +35,6 @@
 namespace lvkv {
 namespace {
 
-constexpr uint32_t kAT = 1024;  // threads of the one workgroup
 
 enum : uint32_t { kIdle = 0, kInFrag = 1, kStopped = 2, kUnknown = 3 };
 
@@ -42,6 +46,7 @@ struct Summ {
   uint64_t scratch;  // !pass, c == kInFrag: bytes of the open fragment
   uint32_t first;    // !pass, c == kInFrag: its FIRST, candidates from the run's start
   uint32_t nrec;     // candidate records in the run (additive)
+  uint32_t stop5;    // c == kStopped because of a header of type 5
 };
 
 __device__ __forceinline__ Summ compose(const Summ& x, const Summ& y) {
@@ -64,10 +69,11 @@ __device__ __forceinline__ Summ compose(const Summ& x, const Summ& y) {
 
 // The reader's state while a chunk is replayed.
 struct Reader {
-  uint32_t st;       // kIdle / kInFrag / kStopped, or kUnknown (pass 1)
+  uint32_t st;       // kIdle / kInFrag / kStopped, or kUnknown (summaries)
   uint32_t first;    // kInFrag: the fragment's FIRST
   uint64_t scratch;  // kInFrag (kUnknown: MIDDLE bytes so far)
   uint32_t stopped;  // a kEof-type header stopped the reader here
+  uint64_t first_off;  // kInFrag, emit pass: the FIRST's header offset
 };
 
 // Output sinks: pass 2 counts, pass 3 writes.
@@ -90,10 +96,11 @@ struct Sink {
     }
     ++nrep;
   }
-  __device__ __forceinline__ void record(uint32_t first, uint32_t nfrags, uint64_t len) {
+  __device__ __forceinline__ void record(uint64_t off, uint32_t first, uint32_t nfrags,
+                                         uint64_t len) {
     if (write && nrec < rec_cap) {
       lvkv_log_record r;
-      r.offset = 0;  // LastRecordOffset: filled in after the pass
+      r.offset = off;
       r.length = len;
       r.first = first;
       r.nfrags = nfrags;
@@ -104,11 +111,12 @@ struct Sink {
   }
 };
 
-// One event (item `ev`, candidate index j for a record) through ReadRecord's
-// switch (log_reader.cc:86-166). kUnknown (pass 1) emits nothing: a MIDDLE
-// keeps it, any other event resolves it.
+// One event (item `ev`; for a record its candidate index j and header offset
+// hoff) through ReadRecord's switch (log_reader.cc:86-166). kUnknown (the
+// summaries) emits nothing: a MIDDLE keeps it, any other event resolves it.
 template <bool kOut>
-__device__ __forceinline__ void step(Reader& r, uint32_t ev, uint32_t j, Sink& out) {
+__device__ __forceinline__ void step(Reader& r, uint32_t ev, uint32_t j, uint64_t hoff,
+                                     Sink& out) {
   const uint32_t kind = ev & 15u;
   const uint64_t n = ev >> 16;  // payload bytes / drop bytes
   if (r.st == kStopped || kind == kEvSkip || kind == kEvNone) return;
@@ -129,13 +137,14 @@ __device__ __forceinline__ void step(Reader& r, uint32_t ev, uint32_t j, Sink& o
   switch (type) {
     case 1:  // kFullType (:86-98)
       if (kOut && in && r.scratch != 0) out.report(r.scratch, LVKV_LOGR_PARTIAL_1, 0);
-      if (kOut) out.record(j, 1, n);
+      if (kOut) out.record(hoff, j, 1, n);
       r.st = kIdle;
       break;
     case 2:  // kFirstType (:100-112)
       if (kOut && in && r.scratch != 0) out.report(r.scratch, LVKV_LOGR_PARTIAL_2, 0);
       r.st = kInFrag;
       r.first = j;
+      r.first_off = hoff;
       r.scratch = n;
       break;
     case 3:  // kMiddleType (:114-121)
@@ -147,7 +156,7 @@ __device__ __forceinline__ void step(Reader& r, uint32_t ev, uint32_t j, Sink& o
       break;
     case 4:  // kLastType (:123-134)
       if (in) {
-        if (kOut) out.record(r.first, j - r.first + 1u, r.scratch + n);
+        if (kOut) out.record(r.first_off, r.first, j - r.first + 1u, r.scratch + n);
       } else if (kOut && r.st == kIdle) {
         out.report(n, LVKV_LOGR_MISSING_2, 0);
       }
@@ -168,154 +177,342 @@ __device__ __forceinline__ void step(Reader& r, uint32_t ev, uint32_t j, Sink& o
   }
 }
 
-// Replays items [k0, k1) (candidate records from j0 on) from `r`, eight
-// event loads in flight at a time.
-template <bool kOut>
-__device__ __forceinline__ uint32_t replay(const uint32_t* events, uint32_t k0, uint32_t k1,
-                                           uint32_t j0, Reader& r, Sink& out) {
-  uint32_t j = j0;
-  for (uint32_t k = k0; k < k1; k += 8) {
-    uint32_t ev[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      ev[i] = k + i < k1 ? events[k + i] : log_event(kEvNone, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      step<kOut>(r, ev[i], j, out);
-      const uint32_t kind = ev[i] & 15u;
-      j += (kind == kEvRec || kind == kEvSkip) ? 1u : 0u;
-    }
-  }
-  return j;
+constexpr uint32_t kChunk = 4;   // items per thread (one 16-byte load)
+constexpr uint32_t kGT = 256;     // threads per workgroup of the grid launches
+
+__device__ __forceinline__ bool is_candidate(uint32_t ev) {
+  const uint32_t kind = ev & 15u;
+  return kind == kEvRec || kind == kEvSkip;
 }
 
-struct AsmArgs {
-  const uint32_t* events;
-  const uint64_t* hdr_off;
-  const lvkv_log_report* phys;
-  uint64_t size;
-  uint32_t nblocks;
-  uint32_t rec_cap, rep_cap;
-  lvkv_log_record* recs;
-  lvkv_log_corruption* reps;
-  lvkv_log_read_report* out;
+// The chunk's items [k0, k1) into registers (the rest "no event"). k0 is a
+// multiple of kChunk and the event array 16-byte aligned.
+__device__ __forceinline__ void load_chunk(const uint32_t* events, uint32_t k0, uint32_t k1,
+                                           uint32_t (&ev)[kChunk]) {
+  const uint4 v = k0 < k1 ? reinterpret_cast<const uint4*>(events + k0)[0] : make_uint4(0, 0, 0, 0);
+  ev[0] = v.x;
+  ev[1] = v.y;
+  ev[2] = v.z;
+  ev[3] = v.w;
+#pragma unroll
+  for (uint32_t i = 0; i < kChunk; ++i)
+    if (k0 + i >= k1) ev[i] = log_event(kEvNone, 0, 0);
+}
+
+// The chunk through step(); hoff[c] = header offset of its c-th candidate.
+template <bool kOut>
+__device__ __forceinline__ void replay(const uint32_t (&ev)[kChunk], const uint64_t (&hoff)[kChunk],
+                                       uint32_t j0, Reader& r, Sink& out) {
+  uint32_t c = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kChunk; ++i) {
+    step<kOut>(r, ev[i], j0 + c, hoff[c], out);
+    c += is_candidate(ev[i]) ? 1u : 0u;
+  }
+}
+
+constexpr Summ kIdentity = {1, kIdle, 0, 0, 0, 0, 0};  // no events
+
+// A starting state as the counts see it: idle, in a fragment with bytes,
+// in an empty fragment, stopped.
+enum : uint32_t { kScIdle = 0, kScFrag = 1, kScEmpty = 2, kScStopped = 3 };
+
+__device__ __forceinline__ uint32_t scenario(uint32_t st, uint64_t scratch) {
+  return st == kIdle ? kScIdle : st == kStopped ? kScStopped : scratch != 0 ? kScFrag : kScEmpty;
+}
+
+// A chunk's start given its workgroup's start (scenario sw) and the
+// composed summary `x` of the chunks before it in the workgroup.
+__device__ __forceinline__ uint32_t chunk_scenario(uint32_t sw, const Summ& x) {
+  if (!x.pass) return scenario(x.c, x.scratch);
+  if (sw == kScEmpty && x.len != 0) return kScFrag;
+  return sw;
+}
+
+// One thread's chunk: events, summary and counts from each starting state.
+struct Chunk {
+  uint32_t ev[kChunk];
+  Summ s;
+  uint32_t nrec[3], nrep[3];
 };
 
-__global__ void __launch_bounds__(kAT, 1) log_assemble_kernel(AsmArgs a) {
-  __shared__ Summ sm[2][kAT];
-  __shared__ uint32_t cnt[2][kAT][2];
-  __shared__ unsigned long long byt[2][kAT];
-  __shared__ uint32_t stop_any;
-  const uint32_t tid = threadIdx.x;
-  const bool ok = a.phys->status == LVKV_OK;
-  // candidate records the verify placed (0 when they did not fit)
-  const uint32_t nrec = ok ? a.phys->count_ : 0u;
-  const uint32_t K = ok ? nrec + a.nblocks : 0u;
-  const uint32_t k0 = static_cast<uint32_t>(static_cast<uint64_t>(tid) * K / kAT);
-  const uint32_t k1 = static_cast<uint32_t>(static_cast<uint64_t>(tid + 1) * K / kAT);
-  if (tid == 0) stop_any = 0;
-
-  // 1. the chunk's summary, then an inclusive scan of the summaries
+__device__ __forceinline__ void chunk_of(const uint32_t* events, uint32_t K, uint32_t t, Chunk& c) {
+  const uint32_t k0 = t * kChunk;
+  load_chunk(events, k0, min(K, k0 + kChunk), c.ev);
+  uint64_t hz[kChunk];
+#pragma unroll
+  for (uint32_t i = 0; i < kChunk; ++i) hz[i] = 0;
   Sink none = {false, 0, 0, 0, nullptr, 0, nullptr, 0};
-  Reader u = {kUnknown, 0, 0, 0};
-  const uint32_t jend = replay<false>(a.events, k0, k1, 0, u, none);
-  Summ s;
-  s.pass = u.st == kUnknown ? 1u : 0u;
-  s.c = u.st;
-  s.len = s.pass ? u.scratch : 0;
-  s.scratch = u.scratch;
-  s.first = u.first;
-  s.nrec = jend;
+  Reader u = {kUnknown, 0, 0, 0, 0};
+  replay<false>(c.ev, hz, 0, u, none);
+  c.s.pass = u.st == kUnknown ? 1u : 0u;
+  c.s.c = c.s.pass ? kIdle : u.st;
+  c.s.len = c.s.pass ? u.scratch : 0;
+  c.s.scratch = c.s.pass ? 0 : u.scratch;
+  c.s.first = u.first;
+  c.s.stop5 = u.stopped;
+  uint32_t n = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kChunk; ++i) n += is_candidate(c.ev[i]) ? 1u : 0u;
+  c.s.nrec = n;
+#pragma unroll
+  for (uint32_t sc = 0; sc < 3; ++sc) {
+    Sink cnt = {false, 0, 0, 0, nullptr, 0, nullptr, 0};
+    Reader r = {sc == kScIdle ? kIdle : kInFrag, 0, sc == kScFrag ? 1u : 0u, 0, 0};
+    replay<true>(c.ev, hz, 0, r, cnt);
+    c.nrec[sc] = cnt.nrec;
+    c.nrep[sc] = cnt.nrep;
+  }
+}
+
+// Workgroup-wide exclusive scan of `s` under compose; *all = the aggregate.
+__device__ __forceinline__ Summ wg_scan_excl(Summ s, Summ (&sm)[2][kGT], uint32_t tid, Summ* all) {
   uint32_t cur = 0;
   sm[cur][tid] = s;
   __syncthreads();
-  for (uint32_t d = 1; d < kAT; d <<= 1) {
+  for (uint32_t d = 1; d < kGT; d <<= 1) {
     if (tid >= d) s = compose(sm[cur][tid - d], s);
     sm[cur ^ 1u][tid] = s;
     cur ^= 1u;
     __syncthreads();
   }
-  // the reader's state at the chunk's start: the log starts idle
-  Reader r = {kIdle, 0, 0, 0};
-  uint32_t j0 = 0;
-  if (tid > 0) {
-    const Summ p = sm[cur][tid - 1];
-    j0 = p.nrec;
-    if (!p.pass) {
-      r.st = p.c;
-      r.first = p.first;
-      r.scratch = p.scratch;
-    }
-  }
+  *all = sm[cur][kGT - 1];
+  const Summ e = tid ? sm[cur][tid - 1] : kIdentity;
+  __syncthreads();  // sm is reused
+  return e;
+}
 
-  // 2. counts from that state, exclusive scans of them
-  Sink cnt_sink = {false, 0, 0, 0, nullptr, 0, nullptr, 0};
-  {
-    Reader rr = r;
-    replay<true>(a.events, k0, k1, j0, rr, cnt_sink);
-    if (rr.stopped) atomicOr(&stop_any, 1u);
-  }
-  uint32_t c0 = cnt_sink.nrec, c1 = cnt_sink.nrep;
-  unsigned long long bb = cnt_sink.bytes;
-  cur = 0;
-  cnt[cur][tid][0] = c0;
-  cnt[cur][tid][1] = c1;
-  byt[cur][tid] = bb;
+// Workgroup-wide exclusive sum of (a, b); *ta / *tb = the totals.
+__device__ __forceinline__ void wg_sum_excl(uint32_t& a, uint32_t& b, uint32_t (&cn)[2][kGT][2],
+                                            uint32_t tid, uint32_t* ta, uint32_t* tb) {
+  uint32_t x = a, y = b, cur = 0;
+  cn[cur][tid][0] = x;
+  cn[cur][tid][1] = y;
   __syncthreads();
-  for (uint32_t d = 1; d < kAT; d <<= 1) {
+  for (uint32_t d = 1; d < kGT; d <<= 1) {
     if (tid >= d) {
-      c0 += cnt[cur][tid - d][0];
-      c1 += cnt[cur][tid - d][1];
-      bb += byt[cur][tid - d];
+      x += cn[cur][tid - d][0];
+      y += cn[cur][tid - d][1];
     }
-    cnt[cur ^ 1u][tid][0] = c0;
-    cnt[cur ^ 1u][tid][1] = c1;
-    byt[cur ^ 1u][tid] = bb;
+    cn[cur ^ 1u][tid][0] = x;
+    cn[cur ^ 1u][tid][1] = y;
     cur ^= 1u;
     __syncthreads();
   }
-  const uint32_t rec_base = c0 - cnt_sink.nrec, rep_base = c1 - cnt_sink.nrep;
-  const uint32_t nrec_total = cnt[cur][kAT - 1][0], nrep_total = cnt[cur][kAT - 1][1];
-
-  // 3. write them
-  Sink w = {true, 0, 0, 0, a.recs + rec_base,
-            a.rec_cap > rec_base ? a.rec_cap - rec_base : 0u, a.reps + rep_base,
-            a.rep_cap > rep_base ? a.rep_cap - rep_base : 0u};
-  replay<true>(a.events, k0, k1, j0, r, w);
+  *ta = cn[cur][kGT - 1][0];
+  *tb = cn[cur][kGT - 1][1];
+  a = x - a;
+  b = y - b;
   __syncthreads();
-  const uint32_t nr = min(nrec_total, a.rec_cap);
-  for (uint32_t i = tid; i < nr; i += kAT) a.recs[i].offset = a.hdr_off[a.recs[i].first];
-  if (tid == 0) {
+}
+
+struct WgAgg {  // log_asm_reduce -> log_asm_scan
+  Summ s;
+  uint32_t nrec[3], nrep[3];  // from each starting scenario (kScIdle .. kScEmpty)
+};
+struct WgIn {   // log_asm_scan -> log_asm_emit
+  uint64_t scratch;  // the reader's state at the workgroup's start
+  uint32_t st, first;
+  uint32_t j0;       // candidates before it
+  uint32_t rec_base, rep_base, pad_;
+};
+
+struct AsmArgs {
+  const uint32_t* events;
+  const uint64_t* hdr_off;
+  const lvkv_log_report* phys;
+  uint32_t nblocks;
+  uint32_t rec_cap, rep_cap;
+  uint32_t groups;  // workgroups of the grid launches
+  lvkv_log_record* recs;
+  lvkv_log_corruption* reps;
+  lvkv_log_read_report* out;
+  WgAgg* aggs;
+  WgIn* ins;
+};
+
+// Items on the device: candidate records the verify placed, plus blocks.
+__device__ __forceinline__ uint32_t asm_items(const AsmArgs& a) {
+  return a.phys->status == LVKV_OK ? a.phys->count_ + a.nblocks : 0u;
+}
+
+__global__ void __launch_bounds__(kGT) log_asm_reduce(AsmArgs a) {
+  __shared__ Summ sm[2][kGT];
+  __shared__ uint32_t cn[2][kGT][2];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t K = asm_items(a);
+  if (blockIdx.x * kGT * kChunk >= K) return;  // the whole workgroup
+  Chunk c;
+  chunk_of(a.events, K, blockIdx.x * kGT + tid, c);
+  WgAgg agg;
+  const Summ x = wg_scan_excl(c.s, sm, tid, &agg.s);
+#pragma unroll
+  for (uint32_t sw = 0; sw < 3; ++sw) {
+    const uint32_t sc = chunk_scenario(sw, x);
+    uint32_t r = sc == kScStopped ? 0u : c.nrec[sc], p = sc == kScStopped ? 0u : c.nrep[sc];
+    wg_sum_excl(r, p, cn, tid, &agg.nrec[sw], &agg.nrep[sw]);
+  }
+  if (tid == 0) a.aggs[blockIdx.x] = agg;
+}
+
+constexpr uint32_t kST = 1024;  // threads of log_asm_scan
+
+__global__ void __launch_bounds__(kST, 1) log_asm_scan(AsmArgs a) {
+  __shared__ Summ sm[2][kST];
+  __shared__ Summ tot;
+  __shared__ uint32_t cn[2][kST][2];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t K = asm_items(a);
+  const uint32_t G = min(a.groups, (K + kGT * kChunk - 1) / (kGT * kChunk));
+  const uint32_t per = (G + kST - 1) / kST;
+  const uint32_t g0 = min(G, tid * per), g1 = min(G, g0 + per);
+  // 1. this thread's run of aggregates, composed; scanned across threads
+  Summ s = kIdentity;
+  for (uint32_t g = g0; g < g1; ++g) s = compose(s, a.aggs[g].s);
+  uint32_t cur = 0;
+  sm[cur][tid] = s;
+  __syncthreads();
+  for (uint32_t d = 1; d < kST; d <<= 1) {
+    if (tid >= d) s = compose(sm[cur][tid - d], s);
+    sm[cur ^ 1u][tid] = s;
+    cur ^= 1u;
+    __syncthreads();
+  }
+  if (tid == kST - 1) tot = s;
+  const Summ p0 = tid ? sm[cur][tid - 1] : kIdentity;
+  // 2. each workgroup's counts from its starting state; output positions
+  uint32_t nrec = 0, nrep = 0;
+  Summ p = p0;
+  for (uint32_t g = g0; g < g1; ++g) {
+    const uint32_t sc = p.pass ? kScIdle : scenario(p.c, p.scratch);
+    if (sc != kScStopped) {
+      nrec += a.aggs[g].nrec[sc];
+      nrep += a.aggs[g].nrep[sc];
+    }
+    p = compose(p, a.aggs[g].s);
+  }
+  uint32_t r0 = nrec, r1 = nrep;
+  cur = 0;
+  __syncthreads();
+  cn[cur][tid][0] = r0;
+  cn[cur][tid][1] = r1;
+  __syncthreads();
+  for (uint32_t d = 1; d < kST; d <<= 1) {
+    if (tid >= d) {
+      r0 += cn[cur][tid - d][0];
+      r1 += cn[cur][tid - d][1];
+    }
+    cn[cur ^ 1u][tid][0] = r0;
+    cn[cur ^ 1u][tid][1] = r1;
+    cur ^= 1u;
+    __syncthreads();
+  }
+  uint32_t rb = r0 - nrec, pb = r1 - nrep;
+  p = p0;
+  for (uint32_t g = g0; g < g1; ++g) {
+    WgIn in;
+    in.st = p.pass ? kIdle : p.c;
+    in.first = p.first;
+    in.scratch = p.pass ? 0 : p.scratch;
+    in.j0 = p.nrec;
+    in.rec_base = rb;
+    in.rep_base = pb;
+    in.pad_ = 0;
+    a.ins[g] = in;
+    const uint32_t sc = scenario(in.st, in.scratch);
+    if (sc != kScStopped) {
+      rb += a.aggs[g].nrec[sc];
+      pb += a.aggs[g].nrep[sc];
+    }
+    p = compose(p, a.aggs[g].s);
+  }
+  if (tid == kST - 1) {
     lvkv_log_read_report o;
-    o.status = (!ok || nrec_total > a.rec_cap || nrep_total > a.rep_cap) ? LVKV_LOG_CAPACITY
-                                                                          : LVKV_OK;
-    o.nrecords = nrec_total;
-    o.nreports = nrep_total;
-    o.stopped = stop_any;
-    o.bytes = byt[cur][kAT - 1];
+    o.status = (a.phys->status != LVKV_OK || r0 > a.rec_cap || r1 > a.rep_cap) ? LVKV_LOG_CAPACITY
+                                                                                : LVKV_OK;
+    o.nrecords = r0;
+    o.nreports = r1;
+    o.stopped = (!tot.pass && tot.c == kStopped) ? tot.stop5 : 0u;
+    o.bytes = 0;  // log_asm_emit adds the records' bytes
     *a.out = o;
   }
 }
 
+__global__ void __launch_bounds__(kGT) log_asm_emit(AsmArgs a) {
+  __shared__ Summ sm[2][kGT];
+  __shared__ uint32_t cn[2][kGT][2];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t K = asm_items(a);
+  if (blockIdx.x * kGT * kChunk >= K) return;  // the whole workgroup
+  const WgIn in = a.ins[blockIdx.x];
+  Chunk c;
+  chunk_of(a.events, K, blockIdx.x * kGT + tid, c);
+  Summ all;
+  const Summ x = wg_scan_excl(c.s, sm, tid, &all);
+  // this chunk's starting state
+  const uint32_t sw = scenario(in.st, in.scratch);
+  Reader r = {in.st, in.first, in.scratch, 0, 0};
+  if (!x.pass) {
+    r.st = x.c;
+    r.first = in.j0 + x.first;
+    r.scratch = x.scratch;
+  } else if (r.st == kInFrag) {
+    r.scratch += x.len;
+  }
+  const uint32_t sc = chunk_scenario(sw, x);
+  uint32_t rb = sc == kScStopped ? 0u : c.nrec[sc], pb = sc == kScStopped ? 0u : c.nrep[sc];
+  uint32_t tr, tp;
+  wg_sum_excl(rb, pb, cn, tid, &tr, &tp);
+  rb += in.rec_base;
+  pb += in.rep_base;
+  const uint32_t j0 = in.j0 + x.nrec;
+  uint64_t hoff[kChunk];
+#pragma unroll
+  for (uint32_t i = 0; i < kChunk; ++i) hoff[i] = i < c.s.nrec ? a.hdr_off[j0 + i] : 0;
+  if (r.st == kInFrag) r.first_off = a.hdr_off[r.first];
+  Sink w = {true, 0, 0, 0, a.recs + rb, a.rec_cap > rb ? a.rec_cap - rb : 0u, a.reps + pb,
+            a.rep_cap > pb ? a.rep_cap - pb : 0u};
+  replay<true>(c.ev, hoff, j0, r, w);
+  // the records' bytes: one atomic per wave
+  unsigned long long bytes = w.bytes;
+  for (int d = 32; d >= 1; d >>= 1) bytes += __shfl_xor(bytes, d, 64);
+  if ((tid & 63u) == 0 && bytes)
+    atomicAdd(reinterpret_cast<unsigned long long*>(&a.out->bytes), bytes);
+}
+
 }  // namespace
 
+size_t log_asm_scratch_bytes(size_t max_items) {
+  const size_t groups = (max_items + kGT * kChunk - 1) / (kGT * kChunk);
+  return groups * (sizeof(WgAgg) + sizeof(WgIn)) + 16;
+}
+
+// `scratch`: log_asm_scratch_bytes(capacity + nblocks) bytes, 16-byte aligned.
 hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
-                               const lvkv_log_report* phys, uint64_t size,
+                               const lvkv_log_report* phys, uint64_t size, uint32_t capacity,
                                lvkv_log_record* recs, uint32_t rec_cap,
                                lvkv_log_corruption* reps, uint32_t rep_cap,
-                               lvkv_log_read_report* out, hipStream_t stream) {
+                               lvkv_log_read_report* out, void* scratch, hipStream_t stream) {
   AsmArgs a;
   a.events = events;
   a.hdr_off = hdr_off;
   a.phys = phys;
-  a.size = size;
   a.nblocks = static_cast<uint32_t>((size + 32767) / 32768);
   a.rec_cap = rec_cap;
   a.rep_cap = rep_cap;
+  const uint64_t items = uint64_t{capacity} + a.nblocks;
+  a.groups = static_cast<uint32_t>((items + kGT * kChunk - 1) / (kGT * kChunk));
   a.recs = recs;
   a.reps = reps;
   a.out = out;
-  hipLaunchKernelGGL(log_assemble_kernel, dim3(1), dim3(kAT), 0, stream, a);
+  a.aggs = static_cast<WgAgg*>(scratch);
+  a.ins = reinterpret_cast<WgIn*>(a.aggs + a.groups);
+  hipLaunchKernelGGL(log_asm_reduce, dim3(a.groups), dim3(kGT), 0, stream, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(log_asm_scan, dim3(1), dim3(kST), 0, stream, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(log_asm_emit, dim3(a.groups), dim3(kGT), 0, stream, a);
   return hipGetLastError();
 }
 
