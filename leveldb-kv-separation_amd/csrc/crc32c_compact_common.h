@@ -174,7 +174,8 @@ __device__ __forceinline__ uint32_t zshift_g(const uint32_t* zpow, uint32_t v, u
 // Register after [s, e) (e 4-byte aligned, e - s <= kLongSeg) from state
 // init ^ ~0: the end-aligned row walk of the uniform kernels, 16-row chunks,
 // the next chunk's loads in flight while one is walked.
-__device__ uint32_t segment_register(const uint32_t* lds, uint64_t s, uint64_t e, uint32_t init,
+__device__ __forceinline__ uint32_t segment_register(const uint32_t* lds, uint64_t s, uint64_t e,
+                                                    uint32_t init,
                                      const LaneKeys& keys, uint32_t lane, uint32_t lane_base) {
   const uint32_t len = static_cast<uint32_t>(e - s);
   UniGeo g;
@@ -306,6 +307,14 @@ __device__ __forceinline__ uint32_t apply_cols(const uint32_t* cols, uint32_t v)
   return r;
 }
 
+// The same with the columns held one per lane: lanes 32 h + b hold column b
+// of operator h; v wave-uniform; one DPP xor-reduction.
+__device__ __forceinline__ uint32_t apply_lane_cols(uint32_t colv, uint32_t v, uint32_t h,
+                                                    uint32_t lane) {
+  const bool on = (lane >> 5) == h && ((v >> (lane & 31u)) & 1u);
+  return wave_xor_dpp(on ? colv : 0u);
+}
+
 // Bitwise register update over the n (< 4) little-endian bytes of `bytes`.
 __device__ __forceinline__ uint32_t crc_bytes_bitwise(uint32_t reg, uint32_t bytes, uint32_t n) {
   for (uint32_t i = 0; i < n; ++i) {
@@ -341,7 +350,10 @@ __device__ inline uint32_t group_crc_part(const uint32_t* lds, uint64_t start, u
   const uint32_t m = static_cast<uint32_t>((e4 - start + seg - 1) >> log2seg);
   if (gw >= m) return 0u;
   const uint32_t jmax = gw + ((m - 1u - gw) / GW) * GW;
-  const uint32_t* stride_cols = zmul_cols(zpow, log2seg, GW);
+  // both operators' columns, loaded before the walks: lanes [0, 32) hold
+  // Z_{GW S}, lanes [32, 64) Z_{gw S}
+  const uint32_t colv = lane < 32u ? zmul_cols(zpow, log2seg, GW)[lane]
+                                   : (gw ? zmul_cols(zpow, log2seg, gw)[lane - 32u] : 0u);
   uint32_t acc = 0;
   for (uint32_t j = jmax;; j -= GW) {
     const uint64_t e = e4 - uint64_t{j} * seg;
@@ -349,10 +361,10 @@ __device__ inline uint32_t group_crc_part(const uint32_t* lds, uint64_t start, u
     const uint64_t s = front ? start : e - seg;
     const uint32_t reg =
         segment_register(lds, s, e, front ? init : 0xffffffffu, keys, lane, lane_base);
-    acc = (j == jmax ? 0u : apply_cols(stride_cols, acc)) ^ reg;
+    acc = (j == jmax ? 0u : apply_lane_cols(colv, acc, 0, lane)) ^ reg;
     if (j < GW) break;
   }
-  return gw ? apply_cols(zmul_cols(zpow, log2seg, gw), acc) : acc;
+  return gw ? apply_lane_cols(colv, acc, 1, lane) : acc;
 }
 
 // CRC of [start, end) from the xor of the group's shares and `tail`, the

@@ -215,10 +215,12 @@ __device__ void parse_footer(Head& h, const uint8_t* f, uint64_t size) {
 // over the staged metaindex m[0, msize) (kNoCompression, CRC verified): a
 // linear walk keeping the length of the common prefix of the current key and
 // the target, so no key buffer is needed. Sets the filter handle on a match.
-__device__ void find_filter(Head& h, const uint8_t* m, uint64_t msize, const FilterKey& fk,
-                            const Table& tb) {
-  h.has_filter = 0;
-  if (fk.len == 0 || msize < 4) return;
+// One wave: entries are decoded lane-uniformly; each key's bytes are
+// compared 64 at a time, one lane per byte (a ballot gives the prefix).
+__device__ void find_filter(Head& h, const uint8_t* m, uint64_t msize, const uint8_t* key,
+                            uint32_t key_len, const Table& tb, uint32_t lane) {
+  if (lane == 0) h.has_filter = 0;
+  if (key_len == 0 || msize < 4) return;
   const uint32_t nr = ld_le32(m + msize - 4);
   if (nr > (msize - 4) / 4) return;
   const uint8_t* limit = m + (msize - (1 + static_cast<uint64_t>(nr)) * 4);
@@ -229,18 +231,29 @@ __device__ void find_filter(Head& h, const uint8_t* m, uint64_t msize, const Fil
     const uint8_t* q = decode_entry(p, limit, &sh, &ns, &vl);
     if (q == nullptr || sh > klen) return;  // Block::Iter: "bad entry in block"
     uint32_t l = min(sh, lcp);
-    if (l == sh)
-      for (uint32_t i = 0; i < ns && sh + i < fk.len && q[i] == fk.key[sh + i]; ++i) l = sh + i + 1;
+    if (l == sh) {
+      // leading bytes of q[0, ns) equal to key[sh, key_len)
+      for (uint32_t i0 = 0; i0 < ns && sh + i0 < key_len; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const bool eq = i < ns && sh + i < key_len && q[i] == key[sh + i];
+        const uint64_t miss = ~__ballot(eq);
+        const uint32_t run = miss ? static_cast<uint32_t>(__builtin_ctzll(miss)) : 64u;
+        l = sh + i0 + run;
+        if (run < 64) break;
+      }
+    }
     lcp = l;
     klen = sh + ns;
-    if (klen == fk.len && lcp == fk.len) {
+    if (klen == key_len && lcp == key_len) {
       uint64_t fo, fsz;
       if (!decode_handle(q + ns, q + ns + vl, &fo, &fsz, nullptr)) return;  // ReadFilter: ignored
       const Fit f = handle_fit(fo, fsz, tb.size);
-      h.fo = f == kFitOk ? fo : 0;
-      h.fs = f == kFitOk ? fsz : 0;
-      h.filter_status = f == kFitOk ? LVKV_BLOCK_OK : unfit_status(tb.img, f, fo);
-      h.has_filter = 1;
+      if (lane == 0) {
+        h.fo = f == kFitOk ? fo : 0;
+        h.fs = f == kFitOk ? fsz : 0;
+        h.filter_status = f == kFitOk ? LVKV_BLOCK_OK : unfit_status(tb.img, f, fo);
+        h.has_filter = 1;
+      }
       return;
     }
     p = q + ns + vl;
@@ -343,13 +356,24 @@ __device__ void emit_entry(const uint8_t* idx, uint64_t ro, uint64_t nr, uint32_
 }
 
 // What a table's workgroup keeps in LDS after the 64 KiB CRC image.
+constexpr uint32_t kFilterKeyWords = (kMaxFilterKey + 4) / 4;
+
 struct SstHeadLds {
   uint32_t acc[16];  // per-wave CRC shares
+  uint32_t fkey[kFilterKeyWords];  // the metaindex key sought, from the kernel argument
   uint8_t foot[kFooterLen];
   uint8_t mbuf[kMetaStage];
   Head h;
   uint64_t win_lo, win_hi;
 };
+
+// Probe build: phase timestamps (s_memrealtime, 100 MHz) of table t's head
+// and of the first CRC workgroup, 16 u64 per table (tools/probe/sst_probe.py).
+__device__ __forceinline__ void sst_stamp(uint64_t* stamps, uint32_t t, int slot) {
+#ifdef LVKV_PROBE_BUILD
+  if (stamps != nullptr && threadIdx.x == 0) stamps[t * 16u + slot] = __builtin_amdgcn_s_memrealtime();
+#endif
+}
 
 // Index bytes prefetched into registers during the CRCs, per thread: an
 // index of up to 64 W * kIndexPf dwords is staged from these, without a
@@ -369,7 +393,8 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
                          const uint64_t* tsize, uint64_t single_size, uint32_t t,
                          uint32_t ntables, uint32_t capacity, uint32_t gen, const FilterKey& fk,
                          lvkv_sst_report* reports, uint64_t* out_off, uint32_t* out_size,
-                         uint8_t* out_status, const uint32_t* zpow, const uint32_t* lane_cols) {
+                         uint8_t* out_status, const uint32_t* zpow, const uint32_t* lane_cols,
+                         uint64_t* stamps) {
   constexpr uint32_t kT = 64 * W;
   SstHeadLds& L = *reinterpret_cast<SstHeadLds*>(lds + kCompactLdsBytes / 4);
   Head& h = L.h;
@@ -379,12 +404,32 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
   const Table tb = table_of(file, toff, tsize, single_size, t);
   lvkv_sst_report* r = reports + t;
 
-  // 1. Footer bytes (48 lanes) while the workgroup builds its LDS image.
+  sst_stamp(stamps, t, 0);
+  // 1. Footer bytes (48 lanes) while the workgroup builds its LDS image;
+  //    the filter key into LDS (constant word indices: the kernel argument
+  //    is read with scalar loads, never copied to scratch for a byte walk).
   if (tid < kFooterLen && tb.size >= kFooterLen) L.foot[tid] = tb.img[tb.size - kFooterLen + tid];
+  {
+    const uint32_t* kw = reinterpret_cast<const uint32_t*>(fk.key);
+#pragma unroll
+    for (uint32_t w = 0; w < kFilterKeyWords; ++w)
+      if (tid == 64u + w) L.fkey[w] = kw[w];
+  }
+  // the table's last 32 KiB (where the index and metaindex usually sit)
+  // pulled towards the CUs beside the footer: the CRC phase's loads then hit
+  // the cache. The values are only "used" by an empty asm after the footer.
+  uint32_t warm = 0;
+  {
+    const uint64_t span = min<uint64_t>(tb.size, uint64_t{32} * 1024) & ~uint64_t{63};
+    const uint64_t at = tb.size - span;
+    if (64u * tid < span) warm = *reinterpret_cast<const uint32_t*>(tb.img + ((at + 64u * tid) & ~uint64_t{3}));
+  }
   build_compact_image<W>(lds, zpow, lane_cols, tid, wave, lane);  // ends with a barrier
   if (tid == 0) parse_footer(h, L.foot, tb.size);
   __syncthreads();
+  asm volatile("" ::"v"(warm));
   const bool footer_ok = h.status == LVKV_SST_OK;  // workgroup-uniform from here on
+  sst_stamp(stamps, t, 1);
   const bool ifit = footer_ok && h.ifit == kFitOk;
   const bool mfit = footer_ok && h.mfit == kFitOk;
   const uint64_t istart = reinterpret_cast<uint64_t>(tb.img) + h.io, iend = istart + h.is + 1;
@@ -439,6 +484,7 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
   }
   if (lane == 0) L.acc[wave] = part;
   __syncthreads();
+  sst_stamp(stamps, t, 2);
 
   // 4. Verdicts (ReadBlock's order), restart array.
   if (tid == 0 && footer_ok) {
@@ -482,6 +528,7 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
   // Table::Open succeeded iff the index block was read (Block::Block's
   // restart test only makes the index iterator fail, table.cc:62-75); then
   // ReadMeta runs (:76).
+  sst_stamp(stamps, t, 3);
   const bool index_read = footer_ok && h.index_status == LVKV_BLOCK_OK;
   const bool index_usable = h.status == LVKV_SST_OK;
   const bool stage_meta = index_read && h.meta_status == LVKV_BLOCK_OK && h.ms < kMetaStage;
@@ -500,15 +547,17 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
     }
   }
   __syncthreads();
-  if (tid == 0) {
-    if (index_read && h.meta_status == LVKV_BLOCK_OK)
-      find_filter(h, stage_meta ? L.mbuf : tb.img + h.mo, h.ms, fk, tb);
-    // entries: the data blocks the index lists (none when its restart array
-    // is unusable), then the filter block
-    h.nb = (index_usable ? h.nr : 0u) + h.has_filter;
-  }
+  sst_stamp(stamps, t, 4);
+  if (wave == 0 && index_read && h.meta_status == LVKV_BLOCK_OK)
+    find_filter(h, stage_meta ? L.mbuf : tb.img + h.mo, h.ms,
+                reinterpret_cast<const uint8_t*>(L.fkey), fk.len, tb, lane);
+  __syncthreads();
+  // entries: the data blocks the index lists (none when its restart array is
+  // unusable), then the filter block
+  if (tid == 0) h.nb = (index_usable ? h.nr : 0u) + h.has_filter;
   __syncthreads();
 
+  sst_stamp(stamps, t, 5);
   // 5. Place this table's entries in the shared arrays.
   if (wave == 0) {
     uint32_t total = 0, first = 0;
@@ -540,6 +589,7 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
     }
   }
   __syncthreads();
+  sst_stamp(stamps, t, 6);
   if (h.status == LVKV_SST_CAPACITY || h.nb == 0) return;
 
   // 6. Every entry: index entries 0..nr-1, then the filter block.
@@ -603,11 +653,13 @@ __global__ void __launch_bounds__(64 * kW, 1)
                      uint64_t single_size, uint32_t ntables, uint32_t capacity, uint32_t gen,
                      FilterKey fk, lvkv_sst_report* reports, uint64_t* out_off,
                      uint32_t* out_size, uint8_t* out_status, const uint32_t* zpow,
-                     const uint32_t* lane_cols) {
+                     const uint32_t* lane_cols, uint64_t* stamps) {
   __shared__ __attribute__((aligned(16)))
   uint32_t lds[kCompactLdsBytes / 4 + (sizeof(SstHeadLds) + 3) / 4];
   sst_head<kW>(lds, file, toff, tsize, single_size, blockIdx.x, ntables, capacity, gen, fk,
-               reports, out_off, out_size, out_status, zpow, lane_cols);
+               reports, out_off, out_size, out_status, zpow, lane_cols, stamps);
+  __syncthreads();
+  sst_stamp(stamps, blockIdx.x, 7);
 }
 
 constexpr uint32_t kHeadLdsDwords =
@@ -627,25 +679,27 @@ __global__ void __launch_bounds__(64 * kFW, 2)
     sst_fused_kernel(KernelArgs a, const uint8_t* file, const uint64_t* toff,
                      const uint64_t* tsize, uint64_t single_size, uint32_t ntables,
                      uint32_t capacity, uint32_t gen, FilterKey fk, lvkv_sst_report* reports,
-                     const uint32_t* zpow, const uint32_t* lane_cols) {
+                     const uint32_t* zpow, const uint32_t* lane_cols, uint64_t* stamps) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFusedLdsDwords];
   const uint32_t tid = threadIdx.x;
   if (blockIdx.x < ntables) {
     sst_head<kFW>(lds, file, toff, tsize, single_size, blockIdx.x, ntables, capacity, gen, fk,
                   reports, const_cast<uint64_t*>(a.offsets), const_cast<uint32_t*>(a.lengths),
-                  a.out_status, zpow, lane_cols);
+                  a.out_status, zpow, lane_cols, stamps);
     // every wave's stores are done at the barrier; one agent-scope release
     // (writes this XCD's L2 back) publishes them with the tag
     __syncthreads();
     if (tid == 0)
       __hip_atomic_store(&reports[blockIdx.x].done_, gen, __ATOMIC_RELEASE,
                          __HIP_MEMORY_SCOPE_AGENT);
+    sst_stamp(stamps, blockIdx.x, 7);
     return;
   }
   const uint32_t lane = lane_id();
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (tid == 0) lds[RagLds<kFW>::kFlag] = 0;
   build_compact_image<kFW>(lds, zpow, lane_cols, tid, wave, lane);  // ends with a barrier
+  if (blockIdx.x == ntables) sst_stamp(stamps, 0, 10);
   // Wait for every head. No acquire fence afterwards (one per workgroup
   // would invalidate the XCD's L2 hundreds of times): everything the heads
   // wrote is read with agent-scope atomic loads (desc_u64/_u32, the
@@ -656,16 +710,26 @@ __global__ void __launch_bounds__(64 * kFW, 2)
         __builtin_amdgcn_s_sleep(8);
   }
   __syncthreads();
+  const bool probe = blockIdx.x == ntables;  // the first CRC workgroup's stamps (table 0's row)
+  if (probe) sst_stamp(stamps, 0, 8);
   const uint32_t total = min(
       capacity, __builtin_amdgcn_readfirstlane(__hip_atomic_load(
                     &reports[0].total_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
   ragged_run<kFW, 2, 24>(a, zpow, lane_cols, lds, blockIdx.x - ntables, gridDim.x - ntables, total,
                          true);
+  if (probe) sst_stamp(stamps, 0, 9);
 }
 
 }  // namespace
 
 hipError_t launch_crc32c_general(const KernelArgs& a, int cus, hipStream_t stream);
+
+#ifdef LVKV_PROBE_BUILD
+uint64_t* g_sst_stamps = nullptr;  // lvkv_debug_sst_stamps
+static uint64_t* sst_stamps() { return g_sst_stamps; }
+#else
+static uint64_t* sst_stamps() { return nullptr; }
+#endif
 
 // Whole-table verify of `ntables` images (toff/tsize device arrays, or
 // nullptr and `single_size` for one image at d_file); `verify` carries the
@@ -699,12 +763,13 @@ hipError_t launch_sst_tables(const uint8_t* file, const uint64_t* toff, const ui
     // two workgroups per CU resident; the heads come first
     const uint32_t grid = max(2u * static_cast<uint32_t>(groups), ntables + static_cast<uint32_t>(groups));
     hipLaunchKernelGGL(sst_fused_kernel, dim3(grid), dim3(64 * kFW), 0, stream, a, file, toff,
-                       tsize, single_size, ntables, capacity, gen, fk, reports, zpow, lane_cols);
+                       tsize, single_size, ntables, capacity, gen, fk, reports, zpow, lane_cols,
+                       sst_stamps());
     return hipGetLastError();
   }
   hipLaunchKernelGGL(sst_table_kernel, dim3(ntables), dim3(64 * kW), 0, stream, file, toff,
                      tsize, single_size, ntables, capacity, gen, fk, reports, d_off, d_size,
-                     d_status, zpow, lane_cols);
+                     d_status, zpow, lane_cols, sst_stamps());
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return launch_crc32c_general(a, groups, stream);

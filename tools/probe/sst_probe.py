@@ -105,6 +105,32 @@ def main():
     us = (time.perf_counter() - t0) / 50 * 1e6
     print(f"sst_verify form {form}, {nblocks} blocks, {len(img)} bytes: {us:.1f} us/call",
           flush=True)
+    if "--stamps" in sys.argv:
+        # phase stamps from the probe build (10 ns units -> us from the head's start)
+        P = ctypes.CDLL(str(HERE / "liblvkv_probe.so"))
+        P.lvkv_debug_sst_stamps.argtypes = [vp]
+        P.lvkv_debug_set_sst_form.argtypes = [ctypes.c_int]
+        P.lvkv_debug_set_sst_form(form)
+        P.lvkv_sst_verify_table_device.argtypes = [vp, ctypes.c_uint64, vp, vp, vp, vp,
+                                                   ctypes.c_size_t, ctypes.c_char_p, vp, vp]
+        stz = torch.zeros(16, dtype=torch.int64, device=dev)
+        P.lvkv_debug_sst_stamps(vp(stz.data_ptr()))
+        rows = []
+        for _ in range(8):
+            stz.zero_()
+            torch.cuda.synchronize()
+            rc = P.lvkv_sst_verify_table_device(vp(buf.data_ptr()), len(img), vp(o.data_ptr()),
+                                                vp(sz.data_ptr()), vp(ac.data_ptr()),
+                                                vp(st.data_ptr()), cap, pol, vp(rp.data_ptr()), h)
+            assert rc == 0
+            torch.cuda.synchronize()
+            x = stz.cpu().numpy().astype(np.int64)
+            rows.append([(v - x[0]) / 100.0 if v else float("nan") for v in x[:11]])
+        med = np.nanmedian(np.array(rows), axis=0)
+        names = ["start", "footer", "crcs", "verdicts", "staged", "filter", "placed", "done",
+                 "crc_wg_waited", "crc_wg_end", "crc_wg_image"]
+        print("  " + "  ".join(f"{n} {v:.2f}" for n, v in zip(names, med)), flush=True)
+        P.lvkv_debug_sst_stamps(None)
 
 
 if __name__ == "__main__":
