@@ -64,18 +64,25 @@ __device__ __forceinline__ BlockSpan block_span(uint64_t b, uint64_t size) {
 
 // Walks one block's headers in LDS, blk[0, n), to the first stop (bad
 // length, zero record, end) like ReadPhysicalRecord, with the stop position:
-// one LDS round trip per header; returns the verdict,
-// *stop = the block offset after the last record.
+// one LDS round trip per header; returns the verdict, *stop = the block
+// offset after the last record. Called by a whole wave with uniform
+// arguments: every lane reads the same dwords (a broadcast) and the header
+// arithmetic runs on the scalar unit (readfirstlane), so a step is the LDS
+// latency plus a few SALU cycles; lane 0 writes the positions.
 __device__ __forceinline__ uint8_t walk_positions(const uint8_t* blk, uint32_t n, bool eof,
                                                   uint16_t* pos, uint32_t* count, uint32_t* stop) {
   uint32_t p = 0, k = 0;
   uint8_t v = 0xff;
+  const bool writer = (threadIdx.x & 63u) == 0;
   while (n - p >= kLogHeader) {
     // bytes p + 4 .. p + 6 (length, type) from the two aligned dwords around
     // them, read together (one ds_read2, one round trip)
     const uint32_t x = p + 4;
     const uint32_t* d = reinterpret_cast<const uint32_t*>(blk + (x & ~3u));
-    const uint32_t w = __builtin_amdgcn_alignbyte(d[1], d[0], x & 3u);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(d[0]);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(d[1]);
+    const uint32_t sh = 8u * (x & 3u);
+    const uint32_t w = sh ? (lo >> sh) | (hi << (32u - sh)) : lo;
     const uint32_t length = w & 0xffffu;
     const uint32_t type = (w >> 16) & 0xffu;
     if (kLogHeader + length > n - p) {  // :221-232
@@ -86,7 +93,8 @@ __device__ __forceinline__ uint8_t walk_positions(const uint8_t* blk, uint32_t n
       v = LVKV_LOGBLK_ZERO;
       break;
     }
-    pos[k++] = static_cast<uint16_t>(p);
+    if (writer) pos[k] = static_cast<uint16_t>(p);
+    ++k;
     p += kLogHeader + length;
   }
   if (v == 0xff) v = (eof && p < n) ? LVKV_LOGBLK_EOF : LVKV_LOGBLK_OK;  // :206-213
@@ -356,15 +364,18 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
   }
   __syncthreads();
   if (b0 < a.nblocks) {
-    if (tid == 0) {
+    if (wave == 0) {
       const BlockSpan s = block_span(b0, a.size);
       uint32_t c, st;
-      walked[0] = walk_positions(buf[0], static_cast<uint32_t>(s.end - s.start), s.eof, pos[0],
-                                 &c, &st);
-      cnt[0] = c;
-      stop[0] = st;
-      __hip_atomic_store(&a.agg[b0], link_word(a.gen, kFlagAgg, c), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+      const uint8_t v = walk_positions(buf[0], static_cast<uint32_t>(s.end - s.start), s.eof,
+                                       pos[0], &c, &st);
+      if (lane == 0) {
+        walked[0] = v;
+        cnt[0] = c;
+        stop[0] = st;
+        __hip_atomic_store(&a.agg[b0], link_word(a.gen, kFlagAgg, c), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     if (b0 + G < a.nblocks) load_block(a, b0 + G, tid, pre);
   }
@@ -413,11 +424,15 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
       }
       if (nb + G < a.nblocks) load_block(a, nb + G, tid, pre);
     } else if (wave == 1 && nb < a.nblocks) {
+      // the walk is the iteration's longest chain: this wave issues first
+      __builtin_amdgcn_s_setprio(3);
+      const BlockSpan ns = block_span(nb, a.size);
+      uint32_t nc, nst;
+      const uint8_t v = walk_positions(buf[cur ^ 1u], static_cast<uint32_t>(ns.end - ns.start),
+                                       ns.eof, pos[cur ^ 1u], &nc, &nst);
+      __builtin_amdgcn_s_setprio(0);
       if (lane == 0) {
-        const BlockSpan ns = block_span(nb, a.size);
-        uint32_t nc, nst;
-        walked[cur ^ 1u] = walk_positions(buf[cur ^ 1u], static_cast<uint32_t>(ns.end - ns.start),
-                                          ns.eof, pos[cur ^ 1u], &nc, &nst);
+        walked[cur ^ 1u] = v;
         cnt[cur ^ 1u] = nc;
         stop[cur ^ 1u] = nst;
         __hip_atomic_store(&a.agg[nb], link_word(a.gen, kFlagAgg, nc), __ATOMIC_RELAXED,
