@@ -71,33 +71,36 @@ __device__ __forceinline__ BlockSpan block_span(uint64_t b, uint64_t size) {
 // latency plus a few SALU cycles; lane 0 writes the positions.
 __device__ __forceinline__ uint8_t walk_positions(const uint8_t* blk, uint32_t n, bool eof,
                                                   uint16_t* pos, uint32_t* count, uint32_t* stop) {
-  uint32_t p = 0, k = 0;
-  uint8_t v = 0xff;
-  const bool writer = (threadIdx.x & 63u) == 0;
+  uint32_t p = 0, k = 0, length = 0, w = 0;
+  // positions collect in a register, record k in lane k % 64 (a select),
+  // written to pos[] 64 at a time: no per-step masked LDS store
+  uint32_t held = 0;
+  const uint32_t lane = threadIdx.x & 63u;
   while (n - p >= kLogHeader) {
     // bytes p + 4 .. p + 6 (length, type) from the two aligned dwords around
-    // them, read together (one ds_read2, one round trip)
+    // them (one ds_read2), a 64-bit funnel shift on the scalar unit
     const uint32_t x = p + 4;
     const uint32_t* d = reinterpret_cast<const uint32_t*>(blk + (x & ~3u));
     const uint32_t lo = __builtin_amdgcn_readfirstlane(d[0]);
     const uint32_t hi = __builtin_amdgcn_readfirstlane(d[1]);
-    const uint32_t sh = 8u * (x & 3u);
-    const uint32_t w = sh ? (lo >> sh) | (hi << (32u - sh)) : lo;
-    const uint32_t length = w & 0xffffu;
-    const uint32_t type = (w >> 16) & 0xffu;
-    if (kLogHeader + length > n - p) {  // :221-232
-      v = eof ? LVKV_LOGBLK_EOF : LVKV_LOGBLK_BAD_LENGTH;
-      break;
-    }
-    if (type == 0 && length == 0) {  // :234-240 (preallocated)
-      v = LVKV_LOGBLK_ZERO;
-      break;
-    }
-    if (writer) pos[k] = static_cast<uint16_t>(p);
+    w = static_cast<uint32_t>(((static_cast<uint64_t>(hi) << 32) | lo) >> (8u * (x & 3u)));
+    length = w & 0xffffu;
+    // a bad length (:221-232) or a zero record (:234-240) ends the walk
+    if (kLogHeader + length > n - p) break;
+    if ((w & 0xffffffu) == 0) break;
+    held = lane == (k & 63u) ? p : held;
     ++k;
+    if ((k & 63u) == 0) pos[k - 64u + lane] = static_cast<uint16_t>(held);
     p += kLogHeader + length;
   }
-  if (v == 0xff) v = (eof && p < n) ? LVKV_LOGBLK_EOF : LVKV_LOGBLK_OK;  // :206-213
+  if (lane < (k & 63u)) pos[(k & ~63u) + lane] = static_cast<uint16_t>(held);
+  uint8_t v;
+  if (n - p < kLogHeader)
+    v = (eof && p < n) ? LVKV_LOGBLK_EOF : LVKV_LOGBLK_OK;  // :206-213
+  else if (kLogHeader + length > n - p)
+    v = eof ? LVKV_LOGBLK_EOF : LVKV_LOGBLK_BAD_LENGTH;
+  else
+    v = LVKV_LOGBLK_ZERO;
   *count = k;
   *stop = p;
   return v;
