@@ -87,7 +87,7 @@ __device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {
 
 // GetVarint64Ptr / GetVarint32Ptr (util/coding.cc): bytes consumed, 0 on
 // failure (runs past `limit` or longer than the type allows).
-__device__ uint32_t get_varint(const uint8_t* p, const uint8_t* limit, uint32_t max_shift,
+__device__ __forceinline__ uint32_t get_varint(const uint8_t* p, const uint8_t* limit, uint32_t max_shift,
                                uint64_t* v) {
   uint64_t result = 0;
   uint32_t i = 0;
@@ -104,7 +104,7 @@ __device__ uint32_t get_varint(const uint8_t* p, const uint8_t* limit, uint32_t 
 }
 
 // BlockHandle::DecodeFrom over [p, limit): true and (off, size) on success.
-__device__ bool decode_handle(const uint8_t* p, const uint8_t* limit, uint64_t* off,
+__device__ __forceinline__ bool decode_handle(const uint8_t* p, const uint8_t* limit, uint64_t* off,
                               uint64_t* size, const uint8_t** next) {
   const uint32_t n1 = get_varint(p, limit, 63, off);
   if (n1 == 0) return false;
@@ -144,7 +144,7 @@ __device__ __forceinline__ uint8_t read_status(bool crc_ok, uint8_t type) {
 }
 
 // DecodeEntry (table/block.cc:55-75): pointer to the key delta or nullptr.
-__device__ const uint8_t* decode_entry(const uint8_t* p, const uint8_t* limit, uint32_t* shared,
+__device__ __forceinline__ const uint8_t* decode_entry(const uint8_t* p, const uint8_t* limit, uint32_t* shared,
                                        uint32_t* non_shared, uint32_t* value_len) {
   if (limit - p < 3) return nullptr;
   uint64_t v;
@@ -179,7 +179,7 @@ struct Head {
 };
 
 // Footer::DecodeFrom (format.cc:43-67) on the 48 staged footer bytes.
-__device__ void parse_footer(Head& h, const uint8_t* f, uint64_t size) {
+__device__ __forceinline__ void parse_footer(Head& h, const uint8_t* f, uint64_t size) {
   h.status = LVKV_SST_OK;
   h.mo = h.ms = h.io = h.is = 0;
   h.ifit = h.mfit = kFitShort;
@@ -217,7 +217,7 @@ __device__ void parse_footer(Head& h, const uint8_t* f, uint64_t size) {
 // the target, so no key buffer is needed. Sets the filter handle on a match.
 // One wave: entries are decoded lane-uniformly; each key's bytes are
 // compared 64 at a time, one lane per byte (a ballot gives the prefix).
-__device__ void find_filter(Head& h, const uint8_t* m, uint64_t msize, const uint8_t* key,
+__device__ __forceinline__ void find_filter(Head& h, const uint8_t* m, uint64_t msize, const uint8_t* key,
                             uint32_t key_len, const Table& tb, uint32_t lane) {
   if (lane == 0) h.has_filter = 0;
   if (key_len == 0 || msize < 4) return;
@@ -315,7 +315,7 @@ __device__ uint32_t place_table(lvkv_sst_report* reports, uint32_t t, uint32_t n
 // block handle and status in the shared arrays at first + i. The entry bytes
 // are read from `w` (a copy of index bytes [wlo, whi)) when they lie inside
 // it, else from the index `idx` itself; `ro` is the restart array's offset.
-__device__ void emit_entry(const uint8_t* idx, uint64_t ro, uint64_t nr, uint32_t i,
+__device__ __forceinline__ void emit_entry(const uint8_t* idx, uint64_t ro, uint64_t nr, uint32_t i,
                            const uint8_t* w, uint64_t wlo, uint64_t whi, const Table& tb,
                            uint32_t first, uint64_t* out_off, uint32_t* out_size,
                            uint8_t* out_status) {
