@@ -119,6 +119,48 @@ def test_log_report_struct_layout(tmp_path, lvkv):
         assert getattr(S, name).offset == int(off), name
 
 
+def test_log_read_struct_layouts(tmp_path, lvkv):
+    # lvkv_log_read_device's outputs as the Python log_read() decodes them:
+    # lvkv_log_read_report (ctypes mirror), lvkv_log_record (24 bytes: offset,
+    # length, first | nfrags << 32) and lvkv_log_corruption (16 bytes: bytes,
+    # reason | type << 32), and the reason codes the wrapper names.
+    src = tmp_path / "layout.c"
+    src.write_text(textwrap.dedent("""
+        #include <stddef.h>
+        #include <stdio.h>
+        #include "lvkv_crc32c.h"
+        #define R(x) printf("r.%s %zu\\n", #x, offsetof(lvkv_log_read_report, x));
+        int main(void) {
+          printf("r.size %zu\\n", sizeof(lvkv_log_read_report));
+          R(status) R(nrecords) R(nreports) R(stopped) R(bytes)
+          printf("rec %zu %zu %zu %zu %zu\\n", sizeof(lvkv_log_record),
+                 offsetof(lvkv_log_record, offset), offsetof(lvkv_log_record, length),
+                 offsetof(lvkv_log_record, first), offsetof(lvkv_log_record, nfrags));
+          printf("cor %zu %zu %zu %zu\\n", sizeof(lvkv_log_corruption),
+                 offsetof(lvkv_log_corruption, bytes), offsetof(lvkv_log_corruption, reason),
+                 offsetof(lvkv_log_corruption, type));
+          printf("why %d %d %d %d %d %d %d %d\\n", LVKV_LOGR_CHECKSUM, LVKV_LOGR_BAD_LENGTH,
+                 LVKV_LOGR_PARTIAL_1, LVKV_LOGR_PARTIAL_2, LVKV_LOGR_MISSING_1,
+                 LVKV_LOGR_MISSING_2, LVKV_LOGR_MIDDLE, LVKV_LOGR_UNKNOWN_TYPE);
+          return 0;
+        }"""))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", str(REPO / "include"), str(src), "-o", str(exe)], check=True)
+    lines = subprocess.run([str(exe)], capture_output=True, text=True,
+                           check=True).stdout.splitlines()
+    got = {l.split()[0]: l.split()[1:] for l in lines}
+    S = lvkv.LogReadReport
+    assert int(got.pop("r.size")[0]) == ctypes.sizeof(S)
+    for name in ("status", "nrecords", "nreports", "stopped", "bytes"):
+        assert getattr(S, name).offset == int(got["r." + name][0]), name
+    assert [int(x) for x in got["rec"]] == [24, 0, 8, 16, 20]
+    assert [int(x) for x in got["cor"]] == [16, 0, 8, 12]
+    codes = [int(x) for x in got["why"]]
+    assert sorted(lvkv.LOG_REASONS) == codes
+    assert lvkv.LOG_REASONS[1] == "checksum mismatch"
+    assert lvkv.LOG_REASONS[7] == "error in middle of record"
+
+
 # ---------------------------------------------------------------- GPU -----
 
 def _device(lvkv, img: bytes, gpu, capacity=None):
