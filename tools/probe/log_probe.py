@@ -78,6 +78,33 @@ def main():
                                                  vp(rp.data_ptr()), h)
             assert rc == 0
             torch.cuda.synchronize()
+        # A/B in this process: the probe library with the knob, unstamped
+        P.lvkv_debug_log_stamps(None)
+        for kn in (0, knobs):
+            P.lvkv_debug_log_knobs(kn)
+            for _ in range(5):
+                P.lvkv_log_verify_blocks_device(vp(buf.data_ptr()), len(img), vp(hdr.data_ptr()),
+                                                vp(act.data_ptr()), vp(rst.data_ptr()), cap,
+                                                vp(bst.data_ptr()), vp(bdr.data_ptr()),
+                                                vp(rp.data_ptr()), h)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(50):
+                P.lvkv_log_verify_blocks_device(vp(buf.data_ptr()), len(img), vp(hdr.data_ptr()),
+                                                vp(act.data_ptr()), vp(rst.data_ptr()), cap,
+                                                vp(bst.data_ptr()), vp(bdr.data_ptr()),
+                                                vp(rp.data_ptr()), h)
+            torch.cuda.synchronize()
+            ab = (time.perf_counter() - t1) / 50 * 1e6
+            a_ = act.cpu().numpy().copy() if kn == 0 else None
+            if kn == 0:
+                ref_act, ref_rst = act.cpu().numpy().copy(), rst.cpu().numpy().copy()
+            else:
+                same = (np.array_equal(ref_act, act.cpu().numpy()) and
+                        np.array_equal(ref_rst, rst.cpu().numpy()))
+                print(f"  outputs equal to knob 0: {same}", flush=True)
+            print(f"  probe lib knobs {kn}: {ab:.1f} us/call", flush=True)
+        P.lvkv_debug_log_knobs(knobs)
         x = st.cpu().numpy().reshape(256, 16, 8).astype(np.int64)
         t0 = x[:, 0, 0][x[:, 0, 0] > 0].min()
         for k in range(9):
