@@ -334,8 +334,8 @@ typedef struct lvkv_log_read_report {
   uint64_t bytes;    /* total bytes of the returned records */
 } lvkv_log_read_report;
 
-/* log::Reader(reporter, checksum = true, initial_offset = 0) over a whole
- * log image in device memory: ReadRecord until it returns false
+/* log::Reader(reporter, checksum = true, initial_offset) over a whole log
+ * image in device memory: ReadRecord until it returns false
  * (db/log_reader.cc:55-176 over ReadPhysicalRecord :189-271). Runs
  * lvkv_log_verify_blocks_device (same physical outputs, same meaning) and then
  * the logical layer on the device: FULL records, FIRST MIDDLE* LAST
@@ -344,14 +344,19 @@ typedef struct lvkv_log_read_report {
  * without end", "missing start of fragmented record", "error in middle of
  * record", "unknown record type"). d_records[i] locates logical record i
  * (its fragments are consecutive physical records); d_reports[i] is the
- * i-th Reporter call. Two launches on `stream`, no host synchronisation;
- * totals in *d_read. */
+ * i-th Reporter call. initial_offset as log::Reader's (db/log_reader.cc:29-54,
+ * :80-89, :182-187, :261-266): reading starts at the block that can hold it,
+ * records that start before it are skipped, MIDDLE fragments and one LAST at
+ * the start are skipped (resync), and reports of bytes before it are not
+ * made; the physical outputs still cover the whole image. Asynchronous on
+ * `stream`, no host synchronisation; totals in *d_read. */
 int lvkv_log_read_device(const void* d_file, uint64_t file_size, uint64_t* d_hdr_offsets,
                          uint32_t* d_actual, uint8_t* d_rec_status, size_t capacity,
                          uint8_t* d_block_status, uint32_t* d_block_drop,
                          lvkv_log_report* d_report, lvkv_log_record* d_records,
                          size_t record_capacity, lvkv_log_corruption* d_reports,
-                         size_t report_capacity, lvkv_log_read_report* d_read, void* stream);
+                         size_t report_capacity, uint64_t initial_offset,
+                         lvkv_log_read_report* d_read, void* stream);
 
 /* ---- batched, host-resident (end-to-end incl. PCIe) ------------------- */
 /* Blocks live in host memory (pageable or pinned). The library packs them

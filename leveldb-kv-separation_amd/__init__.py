@@ -87,7 +87,8 @@ def _load() -> ctypes.CDLL:
     L.lvkv_log_fill_headers_device.restype = i32
     L.lvkv_log_verify_blocks_device.argtypes = [vp, u64, vp, vp, vp, sz, vp, vp, vp, vp]
     L.lvkv_log_verify_blocks_device.restype = i32
-    L.lvkv_log_read_device.argtypes = [vp, u64, vp, vp, vp, sz, vp, vp, vp, vp, sz, vp, sz, vp, vp]
+    L.lvkv_log_read_device.argtypes = [vp, u64, vp, vp, vp, sz, vp, vp, vp, vp, sz, vp, sz, u64,
+                                       vp, vp]
     L.lvkv_log_read_device.restype = i32
     L.lvkv_debug_set_sst_form.argtypes = [i32]
     L.lvkv_debug_set_sst_form.restype = i32
@@ -503,9 +504,10 @@ LOG_REASONS = {1: "checksum mismatch", 2: "bad record length",
                8: "unknown record type {}"}
 
 
-def log_read(file_buf, *, capacity: Optional[int] = None, record_capacity: Optional[int] = None,
-             report_capacity: Optional[int] = None, stream=None):
-    """log::Reader(reporter, checksum=True, initial_offset=0) over the log image
+def log_read(file_buf, *, initial_offset: int = 0, capacity: Optional[int] = None,
+             record_capacity: Optional[int] = None, report_capacity: Optional[int] = None,
+             stream=None):
+    """log::Reader(reporter, checksum=True, initial_offset) over the log image
     in `file_buf` (uint8 CUDA tensor), all on the device
     (lvkv_log_read_device): ReadRecord until it returns false.
 
@@ -516,6 +518,8 @@ def log_read(file_buf, *, capacity: Optional[int] = None, record_capacity: Optio
     Capacities default to sizes that always fit; a LVKV_LOG_CAPACITY result
     from smaller ones is returned as is."""
     import numpy as np
+    if initial_offset < 0:
+        raise ValueError("initial_offset must be >= 0")
     torch = _torch()
     dev = file_buf.device
     size = file_buf.numel()
@@ -538,7 +542,7 @@ def log_read(file_buf, *, capacity: Optional[int] = None, record_capacity: Optio
             _dev_ptr(hdr, "hdr"), _dev_ptr(actual, "actual"), _dev_ptr(rst, "rec_status"), cap,
             _dev_ptr(bst, "block_status"), _dev_ptr(bdrop, "block_drop"), _dev_ptr(rep, "report"),
             _dev_ptr(recs, "records"), rcap, _dev_ptr(reps, "reports"), pcap,
-            _dev_ptr(rd, "read"), _stream_handle(stream, dev))
+            int(initial_offset), _dev_ptr(rd, "read"), _stream_handle(stream, dev))
     _check("lvkv_log_read_device", rc)
     r = LogReport.from_buffer_copy(bytes(rep.cpu().numpy()))
     o = LogReadReport.from_buffer_copy(bytes(rd.cpu().numpy()))

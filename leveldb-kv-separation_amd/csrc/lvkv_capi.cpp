@@ -59,7 +59,7 @@ hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_o
 size_t log_scratch_bytes(uint64_t size);
 hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
                                const lvkv_log_report* phys, uint64_t size, uint32_t capacity,
-                               lvkv_log_record* recs, uint32_t rec_cap,
+                               uint64_t initial_offset, lvkv_log_record* recs, uint32_t rec_cap,
                                lvkv_log_corruption* reps, uint32_t rep_cap,
                                lvkv_log_read_report* out, void* scratch, hipStream_t stream);
 size_t log_asm_scratch_bytes(size_t max_items);
@@ -600,7 +600,8 @@ int lvkv_log_read_device(const void* d_file, uint64_t file_size, uint64_t* d_hdr
                          uint8_t* d_block_status, uint32_t* d_block_drop,
                          lvkv_log_report* d_report, lvkv_log_record* d_records,
                          size_t record_capacity, lvkv_log_corruption* d_reports,
-                         size_t report_capacity, lvkv_log_read_report* d_read, void* stream) {
+                         size_t report_capacity, uint64_t initial_offset,
+                         lvkv_log_read_report* d_read, void* stream) {
   if ((!d_file && file_size) || !d_hdr_offsets || !d_actual || !d_rec_status || !d_block_status ||
       !d_block_drop || !d_report || !d_read || (!d_records && record_capacity) ||
       (!d_reports && report_capacity) || capacity == 0 || capacity > kMaxBlocksPerLaunch ||
@@ -629,7 +630,7 @@ int lvkv_log_read_device(const void* d_file, uint64_t file_size, uint64_t* d_hdr
                           events, hs);
   if (e == hipSuccess)
     e = launch_log_assemble(events, d_hdr_offsets, d_report, file_size,
-                            static_cast<uint32_t>(capacity), d_records,
+                            static_cast<uint32_t>(capacity), initial_offset, d_records,
                             static_cast<uint32_t>(record_capacity), d_reports,
                             static_cast<uint32_t>(report_capacity), d_read, sb + asm_at, hs);
   return e == hipSuccess ? LVKV_OK : hip_fail(e);

@@ -1,5 +1,5 @@
-// log::Reader::ReadRecord (db/log_reader.cc:55-176, checksum = true,
-// initial_offset = 0) over a whole WAL / MANIFEST image on the device: the
+// log::Reader::ReadRecord (db/log_reader.cc:55-176, checksum = true, any
+// initial_offset) over a whole WAL / MANIFEST image on the device: the
 // logical records the reader returns (FULL, or FIRST MIDDLE* LAST) and every
 // Reporter::Corruption call, physical and logical, in the reader's order.
 //
@@ -25,8 +25,18 @@
 //   3. log_asm_emit (grid): the same chunk work again, now from the known
 //      starting state, writing records (LastRecordOffset from the verify's
 //      header offsets, loaded beside the events) and reports.
+//
+// An initial offset (log_reader.cc:29-54, :80-89, :182-187, :261-266) is
+// applied to the events as they are loaded: the blocks before the first one
+// the reader reads pass nothing on; in that block, records that start before
+// the offset become silent kBadRecords (kEvPre) and a physical report whose
+// header lies before the offset is dropped; and the reader starts in a
+// fourth state, resyncing (MIDDLE and one LAST consumed silently). A
+// one-wave launch first finds that block's candidates (log_asm_seek).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <algorithm>
 
 #include "crc32c_device_common.h"
 #include "lvkv_crc32c.h"
@@ -36,7 +46,7 @@ namespace lvkv {
 namespace {
 
 
-enum : uint32_t { kIdle = 0, kInFrag = 1, kStopped = 2, kUnknown = 3 };
+enum : uint32_t { kIdle = 0, kInFrag = 1, kStopped = 2, kUnknown = 3, kResync = 4 };
 
 // A run of events as a transformer of the reader's state.
 struct Summ {
@@ -69,7 +79,7 @@ __device__ __forceinline__ Summ compose(const Summ& x, const Summ& y) {
 
 // The reader's state while a chunk is replayed.
 struct Reader {
-  uint32_t st;       // kIdle / kInFrag / kStopped, or kUnknown (summaries)
+  uint32_t st;       // kIdle / kInFrag / kStopped / kResync, or kUnknown (summaries)
   uint32_t first;    // kInFrag: the fragment's FIRST
   uint64_t scratch;  // kInFrag (kUnknown: MIDDLE bytes so far)
   uint32_t stopped;  // a kEof-type header stopped the reader here
@@ -114,6 +124,8 @@ struct Sink {
 // One event (item `ev`; for a record its candidate index j and header offset
 // hoff) through ReadRecord's switch (log_reader.cc:86-166). kUnknown (the
 // summaries) emits nothing: a MIDDLE keeps it, any other event resolves it.
+// kResync (:80-89) acts as kIdle except that a MIDDLE is consumed silently
+// and a LAST silently ends it.
 template <bool kOut>
 __device__ __forceinline__ void step(Reader& r, uint32_t ev, uint32_t j, uint64_t hoff,
                                      Sink& out) {
@@ -126,7 +138,8 @@ __device__ __forceinline__ void step(Reader& r, uint32_t ev, uint32_t j, uint64_
       r.st = kStopped;
       return;
     }
-    // kBadRecord; ReadPhysicalRecord reported it first (:221-255)
+    // kBadRecord; ReadPhysicalRecord reported it first (:221-255); kEvPre /
+    // kEvZero: silently
     if (kOut && kind == kEvChecksum) out.report(n, LVKV_LOGR_CHECKSUM, 0);
     if (kOut && kind == kEvBadLength) out.report(n, LVKV_LOGR_BAD_LENGTH, 0);
     if (kOut && in) out.report(r.scratch, LVKV_LOGR_MIDDLE, 0);  // :145-151
@@ -150,7 +163,7 @@ __device__ __forceinline__ void step(Reader& r, uint32_t ev, uint32_t j, uint64_
     case 3:  // kMiddleType (:114-121)
       if (in || r.st == kUnknown) {
         r.scratch += n;
-      } else if (kOut) {
+      } else if (kOut && r.st == kIdle) {
         out.report(n, LVKV_LOGR_MISSING_1, 0);
       }
       break;
@@ -182,12 +195,39 @@ constexpr uint32_t kGT = 256;     // threads per workgroup of the grid launches
 
 __device__ __forceinline__ bool is_candidate(uint32_t ev) {
   const uint32_t kind = ev & 15u;
-  return kind == kEvRec || kind == kEvSkip;
+  return kind == kEvRec || kind == kEvSkip || kind == kEvPre;
+}
+
+// Where an initial offset puts the reader (log_asm_seek's result): block b0
+// is the first it reads; its candidates are [lo, hi).
+struct Seek {
+  uint64_t offset;     // initial_offset; 0: no transform
+  uint64_t b0;
+  uint64_t b0_end;     // file offset of b0's end (the end of its buffer)
+  const uint32_t* lohi;
+};
+
+// Item k (event ev) as a reader with an initial offset sees it.
+__device__ __forceinline__ uint32_t seek_event(const Seek& sk, const uint64_t* hdr_off, uint32_t k,
+                                               uint32_t ev) {
+  if (sk.offset == 0) return ev;
+  const uint32_t kind = ev & 15u;
+  const bool cand = kind == kEvRec || kind == kEvSkip;
+  const uint64_t lo = sk.lohi[0] + sk.b0, hi = sk.lohi[1] + sk.b0;
+  if (k < lo) return cand ? log_event(kEvSkip, 0, 0) : log_event(kEvNone, 0, 0);
+  if (k < hi) {  // b0's candidates: those before the offset are skipped silently
+    return kind == kEvRec && hdr_off[k - sk.b0] < sk.offset ? log_event(kEvPre, 0, 0) : ev;
+  }
+  if (k == hi && (kind == kEvChecksum || kind == kEvBadLength) &&
+      sk.b0_end - (ev >> 16) < sk.offset)  // ReportDrop's filter: header before the offset
+    return log_event(kEvZero, 0, 0);
+  return ev;
 }
 
 // The chunk's items [k0, k1) into registers (the rest "no event"). k0 is a
 // multiple of kChunk and the event array 16-byte aligned.
-__device__ __forceinline__ void load_chunk(const uint32_t* events, uint32_t k0, uint32_t k1,
+__device__ __forceinline__ void load_chunk(const uint32_t* events, const uint64_t* hdr_off,
+                                           const Seek& sk, uint32_t k0, uint32_t k1,
                                            uint32_t (&ev)[kChunk]) {
   const uint4 v = k0 < k1 ? reinterpret_cast<const uint4*>(events + k0)[0] : make_uint4(0, 0, 0, 0);
   ev[0] = v.x;
@@ -196,7 +236,7 @@ __device__ __forceinline__ void load_chunk(const uint32_t* events, uint32_t k0, 
   ev[3] = v.w;
 #pragma unroll
   for (uint32_t i = 0; i < kChunk; ++i)
-    if (k0 + i >= k1) ev[i] = log_event(kEvNone, 0, 0);
+    ev[i] = k0 + i >= k1 ? log_event(kEvNone, 0, 0) : seek_event(sk, hdr_off, k0 + i, ev[i]);
 }
 
 // The chunk through step(); hoff[c] = header offset of its c-th candidate.
@@ -214,11 +254,16 @@ __device__ __forceinline__ void replay(const uint32_t (&ev)[kChunk], const uint6
 constexpr Summ kIdentity = {1, kIdle, 0, 0, 0, 0, 0};  // no events
 
 // A starting state as the counts see it: idle, in a fragment with bytes,
-// in an empty fragment, stopped.
-enum : uint32_t { kScIdle = 0, kScFrag = 1, kScEmpty = 2, kScStopped = 3 };
+// in an empty fragment, resyncing, stopped.
+enum : uint32_t { kScIdle = 0, kScFrag = 1, kScEmpty = 2, kScResync = 3, kScStopped = 4 };
+constexpr uint32_t kScenarios = 4;  // the ones with counts
 
 __device__ __forceinline__ uint32_t scenario(uint32_t st, uint64_t scratch) {
-  return st == kIdle ? kScIdle : st == kStopped ? kScStopped : scratch != 0 ? kScFrag : kScEmpty;
+  return st == kIdle      ? kScIdle
+         : st == kStopped ? kScStopped
+         : st == kResync  ? kScResync
+         : scratch != 0   ? kScFrag
+                          : kScEmpty;
 }
 
 // A chunk's start given its workgroup's start (scenario sw) and the
@@ -233,12 +278,13 @@ __device__ __forceinline__ uint32_t chunk_scenario(uint32_t sw, const Summ& x) {
 struct Chunk {
   uint32_t ev[kChunk];
   Summ s;
-  uint32_t nrec[3], nrep[3];
+  uint32_t nrec[kScenarios], nrep[kScenarios];
 };
 
-__device__ __forceinline__ void chunk_of(const uint32_t* events, uint32_t K, uint32_t t, Chunk& c) {
+__device__ __forceinline__ void chunk_of(const uint32_t* events, const uint64_t* hdr_off,
+                                         const Seek& sk, uint32_t K, uint32_t t, Chunk& c) {
   const uint32_t k0 = t * kChunk;
-  load_chunk(events, k0, min(K, k0 + kChunk), c.ev);
+  load_chunk(events, hdr_off, sk, k0, min(K, k0 + kChunk), c.ev);
   uint64_t hz[kChunk];
 #pragma unroll
   for (uint32_t i = 0; i < kChunk; ++i) hz[i] = 0;
@@ -256,9 +302,10 @@ __device__ __forceinline__ void chunk_of(const uint32_t* events, uint32_t K, uin
   for (uint32_t i = 0; i < kChunk; ++i) n += is_candidate(c.ev[i]) ? 1u : 0u;
   c.s.nrec = n;
 #pragma unroll
-  for (uint32_t sc = 0; sc < 3; ++sc) {
+  for (uint32_t sc = 0; sc < kScenarios; ++sc) {
     Sink cnt = {false, 0, 0, 0, nullptr, 0, nullptr, 0};
-    Reader r = {sc == kScIdle ? kIdle : kInFrag, 0, sc == kScFrag ? 1u : 0u, 0, 0};
+    Reader r = {sc == kScIdle ? kIdle : sc == kScResync ? kResync : kInFrag, 0,
+                sc == kScFrag ? 1u : 0u, 0, 0};
     replay<true>(c.ev, hz, 0, r, cnt);
     c.nrec[sc] = cnt.nrec;
     c.nrep[sc] = cnt.nrep;
@@ -308,7 +355,7 @@ __device__ __forceinline__ void wg_sum_excl(uint32_t& a, uint32_t& b, uint32_t (
 
 struct WgAgg {  // log_asm_reduce -> log_asm_scan
   Summ s;
-  uint32_t nrec[3], nrep[3];  // from each starting scenario (kScIdle .. kScEmpty)
+  uint32_t nrec[kScenarios], nrep[kScenarios];  // from each starting scenario
 };
 struct WgIn {   // log_asm_scan -> log_asm_emit
   uint64_t scratch;  // the reader's state at the workgroup's start
@@ -324,6 +371,9 @@ struct AsmArgs {
   uint32_t nblocks;
   uint32_t rec_cap, rep_cap;
   uint32_t groups;  // workgroups of the grid launches
+  uint32_t init_st; // the reader's first state: kIdle, or kResync with an offset
+  Seek seek;
+  uint32_t* lohi;   // log_asm_seek's output (seek.lohi)
   lvkv_log_record* recs;
   lvkv_log_corruption* reps;
   lvkv_log_read_report* out;
@@ -336,6 +386,37 @@ __device__ __forceinline__ uint32_t asm_items(const AsmArgs& a) {
   return a.phys->status == LVKV_OK ? a.phys->count_ + a.nblocks : 0u;
 }
 
+// lower_bound(hdr_off[0, n), key) by one wave: a 64-way search, one round of
+// loads per factor of 64.
+__device__ uint32_t wave_lower_bound(const uint64_t* hdr_off, uint32_t n, uint64_t key,
+                                     uint32_t lane) {
+  uint32_t lo = 0, len = n;
+  while (len > 64) {
+    const uint32_t s = (len + 63) / 64;
+    const uint32_t idx = lo + (lane + 1) * s - 1;
+    const bool below = idx < lo + len && hdr_off[idx] < key;
+    const uint32_t c = __popcll(__ballot(below));  // segments wholly below: a prefix
+    const uint32_t nlo = lo + c * s;
+    len = nlo >= lo + len ? 0u : min(s, lo + len - nlo);
+    lo = nlo;
+  }
+  const bool below = lane < len && hdr_off[lo + lane] < key;
+  return lo + static_cast<uint32_t>(__popcll(__ballot(below)));
+}
+
+// The first block the reader reads (b0, log_reader.cc:33-54): its candidates
+// [lo, hi) among the verify's, which are in file order.
+__global__ void __launch_bounds__(64) log_asm_seek(AsmArgs a) {
+  const uint32_t lane = threadIdx.x;
+  const uint32_t n = a.phys->status == LVKV_OK ? a.phys->count_ : 0u;
+  const uint32_t lo = wave_lower_bound(a.hdr_off, n, a.seek.b0 * 32768ull, lane);
+  const uint32_t hi = wave_lower_bound(a.hdr_off, n, (a.seek.b0 + 1) * 32768ull, lane);
+  if (lane == 0) {
+    a.lohi[0] = lo;
+    a.lohi[1] = hi;
+  }
+}
+
 __global__ void __launch_bounds__(kGT) log_asm_reduce(AsmArgs a) {
   __shared__ Summ sm[2][kGT];
   __shared__ uint32_t cn[2][kGT][2];
@@ -343,11 +424,11 @@ __global__ void __launch_bounds__(kGT) log_asm_reduce(AsmArgs a) {
   const uint32_t K = asm_items(a);
   if (blockIdx.x * kGT * kChunk >= K) return;  // the whole workgroup
   Chunk c;
-  chunk_of(a.events, K, blockIdx.x * kGT + tid, c);
+  chunk_of(a.events, a.hdr_off, a.seek, K, blockIdx.x * kGT + tid, c);
   WgAgg agg;
   const Summ x = wg_scan_excl(c.s, sm, tid, &agg.s);
 #pragma unroll
-  for (uint32_t sw = 0; sw < 3; ++sw) {
+  for (uint32_t sw = 0; sw < kScenarios; ++sw) {
     const uint32_t sc = chunk_scenario(sw, x);
     uint32_t r = sc == kScStopped ? 0u : c.nrec[sc], p = sc == kScStopped ? 0u : c.nrep[sc];
     wg_sum_excl(r, p, cn, tid, &agg.nrec[sw], &agg.nrep[sw]);
@@ -384,7 +465,7 @@ __global__ void __launch_bounds__(kST, 1) log_asm_scan(AsmArgs a) {
   uint32_t nrec = 0, nrep = 0;
   Summ p = p0;
   for (uint32_t g = g0; g < g1; ++g) {
-    const uint32_t sc = p.pass ? kScIdle : scenario(p.c, p.scratch);
+    const uint32_t sc = scenario(p.pass ? a.init_st : p.c, p.pass ? 0 : p.scratch);
     if (sc != kScStopped) {
       nrec += a.aggs[g].nrec[sc];
       nrep += a.aggs[g].nrep[sc];
@@ -411,7 +492,7 @@ __global__ void __launch_bounds__(kST, 1) log_asm_scan(AsmArgs a) {
   p = p0;
   for (uint32_t g = g0; g < g1; ++g) {
     WgIn in;
-    in.st = p.pass ? kIdle : p.c;
+    in.st = p.pass ? a.init_st : p.c;
     in.first = p.first;
     in.scratch = p.pass ? 0 : p.scratch;
     in.j0 = p.nrec;
@@ -446,7 +527,7 @@ __global__ void __launch_bounds__(kGT) log_asm_emit(AsmArgs a) {
   if (blockIdx.x * kGT * kChunk >= K) return;  // the whole workgroup
   const WgIn in = a.ins[blockIdx.x];
   Chunk c;
-  chunk_of(a.events, K, blockIdx.x * kGT + tid, c);
+  chunk_of(a.events, a.hdr_off, a.seek, K, blockIdx.x * kGT + tid, c);
   Summ all;
   const Summ x = wg_scan_excl(c.s, sm, tid, &all);
   // this chunk's starting state
@@ -484,13 +565,13 @@ __global__ void __launch_bounds__(kGT) log_asm_emit(AsmArgs a) {
 
 size_t log_asm_scratch_bytes(size_t max_items) {
   const size_t groups = (max_items + kGT * kChunk - 1) / (kGT * kChunk);
-  return groups * (sizeof(WgAgg) + sizeof(WgIn)) + 16;
+  return groups * (sizeof(WgAgg) + sizeof(WgIn)) + 16;  // + log_asm_seek's two words
 }
 
 // `scratch`: log_asm_scratch_bytes(capacity + nblocks) bytes, 16-byte aligned.
 hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
                                const lvkv_log_report* phys, uint64_t size, uint32_t capacity,
-                               lvkv_log_record* recs, uint32_t rec_cap,
+                               uint64_t initial_offset, lvkv_log_record* recs, uint32_t rec_cap,
                                lvkv_log_corruption* reps, uint32_t rep_cap,
                                lvkv_log_read_report* out, void* scratch, hipStream_t stream) {
   AsmArgs a;
@@ -507,9 +588,22 @@ hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
   a.out = out;
   a.aggs = static_cast<WgAgg*>(scratch);
   a.ins = reinterpret_cast<WgIn*>(a.aggs + a.groups);
+  a.lohi = reinterpret_cast<uint32_t*>(a.ins + a.groups);
+  a.init_st = initial_offset ? kResync : kIdle;
+  a.seek.offset = initial_offset;
+  // SkipToInitialBlock (log_reader.cc:33-54): the block holding the offset,
+  // or the next one when the offset lies in the last 5 bytes (the trailer)
+  const uint64_t in_block = initial_offset % 32768;
+  a.seek.b0 = (initial_offset - in_block) / 32768 + (in_block > 32768 - 6 ? 1 : 0);
+  a.seek.b0_end = std::min<uint64_t>(size, (a.seek.b0 + 1) * 32768);
+  a.seek.lohi = a.lohi;
+  hipError_t e;
+  if (initial_offset) {
+    hipLaunchKernelGGL(log_asm_seek, dim3(1), dim3(64), 0, stream, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(log_asm_reduce, dim3(a.groups), dim3(kGT), 0, stream, a);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(log_asm_scan, dim3(1), dim3(kST), 0, stream, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(log_asm_emit, dim3(a.groups), dim3(kGT), 0, stream, a);

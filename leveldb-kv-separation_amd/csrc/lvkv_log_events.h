@@ -25,6 +25,9 @@ enum : uint32_t {
   kEvBadLength = 4, // kBadRecord, "bad record length" reported (:221-232)
   kEvZero = 5,      // kBadRecord, silent (zero-type zero-length, :234-240)
   kEvEof = 6,       // kEof: truncated record or header at the end (:206-213, :228)
+  // Written by the logical layer only, for a reader with an initial offset:
+  kEvPre = 7,       // a candidate that started before initial_offset: a silent
+                    // kBadRecord (:261-266)
 };
 
 __host__ __device__ inline uint32_t log_event(uint32_t kind, uint32_t type, uint32_t len) {

@@ -18,10 +18,11 @@
 //       exact Seek("filter." + policy->Name()), ReadFilter's ReadBlock.
 //   damage_wal.json  per case: the patches / truncation, then every
 //     Reporter::Corruption(bytes, status) of log::Reader(checksum = true,
-//     initial_offset = 0) (db/log_reader.cc) and every returned record
+//     the case's initial_offset) (db/log_reader.cc) and every returned record
 //     (LastRecordOffset, length, CRC32C of the contents).
 //   sst_alt_filter.sst / sst_two_filters.sst  small tables whose metaindex
 //     holds a filter key of another policy name, and two "filter." keys.
+#include <algorithm>
 #include <cinttypes>
 #include <cstdio>
 #include <cstdlib>
@@ -498,16 +499,18 @@ class RecordingReporter : public leveldb::log::Reader::Reporter {
 };
 
 void run_wal_case(FILE* j, bool first, const std::string& name, const std::string& base,
-                  const std::vector<Patch>& ps, size_t truncate_to) {
+                  const std::vector<Patch>& ps, size_t truncate_to, uint64_t initial_offset) {
   const std::string img = apply(base, ps, truncate_to);
-  std::fprintf(j, "%s    {\"name\": \"%s\", \"truncate_to\": %zu, \"patches\": [",
+  std::fprintf(j,
+               "%s    {\"name\": \"%s\", \"truncate_to\": %zu, \"initial_offset\": %" PRIu64
+               ", \"patches\": [",
                first ? "" : ",\n", name.c_str(),
-               truncate_to < base.size() ? truncate_to : base.size());
+               truncate_to < base.size() ? truncate_to : base.size(), initial_offset);
   for (size_t i = 0; i < ps.size(); ++i)
     std::fprintf(j, "%s[%" PRIu64 ", \"%s\"]", i ? ", " : "", ps[i].off, hex(ps[i].bytes).c_str());
   StringSequential src(&img);
   RecordingReporter rep;
-  leveldb::log::Reader r(&src, &rep, /*checksum=*/true, /*initial_offset=*/0);
+  leveldb::log::Reader r(&src, &rep, /*checksum=*/true, initial_offset);
   Slice rec;
   std::string scratch;
   std::fprintf(j, "], \"records\": [");
@@ -545,8 +548,9 @@ void write_wal_cases(const std::string& dir) {
                   "  \"cases\": [\n",
                hdrs.size());
   bool first = true;
-  auto add = [&](const std::string& name, const std::vector<Patch>& ps, size_t trunc = SIZE_MAX) {
-    run_wal_case(j, first, name, base, ps, trunc);
+  auto add = [&](const std::string& name, const std::vector<Patch>& ps, size_t trunc = SIZE_MAX,
+                 uint64_t initial = 0) {
+    run_wal_case(j, first, name, base, ps, trunc, initial);
     first = false;
   };
   auto flip = [&](uint64_t off, int x) { return Patch{off, byte_at(base, off, x)}; };
@@ -614,6 +618,64 @@ void write_wal_cases(const std::string& dir) {
       ps.push_back(flip(off, 1 + static_cast<int>(splitmix_next(&rs) % 255)));
     }
     add("random_" + std::to_string(c), ps);
+  }
+  // log::Reader's initial_offset (log_reader.cc:29-54, :80-89, :182-187,
+  // :261-266): the skip to the first block that can hold the record, the
+  // trailer rule, the resync over MIDDLE / LAST fragments at a block start,
+  // silent physical records before the offset, and ReportDrop's filter.
+  {
+    const uint64_t kB = leveldb::log::kBlockSize;
+    std::vector<uint64_t> offs = {1, kB - 7, kB - 6, kB - 5, kB, kB + 1, base.size(),
+                                  base.size() + 1, base.size() + 3 * kB};
+    for (size_t k = 0; k < hdrs.size(); ++k) {
+      offs.push_back(hdrs[k]);
+      offs.push_back(hdrs[k] + 1);
+      if (hdrs[k] > 0) offs.push_back(hdrs[k] - 1);
+    }
+    for (uint64_t b = 2; b * kB < base.size(); ++b) {
+      offs.push_back(b * kB);
+      offs.push_back(b * kB - 6);
+      offs.push_back(b * kB - 5);
+    }
+    std::sort(offs.begin(), offs.end());
+    offs.erase(std::unique(offs.begin(), offs.end()), offs.end());
+    for (uint64_t o : offs) add("offset_" + std::to_string(o), {}, SIZE_MAX, o);
+    // damage on either side of the offset, in the block the reader starts in
+    for (size_t k : {size_t{3}, size_t{4}, size_t{7}, size_t{9}, size_t{16}}) {
+      const uint64_t h = hdrs[k];
+      const std::string at = std::to_string(k);
+      for (uint64_t o : {h, h + 1, h > 0 ? h - 1 : h + 2}) {
+        const std::string sfx = "_" + at + "_from_" + std::to_string(o);
+        add("offset_crc_flip" + sfx, {flip(h + 1, 0x20)}, SIZE_MAX, o);
+        add("offset_length_grow" + sfx, {flip(h + 5, 0x40)}, SIZE_MAX, o);
+      }
+    }
+    for (uint64_t o : {uint64_t{16}, uint64_t{30}, uint64_t{5247}}) {
+      const std::string sfx = "_from_" + std::to_string(o);
+      add("offset_zero_record" + sfx, {{hdrs[3], std::string(7, '\0')}}, SIZE_MAX, o);
+      add("offset_crc_flip_2" + sfx, {flip(hdrs[2] + 1, 0x20)}, SIZE_MAX, o);
+    }
+    // retyped headers (CRC fixed) before, at and after the offset
+    auto retyped = [&](uint64_t h, int t) {
+      std::string img = base;
+      img[h + 6] = static_cast<char>(t);
+      const uint32_t len = static_cast<uint8_t>(img[h + 4]) |
+                           (static_cast<uint32_t>(static_cast<uint8_t>(img[h + 5])) << 8);
+      char c[4];
+      leveldb::EncodeFixed32(c,
+                             leveldb::crc32c::Mask(leveldb::crc32c::Value(img.data() + h + 6, 1 + len)));
+      return std::vector<Patch>{{h + 6, std::string(1, static_cast<char>(t))}, {h, std::string(c, 4)}};
+    };
+    for (size_t k : {size_t{2}, size_t{7}, size_t{9}, size_t{10}, size_t{16}})
+      for (int t : {0, 1, 2, 3, 4, 5, 6, 9})
+        for (uint64_t o : {hdrs[k], hdrs[k] + 1}) {
+          if (t == static_cast<uint8_t>(base[hdrs[k] + 6])) continue;
+          add("offset_retype_" + std::to_string(k) + "_to_" + std::to_string(t) + "_from_" +
+                  std::to_string(o),
+              retyped(hdrs[k], t), SIZE_MAX, o);
+        }
+    add("offset_truncated_mid_record", {}, hdrs[hdrs.size() - 2] + 20, hdrs[hdrs.size() - 3] + 1);
+    add("offset_truncated_block_edge", {}, kB + 5, kB);
   }
   std::fprintf(j, "\n  ]\n}\n");
   std::fclose(j);

@@ -3,7 +3,8 @@ record walk, the checker for lvkv_log_verify_blocks_device (SURVEY.md §8f
 row 2).
 
 Restates log::Reader::ReadPhysicalRecord (db/log_reader.cc:189-271) with
-checksum = true and initial_offset = 0 over a whole log image: 32 KiB reads
+checksum = true over a whole log image (initial_offset = 0; class Reader
+restates the whole reader with an initial offset): 32 KiB reads
 (db/log_format.h kBlockSize), the short-read EOF rule, the 7-byte header
 [masked crc u32][length u16][type u8] (kHeaderSize), "bad record length"
 (reported unless at EOF), the zero-type/zero-length skip (silent), "checksum
@@ -238,9 +239,150 @@ def assemble(img: bytes, events):
             return records, reports
 
 
-def read_records(img: bytes):
-    """log::Reader(checksum = true, initial_offset = 0) over the whole image."""
-    return assemble(img, physical_events(img))
+class Reader:
+    """log::Reader(file, reporter, checksum = true, initial_offset) as the
+    reference has it (db/log_reader.cc:18-271), statement by statement, over
+    an in-memory image whose Skip clamps at the end like a posix file: the
+    restatement the initial-offset paths are checked against (resync, the
+    trailer rule, ReportDrop's filter, physical records before the offset)."""
+
+    def __init__(self, img: bytes, initial_offset: int = 0):
+        self.img = img
+        self.pos = 0                       # SequentialFile position
+        self.buf = (0, 0)                  # buffer_ = img[buf[0]:buf[1]]
+        self.eof = False
+        self.last_record_offset = 0
+        self.end_of_buffer_offset = 0
+        self.initial_offset = initial_offset
+        self.resyncing = initial_offset > 0  # :29
+        self.reports = []
+        self.stopped5 = False              # a header of type kEof ended ReadRecord
+
+    def _bufsize(self):
+        return self.buf[1] - self.buf[0]
+
+    def _report_drop(self, nbytes, reason):  # :182-187 (unsigned arithmetic)
+        if (self.end_of_buffer_offset - self._bufsize() - nbytes) % (1 << 64) >= self.initial_offset:
+            self.reports.append((nbytes, reason))
+
+    def _skip_to_initial_block(self):  # :33-54
+        in_block = self.initial_offset % K_BLOCK
+        start = self.initial_offset - in_block
+        if in_block > K_BLOCK - 6:
+            start += K_BLOCK
+        self.end_of_buffer_offset = start
+        if start > 0:
+            self.pos = min(len(self.img), self.pos + start)
+        return True
+
+    def _read_physical(self):  # :189-271 -> (type, fragment offset, fragment length)
+        img = self.img
+        while True:
+            if self._bufsize() < K_HEADER:
+                if not self.eof:
+                    end = min(len(img), self.pos + K_BLOCK)
+                    self.buf = (self.pos, end)
+                    self.end_of_buffer_offset += end - self.pos
+                    if end - self.pos < K_BLOCK:
+                        self.eof = True
+                    self.pos = end
+                    continue
+                self.buf = (self.buf[1], self.buf[1])
+                return K_EOF, 0, 0
+            h = self.buf[0]
+            length = img[h + 4] | (img[h + 5] << 8)
+            rtype = img[h + 6]
+            if K_HEADER + length > self._bufsize():
+                drop = self._bufsize()
+                self.buf = (self.buf[1], self.buf[1])
+                if not self.eof:
+                    self._report_drop(drop, "bad record length")
+                    return K_BAD_RECORD, 0, 0
+                return K_EOF, 0, 0
+            if rtype == 0 and length == 0:
+                self.buf = (self.buf[1], self.buf[1])
+                return K_BAD_RECORD, 0, 0
+            expected = oracle.unmask(struct.unpack_from("<I", img, h)[0])
+            if oracle.value(img[h + 6: h + 7 + length]) != expected:
+                drop = self._bufsize()
+                self.buf = (self.buf[1], self.buf[1])
+                self._report_drop(drop, "checksum mismatch")
+                return K_BAD_RECORD, 0, 0
+            self.buf = (h + K_HEADER + length, self.buf[1])
+            if self.end_of_buffer_offset - self._bufsize() - K_HEADER - length < self.initial_offset:
+                return K_BAD_RECORD, 0, 0   # :261-266, an empty fragment
+            return rtype, h + K_HEADER, length
+
+    def read_record(self):  # :56-174 -> bytes, or None when it returns false
+        if self.last_record_offset < self.initial_offset:
+            if not self._skip_to_initial_block():
+                return None
+        scratch = b""
+        in_frag = False
+        prospective = 0
+        while True:
+            rtype, fo, flen = self._read_physical()
+            frag = self.img[fo: fo + flen]
+            physical = self.end_of_buffer_offset - self._bufsize() - K_HEADER - flen
+            if self.resyncing:                  # :80-89
+                if rtype == K_MIDDLE:
+                    continue
+                if rtype == K_LAST:
+                    self.resyncing = False
+                    continue
+                self.resyncing = False
+            if rtype == K_FULL:
+                if in_frag and scratch:
+                    self._report_drop(len(scratch), "partial record without end(1)")
+                self.last_record_offset = physical
+                return frag
+            if rtype == K_FIRST:
+                if in_frag and scratch:
+                    self._report_drop(len(scratch), "partial record without end(2)")
+                prospective, scratch, in_frag = physical, frag, True
+            elif rtype == K_MIDDLE:
+                if not in_frag:
+                    self._report_drop(len(frag), "missing start of fragmented record(1)")
+                else:
+                    scratch += frag
+            elif rtype == K_LAST:
+                if not in_frag:
+                    self._report_drop(len(frag), "missing start of fragmented record(2)")
+                else:
+                    scratch += frag
+                    self.last_record_offset = prospective
+                    return scratch
+            elif rtype == K_EOF:
+                # a real kEof, or a header whose own type byte is 5
+                self.stopped5 = fo != 0
+                return None
+            elif rtype == K_BAD_RECORD:
+                if in_frag:
+                    self._report_drop(len(scratch), "error in middle of record")
+                    in_frag, scratch = False, b""
+            else:
+                self._report_drop(len(frag) + (len(scratch) if in_frag else 0),
+                                  f"unknown record type {rtype}")
+                in_frag, scratch = False, b""
+
+
+def read_all(img: bytes, initial_offset: int = 0):
+    """log::Reader(checksum = true, initial_offset) over the whole image:
+    (LastRecordOffset, length, CRC32C of the contents) of every record
+    ReadRecord returns, every Reporter::Corruption(bytes, reason), and
+    whether a header of type kEof ended the reading."""
+    r = Reader(img, initial_offset)
+    records = []
+    while True:
+        rec = r.read_record()
+        if rec is None:
+            return records, r.reports, r.stopped5
+        records.append((r.last_record_offset, len(rec), oracle.value(rec)))
+
+
+def read_records(img: bytes, initial_offset: int = 0):
+    """read_all's records and reports."""
+    return read_all(img, initial_offset)[:2]
 
 
 def events_from_blocks(img: bytes, hdrs, rec_status, block_status, block_drop):

@@ -61,7 +61,9 @@ def test_oracle_sst_matches_reference(case):
 def test_oracle_wal_matches_reference(case):
     img = df.image(case, "wal.log")
     recs, reps = df.wal_expected(case)
-    assert lw.read_records(img) == (recs, reps)
+    assert lw.read_records(img, case["initial_offset"]) == (recs, reps)
+    if case["initial_offset"]:
+        return  # the block form below is the physical layer from offset 0
     v = lw.block_verdicts(img)
     ev = lw.events_from_blocks(img, v.hdrs, v.rec_status, v.block_status, v.block_drop)
     assert lw.assemble(img, ev) == (recs, reps)
@@ -95,6 +97,8 @@ def test_device_sst_matches_reference(lvkv, gpu, sst_form):
 def test_device_wal_matches_reference(lvkv, gpu):
     import torch
     for case in WAL_CASES:
+        if case["initial_offset"]:
+            continue  # the physical layer does not depend on it
         img = df.image(case, "wal.log")
         buf = torch.from_numpy(np.frombuffer(img, dtype=np.uint8).copy()).to(gpu)
         rep, hdr, actual, rst, bst, bdrop = lvkv.log_verify_blocks(buf)
@@ -122,12 +126,13 @@ def _device_log_records(img, records, hdrs):
 def test_device_log_read_matches_reference(lvkv, gpu):
     # The logical layer on the device (lvkv_log_read_device): records and
     # every Reporter call, against the reference's own log::Reader run on
-    # the same damaged images (oracle/gen_damage.cc).
+    # the same damaged images (oracle/gen_damage.cc), from offset 0 and from
+    # the cases' initial offsets.
     import torch
     for case in WAL_CASES:
         img = df.image(case, "wal.log")
         buf = torch.from_numpy(np.frombuffer(img, dtype=np.uint8).copy()).to(gpu)
-        rd, records, reports, phys = lvkv.log_read(buf)
+        rd, records, reports, phys = lvkv.log_read(buf, initial_offset=case["initial_offset"])
         torch.cuda.synchronize()
         assert rd["status"] == 0, case["name"]
         hdrs = [int(x) for x in phys[1].cpu().numpy()]
@@ -135,7 +140,10 @@ def test_device_log_read_matches_reference(lvkv, gpu):
         assert _device_log_records(img, records, hdrs) == want_recs, case["name"]
         assert reports == want_reps, case["name"]
         assert rd["bytes"] == sum(r[1] for r in want_recs), case["name"]
-        assert rd["stopped"] == int(case["name"].endswith("_to_eof")), case["name"]
+        stopped = lw.read_all(img, case["initial_offset"])[2]
+        assert rd["stopped"] == int(stopped), case["name"]
+        if not case["initial_offset"]:
+            assert stopped == case["name"].endswith("_to_eof"), case["name"]
 
 
 @pytest.mark.gpu
@@ -163,6 +171,17 @@ def test_device_log_read_large_and_capacity(lvkv, gpu):
         want_recs, want_reps = lw.read_records(img)
         assert _device_log_records(img, records, hdrs) == want_recs, trial
         assert reports == want_reps, trial
+        # from initial offsets: block starts (resync), the trailer rule,
+        # inside fragmented records, past the end
+        offs = [32768 * 3, 32768 * 7 - 5, 32768 * 7 - 6, len(img), len(img) + 40000]
+        offs += [int(h) + d for h in rng.choice(hdrs, 4, replace=False) for d in (0, 1)]
+        offs += [int(x) for x in rng.integers(1, len(img), 3)]
+        for off in offs:
+            rd, records, reports, phys = lvkv.log_read(buf, initial_offset=off)
+            o_recs, o_reps, stopped = lw.read_all(img, off)
+            assert _device_log_records(img, records, hdrs) == o_recs, (trial, off)
+            assert reports == o_reps, (trial, off)
+            assert rd["stopped"] == int(stopped), (trial, off)
     rd, records, reports, _ = lvkv.log_read(buf, record_capacity=5, report_capacity=1)
     assert rd["status"] == 1 and rd["nrecords"] == len(want_recs)
     assert rd["nreports"] == len(want_reps) and len(records) == 5

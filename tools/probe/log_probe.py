@@ -130,7 +130,7 @@ def main():
                                         vp(act.data_ptr()), vp(rst.data_ptr()), cap,
                                         vp(bst.data_ptr()), vp(bdr.data_ptr()), vp(rp.data_ptr()),
                                         vp(recs.data_ptr()), cap, vp(reps.data_ptr()), cap + nb,
-                                        vp(rd.data_ptr()), h)
+                                        0, vp(rd.data_ptr()), h)
             assert rc == 0
         for _ in range(5):
             read()
