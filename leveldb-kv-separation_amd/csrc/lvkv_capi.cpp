@@ -61,7 +61,8 @@ hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
                                const lvkv_log_report* phys, uint64_t size, uint32_t capacity,
                                uint64_t initial_offset, lvkv_log_record* recs, uint32_t rec_cap,
                                lvkv_log_corruption* reps, uint32_t rep_cap,
-                               lvkv_log_read_report* out, void* scratch, hipStream_t stream);
+                               lvkv_log_read_report* out, void* scratch, uint32_t* done,
+                               hipStream_t stream);
 size_t log_asm_scratch_bytes(size_t max_items);
 hipError_t launch_crc32c_long(const KernelArgs& args, const uint32_t* zpow,
                               const uint32_t* lane_cols, int num_groups, hipStream_t stream);
@@ -632,7 +633,10 @@ int lvkv_log_read_device(const void* d_file, uint64_t file_size, uint64_t* d_hdr
     e = launch_log_assemble(events, d_hdr_offsets, d_report, file_size,
                             static_cast<uint32_t>(capacity), initial_offset, d_records,
                             static_cast<uint32_t>(record_capacity), d_reports,
-                            static_cast<uint32_t>(report_capacity), d_read, sb + asm_at, hs);
+                            static_cast<uint32_t>(report_capacity), d_read, sb + asm_at,
+                            // the verify leaves scratch bytes 8-15 alone (zeroed
+                            // when allocated): the assembly's completion counter
+                            reinterpret_cast<uint32_t*>(sb + 8), hs);
   return e == hipSuccess ? LVKV_OK : hip_fail(e);
 }
 

@@ -13,16 +13,17 @@
 // other event resets the state the same way whatever came before, so the run
 // ends in a state of its own. That makes runs composable (Summ, compose),
 // and the work is reduce-then-scan over chunks of kChunk items, one chunk
-// per thread, in three launches:
+// per thread, in two launches:
 //
 //   1. log_asm_reduce (grid): every chunk's summary and its record / report
 //      counts for each state it may start in (idle; in a fragment with
-//      bytes; in an empty fragment); a workgroup scan of the summaries gives
-//      each chunk's start relative to its workgroup's, and the workgroup's
-//      aggregate (its summary and its counts for each starting state);
-//   2. log_asm_scan (one workgroup): the aggregates scanned: each
-//      workgroup's starting state, first candidate and output positions;
-//   3. log_asm_emit (grid): the same chunk work again, now from the known
+//      bytes; in an empty fragment; resyncing); a workgroup scan of the
+//      summaries gives each chunk's start relative to its workgroup's, and
+//      the workgroup's aggregate (its summary and its counts for each
+//      starting state). The last workgroup to finish (a completion counter
+//      it leaves at 0) scans the aggregates: each workgroup's starting
+//      state, first candidate and output positions, and the totals;
+//   2. log_asm_emit (grid): the same chunk work again, now from the known
 //      starting state, writing records (LastRecordOffset from the verify's
 //      header offsets, loaded beside the events) and reports.
 //
@@ -239,6 +240,16 @@ __device__ __forceinline__ void load_chunk(const uint32_t* events, const uint64_
     ev[i] = k0 + i >= k1 ? log_event(kEvNone, 0, 0) : seek_event(sk, hdr_off, k0 + i, ev[i]);
 }
 
+// v[i] for a run-time i by unrolled selects (no register array in scratch);
+// 0 when i >= N.
+template <typename T, uint32_t N>
+__device__ __forceinline__ T pick(const T (&v)[N], uint32_t i) {
+  T r = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < N; ++k) r = i == k ? v[k] : r;
+  return r;
+}
+
 // The chunk through step(); hoff[c] = header offset of its c-th candidate.
 template <bool kOut>
 __device__ __forceinline__ void replay(const uint32_t (&ev)[kChunk], const uint64_t (&hoff)[kChunk],
@@ -246,7 +257,7 @@ __device__ __forceinline__ void replay(const uint32_t (&ev)[kChunk], const uint6
   uint32_t c = 0;
 #pragma unroll
   for (uint32_t i = 0; i < kChunk; ++i) {
-    step<kOut>(r, ev[i], j0 + c, hoff[c], out);
+    step<kOut>(r, ev[i], j0 + c, pick(hoff, c), out);
     c += is_candidate(ev[i]) ? 1u : 0u;
   }
 }
@@ -281,6 +292,23 @@ struct Chunk {
   uint32_t nrec[kScenarios], nrep[kScenarios];
 };
 
+// A chunk's counts from starting scenario sc (kScStopped: none).
+__device__ __forceinline__ void chunk_counts(const uint32_t (&ev)[kChunk], uint32_t sc,
+                                             uint32_t* nrec, uint32_t* nrep) {
+  uint64_t hz[kChunk];
+#pragma unroll
+  for (uint32_t i = 0; i < kChunk; ++i) hz[i] = 0;
+  Sink cnt = {false, 0, 0, 0, nullptr, 0, nullptr, 0};
+  Reader r = {sc == kScIdle ? kIdle : sc == kScResync ? kResync : sc == kScStopped ? kStopped : kInFrag,
+              0, sc == kScFrag ? 1u : 0u, 0, 0};
+  replay<true>(ev, hz, 0, r, cnt);
+  *nrec = cnt.nrec;
+  *nrep = cnt.nrep;
+}
+
+// The chunk's events and summary; with kCounts, its counts from every
+// starting scenario too.
+template <bool kCounts>
 __device__ __forceinline__ void chunk_of(const uint32_t* events, const uint64_t* hdr_off,
                                          const Seek& sk, uint32_t K, uint32_t t, Chunk& c) {
   const uint32_t k0 = t * kChunk;
@@ -301,56 +329,90 @@ __device__ __forceinline__ void chunk_of(const uint32_t* events, const uint64_t*
 #pragma unroll
   for (uint32_t i = 0; i < kChunk; ++i) n += is_candidate(c.ev[i]) ? 1u : 0u;
   c.s.nrec = n;
+  if (kCounts) {
 #pragma unroll
-  for (uint32_t sc = 0; sc < kScenarios; ++sc) {
-    Sink cnt = {false, 0, 0, 0, nullptr, 0, nullptr, 0};
-    Reader r = {sc == kScIdle ? kIdle : sc == kScResync ? kResync : kInFrag, 0,
-                sc == kScFrag ? 1u : 0u, 0, 0};
-    replay<true>(c.ev, hz, 0, r, cnt);
-    c.nrec[sc] = cnt.nrec;
-    c.nrep[sc] = cnt.nrep;
+    for (uint32_t sc = 0; sc < kScenarios; ++sc) chunk_counts(c.ev, sc, &c.nrec[sc], &c.nrep[sc]);
   }
 }
 
-// Workgroup-wide exclusive scan of `s` under compose; *all = the aggregate.
-__device__ __forceinline__ Summ wg_scan_excl(Summ s, Summ (&sm)[2][kGT], uint32_t tid, Summ* all) {
-  uint32_t cur = 0;
-  sm[cur][tid] = s;
-  __syncthreads();
-  for (uint32_t d = 1; d < kGT; d <<= 1) {
-    if (tid >= d) s = compose(sm[cur][tid - d], s);
-    sm[cur ^ 1u][tid] = s;
-    cur ^= 1u;
-    __syncthreads();
-  }
-  *all = sm[cur][kGT - 1];
-  const Summ e = tid ? sm[cur][tid - 1] : kIdentity;
-  __syncthreads();  // sm is reused
-  return e;
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, uint32_t d) {
+  const uint32_t lo = __shfl_up(static_cast<uint32_t>(v), d, 64);
+  const uint32_t hi = __shfl_up(static_cast<uint32_t>(v >> 32), d, 64);
+  return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
-// Workgroup-wide exclusive sum of (a, b); *ta / *tb = the totals.
-__device__ __forceinline__ void wg_sum_excl(uint32_t& a, uint32_t& b, uint32_t (&cn)[2][kGT][2],
-                                            uint32_t tid, uint32_t* ta, uint32_t* tb) {
-  uint32_t x = a, y = b, cur = 0;
-  cn[cur][tid][0] = x;
-  cn[cur][tid][1] = y;
+__device__ __forceinline__ Summ shfl_up_summ(const Summ& x, uint32_t d) {
+  Summ r;
+  r.pass = __shfl_up(x.pass, d, 64);
+  r.c = __shfl_up(x.c, d, 64);
+  r.len = shfl_up64(x.len, d);
+  r.scratch = shfl_up64(x.scratch, d);
+  r.first = __shfl_up(x.first, d, 64);
+  r.nrec = __shfl_up(x.nrec, d, 64);
+  r.stop5 = __shfl_up(x.stop5, d, 64);
+  return r;
+}
+
+// Workgroup-wide exclusive scan of `s` under compose (kT threads): a shuffle
+// scan in each wave, then the waves' aggregates through LDS (two barriers);
+// *all = the aggregate.
+template <uint32_t kT>
+__device__ __forceinline__ Summ wg_scan_excl(Summ s, Summ (&wagg)[kT / 64], uint32_t tid,
+                                             Summ* all) {
+  const uint32_t lane = tid & 63u, w = tid >> 6;
+  Summ inc = s;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const Summ o = shfl_up_summ(inc, d);
+    if (lane >= d) inc = compose(o, inc);
+  }
+  Summ ex = shfl_up_summ(inc, 1);
+  if (lane == 0) ex = kIdentity;
+  if (lane == 63) wagg[w] = inc;
   __syncthreads();
-  for (uint32_t d = 1; d < kGT; d <<= 1) {
-    if (tid >= d) {
-      x += cn[cur][tid - d][0];
-      y += cn[cur][tid - d][1];
+  Summ pre = kIdentity, tot = kIdentity;
+  for (uint32_t v = 0; v < kT / 64; ++v) {
+    if (v == w) pre = tot;
+    tot = compose(tot, wagg[v]);
+  }
+  *all = tot;
+  __syncthreads();  // wagg is reused
+  return compose(pre, ex);
+}
+
+// Workgroup-wide exclusive sums of N counters per thread (kT threads), the
+// same way; tot[i] = the totals.
+template <uint32_t kT, uint32_t N>
+__device__ __forceinline__ void wg_sum_excl(uint32_t (&v)[N], uint32_t (&wsum)[kT / 64][N],
+                                            uint32_t tid, uint32_t (&tot)[N]) {
+  const uint32_t lane = tid & 63u, w = tid >> 6;
+  uint32_t inc[N];
+#pragma unroll
+  for (uint32_t i = 0; i < N; ++i) inc[i] = v[i];
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+#pragma unroll
+    for (uint32_t i = 0; i < N; ++i) {
+      const uint32_t o = __shfl_up(inc[i], d, 64);
+      if (lane >= d) inc[i] += o;
     }
-    cn[cur ^ 1u][tid][0] = x;
-    cn[cur ^ 1u][tid][1] = y;
-    cur ^= 1u;
-    __syncthreads();
   }
-  *ta = cn[cur][kGT - 1][0];
-  *tb = cn[cur][kGT - 1][1];
-  a = x - a;
-  b = y - b;
+  if (lane == 63) {
+#pragma unroll
+    for (uint32_t i = 0; i < N; ++i) wsum[w][i] = inc[i];
+  }
   __syncthreads();
+#pragma unroll
+  for (uint32_t i = 0; i < N; ++i) {
+    uint32_t pre = 0, all = 0;
+    for (uint32_t u = 0; u < kT / 64; ++u) {
+      if (u < w) pre += wsum[u][i];
+      all += wsum[u][i];
+    }
+    v[i] = pre + inc[i] - v[i];
+    tot[i] = all;
+  }
+  __syncthreads();  // wsum is reused
 }
 
 struct WgAgg {  // log_asm_reduce -> log_asm_scan
@@ -374,6 +436,7 @@ struct AsmArgs {
   uint32_t init_st; // the reader's first state: kIdle, or kResync with an offset
   Seek seek;
   uint32_t* lohi;   // log_asm_seek's output (seek.lohi)
+  uint32_t* done;   // log_asm_reduce's completion counter (0 between calls)
   lvkv_log_record* recs;
   lvkv_log_corruption* reps;
   lvkv_log_read_report* out;
@@ -417,78 +480,38 @@ __global__ void __launch_bounds__(64) log_asm_seek(AsmArgs a) {
   }
 }
 
-__global__ void __launch_bounds__(kGT) log_asm_reduce(AsmArgs a) {
-  __shared__ Summ sm[2][kGT];
-  __shared__ uint32_t cn[2][kGT][2];
-  const uint32_t tid = threadIdx.x;
-  const uint32_t K = asm_items(a);
-  if (blockIdx.x * kGT * kChunk >= K) return;  // the whole workgroup
-  Chunk c;
-  chunk_of(a.events, a.hdr_off, a.seek, K, blockIdx.x * kGT + tid, c);
-  WgAgg agg;
-  const Summ x = wg_scan_excl(c.s, sm, tid, &agg.s);
-#pragma unroll
-  for (uint32_t sw = 0; sw < kScenarios; ++sw) {
-    const uint32_t sc = chunk_scenario(sw, x);
-    uint32_t r = sc == kScStopped ? 0u : c.nrec[sc], p = sc == kScStopped ? 0u : c.nrep[sc];
-    wg_sum_excl(r, p, cn, tid, &agg.nrec[sw], &agg.nrep[sw]);
-  }
-  if (tid == 0) a.aggs[blockIdx.x] = agg;
-}
-
-constexpr uint32_t kST = 1024;  // threads of log_asm_scan
-
-__global__ void __launch_bounds__(kST, 1) log_asm_scan(AsmArgs a) {
-  __shared__ Summ sm[2][kST];
-  __shared__ Summ tot;
-  __shared__ uint32_t cn[2][kST][2];
-  const uint32_t tid = threadIdx.x;
+// The aggregates of log_asm_reduce's G workgroups scanned by one workgroup of
+// kST threads: each workgroup's WgIn, and the totals into *a.out.
+template <uint32_t kST>
+__device__ __forceinline__ void asm_scan(const AsmArgs& a, Summ (&wagg)[kST / 64],
+                                         uint32_t (&wsum)[kST / 64][2], uint32_t tid) {
   const uint32_t K = asm_items(a);
   const uint32_t G = min(a.groups, (K + kGT * kChunk - 1) / (kGT * kChunk));
   const uint32_t per = (G + kST - 1) / kST;
   const uint32_t g0 = min(G, tid * per), g1 = min(G, g0 + per);
+  // this thread's first (with G <= kST its only) aggregate stays in registers
+  WgAgg mine = {};
+  if (g0 < g1) mine = a.aggs[g0];
+  auto agg_at = [&](uint32_t g) -> WgAgg { return g == g0 ? mine : a.aggs[g]; };
   // 1. this thread's run of aggregates, composed; scanned across threads
   Summ s = kIdentity;
-  for (uint32_t g = g0; g < g1; ++g) s = compose(s, a.aggs[g].s);
-  uint32_t cur = 0;
-  sm[cur][tid] = s;
-  __syncthreads();
-  for (uint32_t d = 1; d < kST; d <<= 1) {
-    if (tid >= d) s = compose(sm[cur][tid - d], s);
-    sm[cur ^ 1u][tid] = s;
-    cur ^= 1u;
-    __syncthreads();
-  }
-  if (tid == kST - 1) tot = s;
-  const Summ p0 = tid ? sm[cur][tid - 1] : kIdentity;
+  for (uint32_t g = g0; g < g1; ++g) s = compose(s, agg_at(g).s);
+  Summ tot;
+  const Summ p0 = wg_scan_excl<kST>(s, wagg, tid, &tot);
   // 2. each workgroup's counts from its starting state; output positions
   uint32_t nrec = 0, nrep = 0;
   Summ p = p0;
   for (uint32_t g = g0; g < g1; ++g) {
     const uint32_t sc = scenario(p.pass ? a.init_st : p.c, p.pass ? 0 : p.scratch);
-    if (sc != kScStopped) {
-      nrec += a.aggs[g].nrec[sc];
-      nrep += a.aggs[g].nrep[sc];
-    }
-    p = compose(p, a.aggs[g].s);
+    const WgAgg ag = agg_at(g);
+    nrec += pick(ag.nrec, sc);  // 0 when stopped
+    nrep += pick(ag.nrep, sc);
+    p = compose(p, ag.s);
   }
-  uint32_t r0 = nrec, r1 = nrep;
-  cur = 0;
-  __syncthreads();
-  cn[cur][tid][0] = r0;
-  cn[cur][tid][1] = r1;
-  __syncthreads();
-  for (uint32_t d = 1; d < kST; d <<= 1) {
-    if (tid >= d) {
-      r0 += cn[cur][tid - d][0];
-      r1 += cn[cur][tid - d][1];
-    }
-    cn[cur ^ 1u][tid][0] = r0;
-    cn[cur ^ 1u][tid][1] = r1;
-    cur ^= 1u;
-    __syncthreads();
-  }
-  uint32_t rb = r0 - nrec, pb = r1 - nrep;
+  uint32_t base[2] = {nrec, nrep}, all[2];
+  wg_sum_excl<kST>(base, wsum, tid, all);
+  const uint32_t r0 = all[0], r1 = all[1];  // totals
+  uint32_t rb = base[0], pb = base[1];
   p = p0;
   for (uint32_t g = g0; g < g1; ++g) {
     WgIn in;
@@ -501,13 +524,12 @@ __global__ void __launch_bounds__(kST, 1) log_asm_scan(AsmArgs a) {
     in.pad_ = 0;
     a.ins[g] = in;
     const uint32_t sc = scenario(in.st, in.scratch);
-    if (sc != kScStopped) {
-      rb += a.aggs[g].nrec[sc];
-      pb += a.aggs[g].nrep[sc];
-    }
-    p = compose(p, a.aggs[g].s);
+    const WgAgg ag = agg_at(g);
+    rb += pick(ag.nrec, sc);
+    pb += pick(ag.nrep, sc);
+    p = compose(p, ag.s);
   }
-  if (tid == kST - 1) {
+  if (tid == 0) {
     lvkv_log_read_report o;
     o.status = (a.phys->status != LVKV_OK || r0 > a.rec_cap || r1 > a.rep_cap) ? LVKV_LOG_CAPACITY
                                                                                 : LVKV_OK;
@@ -519,17 +541,58 @@ __global__ void __launch_bounds__(kST, 1) log_asm_scan(AsmArgs a) {
   }
 }
 
+__global__ void __launch_bounds__(kGT) log_asm_reduce(AsmArgs a) {
+  __shared__ Summ wagg[kGT / 64];
+  __shared__ uint32_t wsum[kGT / 64][2 * kScenarios];
+  __shared__ uint32_t wsum2[kGT / 64][2];
+  __shared__ uint32_t last;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t K = asm_items(a);
+  // workgroups with items (at least one, which writes the report)
+  const uint32_t G = max(1u, min(a.groups, (K + kGT * kChunk - 1) / (kGT * kChunk)));
+  if (blockIdx.x >= G) return;  // the whole workgroup
+  Chunk c;
+  chunk_of<true>(a.events, a.hdr_off, a.seek, K, blockIdx.x * kGT + tid, c);
+  WgAgg agg;
+  const Summ x = wg_scan_excl<kGT>(c.s, wagg, tid, &agg.s);
+  // the workgroup's counts from each starting scenario, summed in one scan
+  uint32_t v[2 * kScenarios], tot[2 * kScenarios];
+#pragma unroll
+  for (uint32_t sw = 0; sw < kScenarios; ++sw) {
+    const uint32_t sc = chunk_scenario(sw, x);
+    v[2 * sw] = pick(c.nrec, sc);  // 0 when stopped
+    v[2 * sw + 1] = pick(c.nrep, sc);
+  }
+  wg_sum_excl<kGT>(v, wsum, tid, tot);
+#pragma unroll
+  for (uint32_t sw = 0; sw < kScenarios; ++sw) {
+    agg.nrec[sw] = tot[2 * sw];
+    agg.nrep[sw] = tot[2 * sw + 1];
+  }
+  if (tid == 0) {
+    a.aggs[blockIdx.x] = agg;
+    const uint32_t n = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_ACQ_REL,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    last = n == G - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!last) return;
+  asm_scan<kGT>(a, wagg, wsum2, tid);
+  // the next call on this stream reuses the counter
+  if (tid == 0) __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ void __launch_bounds__(kGT) log_asm_emit(AsmArgs a) {
-  __shared__ Summ sm[2][kGT];
-  __shared__ uint32_t cn[2][kGT][2];
+  __shared__ Summ wagg[kGT / 64];
+  __shared__ uint32_t wsum[kGT / 64][2];
   const uint32_t tid = threadIdx.x;
   const uint32_t K = asm_items(a);
   if (blockIdx.x * kGT * kChunk >= K) return;  // the whole workgroup
   const WgIn in = a.ins[blockIdx.x];
   Chunk c;
-  chunk_of(a.events, a.hdr_off, a.seek, K, blockIdx.x * kGT + tid, c);
+  chunk_of<false>(a.events, a.hdr_off, a.seek, K, blockIdx.x * kGT + tid, c);
   Summ all;
-  const Summ x = wg_scan_excl(c.s, sm, tid, &all);
+  const Summ x = wg_scan_excl<kGT>(c.s, wagg, tid, &all);
   // this chunk's starting state
   const uint32_t sw = scenario(in.st, in.scratch);
   Reader r = {in.st, in.first, in.scratch, 0, 0};
@@ -541,11 +604,10 @@ __global__ void __launch_bounds__(kGT) log_asm_emit(AsmArgs a) {
     r.scratch += x.len;
   }
   const uint32_t sc = chunk_scenario(sw, x);
-  uint32_t rb = sc == kScStopped ? 0u : c.nrec[sc], pb = sc == kScStopped ? 0u : c.nrep[sc];
-  uint32_t tr, tp;
-  wg_sum_excl(rb, pb, cn, tid, &tr, &tp);
-  rb += in.rec_base;
-  pb += in.rep_base;
+  uint32_t v[2], t[2];  // this chunk's counts from its known start (0 when stopped)
+  chunk_counts(c.ev, sc, &v[0], &v[1]);
+  wg_sum_excl<kGT>(v, wsum, tid, t);
+  const uint32_t rb = v[0] + in.rec_base, pb = v[1] + in.rep_base;
   const uint32_t j0 = in.j0 + x.nrec;
   uint64_t hoff[kChunk];
 #pragma unroll
@@ -568,12 +630,15 @@ size_t log_asm_scratch_bytes(size_t max_items) {
   return groups * (sizeof(WgAgg) + sizeof(WgIn)) + 16;  // + log_asm_seek's two words
 }
 
-// `scratch`: log_asm_scratch_bytes(capacity + nblocks) bytes, 16-byte aligned.
+// `scratch`: log_asm_scratch_bytes(capacity + nblocks) bytes, 16-byte aligned;
+// `done`: a u32 that is 0 (zeroed once; every call leaves it at 0), used by
+// calls on this stream only.
 hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
                                const lvkv_log_report* phys, uint64_t size, uint32_t capacity,
                                uint64_t initial_offset, lvkv_log_record* recs, uint32_t rec_cap,
                                lvkv_log_corruption* reps, uint32_t rep_cap,
-                               lvkv_log_read_report* out, void* scratch, hipStream_t stream) {
+                               lvkv_log_read_report* out, void* scratch, uint32_t* done,
+                               hipStream_t stream) {
   AsmArgs a;
   a.events = events;
   a.hdr_off = hdr_off;
@@ -589,6 +654,7 @@ hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
   a.aggs = static_cast<WgAgg*>(scratch);
   a.ins = reinterpret_cast<WgIn*>(a.aggs + a.groups);
   a.lohi = reinterpret_cast<uint32_t*>(a.ins + a.groups);
+  a.done = done;
   a.init_st = initial_offset ? kResync : kIdle;
   a.seek.offset = initial_offset;
   // SkipToInitialBlock (log_reader.cc:33-54): the block holding the offset,
@@ -603,8 +669,6 @@ hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   hipLaunchKernelGGL(log_asm_reduce, dim3(a.groups), dim3(kGT), 0, stream, a);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(log_asm_scan, dim3(1), dim3(kST), 0, stream, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(log_asm_emit, dim3(a.groups), dim3(kGT), 0, stream, a);
   return hipGetLastError();
