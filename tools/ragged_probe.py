@@ -58,6 +58,7 @@ def main():
     res = {}
     for name in args.cases.split(","):
         n, length, stride, first = CASES[name]
+        want = None
         if stride == 0:
             lens = np.random.default_rng(first).integers(0, length, n).astype(np.uint32)
             offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64))]).astype(np.uint64)
@@ -81,8 +82,9 @@ def main():
             torch.cuda.synchronize()
             if host is None:
                 host = data.cpu().numpy()
-            if k == int(args.kernels.split(",")[0]):
+            if want is None:
                 want = oracle.batch(host, offs, lens, None, threads=8)
+            if True:  # every kernel against the oracle
                 assert np.array_equal(out.cpu().numpy().view(np.uint32), want), (name, k)
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
