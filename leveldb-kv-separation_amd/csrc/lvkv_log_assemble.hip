@@ -415,11 +415,11 @@ __device__ __forceinline__ void wg_sum_excl(uint32_t (&v)[N], uint32_t (&wsum)[k
   __syncthreads();  // wsum is reused
 }
 
-struct WgAgg {  // log_asm_reduce -> log_asm_scan
+struct WgAgg {  // log_asm_reduce -> its last workgroup (asm_scan)
   Summ s;
   uint32_t nrec[kScenarios], nrep[kScenarios];  // from each starting scenario
 };
-struct WgIn {   // log_asm_scan -> log_asm_emit
+struct WgIn {   // asm_scan -> log_asm_emit
   uint64_t scratch;  // the reader's state at the workgroup's start
   uint32_t st, first;
   uint32_t j0;       // candidates before it
