@@ -18,6 +18,12 @@ read different windows of a >= 1.25 GiB rotation, so every batch is cold in
 the 256 MiB Infinity Cache; consecutive batches overlap on the device (the
 engine's queues), as in a checksum service with batches in flight.
 
+Ranks: one process per GPU. Under torch.distributed.run (WORLD_SIZE set) the
+launcher's ranks are used and must number --gpus; `python bench.py --gpus N`
+without a launcher starts the N ranks itself (a torch.distributed.run child
+process, before any GPU call). Config 5 below 1 GiB per slice keeps several
+copies of the slice per rank and rotates over them (MALL-cold every step).
+
 Timed region (every config, every rank; `timed_region`): time-based warm-up
 (>= --warmup-ms and >= W steps), barrier, synchronize, t0, K steps, engine
 wait, synchronize, t1, barrier; elapsed = max over ranks of t1 - t0 (common
@@ -89,7 +95,9 @@ def _load_shard():
 
 class Comm:
     """Barrier and max-over-ranks on the process group (RCCL on the GPU box,
-    gloo in the CPU tests); no-ops at world 1."""
+    gloo in the CPU tests); no-ops at world 1. `device` is where the max's
+    one-element tensor lives: the rank's GPU under RCCL, None (host) under
+    gloo."""
 
     def __init__(self, world: int, device=None):
         self.world = world
@@ -153,6 +161,7 @@ def split_measure(make_runner, comm: Comm, rank: int, world: int, steps: int, wa
     value = total * block * steps / elapsed / GIB
     rec = {"workload": CONFIGS["blocks1m_split"][4], "total_blocks": total,
            "block_bytes": block, "ranks": world, "slice_blocks_rank0": shard.shard_range(total, 0, world)[1],
+           "slice_copies": getattr(runner, "nrot", 1),
            "steps": steps, "ms_per_step": round(elapsed / steps * 1e3, 5),
            "value": round(value, 4), "unit": "GiB/s",
            "pct_hbm_peak_per_gpu": round(100.0 * value * GIB / 1e9 / HBM_PEAK_GBS / world, 2),
@@ -347,10 +356,32 @@ def main():
     ap.add_argument("--isolated", type=int, default=0,
                     help="only run N ordered (one-at-a-time) launches and exit: the "
                          "command a rocprofv3 kernel trace of the roofline kernel wraps")
+    ap.add_argument("--split-total", type=int, default=SPLIT_TOTAL,
+                    help="blocks of the config-5 batch (1M; smaller only for plumbing tests)")
+    ap.add_argument("--plumbing-cpu", action="store_true",
+                    help="test only: gloo process group and the library's per-call CPU "
+                         "CRC in place of the device (no GPU touched); exercises the "
+                         "--gpus launch, the slicing and the timed region")
     args = ap.parse_args()
 
-    import torch
+    # --gpus N > 1 outside a launcher: start one rank per GPU here, before
+    # anything touches the GPU, as a child torch.distributed.run (never an
+    # exec), and exit with its status.
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(_launch_ranks(args.gpus))
     world, rank, local = dist_env()
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started {world} rank(s)")
+
+    import torch
+    warm_s = args.warmup_ms / 1e3
+    import __graft_entry__ as g
+    lvkv = g.load_package()
+
+    if args.plumbing_cpu:
+        _plumbing_cpu(args, lvkv, world, rank, warm_s)
+        return
+
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if world > 1:
@@ -358,18 +389,14 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     comm = Comm(world, dev)
 
-    import __graft_entry__ as g
-    lvkv = g.load_package()
-    warm_s = args.warmup_ms / 1e3
-
     if args.config == "blocks1m_split":
         eng = lvkv.Engine(local)
         runner, rec = split_measure(
             lambda s, c: _split_runner(torch, lvkv, eng, dev, rank, s, c), comm, rank, world,
-            args.steps, args.warmup, warm_s)
+            args.steps, args.warmup, warm_s, total=args.split_total)
         if rank == 0:
             line = _line_base(args, world, rec["value"], rec["ms_per_step"] / 1e3,
-                              {"workload": rec["workload"], "total_blocks": SPLIT_TOTAL,
+                              {"workload": rec["workload"], "total_blocks": args.split_total,
                                "block_bytes": BLOCK,
                                "parallelism": f"{world} contiguous slices (no collective)"})
             line["split"] = rec
@@ -448,7 +475,7 @@ def main():
         torch.cuda.empty_cache()
         split_runner, split = split_measure(
             lambda s, c: _split_runner(torch, lvkv, eng, dev, rank, s, c), comm, rank, world,
-            min(args.steps, 20), 2, warm_s)
+            min(args.steps, 20), 2, warm_s, total=args.split_total)
         del split_runner
         torch.cuda.empty_cache()
 
@@ -467,14 +494,22 @@ def main():
     _end(world)
 
 
+SPLIT_ROTATE_BYTES = 1 << 30  # a rank's slice copies span at least this much
+
+
 def _split_runner(torch, lvkv, eng, dev, rank, start, count):
     """This rank's slice [start, start + count) of the config-5 batch,
-    resident in its HBM, checksummed through the engine."""
+    resident in its HBM, checksummed through the engine. Below 1 GiB per
+    slice (4+ ranks) the rank holds several copies of its slice and steps
+    rotate over them, so every step reads its slice cold from HBM (2x the
+    256 MiB Infinity Cache would still be half warm)."""
+    slice_bytes = max(count, 1) * BLOCK
+    nrot = max(1, -(-SPLIT_ROTATE_BYTES // slice_bytes))
     gen = torch.Generator(device=dev).manual_seed(0x5EED + start)
-    buf = torch.randint(0, 256, (max(count, 1) * BLOCK,), dtype=torch.uint8, device=dev,
+    buf = torch.randint(0, 256, (nrot * slice_bytes,), dtype=torch.uint8, device=dev,
                         generator=gen)
     outs = [torch.empty(max(count, 1), dtype=torch.int32, device=dev) for _ in range(2)]
-    r = EngineRunner(lvkv, eng, buf, count, BLOCK, BLOCK, 0, 1, 0, outs)
+    r = EngineRunner(lvkv, eng, buf, count, BLOCK, BLOCK, 0, nrot, slice_bytes, outs)
     r.step(0)
     r.finish()
     r.sync()
@@ -482,6 +517,70 @@ def _split_runner(torch, lvkv, eng, dev, rank, start, count):
         parity_check(buf, outs[0], count, BLOCK, BLOCK, 0, rank, "split")
     r.buf = buf
     return r
+
+
+def _launch_ranks(n: int) -> int:
+    """One process per GPU: this script again under torch.distributed.run
+    (rendezvous on 127.0.0.1), as a child process; returns its exit status."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", f"--master-port={port}",
+           str(Path(__file__).resolve()), *sys.argv[1:]]
+    log(f"bench: --gpus {n}: launching {n} ranks: {' '.join(cmd)}")
+    return subprocess.run(cmd).returncode
+
+
+class CpuPlumbingRunner:
+    """Test-only stand-in for the engine (--plumbing-cpu): the library's
+    per-call CPU CRC32C (lvkv_crc32c_value, the drop-in symbol) over this
+    rank's slice, so a CPU-only run exercises the rank launch, the slicing and
+    the timed region end to end. Never a measured line."""
+
+    def __init__(self, lvkv, start, count):
+        self.value = lvkv.Value
+        data = np.frombuffer(np.random.default_rng(start).bytes(max(count, 1) * BLOCK), np.uint8)
+        self.blocks = [data[i * BLOCK:(i + 1) * BLOCK].tobytes() for i in range(count)]
+        self.count = count
+        self.crc = None
+
+    def step(self, i):
+        self.crc = [self.value(b) for b in self.blocks]
+
+    def finish(self):
+        pass
+
+    def sync(self):
+        pass
+
+
+def _plumbing_cpu(args, lvkv, world, rank, warm_s):
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    comm = Comm(world, None)
+    runner, rec = split_measure(lambda s, c: CpuPlumbingRunner(lvkv, s, c), comm, rank, world,
+                                args.steps, args.warmup, warm_s, total=args.split_total)
+    counts = [runner.count]
+    if world > 1:
+        import torch.distributed as dist
+        gathered = [None] * world
+        dist.all_gather_object(gathered, runner.count)
+        counts = gathered
+    if rank == 0:
+        line = _line_base(args, world, rec["value"], rec["ms_per_step"] / 1e3,
+                          {"workload": "plumbing test (CPU per-call CRC, not a measurement)",
+                           "total_blocks": args.split_total, "block_bytes": BLOCK,
+                           "parallelism": f"{world} contiguous slices (no collective)"})
+        line["split"] = rec
+        line["rank_counts"] = counts
+        line["data"] = "plumbing-cpu: NOT a device measurement"
+        print(json.dumps(line), flush=True)
+    _end(world)
 
 
 def _line_base(args, world, value, sec_per_step, config):

@@ -127,3 +127,41 @@ def test_gloo_world2_split_bench(total, slow_rank):
     assert rec["ms_per_step"] >= 20.0
     assert rec["value"] == pytest.approx(total * 4096 / (rec["ms_per_step"] * 1e-3) / 2**30,
                                          rel=1e-3, abs=1e-3)
+
+
+def _bench(args, env_extra=None, timeout=240):
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, str(REPO / "bench.py"), *args], env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, (json.loads(lines[-1]) if lines else None), p.stderr
+
+
+def test_bench_gpus2_launches_two_ranks():
+    """`bench.py --gpus 2` with no launcher around it starts two ranks itself
+    (torch.distributed.run child, before any GPU call) and the line reports
+    both: n_gpus, the split's ranks and each rank's slice."""
+    rc, line, err = _bench(["--gpus", "2", "--plumbing-cpu", "--config", "blocks1m_split",
+                            "--split-total", "65", "--steps", "3", "--warmup", "1",
+                            "--warmup-ms", "0"])
+    assert rc == 0, err[-2000:]
+    assert line["n_gpus"] == 2
+    assert line["split"]["ranks"] == 2 and line["split"]["total_blocks"] == 65
+    assert line["rank_counts"] == [33, 32]
+
+
+def test_bench_refuses_world_mismatch():
+    """A launcher that started a different number of ranks than --gpus asks
+    for is an error, not a one-GPU line."""
+    rc, line, err = _bench(["--gpus", "2", "--plumbing-cpu", "--config", "blocks1m_split",
+                            "--split-total", "8", "--steps", "1", "--warmup", "1",
+                            "--warmup-ms", "0"],
+                           env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc != 0 and line is None
+    assert "--gpus 2" in err
