@@ -61,6 +61,13 @@ int lvkv_engine_set_priority(struct lvkv_engine* engine, int priority);
  * groups x waves x 8 u64, lvkv_engine_shape). NULL turns it off. */
 int lvkv_engine_set_stamps(struct lvkv_engine* engine, uint64_t* d_stamps, uint64_t areas);
 
+/* The no-hang contract under test: stall = 1 blocks every queue of the
+ * engine behind a barrier packet that waits on a signal only stall = 0
+ * releases (as a faulted or endless dispatch would); every engine wait gives
+ * up after stuck_seconds without progress (default 60) and returns
+ * LVKV_ERR_HIP, after which the engine refuses work. */
+int lvkv_debug_engine_stall(struct lvkv_engine* engine, int stall, double stuck_seconds);
+
 #ifdef __cplusplus
 }
 #endif

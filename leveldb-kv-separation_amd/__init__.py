@@ -114,6 +114,8 @@ def _load() -> ctypes.CDLL:
     L.lvkv_engine_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_double), sz]
     L.lvkv_engine_profile_read.restype = ctypes.c_long
+    L.lvkv_debug_engine_stall.argtypes = [vp, i32, ctypes.c_double]
+    L.lvkv_debug_engine_stall.restype = i32
     L.lvkv_strerror.argtypes = [i32]
     L.lvkv_strerror.restype = ctypes.c_char_p
     L.lvkv_last_hip_error.argtypes = []
@@ -612,6 +614,10 @@ class Engine:
         self.handle = h
         # the raw entry, for callers that pass pointers themselves (bench.py)
         self.submit_ptr = _lib.lvkv_engine_crc32c_uniform
+        # inputs and outputs of submitted batches, held until the wait() that
+        # covers them: the engine reads and writes them outside any torch
+        # stream, so the caching allocator must not hand their memory out
+        self._inflight = []
 
     def crc32c_uniform(self, buf, nblocks: int, length: int, stride: Optional[int] = None, *,
                        init: int = 0, mask: bool = False, ordered: bool = False,
@@ -631,10 +637,12 @@ class Engine:
             self.handle, _dev_ptr(buf, "buf", (torch.uint8, torch.int8)), stride, length,
             init & 0xFFFFFFFF, _dev_ptr(out, "out", (torch.int32,), nblocks), nblocks, flags)
         _check("lvkv_engine_crc32c_uniform", rc)
+        self._inflight.append((buf, out))
         return out
 
     def wait(self) -> None:
         _check("lvkv_engine_wait", _lib.lvkv_engine_wait(self.handle))
+        self._inflight.clear()
 
     def queues(self, n: int = 0) -> int:
         r = int(_lib.lvkv_engine_queues(self.handle, n))

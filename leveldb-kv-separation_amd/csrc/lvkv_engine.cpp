@@ -24,9 +24,11 @@
 //   * kernargs live in VRAM, written through the PCIe BAR, then an HDP flush
 //     (the path HIP's device kernargs take); a ring of kSlots slots, and a
 //     slot is reused only after a fence covering its previous dispatch;
-//   * the first dispatch of every submit acquires at agent scope (inputs other
-//     agents wrote and released are seen); the rest of a submit's dispatches
-//     acquire nothing; no dispatch releases;
+//   * every dispatch acquires at agent scope (inputs other agents wrote and
+//     released are seen; LVKV_FLAG_SYSTEM_ACQUIRE: system scope, for input a
+//     copy engine wrote into a reused buffer), each on its own queue, since a
+//     submit's dispatches rotate over queues and run side by side; no
+//     dispatch releases;
 //   * lvkv_engine_wait (and the slot-reuse fence) puts a barrier-AND packet on
 //     every queue in use, acquire and release at system scope: results are
 //     visible to the host, to HIP streams and to copy engines after it.
@@ -38,6 +40,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <mutex>
@@ -217,6 +220,9 @@ struct Engine {
   uint32_t zcol[32];
   std::mutex mu;
   volatile int queue_error = 0;
+  double stuck_s = 60.0;     // a wait gives up after this long without progress
+  hsa_signal_t hold_sig{};   // lvkv_debug_engine_stall: queues blocked on it
+  bool hold_ok = false;
 };
 
 namespace {
@@ -256,6 +262,7 @@ void destroy(Engine* e) {
     if (q) hsa_queue_destroy(q);
   for (uint32_t i = 0; i < e->nprof_sig; ++i) hsa_signal_destroy(e->prof_sig[i]);
   if (e->fence_ok) hsa_signal_destroy(e->fence_sig);
+  if (e->hold_ok) hsa_signal_destroy(e->hold_sig);
   if (e->kernarg) {
     if (e->kernarg_vram)
       hsa_amd_memory_pool_free(e->kernarg);
@@ -382,11 +389,55 @@ int create(int device, Engine** out) {
   return LVKV_OK;
 }
 
-// Next free packet of queue e.cur (the caller holds e.mu).
+// A wait the engine gives up on: the device never hangs the caller. A
+// queue error (the runtime's callback sets queue_error) ends every wait at
+// once; a signal that does not move for e.stuck_s (60 s) marks the engine broken
+// (queue_error = kStuck) and every later call returns LVKV_ERR_HIP.
+constexpr int kStuck = -1;
+
+double now_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return static_cast<double>(ts.tv_sec) + 1e-9 * static_cast<double>(ts.tv_nsec);
+}
+
+// Waits until `sig` < 1; false on a queue error or a stuck device.
+bool wait_signal(Engine& e, hsa_signal_t sig) {
+  // short active waits (a completion is normally µs away), each bounded so
+  // the error flag and the deadline are re-checked
+  const uint64_t hint = e.tick_us > 0 ? static_cast<uint64_t>(1000.0 / e.tick_us) : 1000000;
+  double deadline = 0;
+  for (;;) {
+    if (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, hint, HSA_WAIT_STATE_ACTIVE) < 1)
+      return true;
+    if (e.queue_error) return false;
+    const double t = now_s();
+    if (deadline == 0) {
+      deadline = t + e.stuck_s;
+    } else if (t > deadline) {
+      e.queue_error = kStuck;
+      return false;
+    }
+  }
+}
+
+// Next free packet of queue e.cur (the caller holds e.mu); nullptr when the
+// queue faulted or never drains.
 void* packet_slot(Engine& e, uint64_t* idx) {
   hsa_queue_t* q = e.queues[e.cur];
   *idx = hsa_queue_add_write_index_screlease(q, 1);
-  while (*idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {
+  double deadline = 0;
+  for (uint64_t spin = 0; *idx - hsa_queue_load_read_index_scacquire(q) >= q->size; ++spin) {
+    if (e.queue_error) return nullptr;
+    if ((spin & 1023u) == 1023u) {
+      const double t = now_s();
+      if (deadline == 0) {
+        deadline = t + e.stuck_s;
+      } else if (t > deadline) {
+        e.queue_error = kStuck;
+        return nullptr;
+      }
+    }
   }
   return static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address) + (*idx & (q->size - 1));
 }
@@ -401,8 +452,10 @@ void publish(Engine& e, void* p, uint16_t header, uint16_t setup, uint64_t idx) 
 // Reads the finished profiled dispatch of signal slot s into the log.
 void collect_profile(Engine& e, uint32_t s) {
   if (!e.prof_pending[s]) return;
-  hsa_signal_wait_scacquire(e.prof_sig[s], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
-                            HSA_WAIT_STATE_ACTIVE);
+  if (!wait_signal(e, e.prof_sig[s])) {
+    e.prof_pending[s] = false;
+    return;
+  }
   hsa_amd_profiling_dispatch_time_t t{};
   const hsa_status_t st = hsa_amd_profiling_get_dispatch_time(e.agent, e.prof_sig[s], &t);
   if (st == HSA_STATUS_SUCCESS) {
@@ -416,14 +469,20 @@ void collect_profile(Engine& e, uint32_t s) {
 // A barrier-AND packet with the barrier bit on every queue in use: each
 // completes after every earlier packet of its queue and releases at system
 // scope (the results visible to the host and to copy engines); then wait for
-// all of them. Caller holds e.mu.
-void fence(Engine& e) {
+// all of them. Caller holds e.mu. LVKV_ERR_HIP if a queue faulted or the
+// device stopped (the wait ends instead of spinning forever).
+int fence(Engine& e) {
+  if (e.queue_error) return LVKV_ERR_HIP;
   hsa_signal_store_relaxed(e.fence_sig, e.nq);
   const int keep = e.cur;
   for (int q = 0; q < e.nq; ++q) {
     e.cur = q;
     uint64_t idx;
     hsa_barrier_and_packet_t* p = static_cast<hsa_barrier_and_packet_t*>(packet_slot(e, &idx));
+    if (p == nullptr) {
+      e.cur = keep;
+      return LVKV_ERR_HIP;
+    }
     p->reserved0 = 0;
     p->reserved1 = 0;
     for (int i = 0; i < 5; ++i) p->dep_signal[i].handle = 0;
@@ -437,12 +496,12 @@ void fence(Engine& e) {
     publish(e, p, header, 0, idx);
   }
   e.cur = keep;
-  hsa_signal_wait_scacquire(e.fence_sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
-                            HSA_WAIT_STATE_ACTIVE);
+  if (!wait_signal(e, e.fence_sig)) return LVKV_ERR_HIP;
   e.fenced = e.next;
   // oldest first: dispatch n used slot n % kProfSlots
   for (uint32_t i = 0; i < kProfSlots; ++i)
     collect_profile(e, static_cast<uint32_t>((e.next + i) % kProfSlots));
+  return e.queue_error ? LVKV_ERR_HIP : LVKV_OK;
 }
 
 // One kernel-dispatch packet; the caller holds e.mu.
@@ -451,7 +510,7 @@ int dispatch(Engine& e, const EngineKernel& k, const UniformArgs& args, bool acq
   if (e.queue_error) return LVKV_ERR_HIP;
   const uint64_t n = e.next;
   // Kernarg slot n % kSlots was last used by dispatch n - kSlots.
-  if (n - e.fenced >= kSlots) fence(e);
+  if (n - e.fenced >= kSlots && fence(e) != LVKV_OK) return LVKV_ERR_HIP;
   e.cur = static_cast<int>(n % static_cast<uint64_t>(e.nq));
   hsa_signal_t done{};
   if (e.profiling) {
@@ -473,6 +532,7 @@ int dispatch(Engine& e, const EngineKernel& k, const UniformArgs& args, bool acq
   }
   uint64_t idx;
   hsa_kernel_dispatch_packet_t* p = static_cast<hsa_kernel_dispatch_packet_t*>(packet_slot(e, &idx));
+  if (p == nullptr) return LVKV_ERR_HIP;
   const uint32_t wg = 64u * k.waves;
   p->workgroup_size_x = static_cast<uint16_t>(wg);
   p->workgroup_size_y = 1;
@@ -535,7 +595,7 @@ int lvkv_engine_crc32c_uniform(lvkv_engine* eng, const void* d_base, uint64_t st
   // An ordered batch runs alone: the other queues drain first (the barrier
   // bit orders a packet only within its own queue), and it gets the kernel
   // shaped for the whole chip.
-  if (ordered && e->nq > 1 && e->fenced != e->next) fence(*e);
+  if (ordered && e->nq > 1 && e->fenced != e->next && fence(*e) != LVKV_OK) return LVKV_ERR_HIP;
   const int v = ordered ? e->ordered_variant : e->variant;
   const EngineKernel& k = (e->probe_on && ordered != e->probe_overlapped) ? e->probe
                           : e->stamps                ? e->kern_stamps[v]
@@ -568,7 +628,9 @@ int lvkv_engine_crc32c_uniform(lvkv_engine* eng, const void* d_base, uint64_t st
       const uint64_t area = groups * k.waves * 8;
       a.stamps = e->stamps + (e->stamp_next++ % e->stamp_areas) * area;
     }
-    const int rc = dispatch(*e, k, a, /*acquire=*/i == 0, /*barrier=*/ordered,
+    // every dispatch acquires: they rotate over queues, so dispatch i > 0
+    // may start before (or during) dispatch 0's acquire on another queue
+    const int rc = dispatch(*e, k, a, /*acquire=*/true, /*barrier=*/ordered,
                             (flags & LVKV_FLAG_SYSTEM_ACQUIRE) != 0);
     if (rc != LVKV_OK) return rc;
     done += n;
@@ -580,7 +642,7 @@ int lvkv_engine_wait(lvkv_engine* eng) {
   if (eng == nullptr) return LVKV_ERR_INVALID;
   Engine* e = reinterpret_cast<Engine*>(eng);
   std::lock_guard<std::mutex> lk(e->mu);
-  if (e->fenced != e->next) fence(*e);
+  if (e->fenced != e->next && fence(*e) != LVKV_OK) return LVKV_ERR_HIP;
   return e->queue_error ? LVKV_ERR_HIP : LVKV_OK;
 }
 
@@ -589,7 +651,7 @@ int lvkv_engine_queues(lvkv_engine* eng, int nq) {
   Engine* e = reinterpret_cast<Engine*>(eng);
   std::lock_guard<std::mutex> lk(e->mu);
   if (nq == 0) return e->nq;
-  if (e->fenced != e->next) fence(*e);
+  if (e->fenced != e->next && fence(*e) != LVKV_OK) return LVKV_ERR_HIP;
   e->nq = nq;
   return nq;
 }
@@ -598,7 +660,7 @@ int lvkv_engine_profile(lvkv_engine* eng, int enable) {
   if (eng == nullptr) return LVKV_ERR_INVALID;
   Engine* e = reinterpret_cast<Engine*>(eng);
   std::lock_guard<std::mutex> lk(e->mu);
-  if (e->fenced != e->next) fence(*e);
+  if (e->fenced != e->next && fence(*e) != LVKV_OK) return LVKV_ERR_HIP;
   e->profiling = enable != 0;
   e->prof_count = 0;
   return LVKV_OK;
@@ -609,7 +671,7 @@ long lvkv_engine_profile_read(lvkv_engine* eng, double* start_us, double* end_us
     return LVKV_ERR_INVALID;
   Engine* e = reinterpret_cast<Engine*>(eng);
   std::lock_guard<std::mutex> lk(e->mu);
-  if (e->fenced != e->next) fence(*e);
+  if (e->fenced != e->next && fence(*e) != LVKV_OK) return LVKV_ERR_HIP;
   const uint64_t have = std::min<uint64_t>(e->prof_count, kProfLog);
   const uint64_t take = std::min<uint64_t>(have, n);
   for (uint64_t i = 0; i < take; ++i) {
@@ -625,7 +687,7 @@ int lvkv_engine_set_stamps(lvkv_engine* eng, uint64_t* d_stamps, uint64_t areas)
   if (eng == nullptr || (d_stamps != nullptr && areas == 0)) return LVKV_ERR_INVALID;
   Engine* e = reinterpret_cast<Engine*>(eng);
   std::lock_guard<std::mutex> lk(e->mu);
-  if (e->fenced != e->next) fence(*e);
+  if (e->fenced != e->next && fence(*e) != LVKV_OK) return LVKV_ERR_HIP;
   e->stamps = d_stamps;
   e->stamp_areas = areas;
   e->stamp_next = 0;
@@ -638,7 +700,7 @@ int lvkv_engine_set_variant(lvkv_engine* eng, int variant, int ordered_variant) 
     return LVKV_ERR_INVALID;
   Engine* e = reinterpret_cast<Engine*>(eng);
   std::lock_guard<std::mutex> lk(e->mu);
-  if (e->fenced != e->next) fence(*e);
+  if (e->fenced != e->next && fence(*e) != LVKV_OK) return LVKV_ERR_HIP;
   e->variant = variant;
   e->ordered_variant = ordered_variant;
   return LVKV_OK;
@@ -650,7 +712,7 @@ int lvkv_engine_load_probe(lvkv_engine* eng, const void* code_object, size_t siz
   if (eng == nullptr) return LVKV_ERR_INVALID;
   Engine* e = reinterpret_cast<Engine*>(eng);
   std::lock_guard<std::mutex> lk(e->mu);
-  if (e->fenced != e->next) fence(*e);
+  if (e->fenced != e->next && fence(*e) != LVKV_OK) return LVKV_ERR_HIP;
   drop_probe(*e);
   if (code_object == nullptr) return LVKV_OK;
   if (kernel == nullptr || waves == 0 || waves > 16 || chains == 0 || per_cu == 0)
@@ -684,7 +746,7 @@ int lvkv_engine_set_scopes(lvkv_engine* eng, int dispatch_acquire, int fence_acq
     if (v < HSA_FENCE_SCOPE_NONE || v > HSA_FENCE_SCOPE_SYSTEM) return LVKV_ERR_INVALID;
   Engine* e = reinterpret_cast<Engine*>(eng);
   std::lock_guard<std::mutex> lk(e->mu);
-  if (e->fenced != e->next) fence(*e);
+  if (e->fenced != e->next && fence(*e) != LVKV_OK) return LVKV_ERR_HIP;
   e->dispatch_acq = dispatch_acquire;
   e->fence_acq = fence_acquire;
   e->fence_rel = fence_release;
@@ -695,11 +757,51 @@ int lvkv_engine_set_priority(lvkv_engine* eng, int priority) {
   if (eng == nullptr || priority < 0 || priority > 2) return LVKV_ERR_INVALID;
   Engine* e = reinterpret_cast<Engine*>(eng);
   std::lock_guard<std::mutex> lk(e->mu);
-  if (e->fenced != e->next) fence(*e);
+  if (e->fenced != e->next && fence(*e) != LVKV_OK) return LVKV_ERR_HIP;
   for (hsa_queue_t* q : e->queues)
     if (hsa_amd_queue_set_priority(q, static_cast<hsa_amd_queue_priority_t>(priority)) !=
         HSA_STATUS_SUCCESS)
       return LVKV_ERR_HIP;
+  return LVKV_OK;
+}
+
+int lvkv_debug_engine_stall(lvkv_engine* eng, int stall, double stuck_seconds) {
+  if (eng == nullptr || stuck_seconds <= 0) return LVKV_ERR_INVALID;
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  std::lock_guard<std::mutex> lk(e->mu);
+  e->stuck_s = stuck_seconds;
+  if (!stall) {
+    if (e->hold_ok) hsa_signal_store_screlease(e->hold_sig, 0);
+    return LVKV_OK;
+  }
+  if (!e->hold_ok) {
+    if (hsa_signal_create(1, 0, nullptr, &e->hold_sig) != HSA_STATUS_SUCCESS) return LVKV_ERR_HIP;
+    e->hold_ok = true;
+  }
+  hsa_signal_store_screlease(e->hold_sig, 1);
+  // a barrier-AND packet on every queue that waits for the hold signal: the
+  // queues stop behind it as they would behind a faulted or endless kernel
+  const int keep = e->cur;
+  for (int q = 0; q < e->nq; ++q) {
+    e->cur = q;
+    uint64_t idx;
+    hsa_barrier_and_packet_t* p = static_cast<hsa_barrier_and_packet_t*>(packet_slot(*e, &idx));
+    if (p == nullptr) {
+      e->cur = keep;
+      return LVKV_ERR_HIP;
+    }
+    p->reserved0 = 0;
+    p->reserved1 = 0;
+    for (int i = 0; i < 5; ++i) p->dep_signal[i].handle = 0;
+    p->dep_signal[0] = e->hold_sig;
+    p->reserved2 = 0;
+    p->completion_signal.handle = 0;
+    publish(*e, p,
+            static_cast<uint16_t>((HSA_PACKET_TYPE_BARRIER_AND << HSA_PACKET_HEADER_TYPE) |
+                                  (1 << HSA_PACKET_HEADER_BARRIER)),
+            0, idx);
+  }
+  e->cur = keep;
   return LVKV_OK;
 }
 

@@ -76,23 +76,53 @@ __device__ __forceinline__ uint8_t walk_positions(const uint8_t* blk, uint32_t n
   // written to pos[] 64 at a time: no per-step masked LDS store
   uint32_t held = 0;
   const uint32_t lane = threadIdx.x & 63u;
-  while (n - p >= kLogHeader) {
-    // bytes p + 4 .. p + 6 (length, type) from the two aligned dwords around
-    // them (one ds_read2), a 64-bit funnel shift on the scalar unit
-    const uint32_t x = p + 4;
-    const uint32_t* d = reinterpret_cast<const uint32_t*>(blk + (x & ~3u));
-    const uint32_t lo = __builtin_amdgcn_readfirstlane(d[0]);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane(d[1]);
-    w = static_cast<uint32_t>(((static_cast<uint64_t>(hi) << 32) | lo) >> (8u * (x & 3u)));
-    length = w & 0xffffu;
-    // a bad length (:221-232) or a zero record (:234-240) ends the walk
-    if (kLogHeader + length > n - p) break;
-    if ((w & 0xffffffu) == 0) break;
-    held = lane == (k & 63u) ? p : held;
-    ++k;
-    if ((k & 63u) == 0) pos[k - 64u + lane] = static_cast<uint16_t>(held);
-    p += kLogHeader + length;
+  // Every lane carries the same p in a VGPR, so the chain from one header to
+  // the next is VALU + one LDS round trip (no readfirstlane, no scalar
+  // funnel shift): the dwords holding bytes p + 4 .. p + 6 are (p & ~3) + 4
+  // and + 8, the bytes shifted out by v_alignbyte(p & 3). The next header's
+  // read is issued before this header's stop test (speculatively, clamped
+  // into the buffer), so the test's compare and branch overlap the LDS trip.
+  // The reads are inline asm so the compiler neither sinks the speculative
+  // one below the branch nor turns the chain scalar; their registers are
+  // tied to explicit lgkmcnt waits (an asm load's destination is written
+  // late, so it must stay live until a wait has seen it land).
+  if (n >= kLogHeader) {
+    const uint32_t base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(blk));
+    uint64_t cur, nxt;
+    // bp = base + p (the buffer is 16-byte aligned, so bp & 3 == p & 3): the
+    // next read's address is two VALU ops from the length. A read past the
+    // block (a bad length, about to stop the walk) lands elsewhere in LDS or
+    // past the allocation (zeros): harmless, its bytes are never used.
+    uint32_t bp = base;
+    asm volatile("ds_read2_b32 %0, %1 offset0:1 offset1:2" : "=v"(cur) : "v"(base));
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur));
+    for (;;) {
+      w = __builtin_amdgcn_alignbyte(static_cast<uint32_t>(cur >> 32), static_cast<uint32_t>(cur),
+                                     bp & 3u);
+      length = w & 0xffffu;
+      const uint32_t nbp = bp + kLogHeader + length;
+      asm volatile("ds_read2_b32 %0, %1 offset0:1 offset1:2" : "=v"(nxt) : "v"(nbp & ~3u));
+      const uint32_t np = p + kLogHeader + length;
+      __builtin_amdgcn_sched_barrier(0);  // the read issues before the tests below
+      // a bad length (:221-232) or a zero record (:234-240) ends the walk
+      // (bit 0); bit 1: the record ends within 7 bytes of the block end
+      const bool bad = np > n || (w & 0xffffffu) == 0;
+      const uint32_t f =
+          __builtin_amdgcn_readfirstlane((bad ? 1u : 0u) | (n - np < kLogHeader ? 2u : 0u));
+      if (f & 1u) break;
+      held = lane == (k & 63u) ? p : held;
+      ++k;
+      if (__builtin_expect((k & 63u) == 0, 0)) pos[k - 64u + lane] = static_cast<uint16_t>(held);
+      p = np;
+      bp = nbp;
+      if (f & 2u) break;
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nxt));
+      cur = nxt;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nxt));
   }
+  p = __builtin_amdgcn_readfirstlane(p);
+  length = __builtin_amdgcn_readfirstlane(length);
   if (lane < (k & 63u)) pos[(k & ~63u) + lane] = static_cast<uint16_t>(held);
   uint8_t v;
   if (n - p < kLogHeader)
@@ -106,7 +136,7 @@ __device__ __forceinline__ uint8_t walk_positions(const uint8_t* blk, uint32_t n
   return v;
 }
 
-constexpr int kVW = 8;  // waves per workgroup
+constexpr int kVW = 16;  // waves per workgroup
 constexpr uint32_t kVThreads = 64 * kVW;
 constexpr uint32_t kMaxRecs = (static_cast<uint32_t>(kLogBlock) + kLogHeader - 1) / kLogHeader;
 constexpr uint32_t kLongRec = 16 * 256;  // CRC bytes walked by one wave, at most

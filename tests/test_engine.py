@@ -124,3 +124,30 @@ def test_engine_reads_a_reused_buffer_after_a_host_copy(oracle, eng, gpu):
     assert np.array_equal(again.cpu().numpy().view(np.uint32),
                           oracle.uniform(host, nb, L, threads=8))
     assert not torch.equal(first, again)
+
+
+def test_engine_wait_gives_up_on_a_stuck_queue(lvkv, gpu):
+    """The no-hang contract (SURVEY.md §8(b) Errors): queues blocked behind a
+    packet that never completes (lvkv_debug_engine_stall, as a faulted or
+    endless dispatch would block them) make wait() return LVKV_ERR_HIP after
+    the stuck timeout instead of spinning forever; the engine then refuses
+    work, and closes cleanly once the queues drain."""
+    import time
+
+    import torch
+    e = lvkv.Engine(gpu)
+    try:
+        buf = _data(torch, gpu, 64 * 4096, 11)
+        assert lvkv.lib.lvkv_debug_engine_stall(e.handle, 1, 1.0) == 0
+        e.crc32c_uniform(buf, 64, 4096)  # queued behind the stall
+        t0 = time.perf_counter()
+        with pytest.raises(lvkv.LvkvError):
+            e.wait()
+        assert 0.9 < time.perf_counter() - t0 < 30
+        with pytest.raises(lvkv.LvkvError):
+            e.crc32c_uniform(buf, 64, 4096)
+    finally:
+        lvkv.lib.lvkv_debug_engine_stall(e.handle, 0, 60.0)
+        time.sleep(0.2)
+        e._inflight.clear()
+        e.close()
