@@ -28,6 +28,7 @@ LIB_PATH = Path(__file__).resolve().parent / "liblvkv_crc32c.so"
 kMaskDelta = 0xA282EAD8  # util/crc32c.h:22
 
 LVKV_OK = 0
+LVKV_ERR_INVALID = -1
 LVKV_FLAG_MASK = 1
 LVKV_FLAG_ORDERED = 2
 LVKV_FLAG_SYSTEM_ACQUIRE = 4

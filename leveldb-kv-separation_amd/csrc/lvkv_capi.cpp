@@ -56,7 +56,7 @@ hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_o
                              uint8_t* block_status, uint32_t* block_drop, lvkv_log_report* r,
                              const uint32_t* zpow, const uint32_t* lane_cols, int cus,
                              void* scratch, uint32_t* events, hipStream_t stream);
-size_t log_scratch_bytes(uint64_t size);
+size_t log_scratch_bytes(uint64_t size, uint32_t capacity, int cus);
 hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
                                const lvkv_log_report* phys, uint64_t size, uint32_t capacity,
                                uint64_t initial_offset, lvkv_log_record* recs, uint32_t rec_cap,
@@ -115,10 +115,18 @@ struct DeviceCtx {
   // (lvkv_debug_set_sst_form)
   std::atomic<int> sst_form{0};
   std::mutex host_mu;  // serialises lvkv_crc32c_batch_host per device
-  // WAL verify scratch, one buffer per stream (calls on one stream are
-  // ordered, so a buffer is never used by two calls at once)
+  // WAL verify scratch: a pool of buffers, each lent to one call at a time
+  // (busy from acquire to the event recorded after the call's launches,
+  // free once that event completes), on any stream
   std::mutex scratch_mu;
-  std::unordered_map<hipStream_t, std::pair<void*, size_t>> log_scratch;
+  struct Scratch {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipEvent_t ev = nullptr;
+    hipStream_t stream = nullptr;  // of its last call
+    bool lent = false;
+  };
+  std::vector<Scratch> log_pool;
   bool stages_ready = false;
   Stage stage[2];
 };
@@ -336,28 +344,79 @@ KernelArgs ctx_args(const DeviceCtx& c) {
   return a;
 }
 
-// The WAL verify scratch of `stream`, grown (stream-ordered) when too small;
-// a fresh buffer's completion counter is zeroed on the stream.
-hipError_t log_scratch_for(DeviceCtx& c, hipStream_t stream, size_t bytes, void** out) {
+// A WAL verify scratch buffer of at least `bytes` for one call on `stream`.
+// A buffer whose last call has finished (its event completed; never
+// recorded counts as completed) is taken as is; else one last used on this
+// same stream, or, with four buffers out, any idle one, is taken behind its
+// event (hipStreamWaitEvent: the new call starts after the old one ends, a
+// no-op on the same stream); else a new buffer is added. A new buffer's
+// counters (bytes [0, 24)) are zeroed on `stream`; every call leaves them at
+// 0. Not capturable: a graph would replay the counters unzeroed.
+hipError_t log_scratch_acquire(DeviceCtx& c, hipStream_t stream, size_t bytes, void** out,
+                               size_t* slot) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  hipError_t e = hipStreamIsCapturing(stream, &cs);
+  if (e != hipSuccess) return e;
+  if (cs != hipStreamCaptureStatusNone) return hipErrorStreamCaptureUnsupported;
   std::lock_guard<std::mutex> lk(c.scratch_mu);
-  auto& slot = c.log_scratch[stream];
-  if (slot.first != nullptr && slot.second >= bytes) {
-    *out = slot.first;
+  constexpr size_t kPoolMax = 4;
+  size_t same = SIZE_MAX, any = SIZE_MAX, idle_small = SIZE_MAX;
+  for (size_t i = 0; i < c.log_pool.size(); ++i) {
+    auto& b = c.log_pool[i];
+    if (b.lent) continue;
+    const bool finished = hipEventQuery(b.ev) == hipSuccess;
+    if (b.bytes < bytes) {
+      if (finished) idle_small = i;
+      continue;
+    }
+    if (finished) {
+      b.lent = true;
+      b.stream = stream;
+      *out = b.p;
+      *slot = i;
+      return hipSuccess;
+    }
+    if (b.stream == stream) same = i;
+    any = i;
+  }
+  size_t pick = same != SIZE_MAX ? same : (c.log_pool.size() >= kPoolMax ? any : SIZE_MAX);
+  if (pick != SIZE_MAX) {
+    auto& b = c.log_pool[pick];
+    if ((e = hipStreamWaitEvent(stream, b.ev, 0)) != hipSuccess) return e;
+    b.lent = true;
+    b.stream = stream;
+    *out = b.p;
+    *slot = pick;
     return hipSuccess;
   }
-  hipError_t e = hipSuccess;
-  if (slot.first != nullptr && (e = hipFreeAsync(slot.first, stream)) != hipSuccess) return e;
-  slot = {nullptr, 0};
-  const size_t cap = std::max<size_t>(bytes, size_t{1} << 16);
-  void* p = nullptr;
-  if ((e = hipMallocAsync(&p, cap, stream)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(p, 0, 16, stream)) != hipSuccess) {
-    (void)hipFreeAsync(p, stream);
-    return e;
+  if (idle_small == SIZE_MAX) {
+    DeviceCtx::Scratch n;
+    if ((e = hipEventCreateWithFlags(&n.ev, hipEventDisableTiming)) != hipSuccess) return e;
+    c.log_pool.push_back(n);
+    idle_small = c.log_pool.size() - 1;
   }
-  slot = {p, cap};
-  *out = p;
+  auto& b = c.log_pool[idle_small];
+  if (b.p != nullptr && (e = hipFree(b.p)) != hipSuccess) return e;
+  b.p = nullptr;
+  b.bytes = 0;
+  const size_t cap = std::max<size_t>(bytes, size_t{1} << 16);
+  if ((e = hipMalloc(&b.p, cap)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(b.p, 0, 24, stream)) != hipSuccess) return e;
+  b.bytes = cap;
+  b.lent = true;
+  b.stream = stream;
+  *out = b.p;
+  *slot = idle_small;
   return hipSuccess;
+}
+
+// Hands the buffer back: busy until the work just launched on `stream` ends.
+hipError_t log_scratch_release(DeviceCtx& c, size_t slot, hipStream_t stream) {
+  std::lock_guard<std::mutex> lk(c.scratch_mu);
+  auto& b = c.log_pool[slot];
+  const hipError_t e = hipEventRecord(b.ev, stream);
+  b.lent = false;
+  return e;
 }
 
 // ---- host-resident pipeline ------------------------------------------
@@ -586,13 +645,17 @@ int lvkv_log_verify_blocks_device(const void* d_file, uint64_t file_size,
   if (c == nullptr) return rc;
   const hipStream_t hs = static_cast<hipStream_t>(stream);
   void* scratch = nullptr;
-  hipError_t e = log_scratch_for(*c, hs, log_scratch_bytes(file_size), &scratch);
-  if (e == hipSuccess)
-    e = launch_log_blocks(static_cast<const uint8_t*>(d_file), file_size, d_hdr_offsets,
-                          d_actual, d_rec_status, static_cast<uint32_t>(capacity),
-                          d_block_status, d_block_drop, d_report, c->d_tables + kZPowOffset,
-                          c->d_tables + kRowTabDwords + kLaneTabDwords, c->groups, scratch,
-                          nullptr, hs);
+  size_t slot = 0;
+  hipError_t e = log_scratch_acquire(*c, hs, log_scratch_bytes(file_size, static_cast<uint32_t>(capacity), c->groups), &scratch, &slot);
+  if (e == hipErrorStreamCaptureUnsupported) return LVKV_ERR_INVALID;
+  if (e != hipSuccess) return hip_fail(e);
+  e = launch_log_blocks(static_cast<const uint8_t*>(d_file), file_size, d_hdr_offsets, d_actual,
+                        d_rec_status, static_cast<uint32_t>(capacity), d_block_status,
+                        d_block_drop, d_report, c->d_tables + kZPowOffset,
+                        c->d_tables + kRowTabDwords + kLaneTabDwords, c->groups, scratch, nullptr,
+                        hs);
+  const hipError_t e2 = log_scratch_release(*c, slot, hs);
+  if (e == hipSuccess) e = e2;
   return e == hipSuccess ? LVKV_OK : hip_fail(e);
 }
 
@@ -616,11 +679,15 @@ int lvkv_log_read_device(const void* d_file, uint64_t file_size, uint64_t* d_hdr
   // scratch: the verify's counters, the event stream (one u32 per candidate
   // record and per block), then the logical layer's per-chunk state
   const size_t nblocks = static_cast<size_t>((file_size + 32767) / 32768);
-  const size_t ev_at = (log_scratch_bytes(file_size) + 15) & ~size_t{15};
+  const size_t ev_at =
+      (log_scratch_bytes(file_size, static_cast<uint32_t>(capacity), c->groups) + 15) & ~size_t{15};
   const size_t asm_at = (ev_at + (capacity + nblocks) * 4 + 15) & ~size_t{15};
   void* scratch = nullptr;
-  hipError_t e = log_scratch_for(*c, hs, asm_at + log_asm_scratch_bytes(capacity + nblocks),
-                                 &scratch);
+  size_t slot = 0;
+  hipError_t e = log_scratch_acquire(*c, hs, asm_at + log_asm_scratch_bytes(capacity + nblocks),
+                                     &scratch, &slot);
+  if (e == hipErrorStreamCaptureUnsupported) return LVKV_ERR_INVALID;
+  if (e != hipSuccess) return hip_fail(e);
   uint8_t* sb = static_cast<uint8_t*>(scratch);
   uint32_t* events = reinterpret_cast<uint32_t*>(sb + ev_at);
   if (e == hipSuccess)
@@ -637,6 +704,8 @@ int lvkv_log_read_device(const void* d_file, uint64_t file_size, uint64_t* d_hdr
                             // the verify leaves scratch bytes 8-15 alone (zeroed
                             // when allocated): the assembly's completion counter
                             reinterpret_cast<uint32_t*>(sb + 8), hs);
+  const hipError_t e2 = log_scratch_release(*c, slot, hs);
+  if (e == hipSuccess) e = e2;
   return e == hipSuccess ? LVKV_OK : hip_fail(e);
 }
 

@@ -5,37 +5,54 @@
 // Headers never straddle a 32 KiB block (the writer pads the tail of a block
 // with zeros, db/log_writer.cc:44-55) and the reader drops the REST OF THE
 // BLOCK on every error, so each block's verdict depends on that block only.
-// One launch, one read of the image:
+// One read of the image, two launches:
 //
-//   log_verify_kernel  persistent, one 512-thread workgroup per CU, blocks
-//                      b = blockIdx.x + k * gridDim.x. Each block is read
-//                      from HBM once (the next one's 16-byte loads in flight
-//                      in registers while the current one is worked on) into
-//                      one of two LDS buffers. Wave 0 walks the headers of
-//                      the NEXT block from LDS (one lane; a few cycles per
-//                      record) and finds the current block's first record
-//                      slot by a decoupled look-back over the per-block
-//                      record counts (published as soon as a block is
-//                      walked, so no workgroup waits on another's CRCs);
-//                      waves 1-7 checksum the current block's records from
-//                      LDS (the end-aligned word grid of the other kernels,
-//                      unaligned words rebuilt with v_alignbyte, rows folded
-//                      with Z_256 on the compact image); records over 4 KiB
-//                      are walked by the whole workgroup. Then the block's
-//                      merge: the first mismatch drops the rest of the block,
-//                      block status and reported drop bytes. The last
-//                      workgroup to finish sums the per-block results into
-//                      the report.
+//   log_verify_kernel  one 1024-thread workgroup per CU with TWO block
+//                      slots in LDS (32 KiB each) beside the 64 KiB CRC
+//                      image. Wave m (m < 2) manages slot m: it claims the
+//                      next block with a ticket (an atomic counter, so no
+//                      workgroup ever waits on one that has not started,
+//                      whatever the residency), copies it into the slot by
+//                      LDS-DMA (buffer_load ... lds, no registers), walks its
+//                      headers, reserves the block's records a run of the
+//                      staging array (an atomic bump), waits for the block's
+//                      CRCs and stages the block's results.
+//                      The walk is a chain of dependent LDS reads (≈ 170 ns a
+//                      header whatever else the CU does, measured with
+//                      tools/probe/walk_probe.hip): it is the kernel's
+//                      critical path, so a CU walks two blocks at once, and
+//                      the fourteen other waves checksum each record as soon as
+//                      the walker has published its position (records two at
+//                      a time, from any slot). Records over kSegBytes are cut
+//                      into 4 KiB segments on the end-aligned grid,
+//                      checksummed by several waves and folded with
+//                      Z_{i·4 KiB} (the zmul columns). The block's merge
+//                      (db/log_reader.cc:221-255): the first mismatch drops
+//                      the rest of the block; block status and drop bytes.
+//                      Nothing waits for a block's place in file order (that
+//                      would wait for the slowest block in flight before it):
+//                      the last workgroup to finish scans the per-block counts
+//                      into each block's first record index and writes the
+//                      report.
+//   log_emit_kernel    one wave per block moves the staged results to their
+//                      places (and writes the ReadRecord event stream).
 //
-// Scratch (per-block record counts and good-record counts, one completion
-// counter) is the caller's per-stream buffer (lvkv_capi.cpp): the count words
-// are tagged with the call's generation, and the counter is left at 0 by the
-// last workgroup of every call, so nothing is cleared per call.
+// The CRC (same arithmetic as every kernel here): rows of 64
+// words folded with Z_256 by four byte lookups in LDS, then each lane's
+// Z_{256-4s} end shift, on the compact 64 KiB image (crc32c_compact_common.h).
+// Three or four slots with a smaller image (row tables in 16-32 KiB, the end
+// shift from columns in registers) walk more blocks at once but make each
+// record's CRC dearer, and measured slower (84 and 94 against 76 µs on the
+// 66 MB log): the workers, not the walks, then set the pace.
+//
+// Scratch (lvkv_capi.cpp, one buffer per call in flight): counters left at 0
+// by the last workgroup of every call, per-block words, the staging array
+// and each slot's overflow positions (blocks of more than kPosLds records).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
 
-#include <atomic>
+#include <algorithm>
 
 #include "crc32c_compact_common.h"
 #include "crc32c_device_common.h"
@@ -49,135 +66,48 @@ namespace {
 constexpr uint64_t kLogBlock = 32768;  // db/log_format.h kBlockSize
 constexpr uint32_t kLogHeader = 7;     // db/log_format.h kHeaderSize
 
-struct BlockSpan {
-  uint64_t start, end;
-  bool eof;  // a short read: the reader's eof_ (log_reader.cc:202-204)
-};
-
-__device__ __forceinline__ BlockSpan block_span(uint64_t b, uint64_t size) {
-  BlockSpan s;
-  s.start = b * kLogBlock;
-  s.end = min(size, s.start + kLogBlock);
-  s.eof = s.end - s.start < kLogBlock;
-  return s;
-}
-
-// Walks one block's headers in LDS, blk[0, n), to the first stop (bad
-// length, zero record, end) like ReadPhysicalRecord, with the stop position:
-// one LDS round trip per header; returns the verdict, *stop = the block
-// offset after the last record. Called by a whole wave with uniform
-// arguments: every lane reads the same dwords (a broadcast) and the header
-// arithmetic runs on the scalar unit (readfirstlane), so a step is the LDS
-// latency plus a few SALU cycles; lane 0 writes the positions.
-__device__ __forceinline__ uint8_t walk_positions(const uint8_t* blk, uint32_t n, bool eof,
-                                                  uint16_t* pos, uint32_t* count, uint32_t* stop) {
-  uint32_t p = 0, k = 0, length = 0, w = 0;
-  // positions collect in a register, record k in lane k % 64 (a select),
-  // written to pos[] 64 at a time: no per-step masked LDS store
-  uint32_t held = 0;
-  const uint32_t lane = threadIdx.x & 63u;
-  // Every lane carries the same p in a VGPR, so the chain from one header to
-  // the next is VALU + one LDS round trip (no readfirstlane, no scalar
-  // funnel shift): the dwords holding bytes p + 4 .. p + 6 are (p & ~3) + 4
-  // and + 8, the bytes shifted out by v_alignbyte(p & 3). The next header's
-  // read is issued before this header's stop test (speculatively, clamped
-  // into the buffer), so the test's compare and branch overlap the LDS trip.
-  // The reads are inline asm so the compiler neither sinks the speculative
-  // one below the branch nor turns the chain scalar; their registers are
-  // tied to explicit lgkmcnt waits (an asm load's destination is written
-  // late, so it must stay live until a wait has seen it land).
-  if (n >= kLogHeader) {
-    const uint32_t base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(blk));
-    uint64_t cur, nxt;
-    // bp = base + p (the buffer is 16-byte aligned, so bp & 3 == p & 3): the
-    // next read's address is two VALU ops from the length. A read past the
-    // block (a bad length, about to stop the walk) lands elsewhere in LDS or
-    // past the allocation (zeros): harmless, its bytes are never used.
-    uint32_t bp = base;
-    asm volatile("ds_read2_b32 %0, %1 offset0:1 offset1:2" : "=v"(cur) : "v"(base));
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur));
-    for (;;) {
-      w = __builtin_amdgcn_alignbyte(static_cast<uint32_t>(cur >> 32), static_cast<uint32_t>(cur),
-                                     bp & 3u);
-      length = w & 0xffffu;
-      const uint32_t nbp = bp + kLogHeader + length;
-      asm volatile("ds_read2_b32 %0, %1 offset0:1 offset1:2" : "=v"(nxt) : "v"(nbp & ~3u));
-      const uint32_t np = p + kLogHeader + length;
-      __builtin_amdgcn_sched_barrier(0);  // the read issues before the tests below
-      // a bad length (:221-232) or a zero record (:234-240) ends the walk
-      // (bit 0); bit 1: the record ends within 7 bytes of the block end
-      const bool bad = np > n || (w & 0xffffffu) == 0;
-      const uint32_t f =
-          __builtin_amdgcn_readfirstlane((bad ? 1u : 0u) | (n - np < kLogHeader ? 2u : 0u));
-      if (f & 1u) break;
-      held = lane == (k & 63u) ? p : held;
-      ++k;
-      if (__builtin_expect((k & 63u) == 0, 0)) pos[k - 64u + lane] = static_cast<uint16_t>(held);
-      p = np;
-      bp = nbp;
-      if (f & 2u) break;
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nxt));
-      cur = nxt;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nxt));
-  }
-  p = __builtin_amdgcn_readfirstlane(p);
-  length = __builtin_amdgcn_readfirstlane(length);
-  if (lane < (k & 63u)) pos[(k & ~63u) + lane] = static_cast<uint16_t>(held);
-  uint8_t v;
-  if (n - p < kLogHeader)
-    v = (eof && p < n) ? LVKV_LOGBLK_EOF : LVKV_LOGBLK_OK;  // :206-213
-  else if (kLogHeader + length > n - p)
-    v = eof ? LVKV_LOGBLK_EOF : LVKV_LOGBLK_BAD_LENGTH;
-  else
-    v = LVKV_LOGBLK_ZERO;
-  *count = k;
-  *stop = p;
-  return v;
-}
-
 constexpr int kVW = 16;  // waves per workgroup
 constexpr uint32_t kVThreads = 64 * kVW;
+constexpr uint32_t kSlots = 2;  // blocks in LDS per workgroup (one manager wave each)
 constexpr uint32_t kMaxRecs = (static_cast<uint32_t>(kLogBlock) + kLogHeader - 1) / kLogHeader;
-constexpr uint32_t kLongRec = 16 * 256;  // CRC bytes walked by one wave, at most
-constexpr uint32_t kMaxLong = static_cast<uint32_t>(kLogBlock) / kLongRec + 1;
+constexpr uint32_t kPosLds = 4096;  // positions per slot in LDS; the rest in scratch
+constexpr uint32_t kPosOver = kMaxRecs - kPosLds;
+// a slot holds the block from its 16-byte aligned start: up to 15 bytes before it
 constexpr uint32_t kBufBytes = static_cast<uint32_t>(kLogBlock) + 16;
-constexpr uint32_t kPerThread = static_cast<uint32_t>(kLogBlock) / (kVThreads * 16u);  // uint4s
-
-// look-back words: generation (26 bits) | flag (2) | value (36)
-constexpr uint64_t kFlagAgg = 1, kFlagInc = 2;
-__device__ __forceinline__ uint64_t link_word(uint32_t gen, uint64_t flag, uint64_t v) {
-  return (static_cast<uint64_t>(gen & 0x3ffffffu) << 38) | (flag << 36) | v;
-}
-__device__ __forceinline__ bool link_is(uint64_t x, uint32_t gen) {
-  return static_cast<uint32_t>(x >> 38) == (gen & 0x3ffffffu) && ((x >> 36) & 3u) != 0;
-}
+constexpr uint32_t kSegBytes = 4096;  // CRC bytes one wave takes at most
+constexpr uint32_t kLog2Seg = 12;
+constexpr uint32_t kMaxLong = static_cast<uint32_t>(kLogBlock) / (kSegBytes + 1) + 1;  // 8
 
 struct LogArgs {
   const uint8_t* file;
   uint64_t size;
-  uint32_t nblocks, capacity, gen, pad_;
+  uint32_t nblocks, capacity;
   uint64_t* hdr_off;
   uint32_t* actual;
   uint8_t* rec_status;
   uint8_t* block_status;
   uint32_t* block_drop;
   lvkv_log_report* r;
-  uint64_t* agg;   // nblocks: the block's record count (published when walked)
-  uint64_t* inc;   // nblocks: records in blocks 0..b (published when placed)
-  uint32_t* good;  // nblocks records the reader returns
-  uint64_t* done;  // finished workgroups (zeroed before the launch)
+  ulonglong2* info;  // nblocks: {count | good << 32, drop | status << 32}
+  uint32_t* stg_off; // nblocks: the block's first entry in `stg`
+  uint32_t* first;   // nblocks: the block's first record index (file order)
+  uint4* stg;        // capacity: per record {actual, pos | len << 16, type, status}
+  uint32_t* over;    // groups x kSlots x kPosOver: positions past kPosLds
+  uint64_t* done;    // finished workgroups (left at 0)
+  uint32_t* ticket;  // blocks claimed (left at 0)
+  uint32_t* stg_top; // staging entries reserved (left at 0)
   const uint32_t* zpow;
   const uint32_t* lane_cols;
   uint32_t* events;  // nullable: the ReadRecord event stream (lvkv_log_events.h)
-  uint64_t* stamps;  // probe build only: 8 u64 per (workgroup, iteration)
-  uint32_t knobs;    // probe build only: 1 no record CRCs, 2 no walk wait, 4 no placement
+  uint64_t* stamps;  // probe build only: 8 u64 per (workgroup, slot, block)
 };
 
-__device__ __forceinline__ void log_stamp(const LogArgs& a, uint32_t k, int slot) {
+// Manager phase stamps (probe build): 0 claimed, 1 in LDS, 2 walked,
+// 3 CRCs done, 4 staged; row (slot 0, k 15) holds the workgroup's own.
+__device__ __forceinline__ void log_stamp(const LogArgs& a, uint32_t m, uint32_t k, int slot) {
 #ifdef LVKV_PROBE_BUILD
   if (a.stamps != nullptr && lane_id() == 0)
-    a.stamps[(static_cast<uint64_t>(blockIdx.x) * 16u + min(k, 15u)) * 8u + slot] =
+    a.stamps[((static_cast<uint64_t>(blockIdx.x) * kSlots + m) * 16u + min(k, 15u)) * 8u + slot] =
         __builtin_amdgcn_s_memrealtime();
 #endif
 }
@@ -189,26 +119,38 @@ __device__ __forceinline__ uint32_t lds_word(const uint8_t* buf, uint32_t x) {
   return (x & 3u) ? __builtin_amdgcn_alignbyte(hi, lo, x & 3u) : lo;
 }
 
-// CRC32C of buf[a, a + n) (LDS, n >= 4) by one wave: the end-aligned word
-// grid (grid word j = the 4 bytes ending 4 * (q - 1 - j) before the end,
-// lane s of row r holds word 64 r + s), Horner over rows with Z_256, lane end
-// shift, xor-reduce; init 0 (~0 xored into the first word, spill into the
-// next), as fix_first_chunk / segment_register do. Two records at once (NR =
-// 2; the second may be empty, n = 0) so their dependent LDS chains overlap.
+// ---- record CRCs from LDS ----------------------------------------------
+
+// A lane's constants on the compact image (crc32c_compact_common.h): its
+// four lookups' v_perm keys and its nibble-table column.
+struct LogLane {
+  LaneKeys keys;
+  uint32_t lane_base;
+};
+
+// CRC32C registers of buf[a, a + n) (LDS, n >= 4) by one wave: the
+// end-aligned word grid (grid word j = the 4 bytes ending 4 * (q - 1 - j)
+// before the end, lane s of row r holds word 64 r + s), Horner over rows
+// with Z_256, lane end shift, xor-reduce. `inj` is xored into the first 4
+// data bytes (spilling into the next word): ~0 for a record (the CRC's
+// initial state), 0 for a segment after the first; `fin` is xored into the
+// result (~0 for a CRC, 0 for a segment's register).
 struct LdsRec {
-  uint32_t first, s0l, sh, spill;
+  uint32_t first, s0l, sh, msk, inj, spill;
 };
 
 // Geometry of a record of n >= 4 bytes at a on a grid of `rows` rows (at
 // least its own; extra rows in front are all-zero words, which leave the
 // register at 0, so two records can share one row count).
-__device__ __forceinline__ LdsRec lds_rec(uint32_t a, uint32_t n, uint32_t rows) {
+__device__ __forceinline__ LdsRec lds_rec(uint32_t a, uint32_t n, uint32_t rows, uint32_t inj) {
   LdsRec r;
   const uint32_t q = (n + 3u) >> 2;
   const uint32_t delta = 4u * q - n;
   r.s0l = 64u * rows - q;
   r.sh = 8u * delta;
-  r.spill = delta ? (0xffffffffu >> (32u - r.sh)) : 0u;
+  r.msk = 0xffffffffu << r.sh;
+  r.inj = inj << r.sh;
+  r.spill = delta ? (inj >> (32u - r.sh)) : 0u;
   r.first = a - delta;  // byte address of grid word s0l
   return r;
 }
@@ -225,7 +167,7 @@ __device__ __forceinline__ uint32_t grid_fix(const LdsRec& g, uint32_t r, uint32
   const uint32_t j = 64u * r + lane;
   uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, x & 3u);
   w = j >= g.s0l ? w : 0u;
-  w = j == g.s0l ? ((w & (0xffffffffu << g.sh)) ^ (0xffffffffu << g.sh)) : w;
+  w = j == g.s0l ? ((w & g.msk) ^ g.inj) : w;
   return j == g.s0l + 1u ? (w ^ g.spill) : w;
 }
 
@@ -235,9 +177,10 @@ __device__ __forceinline__ uint32_t grid_fix(const LdsRec& g, uint32_t r, uint32
 // scheduling barriers keep the compiler from pairing each read with its use.
 template <int NR>
 __device__ __forceinline__ void lds_record_crcs(const uint8_t* buf, const uint32_t (&at)[NR],
-                                                const uint32_t (&n)[NR], const uint32_t* img,
-                                                const LaneKeys& keys, uint32_t lane,
-                                                uint32_t lane_base, uint32_t (&crc)[NR]) {
+                                                const uint32_t (&n)[NR], const uint32_t (&inj)[NR],
+                                                uint32_t fin, const uint32_t* img,
+                                                const LogLane& L, uint32_t lane,
+                                                uint32_t (&crc)[NR]) {
   uint32_t q = 0;
 #pragma unroll
   for (int t = 0; t < NR; ++t) q = max(q, (n[t] + 3u) >> 2);
@@ -248,7 +191,7 @@ __device__ __forceinline__ void lds_record_crcs(const uint8_t* buf, const uint32
     uint32_t x[NR], lo[NR], hi[NR];
 #pragma unroll
     for (int t = 0; t < NR; ++t) {
-      g[t] = lds_rec(at[t], n[t], rows);
+      g[t] = lds_rec(at[t], n[t], rows, inj[t]);
       x[t] = grid_addr(g[t], 0, lane);
       const uint32_t* d = reinterpret_cast<const uint32_t*>(buf + (x[t] & ~3u));
       lo[t] = d[0];
@@ -268,7 +211,7 @@ __device__ __forceinline__ void lds_record_crcs(const uint8_t* buf, const uint32
       hi[t] = d[1];
 #pragma unroll
       for (int p = 0; p < 4; ++p)
-        v[t][p] = lds_ld(img, __builtin_amdgcn_perm(st[t], keys.kpack, keys.sel[p]));
+        v[t][p] = lds_ld(img, __builtin_amdgcn_perm(st[t], L.keys.kpack, L.keys.sel[p]));
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -284,341 +227,546 @@ __device__ __forceinline__ void lds_record_crcs(const uint8_t* buf, const uint32
   for (int t = 0; t < NR; ++t)
 #pragma unroll
     for (int k = 0; k < 8; ++k)
-      e[t][k] = lds_ld(img, (lane_base | (((st[t] >> (4 * k)) & 15u) << 9)) + 8192u * k);
+      e[t][k] = lds_ld(img, (L.lane_base | (((st[t] >> (4 * k)) & 15u) << 9)) + 8192u * k);
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int t = 0; t < NR; ++t) {
     const uint32_t r = xor3(xor3(e[t][0], e[t][1], e[t][2]), xor3(e[t][3], e[t][4], e[t][5]),
                             e[t][6] ^ e[t][7]);
-    crc[t] = wave_xor_dpp(r) ^ 0xffffffffu;
+    crc[t] = wave_xor_dpp(r) ^ fin;
   }
 }
 
-// Bitwise CRC32C of fewer than 4 bytes (lane-uniform).
-__device__ __forceinline__ uint32_t tiny_crc(const uint8_t* p, uint32_t n) {
-  uint32_t reg = 0xffffffffu;
+// Bitwise register update over n (< 4) bytes from `reg` (lane-uniform).
+__device__ __forceinline__ uint32_t tiny_reg(const uint8_t* p, uint32_t n, uint32_t reg) {
   for (uint32_t i = 0; i < n; ++i) {
     reg ^= p[i];
 #pragma unroll
     for (int k = 0; k < 8; ++k) reg = (reg >> 1) ^ (kCastagnoliReflected & (0u - (reg & 1u)));
   }
-  return reg ^ 0xffffffffu;
+  return reg;
 }
 
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(static_cast<unsigned long long>(v), d, 64);
+// ---- the per-slot state in LDS -------------------------------------------
+//
+// Every word a worker reads to decide what to take carries the slot's
+// generation (bumped each time the slot takes a new block), so a worker
+// that lags behind a recycled slot sees a foreign generation and backs off.
+//   next   (gen << 16) | records claimed by workers (two per claim)
+//   prog   (gen << 17) | walk finished << 16 | records walked (published)
+//   lclaim (gen << 16) | long-record segments claimed
+//   lavail (gen << 16) | long-record segments registered by the walker
+constexpr uint32_t kGenShift = 17, kDoneBit = 1u << 16;
+
+struct Slot {
+  uint32_t next, prog, lclaim, lavail;
+  uint32_t crcd;       // records whose CRC is final (this generation)
+  uint32_t first_bad;  // smallest record index whose CRC mismatched
+  uint32_t shift;      // the block starts at buf + shift (its 16-byte misalignment)
+  uint32_t nlong;
+  uint16_t lj[kMaxLong];     // long record: index
+  uint16_t lp[kMaxLong];     // position
+  uint8_t lseg[kMaxLong];    // segments
+  uint8_t lfirst[kMaxLong];  // first segment's index in the slot's segment numbering
+  uint32_t lacc[kMaxLong];   // xor of the segments' shifted registers
+  uint32_t lrem[kMaxLong];   // segments not yet folded in
+};
+
+__device__ __forceinline__ uint32_t lds_load_acq(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store_rel(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Record j's position in its block: LDS for the first kPosLds, the slot's
+// scratch overflow after (stored sc1 by the walker, waited for before it
+// published the count).
+__device__ __forceinline__ uint32_t pos_of(const uint16_t* pos, const uint32_t* over, uint32_t j) {
+  return j < kPosLds ? pos[j]
+                     : __hip_atomic_load(&over[j - kPosLds], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void put_pos(uint16_t* pos, uint32_t* over, uint32_t j, uint32_t p) {
+  if (j < kPosLds) {
+    pos[j] = static_cast<uint16_t>(p);
+  } else {
+    __hip_atomic_store(&over[j - kPosLds], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+// Walks one block's headers in LDS, blk[0, n), to the first stop (bad
+// length, zero record, end) like ReadPhysicalRecord, publishing the records'
+// positions as it goes (8 at a time: positions, then S.prog) and registering
+// records longer than kSegBytes for segmented CRCs. Called by the manager
+// wave with uniform arguments. Returns the verdict; *count, *stop = the
+// records and the block offset after the last one.
+//
+// Every lane carries the same position in a VGPR (bp, its LDS address), so
+// the chain from one header to the next is one LDS round trip and a v_add3:
+// the length is an unaligned ds_read_u16 at bp + 4 (the type byte, for the
+// zero-record test, a ds_read_u8 beside it). The next header's reads are
+// issued before this header's stop test (speculatively: a read past the
+// block, about to stop the walk, lands elsewhere in LDS or past the
+// allocation and is never used), so the test overlaps the LDS trip. The
+// reads are inline asm so the compiler neither sinks the speculative ones
+// below the branch nor turns the chain scalar; their registers are tied to
+// explicit lgkmcnt waits (an asm load's destination is written late, so it
+// must stay live until a wait has seen it land). Positions collect in a
+// register (record k in lane k % 64) and are written 8 at a time.
+__device__ __forceinline__ uint8_t walk_block(const uint8_t* blk, uint32_t n, bool eof,
+                                              uint16_t* pos, uint32_t* over, Slot& S,
+                                              uint32_t gen, uint32_t* count, uint32_t* stop) {
+  const uint32_t lane = lane_id();
+  const uint32_t base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(blk));
+  const uint32_t end = base + n;
+  uint32_t k = 0, bp = base, len = 0, typ = 0;
+  uint32_t nseg = 0;  // long-record segments registered
+  uint32_t held = 0;  // position of record k in lane k % 64
+  if (n >= kLogHeader) {
+    uint32_t nlen, ntyp;
+    asm volatile("ds_read_u16 %0, %2 offset:4\n\tds_read_u8 %1, %2 offset:6\n\ts_waitcnt lgkmcnt(0)"
+                 : "=v"(len), "=v"(typ)
+                 : "v"(bp));
+    for (;;) {
+      const uint32_t nbp = bp + kLogHeader + len;
+      asm volatile("ds_read_u16 %0, %2 offset:4\n\tds_read_u8 %1, %2 offset:6"
+                   : "=v"(nlen), "=v"(ntyp)
+                   : "v"(nbp));
+      __builtin_amdgcn_sched_barrier(0);  // the reads issue before the tests below
+      // bit 0: a bad length (:221-232) or a zero record (:234-240) ends the
+      // walk; bit 1: the record ends within 7 bytes of the block end; bit 2:
+      // a record longer than kSegBytes
+      const uint32_t f = __builtin_amdgcn_readfirstlane(
+          (nbp > end || (len | typ) == 0 ? 1u : 0u) | (end - nbp < kLogHeader ? 2u : 0u) |
+          (len + 1u > kSegBytes ? 4u : 0u));
+      if (f & 1u) break;
+      held = lane == (k & 63u) ? bp - base : held;
+      if (__builtin_expect(f & 4u, 0)) {
+        // a long record: its segments go to the long queue
+        const uint32_t m = (len + 1u + kSegBytes - 1u) / kSegBytes;
+        if (lane == 0) {
+          const uint32_t e = S.nlong++;
+          S.lj[e] = static_cast<uint16_t>(k);
+          S.lp[e] = static_cast<uint16_t>(bp - base);
+          S.lseg[e] = static_cast<uint8_t>(m);
+          S.lfirst[e] = static_cast<uint8_t>(nseg);
+          S.lacc[e] = 0;
+          S.lrem[e] = m;
+        }
+        nseg += m;
+        if (lane == 0) lds_store_rel(&S.lavail, (gen << 16) | nseg);
+      }
+      ++k;
+      if ((k & 7u) == 0) {
+        // records k-8 .. k-1: their lanes write their positions, then the
+        // first of them publishes the count (LDS keeps one wave's order; the
+        // overflow's sc1 stores are waited for first)
+        const uint32_t g0 = (k - 8u) & 63u;
+        if ((lane & ~7u) == g0) {
+          put_pos(pos, over, k - 8u + (lane & 7u), held);
+          if (lane == g0) lds_store_rel(&S.prog, (gen << kGenShift) | k);
+        }
+      }
+      bp = nbp;
+      if (f & 2u) break;
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nlen), "+v"(ntyp));
+      len = nlen;
+      typ = ntyp;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nlen), "+v"(ntyp));
+  }
+  const uint32_t p = __builtin_amdgcn_readfirstlane(bp - base);
+  len = __builtin_amdgcn_readfirstlane(len);
+  // the last 0-7 positions
+  if (lane >= (k & ~7u & 63u) && lane < (k & ~7u & 63u) + (k & 7u))
+    put_pos(pos, over, (k & ~7u) + (lane & 7u), held);
+  uint8_t v;
+  if (n - p < kLogHeader)
+    v = (eof && p < n) ? LVKV_LOGBLK_EOF : LVKV_LOGBLK_OK;  // :206-213
+  else if (kLogHeader + len > n - p)
+    v = eof ? LVKV_LOGBLK_EOF : LVKV_LOGBLK_BAD_LENGTH;
+  else
+    v = LVKV_LOGBLK_ZERO;
+  if (lane == 0) lds_store_rel(&S.prog, (gen << kGenShift) | kDoneBit | k);
+  *count = k;
+  *stop = p;
   return v;
 }
 
-// Wave 0: the first record slot of block b = w + k G (workgroup w, iteration
-// k): this workgroup's own previous block b - G ends at prev_inc (its
-// inclusive count, known locally), and the G - 1 blocks between are all
-// walked an iteration ahead, so their counts are published: one memory round
-// trip, no wait on another workgroup's placement (which would chain every
-// workgroup's iterations together).
-__device__ uint64_t log_base(const LogArgs& a, uint32_t b, uint32_t G, uint64_t prev_inc,
-                             uint32_t lane) {
-  const uint32_t lo = b >= G ? b - G + 1 : 0;
-  uint64_t sum = 0;
-  for (uint32_t j = lo + lane; j < b; j += 64) {
-    uint64_t x;
-    do {
-      x = __hip_atomic_load(&a.agg[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } while (!link_is(x, a.gen));
-    sum += x & ((uint64_t{1} << 36) - 1);
-  }
-  return (b >= G ? prev_inc : 0) + wave_sum64(sum);
+// Writes a record's final CRC into its header's CRC bytes (where the stage
+// step reads it back) and notes a mismatch; lane 0.
+__device__ __forceinline__ void record_done(const uint8_t* blk, uint32_t p, uint32_t crc,
+                                            uint32_t j, Slot& S) {
+  uint8_t* hb = const_cast<uint8_t*>(blk) + p;
+  if (crc != crc_unmask(lds_word(blk, p))) atomicMin(&S.first_bad, j);
+  hb[0] = static_cast<uint8_t>(crc);
+  hb[1] = static_cast<uint8_t>(crc >> 8);
+  hb[2] = static_cast<uint8_t>(crc >> 16);
+  hb[3] = static_cast<uint8_t>(crc >> 24);
 }
 
-// Block b's bytes into registers: 16 per lane-load, kPerThread loads, bounded
-// by the image (a partial last block reads zeros past its end).
-__device__ __forceinline__ void load_block(const LogArgs& a, uint32_t b, uint32_t tid,
-                                           uint4 (&v)[kPerThread]) {
-  const BlockSpan s = block_span(b, a.size);
-  const uint32_t n = static_cast<uint32_t>(s.end - s.start);
-  const uint8_t* src = a.file + s.start;
-  // (a partial last block byte by byte: a buffer load that crosses the
-  // bound returns zeros for the whole load, and the image may end anywhere)
-  if ((reinterpret_cast<uintptr_t>(src) & 3u) == 0 && n == kLogBlock) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(src), 0, static_cast<int>(n), kBufferDword3);
-#pragma unroll
-    for (uint32_t k = 0; k < kPerThread; ++k) {
-      const auto x = __builtin_amdgcn_raw_buffer_load_b128(
-          r, static_cast<int>(16u * (tid + kVThreads * k)), 0, 0);
-      v[k] = make_uint4(x[0], x[1], x[2], x[3]);
-    }
-  } else {  // a partial block, or an image not on a 4-byte boundary
-#pragma unroll
-    for (uint32_t k = 0; k < kPerThread; ++k) {
-      uint32_t w[4];
-      for (uint32_t d = 0; d < 4; ++d) {
-        uint32_t x = 0;
-        for (uint32_t i = 0; i < 4; ++i) {
-          const uint32_t o = 16u * (tid + kVThreads * k) + 4u * d + i;
-          if (o < n) x |= static_cast<uint32_t>(src[o]) << (8 * i);
-        }
-        w[d] = x;
-      }
-      v[k] = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-  }
-}
+// ---- the kernel ------------------------------------------------------------
 
 __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t img[kCompactLdsBytes / 4 + kVW];
-  __shared__ __attribute__((aligned(16))) uint8_t buf[2][kBufBytes];
-  __shared__ uint16_t pos[2][kMaxRecs];
-  __shared__ uint32_t cnt[2], stop[2];
-  __shared__ uint8_t walked[2];
-  __shared__ uint64_t base_s;
-  __shared__ uint32_t ready, first_bad, nlong, bad_s, next_rec;
-  __shared__ uint16_t longs[kMaxLong];
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kSlots][kBufBytes];
+  __shared__ __attribute__((aligned(16))) uint32_t img[kCompactLdsBytes / 4];
+  __shared__ uint16_t pos[kSlots][kPosLds];
+  __shared__ Slot slots[kSlots];
+  __shared__ uint32_t fin;
   __shared__ unsigned long long red_good, red_drop;
   __shared__ uint32_t red_corrupt, red_first, last_s;
+  __shared__ uint64_t wsum_s[kVW];
 
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = lane_id();
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t G = gridDim.x;
-  uint4 pre[kPerThread];
-  uint64_t prev_inc = 0;  // wave 0: records in blocks 0 .. (this workgroup's last block)
-
-  const uint32_t b0 = blockIdx.x;
-  if (b0 < a.nblocks) load_block(a, b0, tid, pre);
+  if (tid < kSlots) {
+    Slot& S = slots[tid];
+    S.next = 0;
+    S.prog = 0;
+    S.lclaim = 0;
+    S.lavail = 0;
+    S.crcd = 0;
+    S.first_bad = 0xffffffffu;
+    S.nlong = 0;
+    S.shift = 0;
+  }
+  if (tid == 0) fin = 0;
+  if (tid == 0) log_stamp(a, 0, 15, 0);
   build_compact_image<kVW>(img, a.zpow, a.lane_cols, tid, wave, lane);  // ends with a barrier
-  const LaneKeys keys = lane_keys(lane);
-  const uint32_t lane_base = compact_lane_base(lane);
-  if (b0 < a.nblocks) {
-#pragma unroll
-    for (uint32_t k = 0; k < kPerThread; ++k)
-      reinterpret_cast<uint4*>(buf[0])[tid + kVThreads * k] = pre[k];
-  }
-  __syncthreads();
-  if (b0 < a.nblocks) {
-    if (wave == 0) {
-      const BlockSpan s = block_span(b0, a.size);
-      uint32_t c, st;
-      const uint8_t v = walk_positions(buf[0], static_cast<uint32_t>(s.end - s.start), s.eof,
-                                       pos[0], &c, &st);
-      if (lane == 0) {
-        walked[0] = v;
-        cnt[0] = c;
-        stop[0] = st;
-        __hip_atomic_store(&a.agg[b0], link_word(a.gen, kFlagAgg, c), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    if (b0 + G < a.nblocks) load_block(a, b0 + G, tid, pre);
-  }
+  if (tid == 0) log_stamp(a, 0, 15, 1);
 
-  for (uint32_t k = 0;; ++k) {
-    const uint32_t b = b0 + k * G;
-    if (b >= a.nblocks) break;
-    const uint32_t cur = k & 1u;
-    const uint32_t nb = b + G;
-    const BlockSpan s = block_span(b, a.size);
-    if (nb < a.nblocks) {
+  if (wave < kSlots) {
+    // ---- manager of slot m ----
+    const uint32_t m = wave;
+    // the walk is the longest chain of the kernel: its wave issues first
+    __builtin_amdgcn_s_setprio(3);
+    Slot& S = slots[m];
+    uint8_t* sbuf = buf[m];
+    uint16_t* spos = pos[m];
+    uint32_t* sover = a.over + (static_cast<uint64_t>(blockIdx.x) * kSlots + m) * kPosOver;
+    uint32_t gen = 0;  // slot generation (gen 0's block is the first)
+    // tickets: the next block's is claimed as soon as this one is in LDS, so
+    // the atomic's round trip overlaps the walk
+    uint32_t tk = 0;
+    if (lane == 0) tk = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t k = 0;; ++k) {
+      const uint32_t b = __builtin_amdgcn_readfirstlane(tk);
+      if (b >= a.nblocks) break;
+      log_stamp(a, m, k, 0);
+      const uint64_t start = uint64_t{b} * kLogBlock;
+      const uint64_t end = min(a.size, start + kLogBlock);
+      const uint32_t n = static_cast<uint32_t>(end - start);
+      const bool eof = n < kLogBlock;
+      // the block into the slot by LDS-DMA from its 16-byte aligned start:
+      // full 16-byte lines as dwordx4, the last 0-15 bytes by byte loads
+      {
+        const uint8_t* src = a.file + start;
+        const uint32_t shift = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src) & 15u);
+        const uint32_t nbytes = shift + n;
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t*>(src - shift), 0, static_cast<int>(nbytes), kBufferDword3);
+        const uint32_t lines = nbytes >> 4;
+        for (uint32_t i = 0; i * 64u < lines; ++i) {
+          const uint32_t line = i * 64u + lane;
+          if (line < lines)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                r, (__attribute__((address_space(3))) void*)(sbuf + 1024u * i), 16,
+                16u * line, 0, 0, 0);
+        }
+        // (a sub-dword LDS-DMA does not land one byte per lane: plain loads)
+        if (lane < (nbytes & 15u)) sbuf[16u * lines + lane] = (src - shift)[16u * lines + lane];
+        __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0): the DMA has landed
+        if (lane == 0) S.shift = shift;
+      }
+      if (lane == 0) tk = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      log_stamp(a, m, k, 1);
+      const uint8_t* blk = sbuf + S.shift;
+      uint32_t c, stop_at;
+      const uint8_t walked = walk_block(blk, n, eof, spos, sover, S, gen, &c, &stop_at);
+      // the block's run of staging entries (the atomic's round trip overlaps
+      // the CRCs: its value is first used by the staging stores)
+      uint32_t off = 0;
+      if (lane == 0) off = __hip_atomic_fetch_add(a.stg_top, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      log_stamp(a, m, k, 2);
+      // while the workers finish, the next block is pulled into L2 (one
+      // dword per 128-byte line), so its DMA is an L2 hit
+      uint32_t sink = 0;
+      {
+        const uint32_t nb = __builtin_amdgcn_readfirstlane(tk);
+        if (nb < a.nblocks) {
+          const uint64_t ns = uint64_t{nb} * kLogBlock;
 #pragma unroll
-      for (uint32_t i = 0; i < kPerThread; ++i)
-        reinterpret_cast<uint4*>(buf[cur ^ 1u])[tid + kVThreads * i] = pre[i];
-    }
-    if (tid == 0) {
-      ready = 0;
-      first_bad = 0xffffffffu;
-      nlong = 0;
-      next_rec = 0;
-    }
-    __syncthreads();  // buf[cur ^ 1] written, pos[cur] / cnt[cur] visible
-    if (tid == 0) log_stamp(a, k, 0);
-    // the block after next into registers; wave 0 issues its share after its
-    // placement loads (a wait on those would otherwise wait for these too)
-    if (wave != 0 && nb + G < a.nblocks) load_block(a, nb + G, tid, pre);
-    const uint32_t c = cnt[cur];
-    const uint8_t* blk = buf[cur];
-
-    // wave 0 places the block, wave 1 walks the next one; then both join the
-    // other waves on this block's records (taken one at a time from an LDS
-    // counter, so the late waves take fewer)
-    if (wave == 0) {
-#ifdef LVKV_PROBE_BUILD
-      const uint64_t base = (a.knobs & 4u) ? uint64_t{b} * 30u : log_base(a, b, G, prev_inc, lane);
-#else
-      const uint64_t base = log_base(a, b, G, prev_inc, lane);
-#endif
-      prev_inc = base + c;
-      if (lane == 0) {
-        __hip_atomic_store(&a.inc[b], link_word(a.gen, kFlagInc, base + c), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        base_s = base;
-        __atomic_store_n(&ready, 1u, __ATOMIC_RELEASE);
-        log_stamp(a, k, 1);
+          for (uint32_t i = 0; i < kLogBlock / 128u / 64u; ++i) {
+            const uint64_t at = ns + 128u * (i * 64u + lane);
+            if (at < a.size) sink ^= *reinterpret_cast<const uint32_t*>(a.file + (at & ~uint64_t{3}));
+          }
+        }
       }
-      if (nb + G < a.nblocks) load_block(a, nb + G, tid, pre);
-    } else if (wave == 1 && nb < a.nblocks) {
-      // the walk is the iteration's longest chain: this wave issues first
-      __builtin_amdgcn_s_setprio(3);
-      const BlockSpan ns = block_span(nb, a.size);
-      uint32_t nc, nst;
-      const uint8_t v = walk_positions(buf[cur ^ 1u], static_cast<uint32_t>(ns.end - ns.start),
-                                       ns.eof, pos[cur ^ 1u], &nc, &nst);
-      __builtin_amdgcn_s_setprio(0);
+      // the block's CRCs (the workers'); the merge (db/log_reader.cc:221-255)
+      while (lds_load_acq(&S.crcd) < c) __builtin_amdgcn_s_sleep(1);
+      asm volatile("" ::"v"(sink));
+      log_stamp(a, m, k, 3);
+      const uint32_t bad = S.first_bad;
+      uint8_t status = walked;
+      uint64_t drop = 0;
+      if (bad != 0xffffffffu) {
+        status = LVKV_LOGBLK_CHECKSUM;
+        drop = end - (start + pos_of(spos, sover, bad));  // ReportCorruption(buffer_.size(), ...)
+      } else if (status == LVKV_LOGBLK_BAD_LENGTH) {
+        drop = n - stop_at;  // ReportCorruption(drop_size, "bad record length")
+      }
+      off = __builtin_amdgcn_readfirstlane(off);
+      // the records, staged: the checksum a worker left in the header's CRC
+      // bytes; those after the first mismatch were dropped with the buffer
+      // (:248-255)
+      for (uint32_t j = lane; j < c && off + j < a.capacity; j += 64) {
+        const uint32_t p = pos_of(spos, sover, j);
+        const uint32_t len =
+            static_cast<uint32_t>(blk[p + 4]) | (static_cast<uint32_t>(blk[p + 5]) << 8);
+        a.stg[off + j] =
+            make_uint4(lds_word(blk, p), p | (len << 16), blk[p + 6],
+                       j < bad ? LVKV_REC_OK : j == bad ? LVKV_REC_CHECKSUM : LVKV_REC_DROPPED);
+      }
       if (lane == 0) {
-        walked[cur ^ 1u] = v;
-        cnt[cur ^ 1u] = nc;
-        stop[cur ^ 1u] = nst;
-        __hip_atomic_store(&a.agg[nb], link_word(a.gen, kFlagAgg, nc), __ATOMIC_RELAXED,
+        a.block_status[b] = status;
+        a.block_drop[b] = static_cast<uint32_t>(drop);
+        a.stg_off[b] = off;
+        // what the last workgroup reads, as sc1 stores (read back with sc1
+        // loads: no agent-scope fence on either side)
+        __hip_atomic_store(&a.info[b].x,
+                           uint64_t{c} | (uint64_t{bad != 0xffffffffu ? bad : c} << 32),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.info[b].y, drop | (uint64_t{status} << 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-        log_stamp(a, k, 2);
+      }
+      log_stamp(a, m, k, 4);
+      // recycle the slot: reset, then open the next generation (workers
+      // claim through `next` / `lclaim` last, so they see the reset state)
+      gen = (gen + 1u) & 0x7fffu;
+      if (lane == 0) {
+        S.crcd = 0;
+        S.first_bad = 0xffffffffu;
+        S.nlong = 0;
+        // the words workers wait on first, the words they claim through last
+        lds_store_rel(&S.lavail, gen << 16);
+        lds_store_rel(&S.prog, gen << kGenShift);
+        lds_store_rel(&S.lclaim, gen << 16);
+        lds_store_rel(&S.next, gen << 16);
       }
     }
-    {
-      bool have_base = false;
-      uint64_t base = 0;
-      for (;;) {
-        // kGrab records per grab, walked together (their dependent LDS chains
-        // overlap); long (> kLongRec) ones are queued for the workgroup, tiny
-        // (< 4 bytes) ones done bitwise
-        constexpr int kGrab = 2;
-        uint32_t j0 = 0;
-        if (lane == 0) j0 = atomicAdd(&next_rec, static_cast<uint32_t>(kGrab));
-        j0 = __builtin_amdgcn_readfirstlane(j0);
-        if (j0 >= c) break;
-        uint32_t pp[kGrab], nn[kGrab], at[kGrab], len[kGrab], crc[kGrab];
-        bool valid[kGrab], rows_ok[kGrab];
+    // No more blocks: the slot's open generation is published as walked and
+    // empty, so a worker whose claim landed in it (after the last recycle)
+    // sees the walk over and drops the claim instead of waiting forever.
+    if (lane == 0) {
+      lds_store_rel(&S.prog, (gen << kGenShift) | kDoneBit);
+      __hip_atomic_fetch_add(&fin, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  } else {
+    // ---- workers: records (two per claim) and long-record segments from
+    // any slot, as soon as the walker has published them. A claim is an
+    // atomic add on `next` / `lclaim`; the generation it returns is the one
+    // it belongs to (even if the slot was recycled since it was looked at),
+    // and a claim of a generation is waited out until the walker has passed
+    // it or stopped, so no record of a generation is ever skipped.
+    LogLane L;
+    L.keys = lane_keys(lane);
+    L.lane_base = compact_lane_base(lane);
+    for (uint32_t idle = 0;;) {
+      bool worked = false;
+#pragma unroll 1
+      for (uint32_t si = 0; si < kSlots; ++si) {
+        const uint32_t s = (wave + si) % kSlots;
+        Slot& S = slots[s];
+        const uint8_t* sbuf = buf[s];
+        const uint32_t* sover = a.over + (static_cast<uint64_t>(blockIdx.x) * kSlots + s) * kPosOver;
+        // long-record segments first: they are the long poles
+        {
+          const uint32_t lav = lds_load_acq(&S.lavail);
+          const uint32_t lcl = lds_load_acq(&S.lclaim);
+          if ((lav >> 16) == (lcl >> 16) && (lcl & 0xffffu) < (lav & 0xffffu)) {
+            uint32_t x = 0;
+            if (lane == 0) x = atomicAdd(&S.lclaim, 2u);
+            x = __builtin_amdgcn_readfirstlane(x);
+            const uint32_t g2 = x >> 16, x0 = x & 0xffffu;
+            // wait until both segments are registered or the walk is over
+            uint32_t av, pr;
+            for (;;) {
+              av = lds_load_acq(&S.lavail);
+              pr = lds_load_acq(&S.prog);
+              if ((av >> 16) != g2 || (pr >> kGenShift) != g2) break;
+              if ((pr & kDoneBit) || (av & 0xffffu) > x0 + 1u) break;
+              __builtin_amdgcn_s_sleep(1);
+            }
+            // a foreign generation: this one is finished, the claim was empty
+            if ((av >> 16) != g2 || (pr >> kGenShift) != g2) continue;
+            av = lds_load_acq(&S.lavail);  // final once the walk is over
+            const uint32_t navail = av & 0xffffu;
+            if (x0 < navail) {
+              worked = true;
+              const uint8_t* blk = sbuf + S.shift;
+              const uint32_t nl = S.nlong;
+              // the two segments: entry e, segment i (0 = the last) of each
+              uint32_t ent[2], seg[2], at[2], len[2], inj[2], raw[2];
+              bool have[2];
+#pragma unroll
+              for (int t = 0; t < 2; ++t) {
+                const uint32_t xi = x0 + t;
+                have[t] = xi < navail;
+                ent[t] = 0;
+                seg[t] = 0;
+                if (have[t]) {
+                  for (uint32_t e = 1; e < nl; ++e)
+                    if (S.lfirst[e] <= xi) ent[t] = e;
+                  const uint32_t e = ent[t];
+                  const uint32_t p = S.lp[e];
+                  const uint32_t nrec = 1u + (static_cast<uint32_t>(blk[p + 4]) |
+                                              (static_cast<uint32_t>(blk[p + 5]) << 8));
+                  const uint32_t m = S.lseg[e];
+                  seg[t] = m - 1u - (xi - S.lfirst[e]);  // numbered from the record's end
+                  const uint32_t segend = p + 6u + nrec - kSegBytes * seg[t];
+                  const bool front = seg[t] == m - 1u;
+                  at[t] = front ? p + 6u : segend - kSegBytes;
+                  len[t] = segend - at[t];
+                  inj[t] = front ? 0xffffffffu : 0u;
+                } else {  // a copy of the first, computed and dropped
+                  at[t] = at[0];
+                  len[t] = len[0];
+                  inj[t] = inj[0];
+                }
+              }
+              // the shift operators' columns (lanes [0,32): Z_{seg0 S}, [32,64): Z_{seg1 S})
+              const uint32_t myseg = lane < 32u ? seg[0] : seg[1];
+              const uint32_t colv = myseg ? zmul_cols(a.zpow, kLog2Seg, myseg)[lane & 31u] : 0u;
+              if (len[0] >= 4u && len[1] >= 4u) {
+                lds_record_crcs<2>(blk, at, len, inj, 0u, img, L, lane, raw);
+              } else {
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                  if (len[t] >= 4u) {
+                    const uint32_t a1[1] = {at[t]}, n1[1] = {len[t]}, i1[1] = {inj[t]};
+                    uint32_t r1[1];
+                    lds_record_crcs<1>(blk, a1, n1, i1, 0u, img, L, lane, r1);
+                    raw[t] = r1[0];
+                  } else {
+                    raw[t] = tiny_reg(blk + at[t], len[t], inj[t]);
+                  }
+                }
+              }
+#pragma unroll
+              for (int t = 0; t < 2; ++t) {
+                if (!have[t]) continue;
+                // the segment's register, shifted to the record's end
+                const uint32_t sh = seg[t] ? apply_lane_cols(colv, raw[t], t, lane) : raw[t];
+                if (lane == 0) {
+                  const uint32_t e = ent[t];
+                  atomicXor(&S.lacc[e], sh);
+                  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                  if (atomicSub(&S.lrem[e], 1u) == 1u) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    record_done(blk, S.lp[e], S.lacc[e] ^ 0xffffffffu, S.lj[e], S);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    atomicAdd(&S.crcd, 1u);
+                  }
+                }
+              }
+            }
+            continue;
+          }
+        }
+        // records
+        const uint32_t nx = lds_load_acq(&S.next);
+        const uint32_t prog = lds_load_acq(&S.prog);
+        if ((nx >> 16) != (prog >> kGenShift)) continue;  // being recycled
+        const uint32_t walked = prog & 0xffffu;
+        if ((nx & 0xffffu) >= walked && ((prog & kDoneBit) || walked == 0)) continue;
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(&S.next, 2u);
+        v = __builtin_amdgcn_readfirstlane(v);
+        const uint32_t g2 = v >> 16, j0 = v & 0xffffu;
+        // wait until the walker has passed both records or stopped
+        uint32_t pr;
+        for (;;) {
+          pr = lds_load_acq(&S.prog);
+          if ((pr >> kGenShift) != g2 || (pr & kDoneBit) || (pr & 0xffffu) > j0 + 1u) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if ((pr >> kGenShift) != g2) continue;  // that generation is over: an empty claim
+        const uint32_t total = pr & 0xffffu;
+        if (j0 >= total) continue;
+        worked = true;
+        const uint8_t* blk = sbuf + S.shift;
+        uint32_t pp[2], nn[2], at[2], len[2], crc[2];
+        bool valid[2], rows_ok[2];
         int lead = -1;
 #pragma unroll
-        for (int t = 0; t < kGrab; ++t) {
+        for (int t = 0; t < 2; ++t) {
           const uint32_t j = j0 + t;
           pp[t] = 0;
           nn[t] = 0;
           valid[t] = false;
-          if (j < c) {
-            pp[t] = pos[cur][j];
+          if (j < total) {
+            pp[t] = pos_of(pos[s], sover, j);
             nn[t] = 1u + (static_cast<uint32_t>(blk[pp[t] + 4]) |
                           (static_cast<uint32_t>(blk[pp[t] + 5]) << 8));
-            if (nn[t] > kLongRec) {
-              if (lane == 0) longs[atomicAdd(&nlong, 1u)] = static_cast<uint16_t>(j);
-            } else {
-              valid[t] = true;
-            }
+            valid[t] = nn[t] <= kSegBytes;  // long ones: the segment path
           }
           rows_ok[t] = valid[t] && nn[t] >= 4u;
           if (rows_ok[t] && lead < 0) lead = t;
         }
-#ifdef LVKV_PROBE_BUILD
-        if (a.knobs & 1u) {  // no CRC (timing only)
-#pragma unroll
-          for (int t = 0; t < kGrab; ++t) valid[t] = rows_ok[t] = false;
-          lead = -1;
-        }
-#endif
         if (lead >= 0) {
           // a record that is absent or tiny is replaced by the first real one
+          const uint32_t inj[2] = {0xffffffffu, 0xffffffffu};
 #pragma unroll
-          for (int t = 0; t < kGrab; ++t) {
+          for (int t = 0; t < 2; ++t) {
             at[t] = rows_ok[t] ? pp[t] + 6 : pp[lead] + 6;
             len[t] = rows_ok[t] ? nn[t] : nn[lead];
           }
-          lds_record_crcs<kGrab>(blk, at, len, img, keys, lane, lane_base, crc);
+          lds_record_crcs<2>(blk, at, len, inj, 0xffffffffu, img, L, lane, crc);
         }
-        if (wave == 2 && !have_base) log_stamp(a, k, 7);
 #pragma unroll
-        for (int t = 0; t < kGrab; ++t)
-          if (valid[t] && !rows_ok[t]) crc[t] = tiny_crc(blk + pp[t] + 6, nn[t]);
-        if (!have_base) {
-          while (__atomic_load_n(&ready, __ATOMIC_ACQUIRE) == 0) __builtin_amdgcn_s_sleep(1);
-          base = base_s;
-          have_base = true;
-        }
+        for (int t = 0; t < 2; ++t)
+          if (valid[t] && !rows_ok[t])
+            crc[t] = tiny_reg(blk + pp[t] + 6, nn[t], 0xffffffffu) ^ 0xffffffffu;
         if (lane == 0) {
+          uint32_t ndone = 0;
 #pragma unroll
-          for (int t = 0; t < kGrab; ++t) {
+          for (int t = 0; t < 2; ++t) {
             if (!valid[t]) continue;
-            const uint32_t j = j0 + t;
-            const bool ok = crc[t] == crc_unmask(lds_word(blk, pp[t]));
-            if (!ok) atomicMin(&first_bad, j);
-            const uint64_t gi = base + j;
-            if (gi < a.capacity) {
-              a.hdr_off[gi] = s.start + pp[t];
-              a.actual[gi] = crc[t];
-              a.rec_status[gi] = ok ? LVKV_REC_OK : LVKV_REC_CHECKSUM;
-              if (a.events != nullptr)
-                a.events[gi + b] = ok ? log_event(kEvRec, blk[pp[t] + 6], nn[t] - 1u)
-                                      : log_event(kEvSkip, 0, 0);
-            }
+            record_done(blk, pp[t], crc[t], j0 + t, S);
+            ++ndone;
+          }
+          if (ndone) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            atomicAdd(&S.crcd, ndone);
           }
         }
       }
-    }
-    if (wave == 2) log_stamp(a, k, 3);
-    __syncthreads();
-    if (tid == 0) log_stamp(a, k, 4);
-    // records over kLongRec: the whole workgroup, from the image (L2-warm)
-    const uint32_t nl = nlong;
-    for (uint32_t i = 0; i < nl; ++i) {
-      const uint32_t j = longs[i];
-      const uint32_t p = pos[cur][j];
-      const uint32_t n = 1u + (static_cast<uint32_t>(blk[p + 4]) |
-                               (static_cast<uint32_t>(blk[p + 5]) << 8));
-      const uint64_t at = reinterpret_cast<uint64_t>(a.file) + s.start + p + 6;
-      const uint32_t crc = workgroup_crc<kVW, 4096>(img, img + kCompactLdsBytes / 4, at, at + n,
-                                                    0u, keys, tid, wave, lane, lane_base, a.zpow);
-      if (tid == 0) {
-        const bool ok = crc == crc_unmask(lds_word(blk, p));
-        if (!ok) first_bad = min(first_bad, j);
-        const uint64_t gi = base_s + j;
-        if (gi < a.capacity) {
-          a.hdr_off[gi] = s.start + p;
-          a.actual[gi] = crc;
-          a.rec_status[gi] = ok ? LVKV_REC_OK : LVKV_REC_CHECKSUM;
-          if (a.events != nullptr)
-            a.events[gi + b] = ok ? log_event(kEvRec, blk[p + 6], n - 1u) : log_event(kEvSkip, 0, 0);
-        }
+      if (worked) {
+        idle = 0;
+        continue;
       }
+      if (lds_load_acq(&fin) == kSlots) break;
+      if (idle < 8)
+        __builtin_amdgcn_s_sleep(1);
+      else
+        __builtin_amdgcn_s_sleep(4);
+      ++idle;
     }
-    // the block's merge (db/log_reader.cc:221-255)
-    if (tid == 0) {
-      log_stamp(a, k, 5);
-      const uint32_t bad = first_bad;
-      uint8_t status = walked[cur];
-      uint64_t drop = 0;
-      if (bad != 0xffffffffu) {
-        status = LVKV_LOGBLK_CHECKSUM;
-        drop = s.end - (s.start + pos[cur][bad]);  // ReportCorruption(buffer_.size(), ...)
-      } else if (status == LVKV_LOGBLK_BAD_LENGTH) {
-        drop = (s.end - s.start) - stop[cur];  // ReportCorruption(drop_size, "bad record length")
-      }
-      a.block_status[b] = status;
-      a.block_drop[b] = static_cast<uint32_t>(drop);
-      // the block's event follows its c records: item base + c + b
-      if (a.events != nullptr && base_s + c <= a.capacity)
-        a.events[base_s + c + b] = log_block_event(status, static_cast<uint32_t>(drop));
-      a.good[b] = bad != 0xffffffffu ? bad : c;
-      bad_s = bad;
-    }
-    __syncthreads();
-    // records after the first mismatch: the reader cleared the buffer (:248-255)
-    const uint32_t bad = bad_s;
-    if (bad != 0xffffffffu)
-      for (uint32_t j = bad + 1 + tid; j < c; j += kVThreads)
-        if (base_s + j < a.capacity) {
-          a.rec_status[base_s + j] = LVKV_REC_DROPPED;
-          if (a.events != nullptr) a.events[base_s + j + b] = log_event(kEvSkip, 0, 0);
-        }
-    __syncthreads();  // pos[cur], ready, first_bad are reused
-    if (tid == 0) log_stamp(a, k, 6);
   }
 
-  // The last workgroup to finish writes the report (one fetch-add each on a
-  // counter zeroed on the stream before the launch: a compare-and-swap loop
-  // over 256 contending workgroups serialises hundreds of memory round trips).
+  // The last workgroup to finish scans the blocks' counts into their first
+  // record indices and writes the report. Every wave's stores are waited for
+  // at the barrier and the per-block words the scan reads were stored sc1,
+  // so one agent-scope add per workgroup publishes them (no fence).
+  __syncthreads();
+  if (tid == 0) log_stamp(a, 0, 15, 2);
   if (tid == 0) {
-    __threadfence();
-    const uint64_t old = __hip_atomic_fetch_add(a.done, uint64_t{1}, __ATOMIC_ACQ_REL,
+    const uint64_t old = __hip_atomic_fetch_add(a.done, uint64_t{1}, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
-    last_s = old + 1 == G ? 1u : 0u;
+    last_s = old + 1 == gridDim.x ? 1u : 0u;
     red_good = 0;
     red_drop = 0;
     red_corrupt = 0;
@@ -626,32 +774,71 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
   }
   __syncthreads();
   if (!last_s) return;
-  __threadfence();
-  // the next call on this stream reuses the scratch: leave the counter at 0
-  if (tid == 0) __hip_atomic_store(a.done, uint64_t{0}, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) log_stamp(a, 0, 15, 3);
+  // the next call with this scratch reuses the counters: leave them at 0
+  if (tid == 0) {
+    __hip_atomic_store(a.done, uint64_t{0}, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.stg_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // thread t: a contiguous run of blocks; its count sum, scanned over the
+  // workgroup (wave shuffles, then the 16 wave sums through LDS)
+  const uint32_t per = (a.nblocks + kVThreads - 1) / kVThreads;
+  const uint32_t b0 = min(a.nblocks, tid * per), b1 = min(a.nblocks, b0 + per);
   unsigned long long g = 0, d = 0;
   uint32_t nc = 0, fb = 0xffffffffu;
-  for (uint32_t b = tid; b < a.nblocks; b += kVThreads) {
-    const uint8_t st = __hip_atomic_load(&a.block_status[b], __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-    g += __hip_atomic_load(&a.good[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t mine = 0;
+  uint32_t cnt[8];  // this thread's blocks' counts (runs of <= 8 here; longer runs reload)
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint64_t x = __hip_atomic_load(&a.info[b].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t y = __hip_atomic_load(&a.info[b].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t st = static_cast<uint32_t>(y >> 32);
+    const uint32_t cb = static_cast<uint32_t>(x);
+    if (b - b0 < 8) cnt[b - b0] = cb;
+    g += x >> 32;
+    mine += cb;
     if (st == LVKV_LOGBLK_CHECKSUM || st == LVKV_LOGBLK_BAD_LENGTH) {
       ++nc;
-      d += __hip_atomic_load(&a.block_drop[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      d += static_cast<uint32_t>(y);
       fb = min(fb, b);
     }
   }
-  atomicAdd(&red_good, g);
-  atomicAdd(&red_drop, d);
-  atomicAdd(&red_corrupt, nc);
-  atomicMin(&red_first, fb);
+  // per-wave sums first: 1024 LDS atomics on one address would serialise
+#pragma unroll
+  for (uint32_t dd = 32; dd >= 1; dd >>= 1) {
+    g += __shfl_xor(g, dd, 64);
+    d += __shfl_xor(d, dd, 64);
+    nc += __shfl_xor(nc, dd, 64);
+    fb = min(fb, static_cast<uint32_t>(__shfl_xor(fb, dd, 64)));
+  }
+  if (lane == 0) {
+    atomicAdd(&red_good, g);
+    atomicAdd(&red_drop, d);
+    atomicAdd(&red_corrupt, nc);
+    atomicMin(&red_first, fb);
+  }
+  uint64_t inc = mine;
+#pragma unroll
+  for (uint32_t dd = 1; dd < 64; dd <<= 1) {
+    const uint64_t o = __shfl_up(static_cast<unsigned long long>(inc), dd, 64);
+    if (lane >= dd) inc += o;
+  }
+  if (lane == 63) wsum_s[wave] = inc;
+  __syncthreads();
+  uint64_t pre = 0, total = 0;
+  for (uint32_t w = 0; w < kVW; ++w) {
+    if (w < wave) pre += wsum_s[w];
+    total += wsum_s[w];
+  }
+  uint64_t at = pre + inc - mine;
+  for (uint32_t b = b0; b < b1; ++b) {
+    a.first[b] = static_cast<uint32_t>(at);
+    at += b - b0 < 8 ? cnt[b - b0]
+                     : static_cast<uint32_t>(__hip_atomic_load(&a.info[b].x, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT));
+  }
   __syncthreads();
   if (tid == 0) {
-    const uint64_t total =
-        a.nblocks ? (__hip_atomic_load(&a.inc[a.nblocks - 1], __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT) &
-                     ((uint64_t{1} << 36) - 1))
-                  : 0;
     lvkv_log_report* r = a.r;
     r->status = total > a.capacity ? LVKV_LOG_CAPACITY : LVKV_OK;
     r->nblocks = a.nblocks;
@@ -662,32 +849,67 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
     r->dropped_bytes = red_drop;
     r->count_ = total > a.capacity ? 0u : static_cast<uint32_t>(total);
     r->reserved_ = 0;
+    log_stamp(a, 0, 15, 4);
   }
+}
+
+// The staged results to their places, one wave per block: record j of block
+// b is record first[b] + j in file order; the block's ReadRecord event
+// follows its records (item first[b] + counts[b] + b, lvkv_log_events.h).
+__global__ void __launch_bounds__(256) log_emit_kernel(LogArgs a) {
+  const uint32_t b = blockIdx.x * 4u + (threadIdx.x >> 6);
+  const uint32_t lane = lane_id();
+  if (b >= a.nblocks) return;
+  const uint32_t c = static_cast<uint32_t>(a.info[b].x), off = a.stg_off[b], base = a.first[b];
+  const uint64_t start = uint64_t{b} * kLogBlock;
+  for (uint32_t j = lane; j < c; j += 64) {
+    const uint64_t gi = uint64_t{base} + j;
+    if (gi >= a.capacity || off + j >= a.capacity) break;
+    const uint4 e = a.stg[off + j];
+    a.hdr_off[gi] = start + (e.y & 0xffffu);
+    a.actual[gi] = e.x;
+    a.rec_status[gi] = static_cast<uint8_t>(e.w);
+    if (a.events != nullptr)
+      a.events[gi + b] = e.w == LVKV_REC_OK ? log_event(kEvRec, e.z, e.y >> 16)
+                                             : log_event(kEvSkip, 0, 0);
+  }
+  if (lane == 0 && a.events != nullptr && uint64_t{base} + c <= a.capacity)
+    a.events[uint64_t{base} + c + b] = log_block_event(a.block_status[b], a.block_drop[b]);
+}
+
+// Scratch: [0, 8) done counter, [8, 16) the logical layer's counter (not
+// touched here), [16, 20) ticket counter, [20, 24) staging counter, then
+// from byte 32 info (16 B per block), stg_off and first (u32 per block),
+// the staging array (16 B per record, `capacity` of them) and the slots'
+// overflow positions (u32, kPosOver per slot of each of the grid's
+// workgroups).
+size_t log_scratch_head(uint64_t nblocks) {
+  return (32 + static_cast<size_t>(nblocks) * 24 + 15) & ~size_t{15};
+}
+
+// One workgroup per CU at most (each takes most of a CU's LDS); blocks are
+// claimed by ticket, so the grid need not be resident all at once.
+uint32_t log_groups(uint64_t nblocks, int cus) {
+  return static_cast<uint32_t>(std::max<uint64_t>(
+      1, std::min<uint64_t>((nblocks + kSlots - 1) / kSlots, static_cast<uint64_t>(cus))));
 }
 
 }  // namespace
 
-uint32_t next_log_generation() {
-  static std::atomic<uint32_t> g{0};
-  uint32_t v;
-  do {
-    v = (g.fetch_add(1, std::memory_order_relaxed) + 1) & 0x3ffffffu;
-  } while (v == 0);
-  return v;
-}
-
 #ifdef LVKV_PROBE_BUILD
 uint64_t* g_log_stamps = nullptr;  // lvkv_debug_log_stamps
-uint32_t g_log_knobs = 0;          // lvkv_debug_log_knobs
+uint32_t g_log_knobs = 0;          // lvkv_debug_log_knobs (no knobs in this kernel)
 #endif
 
-size_t log_scratch_bytes(uint64_t size) {
+size_t log_scratch_bytes(uint64_t size, uint32_t capacity, int cus) {
   const uint64_t nblocks = (size + kLogBlock - 1) / kLogBlock;
-  return 16 + static_cast<size_t>(nblocks) * 20 + 8;
+  return log_scratch_head(nblocks) + size_t{capacity} * 16 +
+         size_t{log_groups(nblocks, cus)} * kSlots * kPosOver * 4;
 }
 
-// `scratch`: log_scratch_bytes(size) bytes, 8-byte aligned, its first word 0
-// (zeroed when allocated; every call leaves it at 0), used by one stream.
+// `scratch`: log_scratch_bytes(size, capacity, cus) bytes, 16-byte aligned,
+// its counters 0 (zeroed when allocated; every call leaves them at 0), used
+// by one call at a time. Two launches: the verify, then the emit.
 hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_off,
                              uint32_t* actual, uint8_t* rec_status, uint32_t capacity,
                              uint8_t* block_status, uint32_t* block_drop, lvkv_log_report* r,
@@ -700,28 +922,32 @@ hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_o
   a.size = size;
   a.nblocks = nblocks;
   a.capacity = capacity;
-  a.gen = next_log_generation();
   a.hdr_off = hdr_off;
   a.actual = actual;
   a.rec_status = rec_status;
   a.block_status = block_status;
   a.block_drop = block_drop;
   a.r = r;
-  a.done = static_cast<uint64_t*>(scratch);
-  a.agg = a.done + 2;
-  a.inc = a.agg + nblocks;
-  a.good = reinterpret_cast<uint32_t*>(a.inc + nblocks);
+  uint8_t* sb = static_cast<uint8_t*>(scratch);
+  a.done = reinterpret_cast<uint64_t*>(sb);
+  a.ticket = reinterpret_cast<uint32_t*>(sb + 16);
+  a.stg_top = reinterpret_cast<uint32_t*>(sb + 20);
+  a.info = reinterpret_cast<ulonglong2*>(sb + 32);
+  a.stg_off = reinterpret_cast<uint32_t*>(a.info + nblocks);
+  a.first = a.stg_off + nblocks;
+  a.stg = reinterpret_cast<uint4*>(sb + log_scratch_head(nblocks));
+  a.over = reinterpret_cast<uint32_t*>(a.stg + capacity);
   a.zpow = zpow;
   a.lane_cols = lane_cols;
   a.events = events;
 #ifdef LVKV_PROBE_BUILD
   a.stamps = g_log_stamps;
-  a.knobs = g_log_knobs;
 #endif
-  // every workgroup resident at once (one per CU): a placement only waits on
-  // block counts, and every block is walked an iteration before it is placed
-  const uint32_t groups = max(1u, min(nblocks, static_cast<uint32_t>(cus)));
-  hipLaunchKernelGGL(log_verify_kernel, dim3(groups), dim3(kVThreads), 0, stream, a);
+  hipLaunchKernelGGL(log_verify_kernel, dim3(log_groups(nblocks, cus)), dim3(kVThreads), 0,
+                     stream, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || nblocks == 0) return e;
+  hipLaunchKernelGGL(log_emit_kernel, dim3((nblocks + 3u) / 4u), dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 

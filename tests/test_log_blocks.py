@@ -262,3 +262,97 @@ def test_device_fill_headers_rebuilds_the_log(lvkv, gpu, source):
     assert bytes(buf.cpu().numpy()) == img
     want = [oracle.value(img[h + 6: h + 7 + (img[h + 4] | img[h + 5] << 8)]) for h in hdrs]
     assert list(crc.cpu().numpy().view(np.uint32)) == want
+
+
+@pytest.mark.gpu
+def test_device_log_two_streams_at_once(lvkv, gpu):
+    """Two WAL verifies in flight on two streams (and back to back on each):
+    blocks are claimed by ticket and each call has its own scratch, so the
+    calls neither deadlock nor share counters; every result equals the
+    one-call result."""
+    import torch
+    L = lvkv.lib
+    vp = ctypes.c_void_p
+    imgs = [log_synth.build_log(6000, seed=21, max_len=3000, big_every=211),
+            log_synth.build_log(9000, seed=22, max_len=1500, big_every=0)]
+    want = [_device(lvkv, img, gpu) for img in imgs]
+    streams = [torch.cuda.Stream(gpu), torch.cuda.Stream(gpu)]
+    outs = []
+    for rep_i in range(3):
+        for k, img in enumerate(imgs):
+            buf = torch.from_numpy(np.frombuffer(img, dtype=np.uint8).copy()).to(gpu)
+            torch.cuda.synchronize()
+            cap = want[k][0]["nrecords"] + 1
+            nb = (len(img) + 32767) // 32768
+            o = dict(buf=buf, hdr=torch.empty(cap, dtype=torch.int64, device=gpu),
+                     act=torch.empty(cap, dtype=torch.int32, device=gpu),
+                     rst=torch.empty(cap, dtype=torch.uint8, device=gpu),
+                     bst=torch.empty(nb, dtype=torch.uint8, device=gpu),
+                     bdr=torch.empty(nb, dtype=torch.int32, device=gpu),
+                     rep=torch.zeros(ctypes.sizeof(lvkv.LogReport), dtype=torch.uint8, device=gpu),
+                     k=k)
+            outs.append(o)
+    # launch everything without a host sync in between, alternating streams
+    for i, o in enumerate(outs):
+        s = streams[i % 2]
+        rc = L.lvkv_log_verify_blocks_device(
+            vp(o["buf"].data_ptr()), o["buf"].numel(), vp(o["hdr"].data_ptr()),
+            vp(o["act"].data_ptr()), vp(o["rst"].data_ptr()), o["hdr"].numel(),
+            vp(o["bst"].data_ptr()), vp(o["bdr"].data_ptr()), vp(o["rep"].data_ptr()),
+            vp(s.cuda_stream))
+        assert rc == 0
+    torch.cuda.synchronize()
+    for o in outs:
+        rep, hdr, actual, rst, bst, bdrop = want[o["k"]]
+        r = lvkv.LogReport.from_buffer_copy(bytes(o["rep"].cpu().numpy())).as_dict()
+        assert r == rep
+        n = rep["nrecords"]
+        assert np.array_equal(o["hdr"][:n].cpu().numpy(), hdr)
+        assert np.array_equal(o["act"][:n].cpu().numpy().view(np.uint32), actual)
+        assert np.array_equal(o["rst"][:n].cpu().numpy(), rst)
+        assert np.array_equal(o["bst"].cpu().numpy(), bst)
+
+
+@pytest.mark.gpu
+def test_device_log_refuses_stream_capture(lvkv, gpu):
+    """The verify's scratch counters are zeroed once and left at 0 by each
+    call: a captured graph would replay them unzeroed, so capture is refused
+    (LVKV_ERR_INVALID) instead of recorded."""
+    import torch
+    img = log_synth.build_log(50, seed=5)
+    buf = torch.from_numpy(np.frombuffer(img, dtype=np.uint8).copy()).to(gpu)
+    L = lvkv.lib
+    vp = ctypes.c_void_p
+    hdr = torch.empty(64, dtype=torch.int64, device=gpu)
+    act = torch.empty(64, dtype=torch.int32, device=gpu)
+    rst = torch.empty(64, dtype=torch.uint8, device=gpu)
+    bst = torch.empty(4, dtype=torch.uint8, device=gpu)
+    bdr = torch.empty(4, dtype=torch.int32, device=gpu)
+    rep = torch.zeros(ctypes.sizeof(lvkv.LogReport), dtype=torch.uint8, device=gpu)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(gpu)
+    rcs = []
+    with torch.cuda.stream(s):
+        g.capture_begin()
+        rcs.append(L.lvkv_log_verify_blocks_device(
+            vp(buf.data_ptr()), len(img), vp(hdr.data_ptr()), vp(act.data_ptr()),
+            vp(rst.data_ptr()), 64, vp(bst.data_ptr()), vp(bdr.data_ptr()), vp(rep.data_ptr()),
+            vp(s.cuda_stream)))
+        hdr.add_(0)  # capture something so the graph is not empty
+        g.capture_end()
+    assert rcs == [lvkv.LVKV_ERR_INVALID]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_len", [1, 24])
+def test_device_log_dense_blocks(lvkv, gpu, max_len):
+    """Blocks of thousands of tiny records (7-30 bytes each: up to 4681 in a
+    block), past what a slot keeps in LDS: the positions beyond it go
+    through the slot's scratch overflow. Also a few damaged ones."""
+    img = log_synth.build_log(12_000, seed=31 + max_len, max_len=max_len)
+    _assert_matches(lvkv, img, gpu)
+    b = bytearray(img)
+    for p in (40_000, 70_001, len(b) // 2 + 3):
+        b[p] ^= 0x10
+    _assert_matches(lvkv, bytes(b), gpu)

@@ -80,6 +80,34 @@ __device__ uint32_t walk_lds_valu(const uint8_t* blk, uint32_t n) {
   return k;
 }
 
+// variant 4: unaligned ds_read_u16 of the length (+ ds_read_u8 of the type),
+// the next header's reads issued before this header's stop test
+__device__ uint32_t walk_lds_u16(const uint8_t* blk, uint32_t n) {
+  uint32_t k = 0;
+  if (n < kHdr) return 0;
+  const uint32_t base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(blk));
+  const uint32_t end = base + n;
+  uint32_t bp = base, len, typ, nlen, ntyp;
+  asm volatile("ds_read_u16 %0, %2 offset:4\n\tds_read_u8 %1, %2 offset:6\n\ts_waitcnt lgkmcnt(0)"
+               : "=v"(len), "=v"(typ) : "v"(bp));
+  for (;;) {
+    const uint32_t nbp = bp + kHdr + len;
+    asm volatile("ds_read_u16 %0, %2 offset:4\n\tds_read_u8 %1, %2 offset:6"
+                 : "=v"(nlen), "=v"(ntyp) : "v"(nbp));
+    __builtin_amdgcn_sched_barrier(0);
+    const bool bad = nbp > end || (len | typ) == 0;
+    if (__builtin_amdgcn_ballot_w64(bad)) break;
+    ++k;
+    bp = nbp;
+    if (__builtin_amdgcn_ballot_w64(end - bp < kHdr)) break;
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nlen), "+v"(ntyp));
+    len = nlen;
+    typ = ntyp;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nlen), "+v"(ntyp));
+  return k;
+}
+
 // variant 2: scalar loads from global memory
 __device__ uint32_t walk_glb_salu(const uint8_t* blk, uint32_t n) {
   uint32_t p = 0, k = 0;
@@ -135,7 +163,7 @@ __global__ void __launch_bounds__(kThreads, 1)
     uint32_t acc = 0;
     for (uint32_t o = lane * 16; o < kBlock; o += 64 * 16) {
       const uint4 v = *reinterpret_cast<const uint4*>(src + o);
-      if (V <= 1) *reinterpret_cast<uint4*>(mine + o) = v;
+      if (V <= 1 || V == 4) *reinterpret_cast<uint4*>(mine + o) = v;
       acc ^= v.x ^ v.y ^ v.z ^ v.w;
     }
     __builtin_amdgcn_s_waitcnt(0);
@@ -146,6 +174,7 @@ __global__ void __launch_bounds__(kThreads, 1)
     if (V == 0) k = walk_lds_salu(mine, kBlock);
     else if (V == 1) k = walk_lds_valu(mine, kBlock);
     else if (V == 2) k = walk_glb_salu(src, kBlock);
+    else if (V == 4) k = walk_lds_u16(mine, kBlock);
     else k = walk_glb_vmem(src, kBlock);
     const uint64_t c1 = __builtin_amdgcn_s_memtime();
     cyc += c1 - c0;
@@ -191,13 +220,12 @@ int main(int argc, char** argv) {
   hipMalloc(&d_out, sizeof(Out) * 256 * 16 + 16);
   int cus = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
-  const char* names[] = {"lds_salu", "lds_valu", "glb_salu", "glb_vmem"};
+  const char* names[] = {"lds_salu", "lds_valu", "glb_salu", "glb_vmem", "lds_u16"};
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  for (int v = 0; v < 4; ++v) {
-    for (uint32_t walkers : {1u, 2u, 4u, 8u, 16u}) {
-      if (v <= 1 && walkers > 4) continue;  // one LDS area per walker
+  for (int v : {0, 1, 4}) {
+    for (uint32_t walkers : {1u, 2u, 4u}) {
       float best = 1e9f;
       std::vector<Out> h(256 * 16);
       for (int rep = 0; rep < 3; ++rep) {
@@ -207,7 +235,8 @@ int main(int argc, char** argv) {
           case 0: hipLaunchKernelGGL(walk_kernel<0>, dim3(cus), dim3(kThreads), 0, 0, d_img, nblk, walkers, d_out); break;
           case 1: hipLaunchKernelGGL(walk_kernel<1>, dim3(cus), dim3(kThreads), 0, 0, d_img, nblk, walkers, d_out); break;
           case 2: hipLaunchKernelGGL(walk_kernel<2>, dim3(cus), dim3(kThreads), 0, 0, d_img, nblk, walkers, d_out); break;
-          default: hipLaunchKernelGGL(walk_kernel<3>, dim3(cus), dim3(kThreads), 0, 0, d_img, nblk, walkers, d_out); break;
+          case 3: hipLaunchKernelGGL(walk_kernel<3>, dim3(cus), dim3(kThreads), 0, 0, d_img, nblk, walkers, d_out); break;
+          default: hipLaunchKernelGGL(walk_kernel<4>, dim3(cus), dim3(kThreads), 0, 0, d_img, nblk, walkers, d_out); break;
         }
         hipEventRecord(e1);
         hipEventSynchronize(e1);
@@ -221,8 +250,10 @@ int main(int argc, char** argv) {
         c += o.cycles;
         k += o.headers;
       }
-      printf("%-9s walkers/CU %2u: %.1f cycles/header (%llu headers), kernel %.1f us for %u blocks\n",
-             names[v], walkers, k ? double(c) / double(k) : 0.0, k, best * 1e3, nblk);
+      printf("%-9s walkers/CU %2u: %.1f ticks/header (%llu headers), kernel %.1f us for %u blocks, "
+             "%.1f ns/header/walker\n",
+             names[v], walkers, k ? double(c) / double(k) : 0.0, k, best * 1e3, nblk,
+             best * 1e6 / (double(k) / (cus * walkers)));
     }
   }
   return 0;
