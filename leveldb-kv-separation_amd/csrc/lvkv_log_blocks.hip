@@ -17,25 +17,25 @@
 //                      headers, reserves the block's records a run of the
 //                      staging array (an atomic bump), waits for the block's
 //                      CRCs and stages the block's results.
-//                      The walk is a chain of dependent LDS reads (≈ 170 ns a
-//                      header whatever else the CU does, measured with
-//                      tools/probe/walk_probe.hip): it is the kernel's
-//                      critical path, so a CU walks two blocks at once, and
-//                      the fourteen other waves checksum each record as soon as
-//                      the walker has published its position (records two at
-//                      a time, from any slot). Records over kSegBytes are cut
-//                      into 4 KiB segments on the end-aligned grid,
-//                      checksummed by several waves and folded with
-//                      Z_{i·4 KiB} (the zmul columns). The block's merge
-//                      (db/log_reader.cc:221-255): the first mismatch drops
-//                      the rest of the block; block status and drop bytes.
-//                      Nothing waits for a block's place in file order (that
-//                      would wait for the slowest block in flight before it):
-//                      the last workgroup to finish scans the per-block counts
-//                      into each block's first record index and writes the
-//                      report.
-//   log_emit_kernel    one wave per block moves the staged results to their
-//                      places (and writes the ReadRecord event stream).
+//                      The walk is a chain of dependent LDS reads (≈ 80 ns
+//                      a header alone, ≈ 200 ns beside the record waves'
+//                      traffic, tools/probe/walk_probe.hip and the phase
+//                      stamps): it is the kernel's critical path, so a CU
+//                      walks two blocks at once. The fourteen other waves
+//                      checksum each record as soon as the walker has
+//                      published its position (records two at a time, from
+//                      any slot). Records over kSegBytes are cut into 4 KiB
+//                      segments on the end-aligned grid, checksummed by
+//                      several waves and folded with Z_{i·4 KiB} (the zmul
+//                      columns). The block's merge (db/log_reader.cc:221-255):
+//                      the first mismatch drops the rest of the block; block
+//                      status and drop bytes. Nothing waits for a block's
+//                      place in file order (that would wait for the slowest
+//                      block in flight before it).
+//   log_emit_kernel    one wave per block: its first record index (the counts
+//                      of the blocks before it, summed by each workgroup), the
+//                      staged results moved to their places (and the ReadRecord
+//                      event stream); the last workgroup writes the report.
 //
 // The CRC (same arithmetic as every kernel here): rows of 64
 // words folded with Z_256 by four byte lookups in LDS, then each lane's
@@ -46,7 +46,7 @@
 // 66 MB log): the workers, not the walks, then set the pace.
 //
 // Scratch (lvkv_capi.cpp, one buffer per call in flight): counters left at 0
-// by the last workgroup of every call, per-block words, the staging array
+// by the emit launch of every call, per-block words, the staging array
 // and each slot's overflow positions (blocks of more than kPosLds records).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -90,16 +90,15 @@ struct LogArgs {
   lvkv_log_report* r;
   ulonglong2* info;  // nblocks: {count | good << 32, drop | status << 32}
   uint32_t* stg_off; // nblocks: the block's first entry in `stg`
-  uint32_t* first;   // nblocks: the block's first record index (file order)
   uint4* stg;        // capacity: per record {actual, pos | len << 16, type, status}
   uint32_t* over;    // groups x kSlots x kPosOver: positions past kPosLds
-  uint64_t* done;    // finished workgroups (left at 0)
-  uint32_t* ticket;  // blocks claimed (left at 0)
-  uint32_t* stg_top; // staging entries reserved (left at 0)
+  uint32_t* ticket;  // blocks claimed (left at 0 by the emit launch)
+  uint32_t* stg_top; // staging entries reserved (left at 0 by the emit launch)
   const uint32_t* zpow;
   const uint32_t* lane_cols;
   uint32_t* events;  // nullable: the ReadRecord event stream (lvkv_log_events.h)
   uint64_t* stamps;  // probe build only: 8 u64 per (workgroup, slot, block)
+  uint32_t knobs;    // probe build only: bit 0 = workers idle, no CRCs (timing)
 };
 
 // Manager phase stamps (probe build): 0 claimed, 1 in LDS, 2 walked,
@@ -315,9 +314,15 @@ __device__ __forceinline__ void put_pos(uint16_t* pos, uint32_t* over, uint32_t 
 // explicit lgkmcnt waits (an asm load's destination is written late, so it
 // must stay live until a wait has seen it land). Positions collect in a
 // register (record k in lane k % 64) and are written 8 at a time.
+// (Measured against: the block held in an 8 KiB register window, each
+// header read by a uniform register index and v_readlane, the chain on the
+// scalar unit: 320 shader clocks a header alone against this walk's 193,
+// tools/probe/walk_probe.hip variant 5; the cross-unit chain is longer than
+// the LDS round trip.)
 __device__ __forceinline__ uint8_t walk_block(const uint8_t* blk, uint32_t n, bool eof,
                                               uint16_t* pos, uint32_t* over, Slot& S,
-                                              uint32_t gen, uint32_t* count, uint32_t* stop) {
+                                              uint32_t gen, uint32_t* count, uint32_t* stop,
+                                              const LogArgs& la, uint32_t sm, uint32_t sk) {
   const uint32_t lane = lane_id();
   const uint32_t base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(blk));
   const uint32_t end = base + n;
@@ -329,6 +334,7 @@ __device__ __forceinline__ uint8_t walk_block(const uint8_t* blk, uint32_t n, bo
     asm volatile("ds_read_u16 %0, %2 offset:4\n\tds_read_u8 %1, %2 offset:6\n\ts_waitcnt lgkmcnt(0)"
                  : "=v"(len), "=v"(typ)
                  : "v"(bp));
+    log_stamp(la, sm, sk, 5);
     for (;;) {
       const uint32_t nbp = bp + kLogHeader + len;
       asm volatile("ds_read_u16 %0, %2 offset:4\n\tds_read_u8 %1, %2 offset:6"
@@ -377,6 +383,7 @@ __device__ __forceinline__ uint8_t walk_block(const uint8_t* blk, uint32_t n, bo
     }
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nlen), "+v"(ntyp));
   }
+  log_stamp(la, sm, sk, 6);
   const uint32_t p = __builtin_amdgcn_readfirstlane(bp - base);
   len = __builtin_amdgcn_readfirstlane(len);
   // the last 0-7 positions
@@ -415,9 +422,6 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
   __shared__ uint16_t pos[kSlots][kPosLds];
   __shared__ Slot slots[kSlots];
   __shared__ uint32_t fin;
-  __shared__ unsigned long long red_good, red_drop;
-  __shared__ uint32_t red_corrupt, red_first, last_s;
-  __shared__ uint64_t wsum_s[kVW];
 
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = lane_id();
@@ -485,7 +489,7 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
       log_stamp(a, m, k, 1);
       const uint8_t* blk = sbuf + S.shift;
       uint32_t c, stop_at;
-      const uint8_t walked = walk_block(blk, n, eof, spos, sover, S, gen, &c, &stop_at);
+      const uint8_t walked = walk_block(blk, n, eof, spos, sover, S, gen, &c, &stop_at, a, m, k);
       // the block's run of staging entries (the atomic's round trip overlaps
       // the CRCs: its value is first used by the staging stores)
       uint32_t off = 0;
@@ -506,7 +510,8 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
         }
       }
       // the block's CRCs (the workers'); the merge (db/log_reader.cc:221-255)
-      while (lds_load_acq(&S.crcd) < c) __builtin_amdgcn_s_sleep(1);
+      if (!(a.knobs & 1u))
+        while (lds_load_acq(&S.crcd) < c) __builtin_amdgcn_s_sleep(1);
       asm volatile("" ::"v"(sink));
       log_stamp(a, m, k, 3);
       const uint32_t bad = S.first_bad;
@@ -575,6 +580,11 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
     L.keys = lane_keys(lane);
     L.lane_base = compact_lane_base(lane);
     for (uint32_t idle = 0;;) {
+      if (a.knobs & 1u) {
+        if (lds_load_acq(&fin) == kSlots) break;
+        __builtin_amdgcn_s_sleep(127);
+        continue;
+      }
       bool worked = false;
 #pragma unroll 1
       for (uint32_t si = 0; si < kSlots; ++si) {
@@ -757,113 +767,111 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
     }
   }
 
-  // The last workgroup to finish scans the blocks' counts into their first
-  // record indices and writes the report. Every wave's stores are waited for
-  // at the barrier and the per-block words the scan reads were stored sc1,
-  // so one agent-scope add per workgroup publishes them (no fence).
-  __syncthreads();
   if (tid == 0) log_stamp(a, 0, 15, 2);
-  if (tid == 0) {
-    const uint64_t old = __hip_atomic_fetch_add(a.done, uint64_t{1}, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-    last_s = old + 1 == gridDim.x ? 1u : 0u;
-    red_good = 0;
-    red_drop = 0;
-    red_corrupt = 0;
-    red_first = 0xffffffffu;
+  // Nothing more: the block counts' scan into file order and the report are
+  // the emit launch's (every workgroup scans the counts before its blocks),
+  // so no workgroup here waits for the last one to finish.
+}
+
+constexpr uint32_t kEmitWaves = 16;  // blocks per emit workgroup (one wave each)
+
+// The staged results to their places, one wave per block: record j of block
+// b is record first[b] + j in file order, first[b] = the counts of the
+// blocks before b (each workgroup sums them: 2 loads a thread for a 66 MB
+// log, all workgroups at once, instead of one workgroup scanning after the
+// verify's last one finished); the block's ReadRecord event follows its
+// records (item first[b] + counts[b] + b, lvkv_log_events.h). The last
+// workgroup also sums everything into the report; workgroup 0 leaves the
+// verify's counters at 0 for the next call (the verify has ended: stream
+// order).
+__global__ void __launch_bounds__(64 * kEmitWaves) log_emit_kernel(LogArgs a) {
+  __shared__ unsigned long long s_cnt[kEmitWaves], s_good[kEmitWaves], s_drop[kEmitWaves];
+  __shared__ uint32_t s_corrupt[kEmitWaves], s_first[kEmitWaves];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t b0 = blockIdx.x * kEmitWaves;
+  const bool last = blockIdx.x + 1 == gridDim.x;
+  if (blockIdx.x == 0 && tid == 0) {
+    *a.ticket = 0;
+    *a.stg_top = 0;
   }
-  __syncthreads();
-  if (!last_s) return;
-  if (tid == 0) log_stamp(a, 0, 15, 3);
-  // the next call with this scratch reuses the counters: leave them at 0
-  if (tid == 0) {
-    __hip_atomic_store(a.done, uint64_t{0}, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(a.stg_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // thread t: a contiguous run of blocks; its count sum, scanned over the
-  // workgroup (wave shuffles, then the 16 wave sums through LDS)
-  const uint32_t per = (a.nblocks + kVThreads - 1) / kVThreads;
-  const uint32_t b0 = min(a.nblocks, tid * per), b1 = min(a.nblocks, b0 + per);
-  unsigned long long g = 0, d = 0;
-  uint32_t nc = 0, fb = 0xffffffffu;
-  uint64_t mine = 0;
-  uint32_t cnt[8];  // this thread's blocks' counts (runs of <= 8 here; longer runs reload)
-  for (uint32_t b = b0; b < b1; ++b) {
-    const uint64_t x = __hip_atomic_load(&a.info[b].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t y = __hip_atomic_load(&a.info[b].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t st = static_cast<uint32_t>(y >> 32);
-    const uint32_t cb = static_cast<uint32_t>(x);
-    if (b - b0 < 8) cnt[b - b0] = cb;
-    g += x >> 32;
-    mine += cb;
-    if (st == LVKV_LOGBLK_CHECKSUM || st == LVKV_LOGBLK_BAD_LENGTH) {
-      ++nc;
-      d += static_cast<uint32_t>(y);
-      fb = min(fb, b);
+  // counts before b0 (and, in the last workgroup, every block's totals)
+  const uint32_t upto = last ? a.nblocks : min(b0, a.nblocks);
+  unsigned long long cnt = 0, good = 0, drop = 0;
+  uint32_t corrupt = 0, fb = 0xffffffffu;
+  for (uint32_t b = tid; b < upto; b += 64 * kEmitWaves) {
+    const ulonglong2 v = a.info[b];
+    const uint32_t c = static_cast<uint32_t>(v.x);
+    if (b < b0) cnt += c;
+    if (last) {
+      const uint32_t st = static_cast<uint32_t>(v.y >> 32);
+      good += v.x >> 32;
+      if (st == LVKV_LOGBLK_CHECKSUM || st == LVKV_LOGBLK_BAD_LENGTH) {
+        ++corrupt;
+        drop += static_cast<uint32_t>(v.y);
+        fb = min(fb, b);
+      }
+      if (b >= b0) cnt += uint64_t{c} << 32;  // this workgroup's own blocks, kept apart
     }
   }
-  // per-wave sums first: 1024 LDS atomics on one address would serialise
 #pragma unroll
   for (uint32_t dd = 32; dd >= 1; dd >>= 1) {
-    g += __shfl_xor(g, dd, 64);
-    d += __shfl_xor(d, dd, 64);
-    nc += __shfl_xor(nc, dd, 64);
+    cnt += __shfl_xor(cnt, dd, 64);
+    good += __shfl_xor(good, dd, 64);
+    drop += __shfl_xor(drop, dd, 64);
+    corrupt += __shfl_xor(corrupt, dd, 64);
     fb = min(fb, static_cast<uint32_t>(__shfl_xor(fb, dd, 64)));
   }
   if (lane == 0) {
-    atomicAdd(&red_good, g);
-    atomicAdd(&red_drop, d);
-    atomicAdd(&red_corrupt, nc);
-    atomicMin(&red_first, fb);
+    s_cnt[wave] = cnt;
+    s_good[wave] = good;
+    s_drop[wave] = drop;
+    s_corrupt[wave] = corrupt;
+    s_first[wave] = fb;
   }
-  uint64_t inc = mine;
+  __syncthreads();
+  unsigned long long before = 0, mine_all = 0;
 #pragma unroll
-  for (uint32_t dd = 1; dd < 64; dd <<= 1) {
-    const uint64_t o = __shfl_up(static_cast<unsigned long long>(inc), dd, 64);
-    if (lane >= dd) inc += o;
+  for (uint32_t w = 0; w < kEmitWaves; ++w) {
+    before += s_cnt[w] & 0xffffffffull;
+    mine_all += s_cnt[w] >> 32;
   }
-  if (lane == 63) wsum_s[wave] = inc;
-  __syncthreads();
-  uint64_t pre = 0, total = 0;
-  for (uint32_t w = 0; w < kVW; ++w) {
-    if (w < wave) pre += wsum_s[w];
-    total += wsum_s[w];
-  }
-  uint64_t at = pre + inc - mine;
-  for (uint32_t b = b0; b < b1; ++b) {
-    a.first[b] = static_cast<uint32_t>(at);
-    at += b - b0 < 8 ? cnt[b - b0]
-                     : static_cast<uint32_t>(__hip_atomic_load(&a.info[b].x, __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_AGENT));
-  }
-  __syncthreads();
-  if (tid == 0) {
+  // (a count is at most kMaxRecs and a log at most 2^32 records: the low
+  // halves do not carry into the high ones)
+  if (last && tid == 0) {
+    unsigned long long g = 0, d = 0;
+    uint32_t nc = 0, f = 0xffffffffu;
+#pragma unroll
+    for (uint32_t w = 0; w < kEmitWaves; ++w) {
+      g += s_good[w];
+      d += s_drop[w];
+      nc += s_corrupt[w];
+      f = min(f, s_first[w]);
+    }
+    const uint64_t total = before + mine_all;
     lvkv_log_report* r = a.r;
     r->status = total > a.capacity ? LVKV_LOG_CAPACITY : LVKV_OK;
     r->nblocks = a.nblocks;
     r->nrecords = static_cast<uint32_t>(total);
-    r->ngood = static_cast<uint32_t>(red_good);
-    r->ncorrupt = red_corrupt;
-    r->first_bad_block = red_first;
-    r->dropped_bytes = red_drop;
+    r->ngood = static_cast<uint32_t>(g);
+    r->ncorrupt = nc;
+    r->first_bad_block = f;
+    r->dropped_bytes = d;
     r->count_ = total > a.capacity ? 0u : static_cast<uint32_t>(total);
     r->reserved_ = 0;
-    log_stamp(a, 0, 15, 4);
   }
-}
-
-// The staged results to their places, one wave per block: record j of block
-// b is record first[b] + j in file order; the block's ReadRecord event
-// follows its records (item first[b] + counts[b] + b, lvkv_log_events.h).
-__global__ void __launch_bounds__(256) log_emit_kernel(LogArgs a) {
-  const uint32_t b = blockIdx.x * 4u + (threadIdx.x >> 6);
-  const uint32_t lane = lane_id();
+  const uint32_t b = b0 + wave;
   if (b >= a.nblocks) return;
-  const uint32_t c = static_cast<uint32_t>(a.info[b].x), off = a.stg_off[b], base = a.first[b];
+  // this wave's place: the counts of the workgroup's blocks before it
+  uint32_t pre = lane < wave ? static_cast<uint32_t>(a.info[b0 + lane].x) : 0u;
+#pragma unroll
+  for (uint32_t dd = 32; dd >= 1; dd >>= 1) pre += __shfl_xor(pre, dd, 64);
+  const uint64_t base = before + pre;
+  const uint32_t c = static_cast<uint32_t>(a.info[b].x), off = a.stg_off[b];
   const uint64_t start = uint64_t{b} * kLogBlock;
   for (uint32_t j = lane; j < c; j += 64) {
-    const uint64_t gi = uint64_t{base} + j;
+    const uint64_t gi = base + j;
     if (gi >= a.capacity || off + j >= a.capacity) break;
     const uint4 e = a.stg[off + j];
     a.hdr_off[gi] = start + (e.y & 0xffffu);
@@ -873,13 +881,13 @@ __global__ void __launch_bounds__(256) log_emit_kernel(LogArgs a) {
       a.events[gi + b] = e.w == LVKV_REC_OK ? log_event(kEvRec, e.z, e.y >> 16)
                                              : log_event(kEvSkip, 0, 0);
   }
-  if (lane == 0 && a.events != nullptr && uint64_t{base} + c <= a.capacity)
-    a.events[uint64_t{base} + c + b] = log_block_event(a.block_status[b], a.block_drop[b]);
+  if (lane == 0 && a.events != nullptr && base + c <= a.capacity)
+    a.events[base + c + b] = log_block_event(a.block_status[b], a.block_drop[b]);
 }
 
-// Scratch: [0, 8) done counter, [8, 16) the logical layer's counter (not
-// touched here), [16, 20) ticket counter, [20, 24) staging counter, then
-// from byte 32 info (16 B per block), stg_off and first (u32 per block),
+// Scratch: [0, 8) unused, [8, 16) the logical layer's counter (not touched
+// here), [16, 20) ticket counter, [20, 24) staging counter, then from byte
+// 32 info (16 B per block), stg_off (u32 per block) and 4 unused bytes per block,
 // the staging array (16 B per record, `capacity` of them) and the slots'
 // overflow positions (u32, kPosOver per slot of each of the grid's
 // workgroups).
@@ -898,7 +906,7 @@ uint32_t log_groups(uint64_t nblocks, int cus) {
 
 #ifdef LVKV_PROBE_BUILD
 uint64_t* g_log_stamps = nullptr;  // lvkv_debug_log_stamps
-uint32_t g_log_knobs = 0;          // lvkv_debug_log_knobs (no knobs in this kernel)
+uint32_t g_log_knobs = 0;          // lvkv_debug_log_knobs (LogArgs::knobs)
 #endif
 
 size_t log_scratch_bytes(uint64_t size, uint32_t capacity, int cus) {
@@ -929,12 +937,10 @@ hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_o
   a.block_drop = block_drop;
   a.r = r;
   uint8_t* sb = static_cast<uint8_t*>(scratch);
-  a.done = reinterpret_cast<uint64_t*>(sb);
   a.ticket = reinterpret_cast<uint32_t*>(sb + 16);
   a.stg_top = reinterpret_cast<uint32_t*>(sb + 20);
   a.info = reinterpret_cast<ulonglong2*>(sb + 32);
   a.stg_off = reinterpret_cast<uint32_t*>(a.info + nblocks);
-  a.first = a.stg_off + nblocks;
   a.stg = reinterpret_cast<uint4*>(sb + log_scratch_head(nblocks));
   a.over = reinterpret_cast<uint32_t*>(a.stg + capacity);
   a.zpow = zpow;
@@ -942,12 +948,16 @@ hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_o
   a.events = events;
 #ifdef LVKV_PROBE_BUILD
   a.stamps = g_log_stamps;
+  a.knobs = g_log_knobs;
 #endif
-  hipLaunchKernelGGL(log_verify_kernel, dim3(log_groups(nblocks, cus)), dim3(kVThreads), 0,
-                     stream, a);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || nblocks == 0) return e;
-  hipLaunchKernelGGL(log_emit_kernel, dim3((nblocks + 3u) / 4u), dim3(256), 0, stream, a);
+  if (nblocks != 0) {
+    hipLaunchKernelGGL(log_verify_kernel, dim3(log_groups(nblocks, cus)), dim3(kVThreads), 0,
+                       stream, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(log_emit_kernel, dim3(std::max<uint32_t>(1, (nblocks + kEmitWaves - 1) / kEmitWaves)),
+                     dim3(64 * kEmitWaves), 0, stream, a);
   return hipGetLastError();
 }
 

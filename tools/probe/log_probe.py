@@ -107,10 +107,9 @@ def main():
         ok = w[:, 0] > 0
         rel = (w[ok] - t0) / 100.0
         print("workgroups: start min/med/max %.2f/%.2f/%.2f, image built med %.2f, "
-              "done min/med/max %.2f/%.2f/%.2f; last workgroup %.2f -> report %.2f" % (
+              "done min/med/max %.2f/%.2f/%.2f" % (
                   rel[:, 0].min(), np.median(rel[:, 0]), rel[:, 0].max(), np.median(rel[:, 1]),
-                  rel[:, 2].min(), np.median(rel[:, 2]), rel[:, 2].max(),
-                  rel[:, 3].max(), rel[:, 4].max()), flush=True)
+                  rel[:, 2].min(), np.median(rel[:, 2]), rel[:, 2].max()), flush=True)
         names = ["claim", "dma", "walk", "crcs", "staged"]
         for k in range(6):
             row = x[:, :, k, :].reshape(-1, 8)
@@ -120,6 +119,12 @@ def main():
             rel = (row[ok] - t0) / 100.0
             med = np.median(rel, axis=0)
             d = np.median(np.diff(rel[:, :5], axis=1), axis=0)
+            wl = row[ok][:, 5] > 0
+            if wl.any():
+                r5 = (row[ok][wl] - t0) / 100.0
+                print(f"   walk split: window {np.median(r5[:, 5] - r5[:, 1]):.2f} loop "
+                      f"{np.median(r5[:, 6] - r5[:, 5]):.2f} tail {np.median(r5[:, 2] - r5[:, 6]):.2f}",
+                      flush=True)
             print(f"block {k}: claimed at {med[0]:.2f} us; phases " +
                   " ".join(f"{n}+{v:.2f}" for n, v in zip(names[1:], d)) +
                   f"; staged at {med[4]:.2f} (max {rel[:, 4].max():.2f}, n {ok.sum()})", flush=True)

@@ -108,6 +108,43 @@ __device__ uint32_t walk_lds_u16(const uint8_t* blk, uint32_t n) {
   return k;
 }
 
+
+// variant 5: the block read from an 8 KiB register window (uniform register
+// index + v_readlane), the chain on the scalar unit -- the round-3 walk
+typedef uint32_t WinRows __attribute__((ext_vector_type(32)));
+__device__ uint32_t walk_regs(const uint8_t* blk, uint32_t n) {
+  const uint32_t lane = lane_id();
+  const uint32_t* sw = reinterpret_cast<const uint32_t*>(blk);
+  uint32_t k = 0, p = 0;
+  if (n < kHdr) return 0;
+  WinRows win;
+  uint32_t wbase = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < 32; ++r) win[r] = sw[64u * r + lane];
+  for (;;) {
+    const uint32_t a = __builtin_amdgcn_readfirstlane(p + 4u);
+    const uint32_t d = a >> 2;
+    if (d + 1u >= wbase + 2048u) {
+      wbase = d & ~63u;
+#pragma unroll
+      for (uint32_t r = 0; r < 32; ++r) win[r] = sw[wbase + 64u * r + lane];
+    }
+    const uint32_t rel = d - wbase;
+    const uint32_t r = rel >> 6, l = rel & 63u;
+    const uint32_t lo = __builtin_amdgcn_readlane(win[r], l);
+    const uint32_t hi = l == 63u ? __builtin_amdgcn_readlane(win[min(r + 1u, 31u)], 0)
+                                 : __builtin_amdgcn_readlane(win[r], l + 1u);
+    const uint32_t w = static_cast<uint32_t>(((static_cast<uint64_t>(hi) << 32) | lo) >> (8u * (a & 3u)));
+    const uint32_t len = w & 0xffffu;
+    const uint32_t np = p + kHdr + len;
+    if (np > n || (w & 0xffffffu) == 0) break;
+    ++k;
+    p = np;
+    if (n - p < kHdr) break;
+  }
+  return k;
+}
+
 // variant 2: scalar loads from global memory
 __device__ uint32_t walk_glb_salu(const uint8_t* blk, uint32_t n) {
   uint32_t p = 0, k = 0;
@@ -163,7 +200,7 @@ __global__ void __launch_bounds__(kThreads, 1)
     uint32_t acc = 0;
     for (uint32_t o = lane * 16; o < kBlock; o += 64 * 16) {
       const uint4 v = *reinterpret_cast<const uint4*>(src + o);
-      if (V <= 1 || V == 4) *reinterpret_cast<uint4*>(mine + o) = v;
+      if (V <= 1 || V >= 4) *reinterpret_cast<uint4*>(mine + o) = v;
       acc ^= v.x ^ v.y ^ v.z ^ v.w;
     }
     __builtin_amdgcn_s_waitcnt(0);
@@ -175,6 +212,7 @@ __global__ void __launch_bounds__(kThreads, 1)
     else if (V == 1) k = walk_lds_valu(mine, kBlock);
     else if (V == 2) k = walk_glb_salu(src, kBlock);
     else if (V == 4) k = walk_lds_u16(mine, kBlock);
+    else if (V == 5) k = walk_regs(mine, kBlock);
     else k = walk_glb_vmem(src, kBlock);
     const uint64_t c1 = __builtin_amdgcn_s_memtime();
     cyc += c1 - c0;
@@ -220,11 +258,11 @@ int main(int argc, char** argv) {
   hipMalloc(&d_out, sizeof(Out) * 256 * 16 + 16);
   int cus = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
-  const char* names[] = {"lds_salu", "lds_valu", "glb_salu", "glb_vmem", "lds_u16"};
+  const char* names[] = {"lds_salu", "lds_valu", "glb_salu", "glb_vmem", "lds_u16", "regs"};
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  for (int v : {0, 1, 4}) {
+  for (int v : {4, 5}) {
     for (uint32_t walkers : {1u, 2u, 4u}) {
       float best = 1e9f;
       std::vector<Out> h(256 * 16);
@@ -236,6 +274,7 @@ int main(int argc, char** argv) {
           case 1: hipLaunchKernelGGL(walk_kernel<1>, dim3(cus), dim3(kThreads), 0, 0, d_img, nblk, walkers, d_out); break;
           case 2: hipLaunchKernelGGL(walk_kernel<2>, dim3(cus), dim3(kThreads), 0, 0, d_img, nblk, walkers, d_out); break;
           case 3: hipLaunchKernelGGL(walk_kernel<3>, dim3(cus), dim3(kThreads), 0, 0, d_img, nblk, walkers, d_out); break;
+          case 5: hipLaunchKernelGGL(walk_kernel<5>, dim3(cus), dim3(kThreads), 0, 0, d_img, nblk, walkers, d_out); break;
           default: hipLaunchKernelGGL(walk_kernel<4>, dim3(cus), dim3(kThreads), 0, 0, d_img, nblk, walkers, d_out); break;
         }
         hipEventRecord(e1);
