@@ -358,6 +358,25 @@ int lvkv_log_read_device(const void* d_file, uint64_t file_size, uint64_t* d_hdr
                          size_t report_capacity, uint64_t initial_offset,
                          lvkv_log_read_report* d_read, void* stream);
 
+/* The records' bytes after lvkv_log_read_device, as ReadRecord hands each
+ * one back (scratch->assign / append of its fragments' payloads, then
+ * *record = Slice(*scratch): db/log_reader.cc:92-137), laid end to end in
+ * record order: record i's contents are d_payload[d_record_pos[i],
+ * + d_records[i].length). This is the buffer DBImpl::RecoverLogFile
+ * (db/db_impl.cc:453) and VersionSet::Recover (db/version_set.cc:910) would
+ * feed to WriteBatchInternal::SetContents / VersionEdit::DecodeFrom, one
+ * record at a time. Same d_file / d_hdr_offsets / capacity / d_report /
+ * d_records / record_capacity / d_read as that call (enqueue on the same
+ * stream after it). payload_capacity >= d_read->bytes is needed for every
+ * record to be written (file_size always suffices); a fragment that does
+ * not fit is skipped. d_record_pos (record_capacity u64, nullable) gets
+ * every returned record's offset in d_payload. One launch, asynchronous. */
+int lvkv_log_gather_device(const void* d_file, const uint64_t* d_hdr_offsets, size_t capacity,
+                           const lvkv_log_report* d_report, const lvkv_log_record* d_records,
+                           size_t record_capacity, const lvkv_log_read_report* d_read,
+                           void* d_payload, uint64_t payload_capacity, uint64_t* d_record_pos,
+                           void* stream);
+
 /* ---- batched, host-resident (end-to-end incl. PCIe) ------------------- */
 /* Blocks live in host memory (pageable or pinned). The library packs them
  * into pinned staging buffers, copies them to the current device with

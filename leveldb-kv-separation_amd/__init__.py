@@ -91,6 +91,8 @@ def _load() -> ctypes.CDLL:
     L.lvkv_log_read_device.argtypes = [vp, u64, vp, vp, vp, sz, vp, vp, vp, vp, sz, vp, sz, u64,
                                        vp, vp]
     L.lvkv_log_read_device.restype = i32
+    L.lvkv_log_gather_device.argtypes = [vp, vp, sz, vp, vp, sz, vp, vp, u64, vp, vp]
+    L.lvkv_log_gather_device.restype = i32
     L.lvkv_debug_set_sst_form.argtypes = [i32]
     L.lvkv_debug_set_sst_form.restype = i32
     L.lvkv_log_verify_device.argtypes = [vp, vp, vp, vp, sz, vp]
@@ -509,7 +511,7 @@ LOG_REASONS = {1: "checksum mismatch", 2: "bad record length",
 
 def log_read(file_buf, *, initial_offset: int = 0, capacity: Optional[int] = None,
              record_capacity: Optional[int] = None, report_capacity: Optional[int] = None,
-             stream=None):
+             gather: bool = False, stream=None):
     """log::Reader(reporter, checksum=True, initial_offset) over the log image
     in `file_buf` (uint8 CUDA tensor), all on the device
     (lvkv_log_read_device): ReadRecord until it returns false.
@@ -518,6 +520,9 @@ def log_read(file_buf, *, initial_offset: int = 0, capacity: Optional[int] = Non
       records  list of (LastRecordOffset, length, first fragment, fragments)
       reports  list of (bytes, reason text) — every Reporter::Corruption call
       physical the log_verify_blocks tuple of the same call
+    With gather=True a fifth element: (payload, positions), the records'
+    bytes as lvkv_log_gather_device lays them end to end on the device
+    (uint8 tensor) and each record's offset in it (int64 tensor).
     Capacities default to sizes that always fit; a LVKV_LOG_CAPACITY result
     from smaller ones is returned as is."""
     import numpy as np
@@ -547,6 +552,16 @@ def log_read(file_buf, *, initial_offset: int = 0, capacity: Optional[int] = Non
             _dev_ptr(recs, "records"), rcap, _dev_ptr(reps, "reports"), pcap,
             int(initial_offset), _dev_ptr(rd, "read"), _stream_handle(stream, dev))
     _check("lvkv_log_read_device", rc)
+    if gather:
+        payload = torch.empty(max(1, size), dtype=torch.uint8, device=dev)
+        pos = torch.zeros(max(1, rcap), dtype=torch.int64, device=dev)
+        with torch.cuda.device(dev):
+            rc = _lib.lvkv_log_gather_device(
+                _dev_ptr(file_buf, "file_buf", (torch.uint8, torch.int8)), _dev_ptr(hdr, "hdr"),
+                cap, _dev_ptr(rep, "report"), _dev_ptr(recs, "records"), rcap,
+                _dev_ptr(rd, "read"), _dev_ptr(payload, "payload"), payload.numel(),
+                _dev_ptr(pos, "positions"), _stream_handle(stream, dev))
+        _check("lvkv_log_gather_device", rc)
     r = LogReport.from_buffer_copy(bytes(rep.cpu().numpy()))
     o = LogReadReport.from_buffer_copy(bytes(rd.cpu().numpy()))
     nrec = min(o.nrecords, rcap)
@@ -561,6 +576,8 @@ def log_read(file_buf, *, initial_offset: int = 0, capacity: Optional[int] = Non
         reports.append((int(x[0]), text.format(typ) if reason == 8 else text))
     n = r.nrecords if r.status == 0 else 0
     physical = (r.as_dict(), hdr[:n], actual[:n], rst[:n], bst[:nblocks], bdrop[:nblocks])
+    if gather:
+        return o.as_dict(), records, reports, physical, (payload, pos[:nrec])
     return o.as_dict(), records, reports, physical
 
 

@@ -44,6 +44,12 @@ hipError_t launch_crc32c_uniform_small(const UniformArgs& args, int variant,
                                        int num_groups, hipStream_t stream);
 hipError_t launch_crc32c_compact(const UniformArgs& args, int cfg, int num_groups,
                                  hipStream_t stream);
+size_t log_gather_scratch_bytes(size_t capacity);
+hipError_t launch_log_gather(const uint8_t* file, const uint64_t* hdr_off, size_t capacity,
+                             const lvkv_log_report* phys, const lvkv_log_record* recs,
+                             uint32_t rec_cap, const lvkv_log_read_report* read, uint8_t* out,
+                             uint64_t out_cap, uint64_t* rec_pos, void* look, uint32_t tag,
+                             hipStream_t stream);
 hipError_t launch_sst_tables(const uint8_t* file, const uint64_t* toff, const uint64_t* tsize,
                              uint64_t single_size, uint32_t ntables, uint64_t* d_off,
                              uint32_t* d_size, uint32_t* d_actual, uint8_t* d_status,
@@ -704,6 +710,43 @@ int lvkv_log_read_device(const void* d_file, uint64_t file_size, uint64_t* d_hdr
                             // the verify leaves scratch bytes 8-15 alone (zeroed
                             // when allocated): the assembly's completion counter
                             reinterpret_cast<uint32_t*>(sb + 8), hs);
+  const hipError_t e2 = log_scratch_release(*c, slot, hs);
+  if (e == hipSuccess) e = e2;
+  return e == hipSuccess ? LVKV_OK : hip_fail(e);
+}
+
+int lvkv_log_gather_device(const void* d_file, const uint64_t* d_hdr_offsets, size_t capacity,
+                           const lvkv_log_report* d_report, const lvkv_log_record* d_records,
+                           size_t record_capacity, const lvkv_log_read_report* d_read,
+                           void* d_payload, uint64_t payload_capacity, uint64_t* d_record_pos,
+                           void* stream) {
+  if (!d_file || !d_hdr_offsets || !d_report || !d_read || (!d_records && record_capacity) ||
+      (!d_payload && payload_capacity) || capacity == 0 || capacity > kMaxBlocksPerLaunch ||
+      record_capacity > kMaxBlocksPerLaunch)
+    return LVKV_ERR_INVALID;
+  if (record_capacity == 0) return LVKV_OK;
+  int rc = LVKV_OK;
+  DeviceCtx* c = current_ctx(&rc);
+  if (c == nullptr) return rc;
+  const hipStream_t hs = static_cast<hipStream_t>(stream);
+  void* scratch = nullptr;
+  size_t slot = 0;
+  // (the pool's buffers keep the verify's counters in bytes [0, 24), which
+  // every call leaves at 0: the look-back slots go after them)
+  hipError_t e =
+      log_scratch_acquire(*c, hs, 32 + log_gather_scratch_bytes(capacity), &scratch, &slot);
+  if (e == hipErrorStreamCaptureUnsupported) return LVKV_ERR_INVALID;
+  if (e != hipSuccess) return hip_fail(e);
+  // the look-back slots' tag: per call, 30 bits, never 0
+  static std::atomic<uint32_t> tags{0};
+  uint32_t tag;
+  do {
+    tag = (tags.fetch_add(1, std::memory_order_relaxed) + 1) & 0x3fffffffu;
+  } while (tag == 0);
+  e = launch_log_gather(static_cast<const uint8_t*>(d_file), d_hdr_offsets, capacity, d_report,
+                        d_records, static_cast<uint32_t>(record_capacity), d_read,
+                        static_cast<uint8_t*>(d_payload), payload_capacity, d_record_pos,
+                        static_cast<uint8_t*>(scratch) + 32, tag, hs);
   const hipError_t e2 = log_scratch_release(*c, slot, hs);
   if (e == hipSuccess) e = e2;
   return e == hipSuccess ? LVKV_OK : hip_fail(e);

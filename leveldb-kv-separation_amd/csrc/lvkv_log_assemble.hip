@@ -623,6 +623,185 @@ __global__ void __launch_bounds__(kGT) log_asm_emit(AsmArgs a) {
     atomicAdd(reinterpret_cast<unsigned long long*>(&a.out->bytes), bytes);
 }
 
+// ---- the records' bytes ---------------------------------------------------
+//
+// ReadRecord hands back each record as one buffer (scratch->assign/append,
+// *record = Slice(*scratch), db/log_reader.cc:92-137). Here every record is
+// written end to end into one output: physical candidate j belongs to a
+// returned record iff the last record whose first fragment is <= j also
+// spans j (records are in order and their fragments disjoint, a binary
+// search over their `first`); its payload goes to dest[j] = the payloads of
+// the returned fragments before it (a scan over candidates), so record i
+// starts at dest[first_i]. One launch: 1024 candidates a workgroup, the scan
+// across workgroups by decoupled look-back (each workgroup publishes its
+// aggregate, then its inclusive prefix, under the call's tag; it waits only
+// on lower workgroups, dispatched before it), then the workgroup's owned
+// fragments copied one per wave, 16 bytes a lane.
+
+constexpr uint32_t kGatherT = 256, kGatherItems = 4, kGatherPer = kGatherT * kGatherItems;
+
+// A workgroup's look-back slot: its aggregate, then its inclusive prefix,
+// each published by a release of `tag` = call tag << 2 | 1 or 2.
+struct LookSlot {
+  unsigned long long agg, incl;
+  uint32_t tag, pad_[3];
+};
+
+struct GatherArgs {
+  const uint8_t* file;
+  const uint64_t* hdr_off;
+  const lvkv_log_report* phys;
+  const lvkv_log_record* recs;
+  const lvkv_log_read_report* read;
+  uint32_t rec_cap;
+  uint32_t tag;           // the call's look-back tag (never 0)
+  uint8_t* out;
+  uint64_t out_cap;
+  uint64_t* rec_pos;      // nullable
+  struct LookSlot* look;  // per workgroup
+};
+
+// The u16 at p (any alignment) from the aligned dword(s) holding it: no
+// misaligned sub-dword global load.
+__device__ __forceinline__ uint32_t ld_u16_any(const uint8_t* p) {
+  const uint64_t x = reinterpret_cast<uint64_t>(p);
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(x & ~uint64_t{3});
+  const uint32_t sh = static_cast<uint32_t>(x & 3u);
+  const uint32_t lo = d[0];
+  const uint32_t hi = sh == 3u ? d[1] : 0u;
+  return __builtin_amdgcn_alignbyte(hi, lo, sh) & 0xffffu;
+}
+
+// Index of the last record whose first fragment is <= j (or -1).
+__device__ __forceinline__ int32_t owner_of(const lvkv_log_record* recs, uint32_t n, uint32_t j) {
+  uint32_t lo = 0, hi = n;  // first record with first > j
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (recs[mid].first <= j) lo = mid + 1; else hi = mid;
+  }
+  return static_cast<int32_t>(lo) - 1;
+}
+
+__global__ void __launch_bounds__(kGatherT) log_gather_kernel(GatherArgs a) {
+  __shared__ unsigned long long wsum[kGatherT / 64];
+  __shared__ unsigned long long base_s;
+  __shared__ uint32_t nown;
+  __shared__ uint32_t own_j[kGatherPer];
+  __shared__ unsigned long long own_dst[kGatherPer];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63u, wave = tid >> 6;
+  const uint32_t N = a.phys->status == LVKV_OK ? a.phys->count_ : 0u;
+  const uint32_t R = a.phys->status == LVKV_OK ? min(a.read->nrecords, a.rec_cap) : 0u;
+  const uint32_t g = blockIdx.x;
+  if (g * kGatherPer >= N) return;  // the whole workgroup; nothing waits on it
+  if (tid == 0) nown = 0;
+  // this thread's candidates: owned payload lengths
+  const uint32_t j0 = g * kGatherPer + tid * kGatherItems;
+  uint32_t len[kGatherItems];
+  int32_t own[kGatherItems];
+  uint64_t mine = 0;
+#pragma unroll
+  for (uint32_t t = 0; t < kGatherItems; ++t) {
+    const uint32_t j = j0 + t;
+    len[t] = 0;
+    own[t] = -1;
+    if (j < N && R != 0) {
+      const int32_t i = owner_of(a.recs, R, j);
+      if (i >= 0 && j < a.recs[i].first + a.recs[i].nfrags) {
+        len[t] = ld_u16_any(a.file + a.hdr_off[j] + 4);
+        own[t] = i;
+      }
+    }
+    mine += len[t];
+  }
+  // workgroup scan
+  uint64_t inc = mine;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint64_t o = __shfl_up(static_cast<unsigned long long>(inc), d, 64);
+    if (lane >= d) inc += o;
+  }
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  uint64_t pre = 0, agg = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < kGatherT / 64; ++w) {
+    if (w < wave) pre += wsum[w];
+    agg += wsum[w];
+  }
+  // look-back (thread 0): publish the aggregate, sum predecessors, publish
+  // the inclusive prefix
+  if (tid == 0) {
+    LookSlot* me = a.look + g;
+    uint64_t before = 0;
+    if (g != 0) {
+      __hip_atomic_store(&me->agg, static_cast<unsigned long long>(agg), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&me->tag, (a.tag << 2) | 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      for (int32_t p = static_cast<int32_t>(g) - 1; p >= 0; --p) {
+        LookSlot* q = a.look + p;
+        uint32_t tw;
+        while (((tw = __hip_atomic_load(&q->tag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) >> 2) !=
+               a.tag)
+          __builtin_amdgcn_s_sleep(1);
+        // an inclusive prefix ends the walk; an aggregate adds and goes on
+        const bool incl = (tw & 3u) == 2u;
+        before += __hip_atomic_load(incl ? &q->incl : &q->agg, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+        if (incl) break;
+      }
+    }
+    __hip_atomic_store(&me->incl, static_cast<unsigned long long>(before + agg), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&me->tag, (a.tag << 2) | 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    base_s = before;
+  }
+  __syncthreads();
+  uint64_t dst = base_s + pre + inc - mine;
+#pragma unroll
+  for (uint32_t t = 0; t < kGatherItems; ++t) {
+    if (own[t] >= 0) {
+      const uint32_t j = j0 + t;
+      if (a.rec_pos != nullptr && a.recs[own[t]].first == j) a.rec_pos[own[t]] = dst;
+      const uint32_t k = atomicAdd(&nown, 1u);
+      own_j[k] = j;
+      own_dst[k] = dst;
+    }
+    dst += len[t];
+  }
+  __syncthreads();
+  // the owned fragments, one wave each
+  const uint32_t n = nown;
+  for (uint32_t k = wave; k < n; k += kGatherT / 64) {
+    const uint32_t j = own_j[k];
+    const uint64_t d = own_dst[k];
+    const uint8_t* src = a.file + a.hdr_off[j] + 7;
+    const uint32_t l = ld_u16_any(src - 3);
+    if (d + l > a.out_cap) continue;
+    // bytes up to the output's next 4-byte boundary, then whole output words
+    // rebuilt from two aligned source dwords (a buffer resource over the
+    // payload's aligned dwords: a dword past them reads as 0, one partly
+    // past a range's end would read as 0 whole), then the last 0-3 bytes
+    const uint32_t hb = min(l, (4u - static_cast<uint32_t>(d & 3u)) & 3u);
+    if (lane < hb) a.out[d + lane] = src[lane];
+    const uint64_t s0 = reinterpret_cast<uint64_t>(src);
+    const uint64_t sa = s0 & ~uint64_t{3};
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(sa), 0, static_cast<int>((s0 + l - sa + 3u) & ~uint64_t{3}),
+        kBufferDword3);
+    const uint32_t nw = (l - hb) >> 2;
+    uint32_t* dw = reinterpret_cast<uint32_t*>(a.out + d + hb);
+    for (uint32_t w = lane; w < nw; w += 64) {
+      const uint32_t so = static_cast<uint32_t>(s0 - sa) + hb + 4u * w;
+      const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(so & ~3u), 0, 0);
+      const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>((so & ~3u) + 4u), 0, 0);
+      dw[w] = __builtin_amdgcn_alignbyte(hi, lo, so & 3u);
+    }
+    const uint32_t tb = (l - hb) & 3u;
+    if (lane < tb) a.out[d + hb + 4u * nw + lane] = src[hb + 4u * nw + lane];
+  }
+}
+
 }  // namespace
 
 size_t log_asm_scratch_bytes(size_t max_items) {
@@ -671,6 +850,34 @@ hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
   hipLaunchKernelGGL(log_asm_reduce, dim3(a.groups), dim3(kGT), 0, stream, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(log_asm_emit, dim3(a.groups), dim3(kGT), 0, stream, a);
+  return hipGetLastError();
+}
+
+// lvkv_log_gather_device: one launch; `look`: 16 bytes per workgroup of
+// ceil(capacity / 1024), any contents (slots of other tags are ignored).
+size_t log_gather_scratch_bytes(size_t capacity) {
+  return ((capacity + kGatherPer - 1) / kGatherPer) * sizeof(LookSlot);
+}
+
+hipError_t launch_log_gather(const uint8_t* file, const uint64_t* hdr_off, size_t capacity,
+                             const lvkv_log_report* phys, const lvkv_log_record* recs,
+                             uint32_t rec_cap, const lvkv_log_read_report* read, uint8_t* out,
+                             uint64_t out_cap, uint64_t* rec_pos, void* look, uint32_t tag,
+                             hipStream_t stream) {
+  GatherArgs a;
+  a.file = file;
+  a.hdr_off = hdr_off;
+  a.phys = phys;
+  a.recs = recs;
+  a.read = read;
+  a.rec_cap = rec_cap;
+  a.tag = tag;
+  a.out = out;
+  a.out_cap = out_cap;
+  a.rec_pos = rec_pos;
+  a.look = static_cast<LookSlot*>(look);
+  const uint32_t groups = static_cast<uint32_t>((capacity + kGatherPer - 1) / kGatherPer);
+  hipLaunchKernelGGL(log_gather_kernel, dim3(groups), dim3(kGatherT), 0, stream, a);
   return hipGetLastError();
 }
 

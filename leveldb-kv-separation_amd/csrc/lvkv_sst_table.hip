@@ -63,6 +63,13 @@ constexpr uint64_t kFooterLen = 48;  // table/format.h:53 (2 * 20 + 8)
 constexpr uint64_t kTrailer = 5;     // table/format.h:79
 constexpr uint32_t kMetaStage = 2048;                // metaindex staged in LDS up to this
 constexpr uint32_t kIndexStage = kCompactLdsBytes;   // index staged in the (spent) image
+// One-table calls leave an index (contents + type) in this range to
+// sst_index_kernel: larger than what the head stages in LDS, and at most 256
+// of its largest chunks (kWideChunkMaxLog2).
+constexpr uint32_t kWideGroups = 64, kWideWaves = 8;
+constexpr uint32_t kWideChunkMinLog2 = 13, kWideChunkMaxLog2 = 19;
+constexpr uint64_t kWideIndexMin = kIndexStage;
+constexpr uint64_t kWideIndexMax = uint64_t{256} << kWideChunkMaxLog2;
 
 struct Table {  // one image of the batch
   const uint8_t* img;
@@ -394,7 +401,7 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
                          uint32_t ntables, uint32_t capacity, uint32_t gen, const FilterKey& fk,
                          lvkv_sst_report* reports, uint64_t* out_off, uint32_t* out_size,
                          uint8_t* out_status, const uint32_t* zpow, const uint32_t* lane_cols,
-                         uint64_t* stamps) {
+                         uint64_t* stamps, bool wide) {
   constexpr uint32_t kT = 64 * W;
   SstHeadLds& L = *reinterpret_cast<SstHeadLds*>(lds + kCompactLdsBytes / 4);
   Head& h = L.h;
@@ -434,6 +441,10 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
   const bool mfit = footer_ok && h.mfit == kFitOk;
   const uint64_t istart = reinterpret_cast<uint64_t>(tb.img) + h.io, iend = istart + h.is + 1;
   const uint64_t mstart = reinterpret_cast<uint64_t>(tb.img) + h.mo, mend = mstart + h.ms + 1;
+  // A large index of a one-table call is left to sst_index_kernel (its CRC
+  // cut over the grid, its entries decoded by every thread of it): here only
+  // its type byte and restart array, provisionally.
+  const bool defer = wide && ifit && h.is + 1 > kWideIndexMin && h.is + 1 <= kWideIndexMax;
 
   // 2. Loads whose values are used after the CRCs, issued before them.
   uint32_t itype = 0, itrail = 0, inr = 0xffffffffu, itail = 0, mtype = 0, mtrail = 0, mtail = 0;
@@ -472,7 +483,7 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
   // 3. Index and metaindex CRCs (contents + type byte) side by side.
   const LaneKeys keys = lane_keys(lane);
   const uint32_t lane_base = compact_lane_base(lane);
-  const uint32_t wi = h.ms + 1 > 4096 ? W / 2 : W - 1;  // waves on the index
+  const uint32_t wi = defer ? 0u : h.ms + 1 > 4096 ? W / 2 : W - 1;  // waves on the index
   uint32_t part = 0;
   if (wave < wi) {
     if (ifit)
@@ -493,13 +504,13 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
     for (int w = 0; w < W; ++w) {
       if (static_cast<uint32_t>(w) < wi) ip ^= L.acc[w]; else mp ^= L.acc[w];
     }
-    h.icrc = ifit ? group_crc_finish(ip, istart, iend, 0u, itail) : 0u;
+    h.icrc = ifit && !defer ? group_crc_finish(ip, istart, iend, 0u, itail) : 0u;
     h.mcrc = mfit ? group_crc_finish(mp, mstart, mend, 0u, mtail) : 0u;
     if (!ifit) {
       h.index_status = unfit_status(tb.img, static_cast<Fit>(h.ifit), h.io);
     } else {
       h.itype = static_cast<uint8_t>(itype);
-      h.index_status = read_status(h.icrc == crc_unmask(itrail), h.itype);
+      h.index_status = read_status(defer || h.icrc == crc_unmask(itrail), h.itype);
     }
     if (!mfit) {
       h.meta_status = unfit_status(tb.img, static_cast<Fit>(h.mfit), h.mo);
@@ -586,6 +597,12 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
       r->meta_offset = h.mo;
       r->meta_size = h.ms;
       if (t == ntables - 1) reports[0].total_ = total;
+      if (wide) {
+        // sst_index_kernel's tag (this call's generation when it has the
+        // index to finish) and its accumulator / arrival words
+        r->link_ = 0;
+        r->done_ = defer ? gen : 0u;
+      }
     }
   }
   __syncthreads();
@@ -601,7 +618,7 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
     out_size[e] = static_cast<uint32_t>(st == LVKV_BLOCK_OK ? h.fs : 0);
     out_status[e] = st;
   }
-  if (nr == 0) return;
+  if (nr == 0 || defer) return;
   const uint64_t ro = h.is - (1 + nr) * 4;
   if (stage_index) {
     for (uint32_t i = tid; i < nr; i += kT)
@@ -653,13 +670,114 @@ __global__ void __launch_bounds__(64 * kW, 1)
                      uint64_t single_size, uint32_t ntables, uint32_t capacity, uint32_t gen,
                      FilterKey fk, lvkv_sst_report* reports, uint64_t* out_off,
                      uint32_t* out_size, uint8_t* out_status, const uint32_t* zpow,
-                     const uint32_t* lane_cols, uint64_t* stamps) {
+                     const uint32_t* lane_cols, uint64_t* stamps, bool wide) {
   __shared__ __attribute__((aligned(16)))
   uint32_t lds[kCompactLdsBytes / 4 + (sizeof(SstHeadLds) + 3) / 4];
   sst_head<kW>(lds, file, toff, tsize, single_size, blockIdx.x, ntables, capacity, gen, fk,
-               reports, out_off, out_size, out_status, zpow, lane_cols, stamps);
+               reports, out_off, out_size, out_status, zpow, lane_cols, stamps, wide);
   __syncthreads();
   sst_stamp(stamps, blockIdx.x, 7);
+}
+
+// Two-launch form of a one-table call, between the head and the CRC launch:
+// the index the head deferred (report.done_ == this call's generation), on
+// kWideGroups workgroups instead of one. Its bytes (contents + type) are cut
+// into chunks of C = 2^c bytes back from e4 = floor4(end); workgroup g takes
+// chunks g, g + G, ...: each chunk's register over its 8 waves
+// (group_crc_part, zero state except the front chunk), shifted to e4 by
+// Z_{k C} = Z_{16 k1 C} Z_{k0 C} (k = k0 + 16 k1, two zmul column sets, no
+// dependent table chain), xored into the report's link_ word. Every entry
+// (block_restart_interval = 1: restart i is entry i) is decoded by one
+// thread of the grid. The last workgroup to arrive (link_'s high word)
+// finishes the CRC with the 0-3 tail bytes and settles the index verdict in
+// ReadBlock's order (checksum, type; then Block::Block's restart test, which
+// the head applied): a bad index leaves the table no entries (total_ 0), as
+// Table::Open's failure does (table/table.cc:62-75).
+__global__ void __launch_bounds__(64 * kWideWaves, 1)
+    sst_index_kernel(const uint8_t* file, uint64_t size, uint32_t gen, lvkv_sst_report* reports,
+                     uint64_t* out_off, uint32_t* out_size, uint8_t* out_status,
+                     const uint32_t* zpow, const uint32_t* lane_cols) {
+  constexpr uint32_t W = kWideWaves, kT = 64 * W;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kCompactLdsBytes / 4];
+  __shared__ uint32_t acc[W];
+  __shared__ uint32_t last_s;
+  lvkv_sst_report* r = reports;
+  if (__hip_atomic_load(&r->done_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen) return;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint64_t io = r->index_offset, is = r->index_size;
+  const uint8_t* idx = file + io;
+  const uint64_t istart = reinterpret_cast<uint64_t>(idx), iend = istart + is + 1;
+  const uint64_t e4 = iend & ~uint64_t{3};
+  uint32_t lc = kWideChunkMinLog2;
+  while (lc < kWideChunkMaxLog2 && (uint64_t{kWideGroups} << lc) < e4 - istart) ++lc;
+  const uint64_t C = uint64_t{1} << lc;
+  const uint32_t m = static_cast<uint32_t>((e4 - istart + C - 1) >> lc);  // <= 256
+  build_compact_image<W>(lds, zpow, lane_cols, tid, wave, lane);  // ends with a barrier
+  const LaneKeys keys = lane_keys(lane);
+  const uint32_t lane_base = compact_lane_base(lane);
+  uint32_t mine = 0;  // the xor of this workgroup's shifted chunk registers (wave-uniform)
+  for (uint32_t k = blockIdx.x; k < m; k += gridDim.x) {
+    const uint64_t ce = e4 - uint64_t{k} * C;
+    const bool front = k == m - 1u;
+    const uint64_t cs = front ? istart : ce - C;
+    const uint32_t part = group_crc_part(lds, cs, ce, front ? 0u : 0xffffffffu, wave, W, lc - 3u,
+                                         keys, lane, lane_base, zpow);
+    if (lane == 0) acc[wave] = part;
+    __syncthreads();
+    uint32_t reg = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < W; ++w) reg ^= acc[w];
+    __syncthreads();
+    // Z_{k C}: lanes [0, 32) hold Z_{k0 C}, lanes [32, 64) Z_{k1 16 C}
+    const uint32_t k0 = k & 15u, k1 = k >> 4;
+    const uint32_t colv = lane < 32u ? (k0 ? zmul_cols(zpow, lc, k0)[lane] : 0u)
+                                     : (k1 ? zmul_cols(zpow, lc + 4u, k1)[lane - 32u] : 0u);
+    if (k0) reg = apply_lane_cols(colv, reg, 0, lane);
+    if (k1) reg = apply_lane_cols(colv, reg, 1, lane);
+    mine ^= reg;
+  }
+  // every entry, from the image (decoded without a window)
+  const uint64_t inr = is >= 4 ? ld_le32(idx + is - 4) : 0u;
+  const bool restarts_ok = is >= 4 && inr <= (is - 4) / 4;
+  const uint32_t first = r->first;
+  const uint64_t nr = restarts_ok ? inr : 0u;
+  const Table tb = table_of(file, nullptr, nullptr, size, 0);
+  if (static_cast<int32_t>(r->status) == LVKV_SST_OK) {
+    const uint64_t ro = is - (1 + nr) * 4;
+    for (uint64_t i = uint64_t{blockIdx.x} * kT + tid; i < nr; i += uint64_t{gridDim.x} * kT)
+      emit_entry(idx, ro, nr, static_cast<uint32_t>(i), idx, 0, 0, tb, first, out_off, out_size,
+                 out_status);
+  }
+  // arrival: this workgroup's register and the count in one 64-bit add
+  // (the registers are xored, so they go through a separate atomic)
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t* words = reinterpret_cast<uint32_t*>(&r->link_);
+    if (mine) __hip_atomic_fetch_xor(&words[0], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t old =
+        __hip_atomic_fetch_add(&words[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last_s = old + 1 == gridDim.x ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!last_s || tid != 0) return;
+  uint32_t* words = reinterpret_cast<uint32_t*>(&r->link_);
+  const uint32_t parts = __hip_atomic_load(&words[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t crc = group_crc_finish(parts, istart, iend, 0u, group_crc_tail(istart, iend));
+  const uint8_t itype = idx[is];
+  const uint8_t st = read_status(crc == crc_unmask(ld_le32(idx + is + 1)), itype);
+  r->index_crc = crc;
+  r->index_status = st;
+  if (st != LVKV_BLOCK_OK) {
+    r->status = st == LVKV_BLOCK_CHECKSUM ? LVKV_SST_INDEX_CHECKSUM : LVKV_SST_INDEX_TYPE;
+    r->ndata = 0;
+    r->has_filter = 0;
+    r->nblocks = 0;
+    r->total_ = 0;
+  }
+  r->link_ = 0;
+  r->done_ = 0;
 }
 
 constexpr uint32_t kHeadLdsDwords =
@@ -685,7 +803,7 @@ __global__ void __launch_bounds__(64 * kFW, 2)
   if (blockIdx.x < ntables) {
     sst_head<kFW>(lds, file, toff, tsize, single_size, blockIdx.x, ntables, capacity, gen, fk,
                   reports, const_cast<uint64_t*>(a.offsets), const_cast<uint32_t*>(a.lengths),
-                  a.out_status, zpow, lane_cols, stamps);
+                  a.out_status, zpow, lane_cols, stamps, false);
     // every wave's stores are done at the barrier; one agent-scope release
     // (writes this XCD's L2 back) publishes them with the tag
     __syncthreads();
@@ -767,11 +885,19 @@ hipError_t launch_sst_tables(const uint8_t* file, const uint64_t* toff, const ui
                        sst_stamps());
     return hipGetLastError();
   }
+  // one table: a large index goes to sst_index_kernel (a no-op launch when
+  // the head kept it)
+  const bool wide = ntables == 1 && toff == nullptr;
   hipLaunchKernelGGL(sst_table_kernel, dim3(ntables), dim3(64 * kW), 0, stream, file, toff,
                      tsize, single_size, ntables, capacity, gen, fk, reports, d_off, d_size,
-                     d_status, zpow, lane_cols, sst_stamps());
+                     d_status, zpow, lane_cols, sst_stamps(), wide);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (wide) {
+    hipLaunchKernelGGL(sst_index_kernel, dim3(kWideGroups), dim3(64 * kWideWaves), 0, stream,
+                       file, single_size, gen, reports, d_off, d_size, d_status, zpow, lane_cols);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
   return launch_crc32c_general(a, groups, stream);
 }
 

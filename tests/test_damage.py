@@ -109,16 +109,23 @@ def test_device_wal_matches_reference(lvkv, gpu):
         assert lw.assemble(img, ev) == df.wal_expected(case), case["name"]
 
 
-def _device_log_records(img, records, hdrs):
+def _device_log_records(img, records, hdrs, gathered):
     """(LastRecordOffset, length, CRC32C of the contents) of each device
-    record: its fragments' payloads concatenated (checker: the oracle)."""
+    record, the contents taken from the device's own gather
+    (lvkv_log_gather_device: the records end to end); the CRC is the
+    checker's (oracle). The fragment list is cross-checked against the
+    image."""
     import oracle
-    out = []
-    for off, length, first, nfrags in records:
-        body = b"".join(img[h + lw.K_HEADER: h + lw.K_HEADER + (img[h + 4] | img[h + 5] << 8)]
-                        for h in hdrs[first: first + nfrags])
-        assert hdrs[first] == off and len(body) == length
-        out.append((off, length, oracle.value(body)))
+    payload, pos = gathered
+    pl = payload.cpu().numpy().tobytes()
+    pos = [int(x) for x in pos.cpu().numpy()]
+    assert len(pos) == len(records)
+    out, at = [], 0
+    for (off, length, first, nfrags), p in zip(records, pos):
+        frag_bytes = sum(img[h + 4] | img[h + 5] << 8 for h in hdrs[first: first + nfrags])
+        assert hdrs[first] == off and frag_bytes == length and p == at
+        at += length
+        out.append((off, length, oracle.value(pl[p: p + length])))
     return out
 
 
@@ -132,12 +139,13 @@ def test_device_log_read_matches_reference(lvkv, gpu):
     for case in WAL_CASES:
         img = df.image(case, "wal.log")
         buf = torch.from_numpy(np.frombuffer(img, dtype=np.uint8).copy()).to(gpu)
-        rd, records, reports, phys = lvkv.log_read(buf, initial_offset=case["initial_offset"])
+        rd, records, reports, phys, gathered = lvkv.log_read(
+            buf, initial_offset=case["initial_offset"], gather=True)
         torch.cuda.synchronize()
         assert rd["status"] == 0, case["name"]
         hdrs = [int(x) for x in phys[1].cpu().numpy()]
         want_recs, want_reps = df.wal_expected(case)
-        assert _device_log_records(img, records, hdrs) == want_recs, case["name"]
+        assert _device_log_records(img, records, hdrs, gathered) == want_recs, case["name"]
         assert reports == want_reps, case["name"]
         assert rd["bytes"] == sum(r[1] for r in want_recs), case["name"]
         stopped = lw.read_all(img, case["initial_offset"])[2]
@@ -166,10 +174,10 @@ def test_device_log_read_large_and_capacity(lvkv, gpu):
                 log_synth.fix_header_crc(img, int(h))
         img = bytes(img)
         buf = torch.from_numpy(np.frombuffer(img, dtype=np.uint8).copy()).to(gpu)
-        rd, records, reports, phys = lvkv.log_read(buf)
+        rd, records, reports, phys, gathered = lvkv.log_read(buf, gather=True)
         hdrs = [int(x) for x in phys[1].cpu().numpy()]
         want_recs, want_reps = lw.read_records(img)
-        assert _device_log_records(img, records, hdrs) == want_recs, trial
+        assert _device_log_records(img, records, hdrs, gathered) == want_recs, trial
         assert reports == want_reps, trial
         # from initial offsets: block starts (resync), the trailer rule,
         # inside fragmented records, past the end
@@ -177,11 +185,15 @@ def test_device_log_read_large_and_capacity(lvkv, gpu):
         offs += [int(h) + d for h in rng.choice(hdrs, 4, replace=False) for d in (0, 1)]
         offs += [int(x) for x in rng.integers(1, len(img), 3)]
         for off in offs:
-            rd, records, reports, phys = lvkv.log_read(buf, initial_offset=off)
+            rd, records, reports, phys, gathered = lvkv.log_read(buf, initial_offset=off,
+                                                                 gather=True)
             o_recs, o_reps, stopped = lw.read_all(img, off)
-            assert _device_log_records(img, records, hdrs) == o_recs, (trial, off)
+            assert _device_log_records(img, records, hdrs, gathered) == o_recs, (trial, off)
             assert reports == o_reps, (trial, off)
             assert rd["stopped"] == int(stopped), (trial, off)
-    rd, records, reports, _ = lvkv.log_read(buf, record_capacity=5, report_capacity=1)
+    rd, records, reports, _, gathered = lvkv.log_read(buf, record_capacity=5, report_capacity=1,
+                                                      gather=True)
     assert rd["status"] == 1 and rd["nrecords"] == len(want_recs)
     assert rd["nreports"] == len(want_reps) and len(records) == 5
+    # the first five records' bytes are still gathered
+    assert _device_log_records(img, records, hdrs, gathered) == want_recs[:5]

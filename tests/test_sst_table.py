@@ -220,6 +220,39 @@ def test_device_table_verify_synthetic(lvkv, gpu, sst_form, n, bs, filt):
         assert rep2["status"] == st.SST_CAPACITY and rep2["ndata"] == n
 
 
+@pytest.mark.gpu
+def test_device_table_verify_wide_index(lvkv, gpu, sst_form):
+    # An index over 64 KiB: under the two-launch form a one-table call hands
+    # it to sst_index_kernel (CRC cut over the grid, entries decoded by every
+    # thread, the verdict settled by the last workgroup). Clean, then every
+    # way the index can fail in ReadBlock's / Block::Block's order, a bad
+    # entry, a bad data block and a short capacity, each against the oracle.
+    img = sst_synth.build_sst(4000, 200, seed=41, index_values={17: b"\xff\xff\xff"})
+    r0 = st.verify_table(img)
+    off, size = r0.index
+    assert size + 1 > 64 * 1024
+    cases = [img]
+    for pos in (off, off + 1, off + size // 2, off + size - 9, off + size - 1):
+        bad = bytearray(img); bad[pos] ^= 0x21; cases.append(bytes(bad))     # index crc
+    bad = bytearray(img); bad[off + size + 2] ^= 1; cases.append(bytes(bad))  # stored crc
+    for t in (1, 2, 7):                                                       # index type
+        bad = bytearray(img); bad[off + size] = t
+        sst_synth.fix_trailer(bad, off, size); cases.append(bytes(bad))
+    bad = bytearray(img); bad[off + size - 4: off + size] = struct.pack("<I", 10 ** 7)
+    sst_synth.fix_trailer(bad, off, size); cases.append(bytes(bad))          # restarts
+    bad = bytearray(img); bad[off + size - 4: off + size] = struct.pack("<I", 10 ** 7)
+    cases.append(bytes(bad))                                                  # restarts, crc bad
+    d_off, d_size = r0.handles[100]
+    bad = bytearray(img); bad[d_off + 3] ^= 1; cases.append(bytes(bad))      # data block
+    for c in cases:
+        _assert_matches_oracle(lvkv, c, gpu)
+    rep, *_ = _device_verify(lvkv, img, gpu, capacity=1000)
+    assert rep["status"] == st.SST_CAPACITY and rep["ndata"] == 4000
+    bad = bytearray(img); bad[off + 5] ^= 1
+    rep, *_ = _device_verify(lvkv, bytes(bad), gpu, capacity=1000)
+    assert rep["status"] == st.SST_INDEX_CHECKSUM and rep["nblocks"] == 0
+
+
 # --------------------------------------------- write side (§8f row 3) -----
 
 @pytest.mark.gpu

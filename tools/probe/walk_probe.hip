@@ -262,8 +262,8 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  for (int v : {4, 5}) {
-    for (uint32_t walkers : {1u, 2u, 4u}) {
+  for (int v : {4, 2, 3}) {
+    for (uint32_t walkers : {1u, 2u, 4u, 8u}) {
       float best = 1e9f;
       std::vector<Out> h(256 * 16);
       for (int rep = 0; rep < 3; ++rep) {
