@@ -34,7 +34,9 @@ SURVEY.md §8(d)) / the launch's duration, from the packet processor's
 start/end timestamps of each dispatch (HSA profiling, the engine's HIP-event
 counterpart): `achieved` prices a launch running alone (ordered dispatches,
 the same kernel a rocprofv3 kernel trace of `--isolated` times); `pipelined`
-prices the device span of K overlapped launches / K.
+prices the device span of K overlapped launches / K. `traffic`: HBM-side
+bytes per isolated launch from a rocprofv3 FETCH_SIZE pass over this run's
+own code (a child profiler process, N = 1 headline only; --no-pmc skips it).
 cpu_baseline: the reference's util/crc32c.cc (compiled in place into
 oracle/_ref) on this host.
 """
@@ -328,14 +330,45 @@ def _cpu_model():
     return "unknown"
 
 
-def load_pmc_traffic():
-    p = REPO / "profiles" / "pmc_traffic.json"
-    if p.exists():
-        try:
-            return json.loads(p.read_text()).get("hbm_bytes_per_launch")
-        except (ValueError, OSError):
+def live_pmc_traffic(launches: int = 16, timeout_s: float = 180.0):
+    """HBM-side bytes per launch of the roofline kernel, measured for the code
+    being benched: a child `rocprofv3 --pmc FETCH_SIZE -- python3 bench.py
+    --isolated N` (the profiler starts its own process; this one never
+    execs), FETCH_SIZE per dispatch of lvkv_ek_uniform_pair, median, KiB x
+    1024 x 2 (gfx950 counts a wide streaming read's bytes at half, per the
+    MI355X guide). None when the profiler is absent or the pass fails."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None
+    out = tempfile.mkdtemp(prefix="lvkv_pmc_", dir="/tmp")
+    cmd = [prof, "--pmc", "FETCH_SIZE", "--output-format", "csv", "-d", out, "-o", "run", "--",
+           sys.executable, str(REPO / "bench.py"), "--isolated", str(launches), "--gpus", "1"]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    env["TMPDIR"] = "/tmp"
+    try:
+        subprocess.run(cmd, cwd="/tmp", env=env, timeout=timeout_s, capture_output=True, check=True)
+        vals = []
+        for f in glob.glob(out + "/**/run_counter_collection.csv", recursive=True):
+            with open(f) as fh:
+                for r in csv.DictReader(fh):
+                    if "lvkv_ek_uniform_pair" in r.get("Kernel_Name", "") and \
+                            r.get("Counter_Name") == "FETCH_SIZE":
+                        vals.append(float(r["Counter_Value"]))
+        if not vals:
             return None
-    return None
+        return {"bytes": int(statistics.median(vals) * 1024 * 2), "dispatches": len(vals),
+                "source": f"rocprofv3 --pmc FETCH_SIZE over {len(vals)} isolated launches of "
+                          "this run's code (KiB x 1024 x 2, gfx950 half-count)"}
+    except (subprocess.SubprocessError, OSError, ValueError, KeyError):
+        return None
+    finally:
+        shutil.rmtree(out, ignore_errors=True)
 
 
 # --------------------------------------------------------------------------
@@ -352,6 +385,8 @@ def main():
     ap.add_argument("--rotate-bytes", type=float, default=1.25 * GIB)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-split", action="store_true", help="skip config 5 in the headline line")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the rocprofv3 FETCH_SIZE pass behind roofline.traffic")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--isolated", type=int, default=0,
                     help="only run N ordered (one-at-a-time) launches and exit: the "
@@ -451,7 +486,7 @@ def main():
         w, c, gr = eng.shape()
         roof.update({
             "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": load_pmc_traffic() if args.config == "headline" else None,
+            "traffic": None,
             "kernel": "lvkv_ek_uniform_pair (ordered launch, 2 workgroups x 8 waves per CU)",
             "kernel_us_avg": round(kern_us, 3), "kernel_us_median": round(statistics.median(d), 3),
             "kernel_us_min": round(min(d), 3), "launches": len(d), "dispatches_per_launch": per,
@@ -478,6 +513,12 @@ def main():
             min(args.steps, 20), 2, warm_s, total=args.split_total)
         del split_runner
         torch.cuda.empty_cache()
+
+    if use_engine and rank == 0 and world == 1 and args.config == "headline" and not args.no_pmc:
+        t = live_pmc_traffic()
+        if t is not None:
+            roof["traffic"] = t["bytes"]
+            roof["traffic_source"] = t["source"]
 
     if rank == 0:
         line = _line_base(args, world, value, ms_per_step / 1e3, {

@@ -68,7 +68,7 @@ hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
                                uint64_t initial_offset, lvkv_log_record* recs, uint32_t rec_cap,
                                lvkv_log_corruption* reps, uint32_t rep_cap,
                                lvkv_log_read_report* out, void* scratch, uint32_t* done,
-                               hipStream_t stream);
+                               unsigned long long* bytes, uint32_t tag, hipStream_t stream);
 size_t log_asm_scratch_bytes(size_t max_items);
 hipError_t launch_crc32c_long(const KernelArgs& args, const uint32_t* zpow,
                               const uint32_t* lane_cols, int num_groups, hipStream_t stream);
@@ -330,6 +330,16 @@ uint32_t next_sst_generation() {
   uint32_t v;
   do {
     v = g.fetch_add(1, std::memory_order_relaxed) + 1;
+  } while (v == 0);
+  return v;
+}
+
+// Per-call tag of the logical layer's look-back slots: 30 bits, never 0.
+uint32_t next_asm_tag() {
+  static std::atomic<uint32_t> t{0};
+  uint32_t v;
+  do {
+    v = (t.fetch_add(1, std::memory_order_relaxed) + 1) & 0x3fffffffu;
   } while (v == 0);
   return v;
 }
@@ -707,9 +717,11 @@ int lvkv_log_read_device(const void* d_file, uint64_t file_size, uint64_t* d_hdr
                             static_cast<uint32_t>(capacity), initial_offset, d_records,
                             static_cast<uint32_t>(record_capacity), d_reports,
                             static_cast<uint32_t>(report_capacity), d_read, sb + asm_at,
-                            // the verify leaves scratch bytes 8-15 alone (zeroed
-                            // when allocated): the assembly's completion counter
-                            reinterpret_cast<uint32_t*>(sb + 8), hs);
+                            // the verify leaves scratch bytes 0-15 alone (zeroed
+                            // when allocated): the assembly's byte sum and
+                            // completion counter
+                            reinterpret_cast<uint32_t*>(sb + 8),
+                            reinterpret_cast<unsigned long long*>(sb), next_asm_tag(), hs);
   const hipError_t e2 = log_scratch_release(*c, slot, hs);
   if (e == hipSuccess) e = e2;
   return e == hipSuccess ? LVKV_OK : hip_fail(e);

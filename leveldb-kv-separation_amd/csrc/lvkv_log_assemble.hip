@@ -191,7 +191,10 @@ __device__ __forceinline__ void step(Reader& r, uint32_t ev, uint32_t j, uint64_
   }
 }
 
-constexpr uint32_t kChunk = 4;   // items per thread (one 16-byte load)
+#ifndef LVKV_ASM_CHUNK
+#define LVKV_ASM_CHUNK 4
+#endif
+constexpr uint32_t kChunk = LVKV_ASM_CHUNK;  // items per thread (one 4 kChunk-byte load)
 constexpr uint32_t kGT = 256;     // threads per workgroup of the grid launches
 
 __device__ __forceinline__ bool is_candidate(uint32_t ev) {
@@ -230,11 +233,19 @@ __device__ __forceinline__ uint32_t seek_event(const Seek& sk, const uint64_t* h
 __device__ __forceinline__ void load_chunk(const uint32_t* events, const uint64_t* hdr_off,
                                            const Seek& sk, uint32_t k0, uint32_t k1,
                                            uint32_t (&ev)[kChunk]) {
-  const uint4 v = k0 < k1 ? reinterpret_cast<const uint4*>(events + k0)[0] : make_uint4(0, 0, 0, 0);
-  ev[0] = v.x;
-  ev[1] = v.y;
-  ev[2] = v.z;
-  ev[3] = v.w;
+  if (kChunk == 4) {
+    const uint4 v = k0 < k1 ? reinterpret_cast<const uint4*>(events + k0)[0] : make_uint4(0, 0, 0, 0);
+    ev[0] = v.x;
+    ev[1 % kChunk] = v.y;
+    ev[2 % kChunk] = v.z;
+    ev[3 % kChunk] = v.w;
+  } else if (kChunk == 2) {
+    const uint2 v = k0 < k1 ? reinterpret_cast<const uint2*>(events + k0)[0] : make_uint2(0, 0);
+    ev[0] = v.x;
+    ev[1 % kChunk] = v.y;
+  } else {
+    ev[0] = k0 < k1 ? events[k0] : 0u;
+  }
 #pragma unroll
   for (uint32_t i = 0; i < kChunk; ++i)
     ev[i] = k0 + i >= k1 ? log_event(kEvNone, 0, 0) : seek_event(sk, hdr_off, k0 + i, ev[i]);
@@ -415,15 +426,21 @@ __device__ __forceinline__ void wg_sum_excl(uint32_t (&v)[N], uint32_t (&wsum)[k
   __syncthreads();  // wsum is reused
 }
 
-struct WgAgg {  // log_asm_reduce -> its last workgroup (asm_scan)
+// A run of events (a chunk, a workgroup, a run of workgroups) as a map of
+// the reader's state: its composed summary and its record / report counts
+// for each state the reader may enter it in. Runs of them compose
+// associatively (agg_compose), which is what the look-back needs.
+struct Agg {
   Summ s;
-  uint32_t nrec[kScenarios], nrep[kScenarios];  // from each starting scenario
+  uint32_t nrec[kScenarios], nrep[kScenarios];
 };
-struct WgIn {   // asm_scan -> log_asm_emit
-  uint64_t scratch;  // the reader's state at the workgroup's start
-  uint32_t st, first;
-  uint32_t j0;       // candidates before it
-  uint32_t rec_base, rep_base, pad_;
+
+// A workgroup's look-back slot: its aggregate, then its inclusive prefix (the
+// composition of every workgroup up to it), each published by a release of
+// `flag` = call tag << 2 | 1 or 2.
+struct AsmSlot {
+  uint32_t flag, pad_[3];
+  Agg agg, incl;
 };
 
 struct AsmArgs {
@@ -436,12 +453,13 @@ struct AsmArgs {
   uint32_t init_st; // the reader's first state: kIdle, or kResync with an offset
   Seek seek;
   uint32_t* lohi;   // log_asm_seek's output (seek.lohi)
-  uint32_t* done;   // log_asm_reduce's completion counter (0 between calls)
+  uint32_t tag;     // this call's look-back tag (never 0, < 2^30)
+  uint32_t* done;   // workgroups finished (left at 0 by the last one)
+  unsigned long long* bytes;  // the records' bytes, summed (left at 0 by the last one)
   lvkv_log_record* recs;
   lvkv_log_corruption* reps;
   lvkv_log_read_report* out;
-  WgAgg* aggs;
-  WgIn* ins;
+  AsmSlot* slots;
 };
 
 // Items on the device: candidate records the verify placed, plus blocks.
@@ -480,147 +498,227 @@ __global__ void __launch_bounds__(64) log_asm_seek(AsmArgs a) {
   }
 }
 
-// The aggregates of log_asm_reduce's G workgroups scanned by one workgroup of
-// kST threads: each workgroup's WgIn, and the totals into *a.out.
-template <uint32_t kST>
-__device__ __forceinline__ void asm_scan(const AsmArgs& a, Summ (&wagg)[kST / 64],
-                                         uint32_t (&wsum)[kST / 64][2], uint32_t tid) {
-  const uint32_t K = asm_items(a);
-  const uint32_t G = min(a.groups, (K + kGT * kChunk - 1) / (kGT * kChunk));
-  const uint32_t per = (G + kST - 1) / kST;
-  const uint32_t g0 = min(G, tid * per), g1 = min(G, g0 + per);
-  // this thread's first (with G <= kST its only) aggregate stays in registers
-  WgAgg mine = {};
-  if (g0 < g1) mine = a.aggs[g0];
-  auto agg_at = [&](uint32_t g) -> WgAgg { return g == g0 ? mine : a.aggs[g]; };
-  // 1. this thread's run of aggregates, composed; scanned across threads
-  Summ s = kIdentity;
-  for (uint32_t g = g0; g < g1; ++g) s = compose(s, agg_at(g).s);
-  Summ tot;
-  const Summ p0 = wg_scan_excl<kST>(s, wagg, tid, &tot);
-  // 2. each workgroup's counts from its starting state; output positions
-  uint32_t nrec = 0, nrep = 0;
-  Summ p = p0;
-  for (uint32_t g = g0; g < g1; ++g) {
-    const uint32_t sc = scenario(p.pass ? a.init_st : p.c, p.pass ? 0 : p.scratch);
-    const WgAgg ag = agg_at(g);
-    nrec += pick(ag.nrec, sc);  // 0 when stopped
-    nrep += pick(ag.nrep, sc);
-    p = compose(p, ag.s);
+// Y after X: the summary composed; for each entering scenario, X's counts
+// and Y's from the state X leaves it in (none once X has stopped the reader).
+__device__ __forceinline__ Agg agg_compose(const Agg& x, const Agg& y) {
+  Agg r;
+  r.s = compose(x.s, y.s);
+#pragma unroll
+  for (uint32_t sc = 0; sc < kScenarios; ++sc) {
+    const uint32_t after = chunk_scenario(sc, x.s);  // kScStopped: pick gives 0
+    r.nrec[sc] = x.nrec[sc] + pick(y.nrec, after);
+    r.nrep[sc] = x.nrep[sc] + pick(y.nrep, after);
   }
-  uint32_t base[2] = {nrec, nrep}, all[2];
-  wg_sum_excl<kST>(base, wsum, tid, all);
-  const uint32_t r0 = all[0], r1 = all[1];  // totals
-  uint32_t rb = base[0], pb = base[1];
-  p = p0;
-  for (uint32_t g = g0; g < g1; ++g) {
-    WgIn in;
-    in.st = p.pass ? a.init_st : p.c;
-    in.first = p.first;
-    in.scratch = p.pass ? 0 : p.scratch;
-    in.j0 = p.nrec;
-    in.rec_base = rb;
-    in.rep_base = pb;
-    in.pad_ = 0;
-    a.ins[g] = in;
-    const uint32_t sc = scenario(in.st, in.scratch);
-    const WgAgg ag = agg_at(g);
-    rb += pick(ag.nrec, sc);
-    pb += pick(ag.nrep, sc);
-    p = compose(p, ag.s);
+  return r;
+}
+
+constexpr Agg kAggIdentity = {kIdentity, {0, 0, 0, 0}, {0, 0, 0, 0}};
+
+__device__ __forceinline__ Agg shfl_agg(const Agg& v, uint32_t src) {
+  Agg r;
+  r.s.pass = __shfl(v.s.pass, src, 64);
+  r.s.c = __shfl(v.s.c, src, 64);
+  r.s.len = __shfl(static_cast<unsigned long long>(v.s.len), src, 64);
+  r.s.scratch = __shfl(static_cast<unsigned long long>(v.s.scratch), src, 64);
+  r.s.first = __shfl(v.s.first, src, 64);
+  r.s.nrec = __shfl(v.s.nrec, src, 64);
+  r.s.stop5 = __shfl(v.s.stop5, src, 64);
+#pragma unroll
+  for (uint32_t i = 0; i < kScenarios; ++i) {
+    r.nrec[i] = __shfl(v.nrec[i], src, 64);
+    r.nrep[i] = __shfl(v.nrep[i], src, 64);
   }
-  if (tid == 0) {
-    lvkv_log_read_report o;
-    o.status = (a.phys->status != LVKV_OK || r0 > a.rec_cap || r1 > a.rep_cap) ? LVKV_LOG_CAPACITY
-                                                                                : LVKV_OK;
-    o.nrecords = r0;
-    o.nreports = r1;
-    o.stopped = (!tot.pass && tot.c == kStopped) ? tot.stop5 : 0u;
-    o.bytes = 0;  // log_asm_emit adds the records' bytes
-    *a.out = o;
+  return r;
+}
+
+// Slot words move as agent-scope relaxed atomics (sc1: through to the
+// coherent level, no L1/L2 maintenance). The publisher's stores are waited
+// for (vmcnt) before its flag store, and a reader reads the words only after
+// seeing the flag: an acquire per wait would invalidate the XCD's L2 each
+// time (a first form with acquire spins took 678 us a call).
+template <typename T>
+__device__ __forceinline__ T sc1_ld(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void sc1_st(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ Agg load_agg(const Agg* p) {
+  Agg r;
+  r.s.pass = sc1_ld(&p->s.pass);
+  r.s.c = sc1_ld(&p->s.c);
+  r.s.len = sc1_ld(&p->s.len);
+  r.s.scratch = sc1_ld(&p->s.scratch);
+  r.s.first = sc1_ld(&p->s.first);
+  r.s.nrec = sc1_ld(&p->s.nrec);
+  r.s.stop5 = sc1_ld(&p->s.stop5);
+#pragma unroll
+  for (uint32_t i = 0; i < kScenarios; ++i) {
+    r.nrec[i] = sc1_ld(&p->nrec[i]);
+    r.nrep[i] = sc1_ld(&p->nrep[i]);
+  }
+  return r;
+}
+
+__device__ __forceinline__ void store_agg(Agg* p, const Agg& v) {
+  sc1_st(&p->s.pass, v.s.pass);
+  sc1_st(&p->s.c, v.s.c);
+  sc1_st(&p->s.len, v.s.len);
+  sc1_st(&p->s.scratch, v.s.scratch);
+  sc1_st(&p->s.first, v.s.first);
+  sc1_st(&p->s.nrec, v.s.nrec);
+  sc1_st(&p->s.stop5, v.s.stop5);
+#pragma unroll
+  for (uint32_t i = 0; i < kScenarios; ++i) {
+    sc1_st(&p->nrec[i], v.nrec[i]);
+    sc1_st(&p->nrep[i], v.nrep[i]);
   }
 }
 
-__global__ void __launch_bounds__(kGT) log_asm_reduce(AsmArgs a) {
+// ReadRecord over every event in ONE launch (reduce, look-back, emit):
+// workgroup g's chunks are summarised and scanned (each chunk's start
+// relative to the workgroup's; the workgroup's aggregate with its counts for
+// each entering state); wave 0 publishes the aggregate, then looks back over
+// the slots of the workgroups before it, 64 at a time (one lane each, all
+// loads at once), composing aggregates back to the nearest published
+// inclusive prefix (a shuffle tree: the composition is associative), and
+// publishes its own prefix. Lower workgroups were dispatched first and
+// publish their aggregates without waiting on anyone, so every wait ends.
+// Then the workgroup's records and reports are written from the known start
+// state and output positions. The last workgroup to finish (a completion
+// counter it leaves at 0) writes the report.
+__global__ void __launch_bounds__(kGT) log_asm_onepass(AsmArgs a) {
   __shared__ Summ wagg[kGT / 64];
   __shared__ uint32_t wsum[kGT / 64][2 * kScenarios];
-  __shared__ uint32_t wsum2[kGT / 64][2];
-  __shared__ uint32_t last;
+  __shared__ Agg start_s;
+  __shared__ uint32_t last_s;
   const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63u;
   const uint32_t K = asm_items(a);
   // workgroups with items (at least one, which writes the report)
   const uint32_t G = max(1u, min(a.groups, (K + kGT * kChunk - 1) / (kGT * kChunk)));
-  if (blockIdx.x >= G) return;  // the whole workgroup
+  const uint32_t g = blockIdx.x;
+  if (g >= G) return;  // the whole workgroup; nothing waits on it
   Chunk c;
-  chunk_of<true>(a.events, a.hdr_off, a.seek, K, blockIdx.x * kGT + tid, c);
-  WgAgg agg;
+  chunk_of<true>(a.events, a.hdr_off, a.seek, K, g * kGT + tid, c);
+  Agg agg;
   const Summ x = wg_scan_excl<kGT>(c.s, wagg, tid, &agg.s);
-  // the workgroup's counts from each starting scenario, summed in one scan
-  uint32_t v[2 * kScenarios], tot[2 * kScenarios];
+  {
+    uint32_t v[2 * kScenarios], tot[2 * kScenarios];
 #pragma unroll
-  for (uint32_t sw = 0; sw < kScenarios; ++sw) {
-    const uint32_t sc = chunk_scenario(sw, x);
-    v[2 * sw] = pick(c.nrec, sc);  // 0 when stopped
-    v[2 * sw + 1] = pick(c.nrep, sc);
-  }
-  wg_sum_excl<kGT>(v, wsum, tid, tot);
+    for (uint32_t sw = 0; sw < kScenarios; ++sw) {
+      const uint32_t sc = chunk_scenario(sw, x);
+      v[2 * sw] = pick(c.nrec, sc);  // 0 when stopped
+      v[2 * sw + 1] = pick(c.nrep, sc);
+    }
+    wg_sum_excl<kGT>(v, wsum, tid, tot);
 #pragma unroll
-  for (uint32_t sw = 0; sw < kScenarios; ++sw) {
-    agg.nrec[sw] = tot[2 * sw];
-    agg.nrep[sw] = tot[2 * sw + 1];
+    for (uint32_t sw = 0; sw < kScenarios; ++sw) {
+      agg.nrec[sw] = tot[2 * sw];
+      agg.nrep[sw] = tot[2 * sw + 1];
+    }
   }
-  if (tid == 0) {
-    a.aggs[blockIdx.x] = agg;
-    const uint32_t n = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_ACQ_REL,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-    last = n == G - 1 ? 1u : 0u;
+  // ---- look-back (wave 0) ----
+  if (tid < 64) {
+    AsmSlot* me = a.slots + g;
+    if (lane == 0) {
+      store_agg(&me->agg, agg);
+      __hip_atomic_store(&me->flag, (a.tag << 2) | 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    Agg before = kAggIdentity;  // every workgroup before g, composed
+    for (int32_t hi = static_cast<int32_t>(g) - 1; hi >= 0; hi -= 64) {
+      // lane l: workgroup hi - 63 + l (lanes below 0: the identity)
+      const int32_t w = hi - 63 + static_cast<int32_t>(lane);
+      uint32_t f = 0;
+      if (w >= 0) {
+        while (((f = __hip_atomic_load(&a.slots[w].flag, __ATOMIC_ACQUIRE,
+                                       __HIP_MEMORY_SCOPE_AGENT)) >> 2) != a.tag)
+          __builtin_amdgcn_s_sleep(1);
+        f &= 3u;
+      }
+      // the nearest inclusive prefix: the window starts there
+      const uint64_t pm = __ballot(f == 2u);
+      const uint32_t from = pm ? 63u - static_cast<uint32_t>(__builtin_clzll(pm)) : 0u;
+      Agg v = kAggIdentity;
+      if (w >= 0 && lane >= from) v = load_agg(lane == from && pm ? &a.slots[w].incl : &a.slots[w].agg);
+      // fold the window in lane order (a shuffle tree: lane 63 ends with all)
+#pragma unroll
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        const Agg o = shfl_agg(v, (lane >= d ? lane - d : lane));
+        if (lane >= d) v = agg_compose(o, v);
+      }
+      const Agg win = shfl_agg(v, 63);
+      before = agg_compose(win, before);
+      if (pm) break;
+    }
+    if (lane == 0) {
+      store_agg(&me->incl, agg_compose(before, agg));
+      __hip_atomic_store(&me->flag, (a.tag << 2) | 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      start_s = before;
+    }
   }
   __syncthreads();
-  if (!last) return;
-  asm_scan<kGT>(a, wagg, wsum2, tid);
-  // the next call on this stream reuses the counter
-  if (tid == 0) __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__global__ void __launch_bounds__(kGT) log_asm_emit(AsmArgs a) {
-  __shared__ Summ wagg[kGT / 64];
-  __shared__ uint32_t wsum[kGT / 64][2];
-  const uint32_t tid = threadIdx.x;
-  const uint32_t K = asm_items(a);
-  if (blockIdx.x * kGT * kChunk >= K) return;  // the whole workgroup
-  const WgIn in = a.ins[blockIdx.x];
-  Chunk c;
-  chunk_of<false>(a.events, a.hdr_off, a.seek, K, blockIdx.x * kGT + tid, c);
-  Summ all;
-  const Summ x = wg_scan_excl<kGT>(c.s, wagg, tid, &all);
-  // this chunk's starting state
-  const uint32_t sw = scenario(in.st, in.scratch);
-  Reader r = {in.st, in.first, in.scratch, 0, 0};
+  // ---- emit from the workgroup's start ----
+  const Agg p = start_s;
+  const uint32_t in_st = p.s.pass ? a.init_st : p.s.c;
+  const uint64_t in_scratch = p.s.pass ? 0 : p.s.scratch;
+  const uint32_t init_sc = scenario(a.init_st, 0);
+  const uint32_t rec_base = pick(p.nrec, init_sc), rep_base = pick(p.nrep, init_sc);
+  const uint32_t j_base = p.s.nrec;
+  Reader r = {in_st, p.s.first, in_scratch, 0, 0};
   if (!x.pass) {
     r.st = x.c;
-    r.first = in.j0 + x.first;
+    r.first = j_base + x.first;
     r.scratch = x.scratch;
   } else if (r.st == kInFrag) {
     r.scratch += x.len;
   }
+  const uint32_t sw = scenario(in_st, in_scratch);
   const uint32_t sc = chunk_scenario(sw, x);
   uint32_t v[2], t[2];  // this chunk's counts from its known start (0 when stopped)
   chunk_counts(c.ev, sc, &v[0], &v[1]);
-  wg_sum_excl<kGT>(v, wsum, tid, t);
-  const uint32_t rb = v[0] + in.rec_base, pb = v[1] + in.rep_base;
-  const uint32_t j0 = in.j0 + x.nrec;
+  {
+    uint32_t (&ws2)[kGT / 64][2] = *reinterpret_cast<uint32_t (*)[kGT / 64][2]>(&wsum[0][0]);
+    wg_sum_excl<kGT>(v, ws2, tid, t);
+  }
+  const uint32_t rb = v[0] + rec_base, pb = v[1] + rep_base;
+  const uint32_t j0 = j_base + x.nrec;
   uint64_t hoff[kChunk];
 #pragma unroll
   for (uint32_t i = 0; i < kChunk; ++i) hoff[i] = i < c.s.nrec ? a.hdr_off[j0 + i] : 0;
   if (r.st == kInFrag) r.first_off = a.hdr_off[r.first];
-  Sink w = {true, 0, 0, 0, a.recs + rb, a.rec_cap > rb ? a.rec_cap - rb : 0u, a.reps + pb,
-            a.rep_cap > pb ? a.rep_cap - pb : 0u};
-  replay<true>(c.ev, hoff, j0, r, w);
+  Sink out = {true, 0, 0, 0, a.recs + rb, a.rec_cap > rb ? a.rec_cap - rb : 0u, a.reps + pb,
+              a.rep_cap > pb ? a.rep_cap - pb : 0u};
+  replay<true>(c.ev, hoff, j0, r, out);
   // the records' bytes: one atomic per wave
-  unsigned long long bytes = w.bytes;
+  unsigned long long bytes = out.bytes;
   for (int d = 32; d >= 1; d >>= 1) bytes += __shfl_xor(bytes, d, 64);
-  if ((tid & 63u) == 0 && bytes)
-    atomicAdd(reinterpret_cast<unsigned long long*>(&a.out->bytes), bytes);
+  if (lane == 0 && bytes) atomicAdd(a.bytes, bytes);
+  // ---- the last workgroup to finish writes the report ----
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_s_waitcnt(0);  // this workgroup's byte atomics have landed
+    const uint32_t n = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_s = n == G - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!last_s || tid != 0) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const Agg tot = load_agg(&a.slots[G - 1].incl);  // published before its arrival
+  const uint32_t r0 = pick(tot.nrec, init_sc), r1 = pick(tot.nrep, init_sc);
+  lvkv_log_read_report o;
+  o.status = (a.phys->status != LVKV_OK || r0 > a.rec_cap || r1 > a.rep_cap) ? LVKV_LOG_CAPACITY
+                                                                              : LVKV_OK;
+  o.nrecords = r0;
+  o.nreports = r1;
+  o.stopped = (!tot.s.pass && tot.s.c == kStopped) ? tot.s.stop5 : 0u;
+  o.bytes = __hip_atomic_load(a.bytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  *a.out = o;
+  // the next call with this scratch reuses the counters
+  __hip_atomic_store(a.bytes, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---- the records' bytes ---------------------------------------------------
@@ -632,11 +730,11 @@ __global__ void __launch_bounds__(kGT) log_asm_emit(AsmArgs a) {
 // spans j (records are in order and their fragments disjoint, a binary
 // search over their `first`); its payload goes to dest[j] = the payloads of
 // the returned fragments before it (a scan over candidates), so record i
-// starts at dest[first_i]. One launch: 1024 candidates a workgroup, the scan
-// across workgroups by decoupled look-back (each workgroup publishes its
-// aggregate, then its inclusive prefix, under the call's tag; it waits only
-// on lower workgroups, dispatched before it), then the workgroup's owned
-// fragments copied one per wave, 16 bytes a lane.
+// starts at dest[first_i]. Two launches: the places (1024 candidates a
+// workgroup, the scan across workgroups by decoupled look-back: each
+// workgroup publishes its aggregate, then its inclusive prefix, under the
+// call's tag, and waits only on lower workgroups, dispatched before it),
+// then the copies, one wave per candidate.
 
 constexpr uint32_t kGatherT = 256, kGatherItems = 4, kGatherPer = kGatherT * kGatherItems;
 
@@ -659,6 +757,7 @@ struct GatherArgs {
   uint64_t out_cap;
   uint64_t* rec_pos;      // nullable
   struct LookSlot* look;  // per workgroup
+  unsigned long long* dst;  // per candidate: its payload's place in `out`, or ~0 (not returned)
 };
 
 // The u16 at p (any alignment) from the aligned dword(s) holding it: no
@@ -685,16 +784,12 @@ __device__ __forceinline__ int32_t owner_of(const lvkv_log_record* recs, uint32_
 __global__ void __launch_bounds__(kGatherT) log_gather_kernel(GatherArgs a) {
   __shared__ unsigned long long wsum[kGatherT / 64];
   __shared__ unsigned long long base_s;
-  __shared__ uint32_t nown;
-  __shared__ uint32_t own_j[kGatherPer];
-  __shared__ unsigned long long own_dst[kGatherPer];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u, wave = tid >> 6;
   const uint32_t N = a.phys->status == LVKV_OK ? a.phys->count_ : 0u;
   const uint32_t R = a.phys->status == LVKV_OK ? min(a.read->nrecords, a.rec_cap) : 0u;
   const uint32_t g = blockIdx.x;
   if (g * kGatherPer >= N) return;  // the whole workgroup; nothing waits on it
-  if (tid == 0) nown = 0;
   // this thread's candidates: owned payload lengths
   const uint32_t j0 = g * kGatherPer + tid * kGatherItems;
   uint32_t len[kGatherItems];
@@ -760,64 +855,79 @@ __global__ void __launch_bounds__(kGatherT) log_gather_kernel(GatherArgs a) {
   uint64_t dst = base_s + pre + inc - mine;
 #pragma unroll
   for (uint32_t t = 0; t < kGatherItems; ++t) {
-    if (own[t] >= 0) {
-      const uint32_t j = j0 + t;
-      if (a.rec_pos != nullptr && a.recs[own[t]].first == j) a.rec_pos[own[t]] = dst;
-      const uint32_t k = atomicAdd(&nown, 1u);
-      own_j[k] = j;
-      own_dst[k] = dst;
+    const uint32_t j = j0 + t;
+    if (j < N) {
+      if (own[t] >= 0 && a.rec_pos != nullptr && a.recs[own[t]].first == j) a.rec_pos[own[t]] = dst;
+      a.dst[j] = own[t] >= 0 ? dst : ~0ull;
     }
     dst += len[t];
   }
-  __syncthreads();
-  // the owned fragments, one wave each
-  const uint32_t n = nown;
-  for (uint32_t k = wave; k < n; k += kGatherT / 64) {
-    const uint32_t j = own_j[k];
-    const uint64_t d = own_dst[k];
-    const uint8_t* src = a.file + a.hdr_off[j] + 7;
-    const uint32_t l = ld_u16_any(src - 3);
-    if (d + l > a.out_cap) continue;
-    // bytes up to the output's next 4-byte boundary, then whole output words
-    // rebuilt from two aligned source dwords (a buffer resource over the
-    // payload's aligned dwords: a dword past them reads as 0, one partly
-    // past a range's end would read as 0 whole), then the last 0-3 bytes
-    const uint32_t hb = min(l, (4u - static_cast<uint32_t>(d & 3u)) & 3u);
-    if (lane < hb) a.out[d + lane] = src[lane];
-    const uint64_t s0 = reinterpret_cast<uint64_t>(src);
-    const uint64_t sa = s0 & ~uint64_t{3};
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(sa), 0, static_cast<int>((s0 + l - sa + 3u) & ~uint64_t{3}),
-        kBufferDword3);
-    const uint32_t nw = (l - hb) >> 2;
-    uint32_t* dw = reinterpret_cast<uint32_t*>(a.out + d + hb);
-    for (uint32_t w = lane; w < nw; w += 64) {
-      const uint32_t so = static_cast<uint32_t>(s0 - sa) + hb + 4u * w;
-      const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(so & ~3u), 0, 0);
-      const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>((so & ~3u) + 4u), 0, 0);
-      dw[w] = __builtin_amdgcn_alignbyte(hi, lo, so & 3u);
+}
+
+// The owned fragments' payloads to their places, one wave per candidate (a
+// grid of N waves: the copies are latency-bound, so as many as the chip
+// holds are in flight; with the copy inside the scan's 61 workgroups it
+// took 680 us for a 66 MB log). Each output word is rebuilt from two aligned
+// source dwords (a buffer resource over the payload's aligned dwords: a
+// dword past them reads as 0; one partly past a range's end would read as 0
+// whole); the 0-3 bytes before the output's first 4-byte boundary and after
+// its last go bytewise.
+__global__ void __launch_bounds__(256) log_gather_copy_kernel(GatherArgs a) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t j = blockIdx.x * 4u + (threadIdx.x >> 6);
+  const uint32_t N = a.phys->status == LVKV_OK ? a.phys->count_ : 0u;
+  if (j >= N) return;
+  const uint64_t d = a.dst[j];
+  if (d == ~0ull) return;
+  const uint8_t* src = a.file + a.hdr_off[j] + 7;
+  const uint32_t l = ld_u16_any(src - 3);
+  if (d + l > a.out_cap) return;
+  const uint32_t hb = min(l, (4u - static_cast<uint32_t>(d & 3u)) & 3u);
+  if (lane < hb) a.out[d + lane] = src[lane];
+  const uint64_t s0 = reinterpret_cast<uint64_t>(src);
+  const uint64_t sa = s0 & ~uint64_t{3};
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>(sa), 0, static_cast<int>((s0 + l - sa + 3u) & ~uint64_t{3}),
+      kBufferDword3);
+  const uint32_t nw = (l - hb) >> 2;
+  uint32_t* dw = reinterpret_cast<uint32_t*>(a.out + d + hb);
+  const uint32_t sb = static_cast<uint32_t>(s0 - sa) + hb;
+  // four words a lane in flight per round
+  for (uint32_t w0 = 0; w0 < nw; w0 += 256) {
+    uint32_t lo[4], hi[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      const uint32_t so = sb + 4u * (w0 + 64u * u + lane);
+      lo[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(so & ~3u), 0, 0);
+      hi[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>((so & ~3u) + 4u), 0, 0);
     }
-    const uint32_t tb = (l - hb) & 3u;
-    if (lane < tb) a.out[d + hb + 4u * nw + lane] = src[hb + 4u * nw + lane];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      const uint32_t w = w0 + 64u * u + lane;
+      if (w < nw) dw[w] = __builtin_amdgcn_alignbyte(hi[u], lo[u], sb & 3u);
+    }
   }
+  const uint32_t tb = (l - hb) & 3u;
+  if (lane < tb) a.out[d + hb + 4u * nw + lane] = src[hb + 4u * nw + lane];
 }
 
 }  // namespace
 
 size_t log_asm_scratch_bytes(size_t max_items) {
   const size_t groups = (max_items + kGT * kChunk - 1) / (kGT * kChunk);
-  return groups * (sizeof(WgAgg) + sizeof(WgIn)) + 16;  // + log_asm_seek's two words
+  return groups * sizeof(AsmSlot) + 16;  // + log_asm_seek's two words
 }
 
-// `scratch`: log_asm_scratch_bytes(capacity + nblocks) bytes, 16-byte aligned;
-// `done`: a u32 that is 0 (zeroed once; every call leaves it at 0), used by
-// calls on this stream only.
+// `scratch`: log_asm_scratch_bytes(capacity + nblocks) bytes, 16-byte aligned
+// (any contents: slots of other tags are ignored); `done` and `bytes`: a u32
+// and a u64 that are 0 (zeroed once; every call leaves them at 0), used by
+// one call at a time; `tag`: this call's, never 0, below 2^30.
 hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
                                const lvkv_log_report* phys, uint64_t size, uint32_t capacity,
                                uint64_t initial_offset, lvkv_log_record* recs, uint32_t rec_cap,
                                lvkv_log_corruption* reps, uint32_t rep_cap,
                                lvkv_log_read_report* out, void* scratch, uint32_t* done,
-                               hipStream_t stream) {
+                               unsigned long long* bytes, uint32_t tag, hipStream_t stream) {
   AsmArgs a;
   a.events = events;
   a.hdr_off = hdr_off;
@@ -830,10 +940,11 @@ hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
   a.recs = recs;
   a.reps = reps;
   a.out = out;
-  a.aggs = static_cast<WgAgg*>(scratch);
-  a.ins = reinterpret_cast<WgIn*>(a.aggs + a.groups);
-  a.lohi = reinterpret_cast<uint32_t*>(a.ins + a.groups);
+  a.slots = static_cast<AsmSlot*>(scratch);
+  a.lohi = reinterpret_cast<uint32_t*>(a.slots + a.groups);
+  a.tag = tag;
   a.done = done;
+  a.bytes = bytes;
   a.init_st = initial_offset ? kResync : kIdle;
   a.seek.offset = initial_offset;
   // SkipToInitialBlock (log_reader.cc:33-54): the block holding the offset,
@@ -847,16 +958,15 @@ hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
     hipLaunchKernelGGL(log_asm_seek, dim3(1), dim3(64), 0, stream, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(log_asm_reduce, dim3(a.groups), dim3(kGT), 0, stream, a);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(log_asm_emit, dim3(a.groups), dim3(kGT), 0, stream, a);
+  hipLaunchKernelGGL(log_asm_onepass, dim3(a.groups), dim3(kGT), 0, stream, a);
   return hipGetLastError();
 }
 
-// lvkv_log_gather_device: one launch; `look`: 16 bytes per workgroup of
-// ceil(capacity / 1024), any contents (slots of other tags are ignored).
+// lvkv_log_gather_device: two launches; `look`: 32 bytes per workgroup of
+// ceil(capacity / 1024) (any contents: slots of other tags are ignored), then
+// 8 bytes per candidate.
 size_t log_gather_scratch_bytes(size_t capacity) {
-  return ((capacity + kGatherPer - 1) / kGatherPer) * sizeof(LookSlot);
+  return ((capacity + kGatherPer - 1) / kGatherPer) * sizeof(LookSlot) + capacity * 8;
 }
 
 hipError_t launch_log_gather(const uint8_t* file, const uint64_t* hdr_off, size_t capacity,
@@ -877,7 +987,12 @@ hipError_t launch_log_gather(const uint8_t* file, const uint64_t* hdr_off, size_
   a.rec_pos = rec_pos;
   a.look = static_cast<LookSlot*>(look);
   const uint32_t groups = static_cast<uint32_t>((capacity + kGatherPer - 1) / kGatherPer);
+  a.dst = reinterpret_cast<unsigned long long*>(a.look + groups);
   hipLaunchKernelGGL(log_gather_kernel, dim3(groups), dim3(kGatherT), 0, stream, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(log_gather_copy_kernel, dim3(static_cast<uint32_t>((capacity + 3) / 4)),
+                     dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -152,6 +152,27 @@ def main():
         torch.cuda.synchronize()
         us2 = (time.perf_counter() - t0) / 50 * 1e6
         print(f"log_read {nrec} records: {us2:.1f} us/call (verify + ReadRecord)", flush=True)
+        # + the records' bytes laid end to end (lvkv_log_gather_device)
+        payload = torch.empty(len(img), dtype=torch.uint8, device=dev)
+        rpos = torch.empty(cap, dtype=torch.int64, device=dev)
+        L.lvkv_log_gather_device.argtypes = [vp, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, vp,
+                                             vp, ctypes.c_uint64, vp, vp]
+
+        def gather():
+            rc = L.lvkv_log_gather_device(vp(buf.data_ptr()), vp(hdr.data_ptr()), cap,
+                                          vp(rp.data_ptr()), vp(recs.data_ptr()), cap,
+                                          vp(rd.data_ptr()), vp(payload.data_ptr()), len(img),
+                                          vp(rpos.data_ptr()), h)
+            assert rc == 0
+        for _ in range(5):
+            gather()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(50):
+            gather()
+        torch.cuda.synchronize()
+        us3 = (time.perf_counter() - t0) / 50 * 1e6
+        print(f"log_gather {nrec} records: {us3:.1f} us/call", flush=True)
 
 
 if __name__ == "__main__":
