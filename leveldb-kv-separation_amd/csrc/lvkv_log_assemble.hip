@@ -754,7 +754,8 @@ struct GatherArgs {
   uint64_t out_cap;
   uint64_t* rec_pos;      // nullable
   struct LookSlot* look;  // per workgroup
-  unsigned long long* dst;  // per candidate: its payload's place in `out`, or ~0 (not returned)
+  ulonglong2* dst;  // per candidate: {its payload's place in `out` (~0: not returned),
+                   //  payload file offset | length << 48}
 };
 
 // The u16 at p (any alignment) from the aligned dword(s) holding it: no
@@ -855,7 +856,10 @@ __global__ void __launch_bounds__(kGatherT) log_gather_kernel(GatherArgs a) {
     const uint32_t j = j0 + t;
     if (j < N) {
       if (own[t] >= 0 && a.rec_pos != nullptr && a.recs[own[t]].first == j) a.rec_pos[own[t]] = dst;
-      a.dst[j] = own[t] >= 0 ? dst : ~0ull;
+      // the copy's whole descriptor in one 16-byte entry: place, and the
+      // payload's file offset with its length in the top 16 bits
+      a.dst[j] = own[t] >= 0 ? make_ulonglong2(dst, (a.hdr_off[j] + 7) | (uint64_t{len[t]} << 48))
+                             : make_ulonglong2(~0ull, 0);
     }
     dst += len[t];
   }
@@ -874,10 +878,11 @@ __global__ void __launch_bounds__(256) log_gather_copy_kernel(GatherArgs a) {
   const uint32_t j = blockIdx.x * 4u + (threadIdx.x >> 6);
   const uint32_t N = a.phys->status == LVKV_OK ? a.phys->count_ : 0u;
   if (j >= N) return;
-  const uint64_t d = a.dst[j];
+  const ulonglong2 de = a.dst[j];
+  const uint64_t d = de.x;
   if (d == ~0ull) return;
-  const uint8_t* src = a.file + a.hdr_off[j] + 7;
-  const uint32_t l = ld_u16_any(src - 3);
+  const uint8_t* src = a.file + (de.y & ((uint64_t{1} << 48) - 1));
+  const uint32_t l = static_cast<uint32_t>(de.y >> 48);
   if (d + l > a.out_cap) return;
   const uint32_t hb = min(l, (4u - static_cast<uint32_t>(d & 3u)) & 3u);
   if (lane < hb) a.out[d + lane] = src[lane];
@@ -961,9 +966,9 @@ hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
 
 // lvkv_log_gather_device: two launches; `look`: 32 bytes per workgroup of
 // ceil(capacity / 1024) (any contents: slots of other tags are ignored), then
-// 8 bytes per candidate.
+// 16 bytes per candidate.
 size_t log_gather_scratch_bytes(size_t capacity) {
-  return ((capacity + kGatherPer - 1) / kGatherPer) * sizeof(LookSlot) + capacity * 8;
+  return ((capacity + kGatherPer - 1) / kGatherPer) * sizeof(LookSlot) + capacity * 16;
 }
 
 hipError_t launch_log_gather(const uint8_t* file, const uint64_t* hdr_off, size_t capacity,
@@ -984,7 +989,7 @@ hipError_t launch_log_gather(const uint8_t* file, const uint64_t* hdr_off, size_
   a.rec_pos = rec_pos;
   a.look = static_cast<LookSlot*>(look);
   const uint32_t groups = static_cast<uint32_t>((capacity + kGatherPer - 1) / kGatherPer);
-  a.dst = reinterpret_cast<unsigned long long*>(a.look + groups);
+  a.dst = reinterpret_cast<ulonglong2*>(a.look + groups);
   hipLaunchKernelGGL(log_gather_kernel, dim3(groups), dim3(kGatherT), 0, stream, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
