@@ -330,7 +330,7 @@ def _cpu_model():
     return "unknown"
 
 
-def live_pmc_traffic(launches: int = 16, timeout_s: float = 180.0):
+def live_pmc_traffic(launches: int = 16, timeout_s: float = 90.0):
     """HBM-side bytes per launch of the roofline kernel, measured for the code
     being benched: a child `rocprofv3 --pmc FETCH_SIZE -- python3 bench.py
     --isolated N` (the profiler starts its own process; this one never
