@@ -108,6 +108,10 @@ __device__ __forceinline__ void burst_body(const UniformArgs& a, const UniGeo& g
                                            bool live) {
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t gw = blockIdx.x * W + wave;
+  // The image is built by the first kBuild waves (all of them when W is a
+  // power of two; the first 8 of a 10- or 12-wave workgroup).
+  constexpr int kBuild = (W & (W - 1)) == 0 ? W : 8;
+  const bool builder = wave < static_cast<uint32_t>(kBuild);
   burst_stamp<F>(a, gw, 0);
   __amdgpu_buffer_rsrc_t r[NV];
 #pragma unroll
@@ -154,15 +158,15 @@ __device__ __forceinline__ void burst_body(const UniformArgs& a, const UniGeo& g
     // the chain D ahead is issued after it, so a wave's row loads never sit
     // between it and the walk of data that has already arrived.
     constexpr int D = (F & kBurstPipe2) ? 2 : 1;
-    LaneTabGen<W> lg;
-    lg.load(a.lane_cols, wave, lane);
+    LaneTabGen<kBuild> lg;
+    if (builder) lg.load(a.lane_cols, wave, lane);
     __builtin_amdgcn_sched_barrier(0);
     load_rows(0, D < NV ? D : NV);
     __builtin_amdgcn_sched_barrier(0);
     burst_stamp<F>(a, gw, 1);
-    burst_fill_rows<W>(lds, a, tid);
+    if (builder) burst_fill_rows<kBuild>(lds, a, tid);
     burst_stamp<F>(a, gw, 3);
-    lg.store(lds, wave, lane);
+    if (builder) lg.store(lds, wave, lane);
     burst_stamp<F>(a, gw, 5);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -206,9 +210,9 @@ __device__ __forceinline__ void burst_body(const UniformArgs& a, const UniGeo& g
   }
 
   // 1. Lane columns, then every row of every chain (or only chain 0).
-  LaneTabGen<W> lg;
-  RowTabStage<64 * W> rt;
-  if (!(F & kBurstNoBuild)) {
+  LaneTabGen<kBuild> lg;
+  RowTabStage<64 * kBuild> rt;
+  if (!(F & kBurstNoBuild) && builder) {
     lg.load(a.lane_cols, wave, lane);
     if (F & kBurstRowsHbm) rt.load(a.zpow, tid);
   }
@@ -217,11 +221,11 @@ __device__ __forceinline__ void burst_body(const UniformArgs& a, const UniGeo& g
   __builtin_amdgcn_sched_barrier(0);
   burst_stamp<F>(a, gw, 1);
   // 2. The LDS image, one barrier.
-  if (!(F & kBurstNoBuild)) {
+  if (!(F & kBurstNoBuild) && builder) {
     if (F & kBurstRowsHbm)
       rt.store(lds, tid);
     else
-      burst_fill_rows<W>(lds, a, tid);
+      burst_fill_rows<kBuild>(lds, a, tid);
     lg.store(lds, wave, lane);
   }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");

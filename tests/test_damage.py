@@ -172,6 +172,10 @@ def test_device_log_read_large_and_capacity(lvkv, gpu):
             for h in rng.choice(hdrs0, 12, replace=False):
                 img[int(h) + 6] = int(rng.integers(0, 8))
                 log_synth.fix_header_crc(img, int(h))
+        if trial == 5:  # a kEof-type header early on: nothing after it is read
+            h = int(lw.block_verdicts(base).hdrs[1500])
+            img[h + 6] = 5
+            log_synth.fix_header_crc(img, h)
         img = bytes(img)
         buf = torch.from_numpy(np.frombuffer(img, dtype=np.uint8).copy()).to(gpu)
         rd, records, reports, phys, gathered = lvkv.log_read(buf, gather=True)
@@ -179,6 +183,7 @@ def test_device_log_read_large_and_capacity(lvkv, gpu):
         want_recs, want_reps = lw.read_records(img)
         assert _device_log_records(img, records, hdrs, gathered) == want_recs, trial
         assert reports == want_reps, trial
+        assert rd["bytes"] == sum(r[1] for r in want_recs), trial
         # from initial offsets: block starts (resync), the trailer rule,
         # inside fragmented records, past the end
         offs = [32768 * 3, 32768 * 7 - 5, 32768 * 7 - 6, len(img), len(img) + 40000]
@@ -191,6 +196,7 @@ def test_device_log_read_large_and_capacity(lvkv, gpu):
             assert _device_log_records(img, records, hdrs, gathered) == o_recs, (trial, off)
             assert reports == o_reps, (trial, off)
             assert rd["stopped"] == int(stopped), (trial, off)
+            assert rd["bytes"] == sum(r[1] for r in o_recs), (trial, off)
     rd, records, reports, _, gathered = lvkv.log_read(buf, record_capacity=5, report_capacity=1,
                                                       gather=True)
     assert rd["status"] == 1 and rd["nrecords"] == len(want_recs)

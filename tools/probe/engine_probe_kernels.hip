@@ -44,3 +44,7 @@ PROBE(pk_w16, 0, 16, 3, 1)
 PROBE(pk_w16_bare, kBurstBare, 16, 3, 1)
 PROBE(pk_one, 0, 8, 5, 1)
 PROBE(pk_one_bare, kBurstBare, 8, 5, 1)
+PROBE(pk_w10c2_pipe1, kBurstPipe1, 10, 2, 2)
+PROBE(pk_w10c2, 0, 10, 2, 2)
+PROBE(pk_w12c2_pipe1, kBurstPipe1, 12, 2, 2)
+PROBE(pk_w10c2_pipe1_s2, kBurstPipe1 | kBurstSplit2, 10, 2, 2)

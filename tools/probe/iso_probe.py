@@ -45,6 +45,8 @@ KERNELS = {
     "pk_pair_pipe2_s2": (8, 3, 2, True), "pk_one_pipe2_s2": (8, 5, 1, True),
     "pk_w16": (16, 3, 1, True), "pk_w16_bare": (16, 3, 1, False),
     "pk_one": (8, 5, 1, True), "pk_one_bare": (8, 5, 1, False),
+    "pk_w10c2_pipe1": (10, 2, 2, True), "pk_w10c2": (10, 2, 2, True),
+    "pk_w12c2_pipe1": (12, 2, 2, True), "pk_w10c2_pipe1_s2": (10, 2, 2, True),
 }
 
 
