@@ -27,6 +27,7 @@ hipError_t launch_crc32c_batch(const KernelArgs& args, bool uniform_aligned,
 hipError_t launch_crc32c_general(const KernelArgs& a, int cus, hipStream_t stream);
 #ifdef LVKV_PROBE_BUILD
 extern uint64_t* g_log_stamps;
+extern uint64_t* g_asm_stamps;
 extern uint64_t* g_sst_stamps;
 extern uint32_t g_log_knobs;
 hipError_t launch_crc32c_probe(const KernelArgs& args, int variant,
@@ -910,6 +911,7 @@ const char* lvkv_cpu_impl(void) { return cpu_crc32c_impl_name(); }
 #ifdef LVKV_PROBE_BUILD
 // Probe entry points (tools/probe/liblvkv_probe.so only).
 void lvkv_debug_log_stamps(uint64_t* d_stamps) { g_log_stamps = d_stamps; }
+void lvkv_debug_asm_stamps(uint64_t* d_stamps) { g_asm_stamps = d_stamps; }
 void lvkv_debug_sst_stamps(uint64_t* d_stamps) { g_sst_stamps = d_stamps; }
 void lvkv_debug_log_knobs(uint32_t knobs) { g_log_knobs = knobs; }
 static uint64_t* g_debug_stamps = nullptr;

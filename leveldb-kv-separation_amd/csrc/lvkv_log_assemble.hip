@@ -13,16 +13,20 @@
 // other event resets the state the same way whatever came before, so the run
 // ends in a state of its own. That makes runs composable (Summ, compose),
 // and so are their record / report counts kept for each state a run may be
-// entered in (Agg, agg_compose). One launch, log_asm_onepass: each thread
-// summarises a chunk of kChunk items; a workgroup scan gives each chunk's
-// start relative to its workgroup's and the workgroup's aggregate; the
-// workgroup publishes it and looks back over the workgroups before it (64 at
-// a time, one lane each) to the nearest published inclusive prefix, which
-// gives its own starting state and output positions; then it writes its
-// records (LastRecordOffset from the verify's header offsets, loaded beside
-// the events) and reports. (The earlier form, a reduce launch whose last
-// workgroup scanned the aggregates and an emit launch redoing the chunks,
-// took the same 29 us on the 62k-record log.)
+// entered in (Agg, agg_compose). Two launches, one item per thread, each
+// item's summary and its counts for each entering state computed
+// straight-line: log_asm_reduce scans each workgroup's items and writes the
+// workgroup's aggregate; log_asm_emit folds the aggregates before its
+// workgroup (64 per wave step, by ballots and wave sums: window_fold) into
+// its starting state and output positions, rescans its items and puts each
+// through step() once, writing records (LastRecordOffset from the verify's
+// header offsets) and reports. Round 3 measured the alternatives on the
+// 62k-record log: chunks of four items replayed through step() five times
+// in one launch with a decoupled look-back, 29.7 us; one item per thread
+// with the look-back, 34 us (release / acquire flags) and 41 us (flags and
+// payloads as device-scope atomics, which contend): the look-back's waits,
+// not the arithmetic, were the cost. A kernel boundary is the cheaper
+// cross-XCD exchange.
 //
 // An initial offset (log_reader.cc:29-54, :80-89, :182-187, :261-266) is
 // applied to the events as they are loaded: the blocks before the first one
@@ -75,7 +79,7 @@ __device__ __forceinline__ Summ compose(const Summ& x, const Summ& y) {
   return r;
 }
 
-// The reader's state while a chunk is replayed.
+// The reader's state before an item.
 struct Reader {
   uint32_t st;       // kIdle / kInFrag / kStopped / kResync, or kUnknown (summaries)
   uint32_t first;    // kInFrag: the fragment's FIRST
@@ -188,11 +192,7 @@ __device__ __forceinline__ void step(Reader& r, uint32_t ev, uint32_t j, uint64_
   }
 }
 
-#ifndef LVKV_ASM_CHUNK
-#define LVKV_ASM_CHUNK 4
-#endif
-constexpr uint32_t kChunk = LVKV_ASM_CHUNK;  // items per thread (one 4 kChunk-byte load)
-constexpr uint32_t kGT = 256;     // threads per workgroup of the grid launches
+constexpr uint32_t kGT = 256;  // threads (= items) per workgroup of the grid launch
 
 __device__ __forceinline__ bool is_candidate(uint32_t ev) {
   const uint32_t kind = ev & 15u;
@@ -225,29 +225,6 @@ __device__ __forceinline__ uint32_t seek_event(const Seek& sk, const uint64_t* h
   return ev;
 }
 
-// The chunk's items [k0, k1) into registers (the rest "no event"). k0 is a
-// multiple of kChunk and the event array 16-byte aligned.
-__device__ __forceinline__ void load_chunk(const uint32_t* events, const uint64_t* hdr_off,
-                                           const Seek& sk, uint32_t k0, uint32_t k1,
-                                           uint32_t (&ev)[kChunk]) {
-  if (kChunk == 4) {
-    const uint4 v = k0 < k1 ? reinterpret_cast<const uint4*>(events + k0)[0] : make_uint4(0, 0, 0, 0);
-    ev[0] = v.x;
-    ev[1 % kChunk] = v.y;
-    ev[2 % kChunk] = v.z;
-    ev[3 % kChunk] = v.w;
-  } else if (kChunk == 2) {
-    const uint2 v = k0 < k1 ? reinterpret_cast<const uint2*>(events + k0)[0] : make_uint2(0, 0);
-    ev[0] = v.x;
-    ev[1 % kChunk] = v.y;
-  } else {
-    ev[0] = k0 < k1 ? events[k0] : 0u;
-  }
-#pragma unroll
-  for (uint32_t i = 0; i < kChunk; ++i)
-    ev[i] = k0 + i >= k1 ? log_event(kEvNone, 0, 0) : seek_event(sk, hdr_off, k0 + i, ev[i]);
-}
-
 // v[i] for a run-time i by unrolled selects (no register array in scratch);
 // 0 when i >= N.
 template <typename T, uint32_t N>
@@ -256,18 +233,6 @@ __device__ __forceinline__ T pick(const T (&v)[N], uint32_t i) {
 #pragma unroll
   for (uint32_t k = 0; k < N; ++k) r = i == k ? v[k] : r;
   return r;
-}
-
-// The chunk through step(); hoff[c] = header offset of its c-th candidate.
-template <bool kOut>
-__device__ __forceinline__ void replay(const uint32_t (&ev)[kChunk], const uint64_t (&hoff)[kChunk],
-                                       uint32_t j0, Reader& r, Sink& out) {
-  uint32_t c = 0;
-#pragma unroll
-  for (uint32_t i = 0; i < kChunk; ++i) {
-    step<kOut>(r, ev[i], j0 + c, pick(hoff, c), out);
-    c += is_candidate(ev[i]) ? 1u : 0u;
-  }
 }
 
 constexpr Summ kIdentity = {1, kIdle, 0, 0, 0, 0, 0};  // no events
@@ -285,61 +250,59 @@ __device__ __forceinline__ uint32_t scenario(uint32_t st, uint64_t scratch) {
                           : kScEmpty;
 }
 
-// A chunk's start given its workgroup's start (scenario sw) and the
-// composed summary `x` of the chunks before it in the workgroup.
+// An item's start given its run's start (scenario sw) and the composed
+// summary `x` of the items before it in the run.
 __device__ __forceinline__ uint32_t chunk_scenario(uint32_t sw, const Summ& x) {
+  if (sw == kScStopped) return kScStopped;  // nothing after a stop counts
   if (!x.pass) return scenario(x.c, x.scratch);
   if (sw == kScEmpty && x.len != 0) return kScFrag;
   return sw;
 }
 
-// One thread's chunk: events, summary and counts from each starting state.
-struct Chunk {
-  uint32_t ev[kChunk];
-  Summ s;
-  uint32_t nrec[kScenarios], nrep[kScenarios];
-};
-
-// A chunk's counts from starting scenario sc (kScStopped: none).
-__device__ __forceinline__ void chunk_counts(const uint32_t (&ev)[kChunk], uint32_t sc,
-                                             uint32_t* nrec, uint32_t* nrep) {
-  uint64_t hz[kChunk];
-#pragma unroll
-  for (uint32_t i = 0; i < kChunk; ++i) hz[i] = 0;
-  Sink cnt = {false, 0, 0, 0, nullptr, 0, nullptr, 0};
-  Reader r = {sc == kScIdle ? kIdle : sc == kScResync ? kResync : sc == kScStopped ? kStopped : kInFrag,
-              0, sc == kScFrag ? 1u : 0u, 0, 0};
-  replay<true>(ev, hz, 0, r, cnt);
-  *nrec = cnt.nrec;
-  *nrep = cnt.nrep;
+// One event as a run: the state it leaves the reader in (step() from an
+// unknown state, straight-line).
+__device__ __forceinline__ Summ event_summ(uint32_t ev) {
+  const uint32_t kind = ev & 15u, type = (ev >> 8) & 255u, n = ev >> 16;
+  Summ s = kIdentity;
+  s.nrec = is_candidate(ev) ? 1u : 0u;
+  const bool rec = kind == kEvRec;
+  if (kind == kEvSkip || kind == kEvNone) return s;
+  if (rec && type == 3) {  // MIDDLE: passes the state through
+    s.len = n;
+    return s;
+  }
+  s.pass = 0;
+  const bool stop = kind == kEvEof || (rec && type == 5);
+  const bool first = rec && type == 2;
+  s.c = stop ? kStopped : first ? kInFrag : kIdle;
+  s.stop5 = rec && type == 5 ? 1u : 0u;
+  s.scratch = first ? n : 0u;
+  return s;
 }
 
-// The chunk's events and summary; with kCounts, its counts from every
-// starting scenario too.
-template <bool kCounts>
-__device__ __forceinline__ void chunk_of(const uint32_t* events, const uint64_t* hdr_off,
-                                         const Seek& sk, uint32_t K, uint32_t t, Chunk& c) {
-  const uint32_t k0 = t * kChunk;
-  load_chunk(events, hdr_off, sk, k0, min(K, k0 + kChunk), c.ev);
-  uint64_t hz[kChunk];
+// One event's record / report counts for each entering scenario, packed
+// rec | rep << 16 (step()'s outputs, straight-line).
+__device__ __forceinline__ void event_counts(uint32_t ev, uint32_t (&cnt)[kScenarios]) {
+  const uint32_t kind = ev & 15u, type = (ev >> 8) & 255u;
+  const bool rec = kind == kEvRec;
+  const bool nop = kind == kEvSkip || kind == kEvNone || kind == kEvEof;
+  const uint32_t phys = (kind == kEvChecksum || kind == kEvBadLength) ? 1u : 0u;
 #pragma unroll
-  for (uint32_t i = 0; i < kChunk; ++i) hz[i] = 0;
-  Sink none = {false, 0, 0, 0, nullptr, 0, nullptr, 0};
-  Reader u = {kUnknown, 0, 0, 0, 0};
-  replay<false>(c.ev, hz, 0, u, none);
-  c.s.pass = u.st == kUnknown ? 1u : 0u;
-  c.s.c = c.s.pass ? kIdle : u.st;
-  c.s.len = c.s.pass ? u.scratch : 0;
-  c.s.scratch = c.s.pass ? 0 : u.scratch;
-  c.s.first = u.first;
-  c.s.stop5 = u.stopped;
-  uint32_t n = 0;
-#pragma unroll
-  for (uint32_t i = 0; i < kChunk; ++i) n += is_candidate(c.ev[i]) ? 1u : 0u;
-  c.s.nrec = n;
-  if (kCounts) {
-#pragma unroll
-    for (uint32_t sc = 0; sc < kScenarios; ++sc) chunk_counts(c.ev, sc, &c.nrec[sc], &c.nrep[sc]);
+  for (uint32_t sc = 0; sc < kScenarios; ++sc) {
+    const uint32_t idle = sc == kScIdle, frag = sc == kScFrag;
+    const uint32_t in = sc == kScFrag || sc == kScEmpty;
+    uint32_t nrec = 0, nrep = 0;
+    if (rec) {
+      nrec = (type == 1 || (type == 4 && in)) ? 1u : 0u;
+      nrep = (type == 1 || type == 2) ? frag
+             : (type == 3 || type == 4) ? idle
+             : type == 5              ? 0u
+             : type == 6              ? in
+                                      : 1u;
+    } else if (!nop) {
+      nrep = phys + in;
+    }
+    cnt[sc] = nrec | (nrep << 16);
   }
 }
 
@@ -349,16 +312,27 @@ __device__ __forceinline__ uint64_t shfl_up64(uint64_t v, uint32_t d) {
   return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
-__device__ __forceinline__ Summ shfl_up_summ(const Summ& x, uint32_t d) {
+// A summary in five dwords for the shuffles: pass, c and stop5 packed; len
+// and scratch share one word (a summary uses len only when pass, scratch
+// only when not).
+__device__ __forceinline__ uint32_t summ_flags(const Summ& x) {
+  return x.pass | (x.c << 1) | (x.stop5 << 4);
+}
+__device__ __forceinline__ Summ summ_unpack(uint32_t f, uint32_t first, uint32_t nrec, uint64_t b) {
   Summ r;
-  r.pass = __shfl_up(x.pass, d, 64);
-  r.c = __shfl_up(x.c, d, 64);
-  r.len = shfl_up64(x.len, d);
-  r.scratch = shfl_up64(x.scratch, d);
-  r.first = __shfl_up(x.first, d, 64);
-  r.nrec = __shfl_up(x.nrec, d, 64);
-  r.stop5 = __shfl_up(x.stop5, d, 64);
+  r.pass = f & 1u;
+  r.c = (f >> 1) & 7u;
+  r.stop5 = f >> 4;
+  r.len = r.pass ? b : 0u;
+  r.scratch = r.pass ? 0u : b;
+  r.first = first;
+  r.nrec = nrec;
   return r;
+}
+
+__device__ __forceinline__ Summ shfl_up_summ(const Summ& x, uint32_t d) {
+  return summ_unpack(__shfl_up(summ_flags(x), d, 64), __shfl_up(x.first, d, 64),
+                     __shfl_up(x.nrec, d, 64), shfl_up64(x.pass ? x.len : x.scratch, d));
 }
 
 // Workgroup-wide exclusive scan of `s` under compose (kT threads): a shuffle
@@ -432,14 +406,6 @@ struct Agg {
   uint32_t nrec[kScenarios], nrep[kScenarios];
 };
 
-// A workgroup's look-back slot: its aggregate, then its inclusive prefix (the
-// composition of every workgroup up to it), each published by a release of
-// `flag` = call tag << 2 | 1 or 2.
-struct AsmSlot {
-  uint32_t flag, pad_[3];
-  Agg agg, incl;
-};
-
 struct AsmArgs {
   const uint32_t* events;
   const uint64_t* hdr_off;
@@ -450,14 +416,22 @@ struct AsmArgs {
   uint32_t init_st; // the reader's first state: kIdle, or kResync with an offset
   Seek seek;
   uint32_t* lohi;   // log_asm_seek's output (seek.lohi)
-  uint32_t tag;     // this call's look-back tag (never 0, < 2^30)
   uint32_t* done;   // workgroups finished (left at 0 by the last one)
   unsigned long long* bytes;  // the records' bytes, summed (left at 0 by the last one)
   lvkv_log_record* recs;
   lvkv_log_corruption* reps;
   lvkv_log_read_report* out;
-  AsmSlot* slots;
+  Agg* aggs;        // per workgroup (log_asm_reduce)
+  uint64_t* stamps;  // probe build only: 8 u64 per workgroup
 };
+
+// Phase stamps of log_asm_emit (probe build): 0 start, 1 prefix folded,
+// 3 scanned, 5 items written.
+__device__ __forceinline__ void asm_stamp(const AsmArgs& a, uint32_t slot) {
+#ifdef LVKV_PROBE_BUILD
+  if (a.stamps != nullptr) a.stamps[blockIdx.x * 8u + slot] = __builtin_amdgcn_s_memrealtime();
+#endif
+}
 
 // Items on the device: candidate records the verify placed, plus blocks.
 __device__ __forceinline__ uint32_t asm_items(const AsmArgs& a) {
@@ -511,211 +485,217 @@ __device__ __forceinline__ Agg agg_compose(const Agg& x, const Agg& y) {
 
 constexpr Agg kAggIdentity = {kIdentity, {0, 0, 0, 0}, {0, 0, 0, 0}};
 
-__device__ __forceinline__ Agg shfl_agg(const Agg& v, uint32_t src) {
-  Agg r;
-  r.s.pass = __shfl(v.s.pass, src, 64);
-  r.s.c = __shfl(v.s.c, src, 64);
-  r.s.len = __shfl(static_cast<unsigned long long>(v.s.len), src, 64);
-  r.s.scratch = __shfl(static_cast<unsigned long long>(v.s.scratch), src, 64);
-  r.s.first = __shfl(v.s.first, src, 64);
-  r.s.nrec = __shfl(v.s.nrec, src, 64);
-  r.s.stop5 = __shfl(v.s.stop5, src, 64);
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 #pragma unroll
-  for (uint32_t i = 0; i < kScenarios; ++i) {
-    r.nrec[i] = __shfl(v.nrec[i], src, 64);
-    r.nrep[i] = __shfl(v.nrep[i], src, 64);
+  for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(static_cast<unsigned long long>(v), d, 64);
+  return v;
+}
+
+// The 64 lanes' aggregates composed in lane order (the look-back window; all
+// 64 lanes active), by ballots and sums instead of a tree of agg_compose:
+// the window's state is the one its last reset lane leaves (plus the MIDDLE
+// bytes after it), or stopped from its first stop lane on; lane l is entered
+// in the state of the last reset lane below it, or in the window's own
+// entering state when there is none.
+__device__ __forceinline__ Agg window_fold(const Agg& A, uint32_t lane) {
+  const bool reset = !A.s.pass;
+  const uint64_t Rm = __ballot(reset);
+  const uint64_t Sm = __ballot(reset && A.s.c == kStopped);
+  const uint64_t Lm = __ballot(A.s.pass && A.s.len != 0);
+  const uint64_t below = (uint64_t{1} << lane) - 1u;
+  Agg r;
+  r.s = kIdentity;
+  r.s.nrec = static_cast<uint32_t>(wave_sum64(A.s.nrec));
+  if (Sm) {
+    r.s.pass = 0;
+    r.s.c = kStopped;
+    r.s.stop5 = __shfl(A.s.stop5, static_cast<uint32_t>(__builtin_ctzll(Sm)), 64);
+  } else if (Rm) {
+    const uint32_t r0 = 63u - static_cast<uint32_t>(__builtin_clzll(Rm));
+    const uint32_t c = __shfl(A.s.c, r0, 64);
+    const uint64_t tail = wave_sum64(lane > r0 ? A.s.len : 0u);
+    r.s.pass = 0;
+    r.s.c = c;
+    r.s.scratch = __shfl(static_cast<unsigned long long>(A.s.scratch), r0, 64) + (c == kInFrag ? tail : 0u);
+    r.s.first = __shfl(A.s.first, r0, 64) + static_cast<uint32_t>(wave_sum64(lane < r0 ? A.s.nrec : 0u));
+  } else {
+    r.s.len = wave_sum64(A.s.len);
+  }
+  // lane l's entering scenario: fixed by the last reset below it, if any
+  const uint64_t rb = Rm & below;
+  const uint32_t rl = rb ? 63u - static_cast<uint32_t>(__builtin_clzll(rb)) : 0u;
+  const uint32_t rc = __shfl(A.s.c, rl, 64);
+  const uint64_t rs = __shfl(static_cast<unsigned long long>(A.s.scratch), rl, 64);
+  const uint64_t between = Lm & below & ~((uint64_t{2} << rl) - 1u);  // lanes in (rl, l)
+  const uint32_t fixed = (Sm & below) ? kScStopped : scenario(rc, rs | (between ? 1u : 0u));
+  const bool len_below = (Lm & below) != 0;
+#pragma unroll
+  for (uint32_t sw = 0; sw < kScenarios; ++sw) {
+    const uint32_t sc = rb ? fixed : (sw == kScEmpty && len_below ? kScFrag : sw);
+    const uint64_t t = wave_sum64(pick(A.nrec, sc) | (uint64_t{pick(A.nrep, sc)} << 32));
+    r.nrec[sw] = static_cast<uint32_t>(t);
+    r.nrep[sw] = static_cast<uint32_t>(t >> 32);
   }
   return r;
 }
 
-// Slot words move as agent-scope relaxed atomics (sc1: through to the
-// coherent level, no L1/L2 maintenance). The publisher's stores are waited
-// for (vmcnt) before its flag store, and a reader reads the words only after
-// seeing the flag: an acquire per wait would invalidate the XCD's L2 each
-// time (a first form with acquire spins took 678 us a call).
+// Counters shared by every workgroup of a launch move as agent-scope atomic
+// read-modify-writes (a fetch-add of 0 reads, an exchange writes): those are
+// performed at the device's coherence point, past every XCD's L2, so no L2
+// writeback or invalidate is needed.
 template <typename T>
-__device__ __forceinline__ T sc1_ld(const T* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ T co_ld(const T* p) {
+  // a zero the compiler cannot see: an atomic add of a known 0 is folded
+  // into a plain load
+  uint32_t z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return __hip_atomic_fetch_add(const_cast<T*>(p), static_cast<T>(z), __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
 }
 template <typename T>
-__device__ __forceinline__ void sc1_st(T* p, T v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void co_st(T* p, T v) {
+  (void)__hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Every earlier memory operation of the wave has completed (and the compiler
+// moves none across).
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-__device__ __forceinline__ Agg load_agg(const Agg* p) {
-  Agg r;
-  r.s.pass = sc1_ld(&p->s.pass);
-  r.s.c = sc1_ld(&p->s.c);
-  r.s.len = sc1_ld(&p->s.len);
-  r.s.scratch = sc1_ld(&p->s.scratch);
-  r.s.first = sc1_ld(&p->s.first);
-  r.s.nrec = sc1_ld(&p->s.nrec);
-  r.s.stop5 = sc1_ld(&p->s.stop5);
+
+
+// The items of workgroup g: the event of each thread's item, its counts
+// for each entering scenario, its summary's exclusive scan in the workgroup
+// (x), its exclusive output positions for each scenario the workgroup may be
+// entered in (v: rec | rep << 16, at most 256 records and 512 reports), and
+// the workgroup's aggregate.
+struct Items {
+  uint32_t ev;
+  Summ x;
+  uint32_t v[kScenarios];
+  Agg agg;
+};
+
+__device__ __forceinline__ void wg_items(const AsmArgs& a, uint32_t K, uint32_t g, uint32_t tid,
+                                         Summ (&wagg)[kGT / 64],
+                                         uint32_t (&wsum)[kGT / 64][kScenarios], Items& it) {
+  const uint32_t k = g * kGT + tid;
+  it.ev = k < K ? seek_event(a.seek, a.hdr_off, k, a.events[k]) : log_event(kEvNone, 0, 0);
+  uint32_t cnt[kScenarios];
+  event_counts(it.ev, cnt);
+  it.x = wg_scan_excl<kGT>(event_summ(it.ev), wagg, tid, &it.agg.s);
+  uint32_t tot[kScenarios];
 #pragma unroll
-  for (uint32_t i = 0; i < kScenarios; ++i) {
-    r.nrec[i] = sc1_ld(&p->nrec[i]);
-    r.nrep[i] = sc1_ld(&p->nrep[i]);
-  }
-  return r;
-}
-
-__device__ __forceinline__ void store_agg(Agg* p, const Agg& v) {
-  sc1_st(&p->s.pass, v.s.pass);
-  sc1_st(&p->s.c, v.s.c);
-  sc1_st(&p->s.len, v.s.len);
-  sc1_st(&p->s.scratch, v.s.scratch);
-  sc1_st(&p->s.first, v.s.first);
-  sc1_st(&p->s.nrec, v.s.nrec);
-  sc1_st(&p->s.stop5, v.s.stop5);
+  for (uint32_t sw = 0; sw < kScenarios; ++sw) it.v[sw] = pick(cnt, chunk_scenario(sw, it.x));
+  wg_sum_excl<kGT>(it.v, wsum, tid, tot);
 #pragma unroll
-  for (uint32_t i = 0; i < kScenarios; ++i) {
-    sc1_st(&p->nrec[i], v.nrec[i]);
-    sc1_st(&p->nrep[i], v.nrep[i]);
+  for (uint32_t sw = 0; sw < kScenarios; ++sw) {
+    it.agg.nrec[sw] = tot[sw] & 0xffffu;
+    it.agg.nrep[sw] = tot[sw] >> 16;
   }
 }
 
-// ReadRecord over every event in ONE launch (reduce, look-back, emit):
-// workgroup g's chunks are summarised and scanned (each chunk's start
-// relative to the workgroup's; the workgroup's aggregate with its counts for
-// each entering state); wave 0 publishes the aggregate, then looks back over
-// the slots of the workgroups before it, 64 at a time (one lane each, all
-// loads at once), composing aggregates back to the nearest published
-// inclusive prefix (a shuffle tree: the composition is associative), and
-// publishes its own prefix. Lower workgroups were dispatched first and
-// publish their aggregates without waiting on anyone, so every wait ends.
-// Then the workgroup's records and reports are written from the known start
-// state and output positions. The last workgroup to finish (a completion
-// counter it leaves at 0) writes the report.
-__global__ void __launch_bounds__(kGT) log_asm_onepass(AsmArgs a) {
+// Workgroups with items (at least one, which writes the report).
+__device__ __forceinline__ uint32_t asm_groups(const AsmArgs& a, uint32_t K) {
+  return max(1u, min(a.groups, (K + kGT - 1) / kGT));
+}
+
+// ReadRecord, launch 1 of 2: each workgroup's aggregate.
+__global__ void __launch_bounds__(kGT) log_asm_reduce(AsmArgs a) {
   __shared__ Summ wagg[kGT / 64];
-  __shared__ uint32_t wsum[kGT / 64][2 * kScenarios];
+  __shared__ uint32_t wsum[kGT / 64][kScenarios];
+  const uint32_t K = asm_items(a);
+  if (blockIdx.x >= asm_groups(a, K)) return;
+  Items it;
+  wg_items(a, K, blockIdx.x, threadIdx.x, wagg, wsum, it);
+  if (threadIdx.x == 0) a.aggs[blockIdx.x] = it.agg;
+}
+
+// ReadRecord, launch 2 of 2: wave 0 folds the aggregates of the workgroups
+// before this one (64 at a time, window_fold) into its entering state and
+// output positions, while the items are rescanned; then each item goes
+// through step() once. Workgroup G - 1 writes the report's counts; the last
+// workgroup to finish (a completion counter it leaves at 0) writes the
+// records' bytes.
+__global__ void __launch_bounds__(kGT) log_asm_emit(AsmArgs a) {
+  __shared__ Summ wagg[kGT / 64];
+  __shared__ uint32_t wsum[kGT / 64][kScenarios];
   __shared__ Agg start_s;
   __shared__ uint32_t last_s;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
   const uint32_t K = asm_items(a);
-  // workgroups with items (at least one, which writes the report)
-  const uint32_t G = max(1u, min(a.groups, (K + kGT * kChunk - 1) / (kGT * kChunk)));
+  const uint32_t G = asm_groups(a, K);
   const uint32_t g = blockIdx.x;
-  if (g >= G) return;  // the whole workgroup; nothing waits on it
-  Chunk c;
-  chunk_of<true>(a.events, a.hdr_off, a.seek, K, g * kGT + tid, c);
-  Agg agg;
-  const Summ x = wg_scan_excl<kGT>(c.s, wagg, tid, &agg.s);
-  {
-    uint32_t v[2 * kScenarios], tot[2 * kScenarios];
-#pragma unroll
-    for (uint32_t sw = 0; sw < kScenarios; ++sw) {
-      const uint32_t sc = chunk_scenario(sw, x);
-      v[2 * sw] = pick(c.nrec, sc);  // 0 when stopped
-      v[2 * sw + 1] = pick(c.nrep, sc);
-    }
-    wg_sum_excl<kGT>(v, wsum, tid, tot);
-#pragma unroll
-    for (uint32_t sw = 0; sw < kScenarios; ++sw) {
-      agg.nrec[sw] = tot[2 * sw];
-      agg.nrep[sw] = tot[2 * sw + 1];
-    }
-  }
-  // ---- look-back (wave 0) ----
+  if (g >= G) return;  // the whole workgroup
+  if (tid == 0) asm_stamp(a, 0);
   if (tid < 64) {
-    AsmSlot* me = a.slots + g;
-    if (lane == 0) {
-      store_agg(&me->agg, agg);
-      __hip_atomic_store(&me->flag, (a.tag << 2) | 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
     Agg before = kAggIdentity;  // every workgroup before g, composed
-    for (int32_t hi = static_cast<int32_t>(g) - 1; hi >= 0; hi -= 64) {
-      // lane l: workgroup hi - 63 + l (lanes below 0: the identity)
-      const int32_t w = hi - 63 + static_cast<int32_t>(lane);
-      uint32_t f = 0;
-      if (w >= 0) {
-        while (((f = __hip_atomic_load(&a.slots[w].flag, __ATOMIC_ACQUIRE,
-                                       __HIP_MEMORY_SCOPE_AGENT)) >> 2) != a.tag)
-          __builtin_amdgcn_s_sleep(1);
-        f &= 3u;
-      }
-      // the nearest inclusive prefix: the window starts there
-      const uint64_t pm = __ballot(f == 2u);
-      const uint32_t from = pm ? 63u - static_cast<uint32_t>(__builtin_clzll(pm)) : 0u;
-      Agg v = kAggIdentity;
-      if (w >= 0 && lane >= from) v = load_agg(lane == from && pm ? &a.slots[w].incl : &a.slots[w].agg);
-      // fold the window in lane order (a shuffle tree: lane 63 ends with all)
-#pragma unroll
-      for (uint32_t d = 1; d < 64; d <<= 1) {
-        const Agg o = shfl_agg(v, (lane >= d ? lane - d : lane));
-        if (lane >= d) v = agg_compose(o, v);
-      }
-      const Agg win = shfl_agg(v, 63);
-      before = agg_compose(win, before);
-      if (pm) break;
+    for (uint32_t base = 0; base < g; base += 64) {
+      const Agg v = base + lane < g ? a.aggs[base + lane] : kAggIdentity;
+      before = agg_compose(before, window_fold(v, lane));
     }
     if (lane == 0) {
-      store_agg(&me->incl, agg_compose(before, agg));
-      __hip_atomic_store(&me->flag, (a.tag << 2) | 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       start_s = before;
+      asm_stamp(a, 1);
     }
   }
-  __syncthreads();
-  // ---- emit from the workgroup's start ----
+  Items it;
+  wg_items(a, K, g, tid, wagg, wsum, it);  // its barriers also publish start_s
+  if (tid == 0) asm_stamp(a, 3);
+  const Summ& x = it.x;
+  const uint32_t ev = it.ev;
   const Agg p = start_s;
   const uint32_t in_st = p.s.pass ? a.init_st : p.s.c;
   const uint64_t in_scratch = p.s.pass ? 0 : p.s.scratch;
   const uint32_t init_sc = scenario(a.init_st, 0);
-  const uint32_t rec_base = pick(p.nrec, init_sc), rep_base = pick(p.nrep, init_sc);
-  const uint32_t j_base = p.s.nrec;
+  const uint32_t sw = scenario(in_st, in_scratch);
+  const uint32_t pos = pick(it.v, sw);  // 0 once stopped
+  const uint32_t rb = pick(p.nrec, init_sc) + (pos & 0xffffu);
+  const uint32_t pb = pick(p.nrep, init_sc) + (pos >> 16);
+  const uint32_t j = p.s.nrec + x.nrec;  // the item's candidate index
   Reader r = {in_st, p.s.first, in_scratch, 0, 0};
-  if (!x.pass) {
+  if (in_st == kStopped) {
+    // a stop before this workgroup: nothing after it is read
+  } else if (!x.pass) {
     r.st = x.c;
-    r.first = j_base + x.first;
+    r.first = p.s.nrec + x.first;
     r.scratch = x.scratch;
   } else if (r.st == kInFrag) {
     r.scratch += x.len;
   }
-  const uint32_t sw = scenario(in_st, in_scratch);
-  const uint32_t sc = chunk_scenario(sw, x);
-  uint32_t v[2], t[2];  // this chunk's counts from its known start (0 when stopped)
-  chunk_counts(c.ev, sc, &v[0], &v[1]);
-  {
-    uint32_t (&ws2)[kGT / 64][2] = *reinterpret_cast<uint32_t (*)[kGT / 64][2]>(&wsum[0][0]);
-    wg_sum_excl<kGT>(v, ws2, tid, t);
-  }
-  const uint32_t rb = v[0] + rec_base, pb = v[1] + rep_base;
-  const uint32_t j0 = j_base + x.nrec;
-  uint64_t hoff[kChunk];
-#pragma unroll
-  for (uint32_t i = 0; i < kChunk; ++i) hoff[i] = i < c.s.nrec ? a.hdr_off[j0 + i] : 0;
-  if (r.st == kInFrag) r.first_off = a.hdr_off[r.first];
+  const uint32_t kind = ev & 15u, type = (ev >> 8) & 255u;
+  const uint64_t hoff = kind == kEvRec && type == 1 && r.st != kStopped ? a.hdr_off[j] : 0;
+  if (r.st == kInFrag && kind == kEvRec && type == 4) r.first_off = a.hdr_off[r.first];
   Sink out = {true, 0, 0, 0, a.recs + rb, a.rec_cap > rb ? a.rec_cap - rb : 0u, a.reps + pb,
               a.rep_cap > pb ? a.rep_cap - pb : 0u};
-  replay<true>(c.ev, hoff, j0, r, out);
+  step<true>(r, ev, j, hoff, out);
+  // the report's counts: the last workgroup's prefix and its own aggregate
+  if (g == G - 1 && tid == 0) {
+    const Agg tot = agg_compose(p, it.agg);
+    const uint32_t r0 = pick(tot.nrec, init_sc), r1 = pick(tot.nrep, init_sc);
+    a.out->status = (a.phys->status != LVKV_OK || r0 > a.rec_cap || r1 > a.rep_cap)
+                        ? LVKV_LOG_CAPACITY
+                        : LVKV_OK;
+    a.out->nrecords = r0;
+    a.out->nreports = r1;
+    a.out->stopped = (!tot.s.pass && tot.s.c == kStopped) ? tot.s.stop5 : 0u;
+  }
   // the records' bytes: one atomic per wave
   unsigned long long bytes = out.bytes;
   for (int d = 32; d >= 1; d >>= 1) bytes += __shfl_xor(bytes, d, 64);
   if (lane == 0 && bytes) atomicAdd(a.bytes, bytes);
-  // ---- the last workgroup to finish writes the report ----
   __syncthreads();
   if (tid == 0) {
+    asm_stamp(a, 5);
     __builtin_amdgcn_s_waitcnt(0);  // this workgroup's byte atomics have landed
     const uint32_t n = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last_s = n == G - 1 ? 1u : 0u;
   }
   __syncthreads();
   if (!last_s || tid != 0) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  const Agg tot = load_agg(&a.slots[G - 1].incl);  // published before its arrival
-  const uint32_t r0 = pick(tot.nrec, init_sc), r1 = pick(tot.nrep, init_sc);
-  lvkv_log_read_report o;
-  o.status = (a.phys->status != LVKV_OK || r0 > a.rec_cap || r1 > a.rep_cap) ? LVKV_LOG_CAPACITY
-                                                                              : LVKV_OK;
-  o.nrecords = r0;
-  o.nreports = r1;
-  o.stopped = (!tot.s.pass && tot.s.c == kStopped) ? tot.s.stop5 : 0u;
-  o.bytes = __hip_atomic_load(a.bytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  *a.out = o;
+  a.out->bytes = co_ld(a.bytes);
   // the next call with this scratch reuses the counters
-  __hip_atomic_store(a.bytes, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  co_st(a.bytes, 0ull);
+  co_st(a.done, 0u);
 }
 
 // ---- the records' bytes ---------------------------------------------------
@@ -727,19 +707,18 @@ __global__ void __launch_bounds__(kGT) log_asm_onepass(AsmArgs a) {
 // spans j (records are in order and their fragments disjoint, a binary
 // search over their `first`); its payload goes to dest[j] = the payloads of
 // the returned fragments before it (a scan over candidates), so record i
-// starts at dest[first_i]. Two launches: the places (1024 candidates a
-// workgroup, the scan across workgroups by decoupled look-back: each
-// workgroup publishes its aggregate, then its inclusive prefix, under the
-// call's tag, and waits only on lower workgroups, dispatched before it),
-// then the copies, one wave per candidate.
+// starts at dest[first_i]. Three launches: each candidate's owner and
+// length (1024 candidates a workgroup) with the workgroup's sum; the places
+// (each workgroup folds the sums before it, 64 per wave step, and scans its
+// own); the copies, one wave per candidate. (With the scan across
+// workgroups as a decoupled look-back in one launch, the first two took
+// 22-28 us on the 62k-record log: waits on other XCDs' flags.)
 
 constexpr uint32_t kGatherT = 256, kGatherItems = 4, kGatherPer = kGatherT * kGatherItems;
 
-// A workgroup's look-back slot: its aggregate, then its inclusive prefix,
-// each published by a release of `tag` = call tag << 2 | 1 or 2.
+// A workgroup's payload bytes (log_gather_own_kernel).
 struct LookSlot {
-  unsigned long long agg, incl;
-  uint32_t tag, pad_[3];
+  unsigned long long sum, pad_;
 };
 
 struct GatherArgs {
@@ -749,12 +728,12 @@ struct GatherArgs {
   const lvkv_log_record* recs;
   const lvkv_log_read_report* read;
   uint32_t rec_cap;
-  uint32_t tag;           // the call's look-back tag (never 0)
   uint8_t* out;
   uint64_t out_cap;
   uint64_t* rec_pos;      // nullable
   struct LookSlot* look;  // per workgroup
-  ulonglong2* dst;  // per candidate: {its payload's place in `out` (~0: not returned),
+  ulonglong2* dst;  // per candidate: {its owner record (launch 1), then its payload's
+                   //  place in `out` (launch 2); ~0: not returned,
                    //  payload file offset | length << 48}
 };
 
@@ -779,35 +758,71 @@ __device__ __forceinline__ int32_t owner_of(const lvkv_log_record* recs, uint32_
   return static_cast<int32_t>(lo) - 1;
 }
 
+// Launch 1: each candidate's owner record and payload length into dst, and
+// the workgroup's sum of owned lengths. A thread's four candidates are
+// consecutive: one binary search, then forward steps.
+__global__ void __launch_bounds__(kGatherT) log_gather_own_kernel(GatherArgs a) {
+  __shared__ unsigned long long wsum[kGatherT / 64];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63u, wave = tid >> 6;
+  const uint32_t N = a.phys->status == LVKV_OK ? a.phys->count_ : 0u;
+  const uint32_t R = a.phys->status == LVKV_OK ? min(a.read->nrecords, a.rec_cap) : 0u;
+  const uint32_t g = blockIdx.x;
+  if (g * kGatherPer >= N) return;
+  const uint32_t j0 = g * kGatherPer + tid * kGatherItems;
+  uint64_t mine = 0;
+  int32_t i = j0 < N && R != 0 ? owner_of(a.recs, R, j0) : -1;
+#pragma unroll
+  for (uint32_t t = 0; t < kGatherItems; ++t) {
+    const uint32_t j = j0 + t;
+    if (j >= N) break;
+    while (static_cast<uint32_t>(i + 1) < R && a.recs[i + 1].first <= j) ++i;
+    uint32_t len = 0;
+    bool owned = false;
+    if (i >= 0 && j < a.recs[i].first + a.recs[i].nfrags) {
+      len = ld_u16_any(a.file + a.hdr_off[j] + 4);
+      owned = true;
+    }
+    a.dst[j] = make_ulonglong2(owned ? static_cast<unsigned long long>(i) : ~0ull,
+                               (a.hdr_off[j] + 7) | (uint64_t{len} << 48));
+    mine += len;
+  }
+  const uint64_t w = wave_sum64(mine);
+  if (lane == 0) wsum[wave] = w;
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t agg = 0;
+#pragma unroll
+    for (uint32_t v = 0; v < kGatherT / 64; ++v) agg += wsum[v];
+    a.look[g].sum = agg;
+  }
+}
+
+// Launch 2: the places. Wave 0 sums the workgroups before this one while
+// every thread reads its candidates' lengths; a workgroup scan; dst[j].x
+// becomes the payload's place (~0: not returned), and each record's first
+// fragment gives its position.
 __global__ void __launch_bounds__(kGatherT) log_gather_kernel(GatherArgs a) {
   __shared__ unsigned long long wsum[kGatherT / 64];
   __shared__ unsigned long long base_s;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u, wave = tid >> 6;
   const uint32_t N = a.phys->status == LVKV_OK ? a.phys->count_ : 0u;
-  const uint32_t R = a.phys->status == LVKV_OK ? min(a.read->nrecords, a.rec_cap) : 0u;
   const uint32_t g = blockIdx.x;
-  if (g * kGatherPer >= N) return;  // the whole workgroup; nothing waits on it
-  // this thread's candidates: owned payload lengths
+  if (g * kGatherPer >= N) return;
   const uint32_t j0 = g * kGatherPer + tid * kGatherItems;
-  uint32_t len[kGatherItems];
-  int32_t own[kGatherItems];
+  ulonglong2 de[kGatherItems];
   uint64_t mine = 0;
 #pragma unroll
   for (uint32_t t = 0; t < kGatherItems; ++t) {
-    const uint32_t j = j0 + t;
-    len[t] = 0;
-    own[t] = -1;
-    if (j < N && R != 0) {
-      const int32_t i = owner_of(a.recs, R, j);
-      if (i >= 0 && j < a.recs[i].first + a.recs[i].nfrags) {
-        len[t] = ld_u16_any(a.file + a.hdr_off[j] + 4);
-        own[t] = i;
-      }
-    }
-    mine += len[t];
+    de[t] = j0 + t < N ? a.dst[j0 + t] : make_ulonglong2(~0ull, 0);
+    mine += de[t].y >> 48;
   }
-  // workgroup scan
+  if (tid < 64) {
+    uint64_t before = 0;
+    for (uint32_t b = 0; b < g; b += 64) before += wave_sum64(b + lane < g ? a.look[b + lane].sum : 0u);
+    if (lane == 0) base_s = before;
+  }
   uint64_t inc = mine;
 #pragma unroll
   for (uint32_t d = 1; d < 64; d <<= 1) {
@@ -816,52 +831,20 @@ __global__ void __launch_bounds__(kGatherT) log_gather_kernel(GatherArgs a) {
   }
   if (lane == 63) wsum[wave] = inc;
   __syncthreads();
-  uint64_t pre = 0, agg = 0;
+  uint64_t pre = 0;
 #pragma unroll
-  for (uint32_t w = 0; w < kGatherT / 64; ++w) {
+  for (uint32_t w = 0; w < kGatherT / 64; ++w)
     if (w < wave) pre += wsum[w];
-    agg += wsum[w];
-  }
-  // look-back (thread 0): publish the aggregate, sum predecessors, publish
-  // the inclusive prefix
-  if (tid == 0) {
-    LookSlot* me = a.look + g;
-    uint64_t before = 0;
-    if (g != 0) {
-      __hip_atomic_store(&me->agg, static_cast<unsigned long long>(agg), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&me->tag, (a.tag << 2) | 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      for (int32_t p = static_cast<int32_t>(g) - 1; p >= 0; --p) {
-        LookSlot* q = a.look + p;
-        uint32_t tw;
-        while (((tw = __hip_atomic_load(&q->tag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) >> 2) !=
-               a.tag)
-          __builtin_amdgcn_s_sleep(1);
-        // an inclusive prefix ends the walk; an aggregate adds and goes on
-        const bool incl = (tw & 3u) == 2u;
-        before += __hip_atomic_load(incl ? &q->incl : &q->agg, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);
-        if (incl) break;
-      }
-    }
-    __hip_atomic_store(&me->incl, static_cast<unsigned long long>(before + agg), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&me->tag, (a.tag << 2) | 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    base_s = before;
-  }
-  __syncthreads();
   uint64_t dst = base_s + pre + inc - mine;
 #pragma unroll
   for (uint32_t t = 0; t < kGatherItems; ++t) {
     const uint32_t j = j0 + t;
     if (j < N) {
-      if (own[t] >= 0 && a.rec_pos != nullptr && a.recs[own[t]].first == j) a.rec_pos[own[t]] = dst;
-      // the copy's whole descriptor in one 16-byte entry: place, and the
-      // payload's file offset with its length in the top 16 bits
-      a.dst[j] = own[t] >= 0 ? make_ulonglong2(dst, (a.hdr_off[j] + 7) | (uint64_t{len[t]} << 48))
-                             : make_ulonglong2(~0ull, 0);
+      const bool owned = de[t].x != ~0ull;
+      if (owned && a.rec_pos != nullptr && a.recs[de[t].x].first == j) a.rec_pos[de[t].x] = dst;
+      a.dst[j].x = owned ? dst : ~0ull;
     }
-    dst += len[t];
+    dst += de[t].y >> 48;
   }
 }
 
@@ -915,15 +898,19 @@ __global__ void __launch_bounds__(256) log_gather_copy_kernel(GatherArgs a) {
 
 }  // namespace
 
+#ifdef LVKV_PROBE_BUILD
+uint64_t* g_asm_stamps = nullptr;  // lvkv_debug_asm_stamps
+#endif
+
 size_t log_asm_scratch_bytes(size_t max_items) {
-  const size_t groups = (max_items + kGT * kChunk - 1) / (kGT * kChunk);
-  return groups * sizeof(AsmSlot) + 16;  // + log_asm_seek's two words
+  const size_t groups = (max_items + kGT - 1) / kGT;
+  return groups * sizeof(Agg) + 16;  // + log_asm_seek's two words
 }
 
 // `scratch`: log_asm_scratch_bytes(capacity + nblocks) bytes, 16-byte aligned
-// (any contents: slots of other tags are ignored); `done` and `bytes`: a u32
-// and a u64 that are 0 (zeroed once; every call leaves them at 0), used by
-// one call at a time; `tag`: this call's, never 0, below 2^30.
+// (any contents); `done` and `bytes`: a u32 and a u64 that are 0 (zeroed
+// once; every call leaves them at 0), used by one call at a time; `tag` is
+// unused (the launches exchange through a kernel boundary).
 hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
                                const lvkv_log_report* phys, uint64_t size, uint32_t capacity,
                                uint64_t initial_offset, lvkv_log_record* recs, uint32_t rec_cap,
@@ -938,13 +925,18 @@ hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
   a.rec_cap = rec_cap;
   a.rep_cap = rep_cap;
   const uint64_t items = uint64_t{capacity} + a.nblocks;
-  a.groups = static_cast<uint32_t>((items + kGT * kChunk - 1) / (kGT * kChunk));
+  a.groups = static_cast<uint32_t>((items + kGT - 1) / kGT);
   a.recs = recs;
   a.reps = reps;
   a.out = out;
-  a.slots = static_cast<AsmSlot*>(scratch);
-  a.lohi = reinterpret_cast<uint32_t*>(a.slots + a.groups);
-  a.tag = tag;
+  a.aggs = static_cast<Agg*>(scratch);
+#ifdef LVKV_PROBE_BUILD
+  a.stamps = g_asm_stamps;
+#else
+  a.stamps = nullptr;
+#endif
+  a.lohi = reinterpret_cast<uint32_t*>(a.aggs + a.groups);
+  (void)tag;
   a.done = done;
   a.bytes = bytes;
   a.init_st = initial_offset ? kResync : kIdle;
@@ -960,13 +952,15 @@ hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
     hipLaunchKernelGGL(log_asm_seek, dim3(1), dim3(64), 0, stream, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(log_asm_onepass, dim3(a.groups), dim3(kGT), 0, stream, a);
+  hipLaunchKernelGGL(log_asm_reduce, dim3(a.groups), dim3(kGT), 0, stream, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(log_asm_emit, dim3(a.groups), dim3(kGT), 0, stream, a);
   return hipGetLastError();
 }
 
-// lvkv_log_gather_device: two launches; `look`: 32 bytes per workgroup of
-// ceil(capacity / 1024) (any contents: slots of other tags are ignored), then
-// 16 bytes per candidate.
+// lvkv_log_gather_device: three launches; `look`: 16 bytes per workgroup of
+// ceil(capacity / 1024), then 16 bytes per candidate (any contents); `tag`
+// is unused (the launches exchange through kernel boundaries).
 size_t log_gather_scratch_bytes(size_t capacity) {
   return ((capacity + kGatherPer - 1) / kGatherPer) * sizeof(LookSlot) + capacity * 16;
 }
@@ -983,16 +977,18 @@ hipError_t launch_log_gather(const uint8_t* file, const uint64_t* hdr_off, size_
   a.recs = recs;
   a.read = read;
   a.rec_cap = rec_cap;
-  a.tag = tag;
+  (void)tag;
   a.out = out;
   a.out_cap = out_cap;
   a.rec_pos = rec_pos;
   a.look = static_cast<LookSlot*>(look);
   const uint32_t groups = static_cast<uint32_t>((capacity + kGatherPer - 1) / kGatherPer);
   a.dst = reinterpret_cast<ulonglong2*>(a.look + groups);
-  hipLaunchKernelGGL(log_gather_kernel, dim3(groups), dim3(kGatherT), 0, stream, a);
+  hipLaunchKernelGGL(log_gather_own_kernel, dim3(groups), dim3(kGatherT), 0, stream, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(log_gather_kernel, dim3(groups), dim3(kGatherT), 0, stream, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(log_gather_copy_kernel, dim3(static_cast<uint32_t>((capacity + 3) / 4)),
                      dim3(256), 0, stream, a);
   return hipGetLastError();
