@@ -306,97 +306,6 @@ __device__ __forceinline__ void event_counts(uint32_t ev, uint32_t (&cnt)[kScena
   }
 }
 
-__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, uint32_t d) {
-  const uint32_t lo = __shfl_up(static_cast<uint32_t>(v), d, 64);
-  const uint32_t hi = __shfl_up(static_cast<uint32_t>(v >> 32), d, 64);
-  return (static_cast<uint64_t>(hi) << 32) | lo;
-}
-
-// A summary in five dwords for the shuffles: pass, c and stop5 packed; len
-// and scratch share one word (a summary uses len only when pass, scratch
-// only when not).
-__device__ __forceinline__ uint32_t summ_flags(const Summ& x) {
-  return x.pass | (x.c << 1) | (x.stop5 << 4);
-}
-__device__ __forceinline__ Summ summ_unpack(uint32_t f, uint32_t first, uint32_t nrec, uint64_t b) {
-  Summ r;
-  r.pass = f & 1u;
-  r.c = (f >> 1) & 7u;
-  r.stop5 = f >> 4;
-  r.len = r.pass ? b : 0u;
-  r.scratch = r.pass ? 0u : b;
-  r.first = first;
-  r.nrec = nrec;
-  return r;
-}
-
-__device__ __forceinline__ Summ shfl_up_summ(const Summ& x, uint32_t d) {
-  return summ_unpack(__shfl_up(summ_flags(x), d, 64), __shfl_up(x.first, d, 64),
-                     __shfl_up(x.nrec, d, 64), shfl_up64(x.pass ? x.len : x.scratch, d));
-}
-
-// Workgroup-wide exclusive scan of `s` under compose (kT threads): a shuffle
-// scan in each wave, then the waves' aggregates through LDS (two barriers);
-// *all = the aggregate.
-template <uint32_t kT>
-__device__ __forceinline__ Summ wg_scan_excl(Summ s, Summ (&wagg)[kT / 64], uint32_t tid,
-                                             Summ* all) {
-  const uint32_t lane = tid & 63u, w = tid >> 6;
-  Summ inc = s;
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const Summ o = shfl_up_summ(inc, d);
-    if (lane >= d) inc = compose(o, inc);
-  }
-  Summ ex = shfl_up_summ(inc, 1);
-  if (lane == 0) ex = kIdentity;
-  if (lane == 63) wagg[w] = inc;
-  __syncthreads();
-  Summ pre = kIdentity, tot = kIdentity;
-  for (uint32_t v = 0; v < kT / 64; ++v) {
-    if (v == w) pre = tot;
-    tot = compose(tot, wagg[v]);
-  }
-  *all = tot;
-  __syncthreads();  // wagg is reused
-  return compose(pre, ex);
-}
-
-// Workgroup-wide exclusive sums of N counters per thread (kT threads), the
-// same way; tot[i] = the totals.
-template <uint32_t kT, uint32_t N>
-__device__ __forceinline__ void wg_sum_excl(uint32_t (&v)[N], uint32_t (&wsum)[kT / 64][N],
-                                            uint32_t tid, uint32_t (&tot)[N]) {
-  const uint32_t lane = tid & 63u, w = tid >> 6;
-  uint32_t inc[N];
-#pragma unroll
-  for (uint32_t i = 0; i < N; ++i) inc[i] = v[i];
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-#pragma unroll
-    for (uint32_t i = 0; i < N; ++i) {
-      const uint32_t o = __shfl_up(inc[i], d, 64);
-      if (lane >= d) inc[i] += o;
-    }
-  }
-  if (lane == 63) {
-#pragma unroll
-    for (uint32_t i = 0; i < N; ++i) wsum[w][i] = inc[i];
-  }
-  __syncthreads();
-#pragma unroll
-  for (uint32_t i = 0; i < N; ++i) {
-    uint32_t pre = 0, all = 0;
-    for (uint32_t u = 0; u < kT / 64; ++u) {
-      if (u < w) pre += wsum[u][i];
-      all += wsum[u][i];
-    }
-    v[i] = pre + inc[i] - v[i];
-    tot[i] = all;
-  }
-  __syncthreads();  // wsum is reused
-}
-
 // A run of events (a chunk, a workgroup, a run of workgroups) as a map of
 // the reader's state: its composed summary and its record / report counts
 // for each state the reader may enter it in. Runs of them compose
@@ -417,7 +326,7 @@ struct AsmArgs {
   Seek seek;
   uint32_t* lohi;   // log_asm_seek's output (seek.lohi)
   uint32_t* done;   // workgroups finished (left at 0 by the last one)
-  unsigned long long* bytes;  // the records' bytes, summed (left at 0 by the last one)
+  unsigned long long* wg_bytes;  // per workgroup: its records' bytes
   lvkv_log_record* recs;
   lvkv_log_corruption* reps;
   lvkv_log_read_report* out;
@@ -574,22 +483,97 @@ struct Items {
   Agg agg;
 };
 
+// The composition of the lanes in `below` (a prefix of the wave) as one
+// summary, from ballots: the state its last reset lane leaves (plus the
+// MIDDLE bytes after it), or stopped from its first stop lane. C / R / S:
+// the candidate / reset / stop lanes; P: MIDDLE bytes of the lanes in
+// `below`; r: the last reset lane in `below` and its state (c_r, sc_r) and
+// inclusive MIDDLE bytes p_r; stop5_0: the first stop lane's stop5.
+__device__ __forceinline__ Summ prefix_summ(uint64_t below, uint64_t C, uint64_t R, uint64_t S,
+                                            uint32_t P, uint32_t r, uint32_t c_r, uint32_t sc_r,
+                                            uint32_t p_r, uint32_t stop5_0) {
+  Summ x = kIdentity;
+  x.nrec = static_cast<uint32_t>(__popcll(C & below));
+  if (S & below) {
+    x.pass = 0;
+    x.c = kStopped;
+    x.stop5 = stop5_0;
+  } else if (R & below) {
+    x.pass = 0;
+    x.c = c_r;
+    x.scratch = sc_r + (c_r == kInFrag ? P - p_r : 0u);
+    x.first = static_cast<uint32_t>(__popcll(C & ((uint64_t{1} << r) - 1u)));
+  } else {
+    x.len = P;
+  }
+  return x;
+}
+
 __device__ __forceinline__ void wg_items(const AsmArgs& a, uint32_t K, uint32_t g, uint32_t tid,
                                          Summ (&wagg)[kGT / 64],
                                          uint32_t (&wsum)[kGT / 64][kScenarios], Items& it) {
+  const uint32_t lane = tid & 63u, w = tid >> 6;
   const uint32_t k = g * kGT + tid;
   it.ev = k < K ? seek_event(a.seek, a.hdr_off, k, a.events[k]) : log_event(kEvNone, 0, 0);
+  const Summ e = event_summ(it.ev);
+  // the wave's exclusive scan of summaries, from ballots
+  const uint64_t below = (uint64_t{1} << lane) - 1u;
+  const uint64_t C = __ballot(e.nrec != 0);
+  const uint64_t R = __ballot(!e.pass);
+  const uint64_t S = __ballot(!e.pass && e.c == kStopped);
+  const uint32_t len = e.pass ? static_cast<uint32_t>(e.len) : 0u;  // < 2^16 an item
+  uint32_t inc = len;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += o;
+  }
+  const uint64_t rb = R & below;
+  const uint32_t r = rb ? 63u - static_cast<uint32_t>(__builtin_clzll(rb)) : 0u;
+  const uint32_t sc = static_cast<uint32_t>(e.scratch);
+  const uint32_t stop5_0 = __shfl(e.stop5, S ? static_cast<uint32_t>(__builtin_ctzll(S)) : 0u, 64);
+  const Summ xw = prefix_summ(below, C, R, S, inc - len, r, __shfl(e.c, r, 64), __shfl(sc, r, 64),
+                              __shfl(inc, r, 64), stop5_0);
+  // the wave's total (shuffles on every lane, then lane 0 writes it)
+  const uint32_t rt = R ? 63u - static_cast<uint32_t>(__builtin_clzll(R)) : 0u;
+  const uint32_t p_all = __shfl(inc, 63, 64), c_rt = __shfl(e.c, rt, 64);
+  const uint32_t sc_rt = __shfl(sc, rt, 64), p_rt = __shfl(inc, rt, 64);
+  if (lane == 0) wagg[w] = prefix_summ(~uint64_t{0}, C, R, S, p_all, rt, c_rt, sc_rt, p_rt, stop5_0);
+  __syncthreads();
+  Summ pre = kIdentity, tot = kIdentity;
+#pragma unroll
+  for (uint32_t v = 0; v < kGT / 64; ++v) {
+    if (v == w) pre = tot;
+    tot = compose(tot, wagg[v]);
+  }
+  it.agg.s = tot;
+  it.x = compose(pre, xw);
+  // output positions for each entering scenario: per item at most one
+  // record and two reports, so the wave's prefix counts are ballots
   uint32_t cnt[kScenarios];
   event_counts(it.ev, cnt);
-  it.x = wg_scan_excl<kGT>(event_summ(it.ev), wagg, tid, &it.agg.s);
-  uint32_t tot[kScenarios];
-#pragma unroll
-  for (uint32_t sw = 0; sw < kScenarios; ++sw) it.v[sw] = pick(cnt, chunk_scenario(sw, it.x));
-  wg_sum_excl<kGT>(it.v, wsum, tid, tot);
 #pragma unroll
   for (uint32_t sw = 0; sw < kScenarios; ++sw) {
-    it.agg.nrec[sw] = tot[sw] & 0xffffu;
-    it.agg.nrep[sw] = tot[sw] >> 16;
+    const uint32_t c = pick(cnt, chunk_scenario(sw, it.x));
+    const uint64_t br = __ballot(c & 1u), b0 = __ballot((c >> 16) & 1u), b1 = __ballot((c >> 17) & 1u);
+    it.v[sw] = static_cast<uint32_t>(__popcll(br & below)) |
+               static_cast<uint32_t>(__popcll(b0 & below) + 2 * __popcll(b1 & below)) << 16;
+    if (lane == 0)
+      wsum[w][sw] = static_cast<uint32_t>(__popcll(br)) |
+                    static_cast<uint32_t>(__popcll(b0) + 2 * __popcll(b1)) << 16;
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t sw = 0; sw < kScenarios; ++sw) {
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (uint32_t v = 0; v < kGT / 64; ++v) {
+      before += v < w ? wsum[v][sw] : 0u;
+      all += wsum[v][sw];
+    }
+    it.v[sw] += before;
+    it.agg.nrec[sw] = all & 0xffffu;
+    it.agg.nrep[sw] = all >> 16;
   }
 }
 
@@ -609,16 +593,18 @@ __global__ void __launch_bounds__(kGT) log_asm_reduce(AsmArgs a) {
   if (threadIdx.x == 0) a.aggs[blockIdx.x] = it.agg;
 }
 
-// ReadRecord, launch 2 of 2: wave 0 folds the aggregates of the workgroups
-// before this one (64 at a time, window_fold) into its entering state and
-// output positions, while the items are rescanned; then each item goes
+// ReadRecord, launch 2 of 2: the waves fold the aggregates of the
+// workgroups before this one (64 at a time, window_fold; each wave a
+// contiguous share) into its entering state and output positions, and the
+// items are rescanned; then each item goes
 // through step() once. Workgroup G - 1 writes the report's counts; the last
 // workgroup to finish (a completion counter it leaves at 0) writes the
 // records' bytes.
 __global__ void __launch_bounds__(kGT) log_asm_emit(AsmArgs a) {
   __shared__ Summ wagg[kGT / 64];
   __shared__ uint32_t wsum[kGT / 64][kScenarios];
-  __shared__ Agg start_s;
+  __shared__ Agg part_s[kGT / 64];
+  __shared__ unsigned long long wbytes_s[kGT / 64];
   __shared__ uint32_t last_s;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
@@ -627,23 +613,26 @@ __global__ void __launch_bounds__(kGT) log_asm_emit(AsmArgs a) {
   const uint32_t g = blockIdx.x;
   if (g >= G) return;  // the whole workgroup
   if (tid == 0) asm_stamp(a, 0);
-  if (tid < 64) {
-    Agg before = kAggIdentity;  // every workgroup before g, composed
-    for (uint32_t base = 0; base < g; base += 64) {
-      const Agg v = base + lane < g ? a.aggs[base + lane] : kAggIdentity;
-      before = agg_compose(before, window_fold(v, lane));
+  {
+    // the workgroups before g, 64 a window; wave w folds its contiguous
+    // share of the windows, the shares are composed below
+    const uint32_t w = tid >> 6, nwin = (g + 63) / 64;
+    Agg part = kAggIdentity;
+    for (uint32_t wi = w * nwin / (kGT / 64); wi < (w + 1) * nwin / (kGT / 64); ++wi) {
+      const uint32_t idx = wi * 64 + lane;
+      part = agg_compose(part, window_fold(idx < g ? a.aggs[idx] : kAggIdentity, lane));
     }
-    if (lane == 0) {
-      start_s = before;
-      asm_stamp(a, 1);
-    }
+    if (lane == 0) part_s[w] = part;
+    if (tid == 0) asm_stamp(a, 1);
   }
   Items it;
-  wg_items(a, K, g, tid, wagg, wsum, it);  // its barriers also publish start_s
+  wg_items(a, K, g, tid, wagg, wsum, it);  // its barriers also publish part_s
   if (tid == 0) asm_stamp(a, 3);
+  Agg p = part_s[0];
+#pragma unroll
+  for (uint32_t w = 1; w < kGT / 64; ++w) p = agg_compose(p, part_s[w]);
   const Summ& x = it.x;
   const uint32_t ev = it.ev;
-  const Agg p = start_s;
   const uint32_t in_st = p.s.pass ? a.init_st : p.s.c;
   const uint64_t in_scratch = p.s.pass ? 0 : p.s.scratch;
   const uint32_t init_sc = scenario(a.init_st, 0);
@@ -679,23 +668,31 @@ __global__ void __launch_bounds__(kGT) log_asm_emit(AsmArgs a) {
     a.out->nreports = r1;
     a.out->stopped = (!tot.s.pass && tot.s.c == kStopped) ? tot.s.stop5 : 0u;
   }
-  // the records' bytes: one atomic per wave
-  unsigned long long bytes = out.bytes;
-  for (int d = 32; d >= 1; d >>= 1) bytes += __shfl_xor(bytes, d, 64);
-  if (lane == 0 && bytes) atomicAdd(a.bytes, bytes);
+  // the records' bytes: the workgroup's sum into its slot (a device-scope
+  // exchange: no contended atomic); the last workgroup to finish sums the
+  // slots (one atomic per workgroup on the completion counter)
+  const uint64_t wb = wave_sum64(out.bytes);
+  if (lane == 0) wbytes_s[tid >> 6] = wb;
   __syncthreads();
   if (tid == 0) {
+    uint64_t t = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kGT / 64; ++w) t += wbytes_s[w];
+    co_st(&a.wg_bytes[g], static_cast<unsigned long long>(t));
     asm_stamp(a, 5);
-    __builtin_amdgcn_s_waitcnt(0);  // this workgroup's byte atomics have landed
+    vm_drain();  // the slot's exchange has landed
     const uint32_t n = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last_s = n == G - 1 ? 1u : 0u;
   }
   __syncthreads();
-  if (!last_s || tid != 0) return;
-  a.out->bytes = co_ld(a.bytes);
-  // the next call with this scratch reuses the counters
-  co_st(a.bytes, 0ull);
-  co_st(a.done, 0u);
+  if (!last_s || tid >= 64) return;
+  uint64_t t = 0;
+  for (uint32_t i = lane; i < G; i += 64) t += co_ld(&a.wg_bytes[i]);
+  t = wave_sum64(t);
+  if (lane == 0) {
+    a.out->bytes = t;
+    co_st(a.done, 0u);  // the next call with this scratch reuses the counter
+  }
 }
 
 // ---- the records' bytes ---------------------------------------------------
@@ -904,7 +901,7 @@ uint64_t* g_asm_stamps = nullptr;  // lvkv_debug_asm_stamps
 
 size_t log_asm_scratch_bytes(size_t max_items) {
   const size_t groups = (max_items + kGT - 1) / kGT;
-  return groups * sizeof(Agg) + 16;  // + log_asm_seek's two words
+  return groups * (sizeof(Agg) + 8) + 16;  // + the byte slots, log_asm_seek's two words
 }
 
 // `scratch`: log_asm_scratch_bytes(capacity + nblocks) bytes, 16-byte aligned
@@ -936,9 +933,10 @@ hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
   a.stamps = nullptr;
 #endif
   a.lohi = reinterpret_cast<uint32_t*>(a.aggs + a.groups);
+  a.wg_bytes = reinterpret_cast<unsigned long long*>(a.lohi + 4);
   (void)tag;
   a.done = done;
-  a.bytes = bytes;
+  (void)bytes;
   a.init_st = initial_offset ? kResync : kIdle;
   a.seek.offset = initial_offset;
   // SkipToInitialBlock (log_reader.cc:33-54): the block holding the offset,
