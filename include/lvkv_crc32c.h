@@ -222,7 +222,8 @@ typedef struct lvkv_sst_report {
  * ReadBlock on every block (table/format.cc:69-160) would with
  * verify_checksums: footer and magic, index and metaindex checksums and type
  * bytes, then every data block the index lists and the filter block, all on
- * the device in two launches (a per-table workgroup for the footer, index and
+ * the device in two launches (three when a single table's index is wide, its
+ * CRC and entries then spread over 64 workgroups) (a per-table workgroup for the footer, index and
  * metaindex CRCs, the filter lookup and the index parse, one entry per
  * restart point as table_builder.cc:35 writes it; then one batched verify
  * with the merge). filter_policy = FilterPolicy::Name() of the reader's
@@ -370,7 +371,7 @@ int lvkv_log_read_device(const void* d_file, uint64_t file_size, uint64_t* d_hdr
  * stream after it). payload_capacity >= d_read->bytes is needed for every
  * record to be written (file_size always suffices); a fragment that does
  * not fit is skipped. d_record_pos (record_capacity u64, nullable) gets
- * every returned record's offset in d_payload. Two launches, asynchronous. */
+ * every returned record's offset in d_payload. Three launches, asynchronous. */
 int lvkv_log_gather_device(const void* d_file, const uint64_t* d_hdr_offsets, size_t capacity,
                            const lvkv_log_report* d_report, const lvkv_log_record* d_records,
                            size_t record_capacity, const lvkv_log_read_report* d_read,
