@@ -10,7 +10,7 @@ Configs (BASELINE.json "configs"; the default line is the headline):
                   ranks (shard.shard_range), aggregate GiB/s.
   blocks1m        config 4: 1M x 4 KiB blocks per GPU per step.
   wal32k          config 3: 16,384 x 32 KiB WAL blocks, CRC over [6, 32768)
-                  (HIP launch path: the engine's kernel holds blocks <= 4 KiB).
+                  (the engine's general walk, lvkv_ek_ragged).
 
 One step = one batch submitted to the AQL engine (lvkv_engine_crc32c_uniform,
 include/lvkv_crc32c.h) over blocks already resident in HBM. Consecutive steps
@@ -187,6 +187,7 @@ class EngineRunner:
         self.nb, self.L, self.stride = nb, L, stride
         self.bases = [buf.data_ptr() + w * window + crc_off for w in range(nrot)]
         self.outs = [o.data_ptr() for o in outs]
+        self.outs_t = outs
         self.nrot = nrot
         self.flags = 0
 
@@ -247,16 +248,24 @@ def make_buffers(torch, dev, rank, nb, stride, rotate_bytes, extra=64):
     return buf, nrot, window
 
 
-def parity_check(buf, outs0, nb, L, stride, crc_off, rank, what):
-    """Spot check outside the timed region against the oracle (checker)."""
+def parity_check(buf, outs0, nb, L, stride, crc_off, rank, what, chunk=1 << 18):
+    """Every block of the batch (a rank's whole slice) against the oracle
+    (checker), once, outside the timed region; in chunks of `chunk` blocks so
+    the host copy stays bounded."""
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle
-    check_n = min(nb, 2000)
-    host = buf[crc_off: crc_off + (check_n - 1) * stride + L].cpu().numpy()
-    want = oracle.uniform(host, check_n, L, stride, threads=8)
-    got = outs0[:check_n].cpu().numpy().view(np.uint32)
-    if not np.array_equal(got, want):
-        raise SystemExit(f"bench: parity check FAILED on rank {rank} ({what})")
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    got_all = outs0[:nb].cpu().numpy().view(np.uint32)
+    for b0 in range(0, nb, chunk):
+        n = min(chunk, nb - b0)
+        lo = crc_off + b0 * stride
+        host = buf[lo: lo + (n - 1) * stride + L].cpu().numpy()
+        want = oracle.uniform(host, n, L, stride, threads=threads)
+        if not np.array_equal(got_all[b0:b0 + n], want):
+            bad = int(np.flatnonzero(got_all[b0:b0 + n] != want)[0]) + b0
+            raise SystemExit(f"bench: parity check FAILED on rank {rank} ({what}): "
+                             f"block {bad} of {nb}")
+    return nb
 
 
 def profile_launches(runner, eng, n, ordered, first):
@@ -440,7 +449,10 @@ def main():
         return
 
     nb, L, stride, crc_off, desc = CONFIGS[args.config]
-    use_engine = L <= 4096 and stride % 4 == 0
+    # every config runs on the AQL engine: the burst kernel for the 4 KiB
+    # blocks, the general walk (lvkv_ek_ragged) for config 3's 32 KiB blocks
+    use_engine = True
+    burst = L <= 16 * 256 and stride % 4 == 0 and (crc_off + L) % 4 == 0
     buf, nrot, window = make_buffers(torch, dev, rank, nb, stride, args.rotate_bytes)
     outs = [torch.empty(nb, dtype=torch.int32, device=dev) for _ in range(4)]
     eng = lvkv.Engine(local) if use_engine else None
@@ -487,12 +499,15 @@ def main():
         roof.update({
             "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None,
-            "kernel": "lvkv_ek_uniform_pair (ordered launch, 2 workgroups x 8 waves per CU)",
+            "kernel": ("lvkv_ek_uniform_pair (ordered launch, 2 workgroups x 8 waves per CU)"
+                       if burst else
+                       "lvkv_ek_ragged (ordered launch, 2 workgroups x 8 waves x 2 chains per CU)"),
             "kernel_us_avg": round(kern_us, 3), "kernel_us_median": round(statistics.median(d), 3),
             "kernel_us_min": round(min(d), 3), "launches": len(d), "dispatches_per_launch": per,
             "timing": "HSA packet-processor start/end per dispatch (engine profiling)",
-            "pipelined": {"kernel": f"lvkv_ek_uniform ({w} waves x {c} chains, {gr} workgroups, "
-                                    f"{eng.queues()} queues)",
+            "pipelined": {"kernel": (f"lvkv_ek_uniform ({w} waves x {c} chains, {gr} workgroups, "
+                                     f"{eng.queues()} queues)" if burst else
+                                     f"lvkv_ek_ragged ({eng.queues()} queues)"),
                           "launches": args.steps, "dispatches": len(pipe),
                           "period_us": round(span, 3),
                           "achieved": round(algo_bytes / (span * 1e-6) / 1e9, 1),
@@ -524,7 +539,8 @@ def main():
         line = _line_base(args, world, value, ms_per_step / 1e3, {
             "workload": desc, "nblocks_per_gpu": nb, "block_bytes": L, "stride": stride,
             "rotation_buffers": nrot, "rotation_bytes": nrot * window,
-            "path": "AQL engine, batches overlapped" if use_engine else "HIP launch, 2 streams",
+            "path": ("AQL engine, batches overlapped" + ("" if burst else ", general walk"))
+                    if use_engine else "HIP launch, 2 streams",
             "parallelism": f"{world} independent block batches (no collective)"})
         line["pct_hbm_peak"] = round(100.0 * value * GIB / 1e9 / HBM_PEAK_GBS / world, 2)
         line["roofline"] = roof

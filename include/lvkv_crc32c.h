@@ -36,8 +36,11 @@ extern "C" {
 #define LVKV_FLAG_MASK 1u
 /* Engine submits only: the batch runs alone — it starts after every earlier
  * dispatch of the engine has completed (host drain of the other queues + AQL
- * barrier bit) and uses the kernel shaped for the whole chip. Without it,
- * consecutive batches overlap, each on half of every CU. */
+ * barrier bit), a batch of several dispatches puts all of them on one queue
+ * with the barrier bit (they run one after another, never side by side), and
+ * it uses the kernel shaped for the whole chip. Later submits are not held
+ * back by it. Without the flag, consecutive batches (and the dispatches of
+ * one large batch) overlap, each on half of every CU. */
 #define LVKV_FLAG_ORDERED 2u
 /* Engine submits only: the batch's first dispatch acquires at system scope
  * (invalidates the L2) instead of agent scope. Needed when the input was
@@ -101,14 +104,46 @@ typedef struct lvkv_engine lvkv_engine;
 int lvkv_engine_create(int device, lvkv_engine** out);
 /* Waits for outstanding work, then frees the queue. NULL is a no-op. */
 void lvkv_engine_destroy(lvkv_engine* engine);
-/* lvkv_crc32c_uniform_device's contract, asynchronous on the engine, for
- * blocks of 4..4348 bytes (16 rows of 256 B) whose ends are 4-byte aligned
- * ((d_base + length) % 4 == 0, stride % 4 == 0); any nblocks (batches
- * beyond one dispatch's capacity become several dispatches). Other shapes:
- * LVKV_ERR_INVALID (use lvkv_crc32c_uniform_device). */
+/* lvkv_crc32c_uniform_device's contract, asynchronous on the engine, for any
+ * length, stride and alignment and any nblocks (batches beyond one
+ * dispatch's capacity become several dispatches). Blocks of 4..4348 bytes
+ * (16 rows of 256 B) whose ends are 4-byte aligned ((d_base + length) % 4 ==
+ * 0, stride % 4 == 0) — the headline's 4 KiB blocks — run the burst kernel;
+ * other shapes (32 KiB WAL blocks at +6, odd lengths) the general walk of
+ * lvkv_engine_crc32c_batch in its uniform layout. */
 int lvkv_engine_crc32c_uniform(lvkv_engine* engine, const void* d_base, uint64_t stride,
                                uint32_t length, uint32_t init, uint32_t* d_out,
                                size_t nblocks, uint32_t flags);
+/* The engine form of lvkv_crc32c_batch_device (util/crc32c.cc:276 over block i
+ * = d_base[d_offsets[i], + d_lengths[i]), init d_init ? d_init[i] : init;
+ * TableBuilder::WriteRawBlock's table_builder.cc:199-203 and
+ * log::Writer::EmitPhysicalRecord's log_writer.cc:94-95 as a batch): any
+ * offsets, lengths and alignment; blocks over 64 KiB are walked by a whole
+ * workgroup inside the same dispatch. Asynchronous; results after
+ * lvkv_engine_wait. */
+int lvkv_engine_crc32c_batch(lvkv_engine* engine, const void* d_base, const uint64_t* d_offsets,
+                             const uint32_t* d_lengths, const uint32_t* d_init, uint32_t init,
+                             uint32_t* d_out, size_t nblocks, uint32_t flags);
+/* The engine forms of lvkv_sst_verify_device (ReadBlock's checksum test,
+ * table/format.cc:92-99), lvkv_log_verify_device (ReadPhysicalRecord's,
+ * db/log_reader.cc:243-247), lvkv_sst_fill_trailers_device
+ * (table/table_builder.cc:192-209) and lvkv_log_fill_headers_device
+ * (db/log_writer.cc:82-108): same arguments and outputs, dispatched into the
+ * engine's queues (flags: LVKV_FLAG_ORDERED / LVKV_FLAG_SYSTEM_ACQUIRE as for
+ * the other submits). The compaction and recovery loops as a checksum
+ * service. */
+int lvkv_engine_sst_verify(lvkv_engine* engine, const void* d_file, const uint64_t* d_offsets,
+                           const uint32_t* d_sizes, uint32_t* d_actual, uint8_t* d_status,
+                           size_t nblocks, uint32_t flags);
+int lvkv_engine_log_verify(lvkv_engine* engine, const void* d_file,
+                           const uint64_t* d_hdr_offsets, uint32_t* d_actual,
+                           uint8_t* d_status, size_t nrecords, uint32_t flags);
+int lvkv_engine_sst_fill_trailers(lvkv_engine* engine, void* d_file, const uint64_t* d_offsets,
+                                  const uint32_t* d_sizes, uint32_t* d_crc, size_t nblocks,
+                                  uint32_t flags);
+int lvkv_engine_log_fill_headers(lvkv_engine* engine, void* d_file,
+                                 const uint64_t* d_hdr_offsets, uint32_t* d_crc,
+                                 size_t nrecords, uint32_t flags);
 /* Blocks until every dispatch submitted so far has completed and its results
  * are visible to the host and other devices (a barrier packet on every queue,
  * system-scope release, host spin-wait). */

@@ -105,6 +105,16 @@ def _load() -> ctypes.CDLL:
     L.lvkv_engine_destroy.restype = None
     L.lvkv_engine_crc32c_uniform.argtypes = [vp, vp, u64, u32, u32, vp, sz, u32]
     L.lvkv_engine_crc32c_uniform.restype = i32
+    L.lvkv_engine_crc32c_batch.argtypes = [vp, vp, vp, vp, vp, u32, vp, sz, u32]
+    L.lvkv_engine_crc32c_batch.restype = i32
+    L.lvkv_engine_sst_verify.argtypes = [vp, vp, vp, vp, vp, vp, sz, u32]
+    L.lvkv_engine_sst_verify.restype = i32
+    L.lvkv_engine_log_verify.argtypes = [vp, vp, vp, vp, vp, sz, u32]
+    L.lvkv_engine_log_verify.restype = i32
+    L.lvkv_engine_sst_fill_trailers.argtypes = [vp, vp, vp, vp, vp, sz, u32]
+    L.lvkv_engine_sst_fill_trailers.restype = i32
+    L.lvkv_engine_log_fill_headers.argtypes = [vp, vp, vp, vp, sz, u32]
+    L.lvkv_engine_log_fill_headers.restype = i32
     L.lvkv_engine_wait.argtypes = [vp]
     L.lvkv_engine_wait.restype = i32
     L.lvkv_engine_queues.argtypes = [vp, i32]
@@ -619,8 +629,8 @@ class Engine:
     fences every queue. Inputs must be complete before a submit (synchronize
     the stream that produced them); results are valid after ``wait()``.
 
-    Same results as ``crc32c_uniform`` for blocks of 4..4348 bytes whose
-    ends are 4-byte aligned."""
+    Same results as ``crc32c_uniform`` / ``crc32c_batch`` / ``sst_verify``
+    / ``log_verify`` / the fill calls, for any block layout."""
 
     def __init__(self, device=None):
         torch = _torch()
@@ -657,6 +667,89 @@ class Engine:
         _check("lvkv_engine_crc32c_uniform", rc)
         self._inflight.append((buf, out))
         return out
+
+    def _flags(self, mask=False, ordered=False, fresh=True):
+        return ((LVKV_FLAG_MASK if mask else 0) | (LVKV_FLAG_ORDERED if ordered else 0) |
+                (LVKV_FLAG_SYSTEM_ACQUIRE if fresh else 0))
+
+    def crc32c_batch(self, buf, offsets, lengths, *, init: int = 0, inits=None,
+                     mask: bool = False, ordered: bool = False, fresh: bool = True, out=None):
+        """lvkv_engine_crc32c_batch: crc32c_batch's contract on the engine."""
+        torch = _torch()
+        n = offsets.numel()
+        if lengths.numel() != n:
+            raise ValueError("offsets and lengths differ in length")
+        out = _u32_out(torch, n, buf.device, out)
+        torch.cuda.current_stream(buf.device).synchronize()
+        rc = _lib.lvkv_engine_crc32c_batch(
+            self.handle, _dev_ptr(buf, "buf", (torch.uint8, torch.int8)),
+            _dev_ptr(offsets, "offsets", (torch.int64,)),
+            _dev_ptr(lengths, "lengths", (torch.int32,)),
+            _dev_ptr(inits, "inits", (torch.int32,), n) if inits is not None else None,
+            init & 0xFFFFFFFF, _dev_ptr(out, "out", (torch.int32,), n), n,
+            self._flags(mask, ordered, fresh))
+        _check("lvkv_engine_crc32c_batch", rc)
+        self._inflight.append((buf, offsets, lengths, inits, out))
+        return out
+
+    def sst_verify(self, file_buf, offsets, sizes, *, ordered=False, fresh=True):
+        """lvkv_engine_sst_verify: (actual int32, status uint8) as sst_verify."""
+        torch = _torch()
+        n = offsets.numel()
+        actual = torch.empty(n, dtype=torch.int32, device=file_buf.device)
+        status = torch.empty(n, dtype=torch.uint8, device=file_buf.device)
+        torch.cuda.current_stream(file_buf.device).synchronize()
+        rc = _lib.lvkv_engine_sst_verify(
+            self.handle, _dev_ptr(file_buf, "file_buf", (torch.uint8, torch.int8)),
+            _dev_ptr(offsets, "offsets", (torch.int64,)), _dev_ptr(sizes, "sizes", (torch.int32,), n),
+            _dev_ptr(actual, "actual"), _dev_ptr(status, "status"), n,
+            self._flags(False, ordered, fresh))
+        _check("lvkv_engine_sst_verify", rc)
+        self._inflight.append((file_buf, offsets, sizes, actual, status))
+        return actual, status
+
+    def log_verify(self, file_buf, hdr_offsets, *, ordered=False, fresh=True):
+        """lvkv_engine_log_verify: (actual int32, status uint8) as log_verify."""
+        torch = _torch()
+        n = hdr_offsets.numel()
+        actual = torch.empty(n, dtype=torch.int32, device=file_buf.device)
+        status = torch.empty(n, dtype=torch.uint8, device=file_buf.device)
+        torch.cuda.current_stream(file_buf.device).synchronize()
+        rc = _lib.lvkv_engine_log_verify(
+            self.handle, _dev_ptr(file_buf, "file_buf", (torch.uint8, torch.int8)),
+            _dev_ptr(hdr_offsets, "hdr_offsets", (torch.int64,)), _dev_ptr(actual, "actual"),
+            _dev_ptr(status, "status"), n, self._flags(False, ordered, fresh))
+        _check("lvkv_engine_log_verify", rc)
+        self._inflight.append((file_buf, hdr_offsets, actual, status))
+        return actual, status
+
+    def sst_fill_trailers(self, file_buf, offsets, sizes, *, ordered=False, fresh=True):
+        """lvkv_engine_sst_fill_trailers: sst_fill_trailers on the engine."""
+        torch = _torch()
+        n = offsets.numel()
+        crc = torch.empty(n, dtype=torch.int32, device=file_buf.device)
+        torch.cuda.current_stream(file_buf.device).synchronize()
+        rc = _lib.lvkv_engine_sst_fill_trailers(
+            self.handle, _dev_ptr(file_buf, "file_buf", (torch.uint8, torch.int8)),
+            _dev_ptr(offsets, "offsets", (torch.int64,)), _dev_ptr(sizes, "sizes", (torch.int32,), n),
+            _dev_ptr(crc, "crc"), n, self._flags(False, ordered, fresh))
+        _check("lvkv_engine_sst_fill_trailers", rc)
+        self._inflight.append((file_buf, offsets, sizes, crc))
+        return crc
+
+    def log_fill_headers(self, file_buf, hdr_offsets, *, ordered=False, fresh=True):
+        """lvkv_engine_log_fill_headers: log_fill_headers on the engine."""
+        torch = _torch()
+        n = hdr_offsets.numel()
+        crc = torch.empty(n, dtype=torch.int32, device=file_buf.device)
+        torch.cuda.current_stream(file_buf.device).synchronize()
+        rc = _lib.lvkv_engine_log_fill_headers(
+            self.handle, _dev_ptr(file_buf, "file_buf", (torch.uint8, torch.int8)),
+            _dev_ptr(hdr_offsets, "hdr_offsets", (torch.int64,)), _dev_ptr(crc, "crc"), n,
+            self._flags(False, ordered, fresh))
+        _check("lvkv_engine_log_fill_headers", rc)
+        self._inflight.append((file_buf, hdr_offsets, crc))
+        return crc
 
     def wait(self) -> None:
         _check("lvkv_engine_wait", _lib.lvkv_engine_wait(self.handle))

@@ -17,6 +17,9 @@
 // no dword outside the block's own is read; dwords before it come back as
 // zeros and the front padding is masked.
 //
+// Layout: per-block offsets and lengths, or (offsets == nullptr, compute
+// mode) block b at base + b * stride of `length` bytes.
+//
 // Work map: G contiguous runs of equal length. A run is walked in rounds of
 // W * NCH blocks: wave w, chain c takes block c * W + w of the round. Each
 // chain's block is read in chunks of R rows, all chains' loads in flight
@@ -117,8 +120,13 @@ __device__ __forceinline__ RagBlock rag_block(const KernelArgs& a, uint32_t b, b
     len = 1u + (len_type & 0xffffu);
     init = 0;
   } else {
-    off = desc_u64(a, b);
-    len = desc_u32(a, b);
+    if (a.offsets == nullptr) {  // uniform layout: block b at base + b * stride
+      off = static_cast<uint64_t>(b) * a.stride;
+      len = a.length;
+    } else {
+      off = desc_u64(a, b);
+      len = desc_u32(a, b);
+    }
     if (a.inits != nullptr) init = sload_u32(a.inits, b);
   }
   if (a.mode == kModeSstVerify || a.mode == kModeSstFill || a.mode == kModeSstTable) {
@@ -451,7 +459,8 @@ __device__ __forceinline__ void ragged_run(const KernelArgs& a, const uint32_t* 
         const uint8_t* h = a.base + fresh_ld(a, a.offsets + start + i);
         clen = 1u + (static_cast<uint32_t>(h[4]) | (static_cast<uint32_t>(h[5]) << 8));
       } else {
-        clen = fresh_ld(a, a.lengths + start + i) + (sst ? 1u : 0u);
+        clen = (a.offsets == nullptr ? a.length : fresh_ld(a, a.lengths + start + i)) +
+               (sst ? 1u : 0u);
       }
       if (clen > a.long_split) lds[kList + atomicAdd(&lds[kCount], 1u)] = start + i;
     }

@@ -50,7 +50,7 @@ hipError_t launch_log_gather(const uint8_t* file, const uint64_t* hdr_off, size_
                              const lvkv_log_report* phys, const lvkv_log_record* recs,
                              uint32_t rec_cap, const lvkv_log_read_report* read, uint8_t* out,
                              uint64_t out_cap, uint64_t* rec_pos, void* look, uint32_t tag,
-                             hipStream_t stream);
+                             int cus, hipStream_t stream);
 hipError_t launch_sst_tables(const uint8_t* file, const uint64_t* toff, const uint64_t* tsize,
                              uint64_t single_size, uint32_t ntables, uint64_t* d_off,
                              uint32_t* d_size, uint32_t* d_actual, uint8_t* d_status,
@@ -364,11 +364,16 @@ KernelArgs ctx_args(const DeviceCtx& c) {
 // A WAL verify scratch buffer of at least `bytes` for one call on `stream`.
 // A buffer whose last call has finished (its event completed; never
 // recorded counts as completed) is taken as is; else one last used on this
-// same stream, or, with four buffers out, any idle one, is taken behind its
-// event (hipStreamWaitEvent: the new call starts after the old one ends, a
-// no-op on the same stream); else a new buffer is added. A new buffer's
-// counters (bytes [0, 24)) are zeroed on `stream`; every call leaves them at
-// 0. Not capturable: a graph would replay the counters unzeroed.
+// same stream, or, with four buffers in the pool, any big enough idle one, is
+// taken behind its event (hipStreamWaitEvent: the new call starts after the
+// old one ends, a no-op on the same stream). When none is big enough, an idle
+// buffer is regrown in place (after its last call has ended: its event is
+// synchronised before the free) or, below four buffers, one is added; the
+// pool exceeds four only while every buffer is lent to a call in progress on
+// another thread. A new buffer's counters (bytes [0, 24)) are zeroed on
+// `stream`; every call leaves them at 0. Not capturable: a graph would replay
+// the counters unzeroed. The buffers live as long as the process (the HIP
+// runtime may be gone by the time static destructors run).
 hipError_t log_scratch_acquire(DeviceCtx& c, hipStream_t stream, size_t bytes, void** out,
                                size_t* slot) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -377,13 +382,16 @@ hipError_t log_scratch_acquire(DeviceCtx& c, hipStream_t stream, size_t bytes, v
   if (cs != hipStreamCaptureStatusNone) return hipErrorStreamCaptureUnsupported;
   std::lock_guard<std::mutex> lk(c.scratch_mu);
   constexpr size_t kPoolMax = 4;
-  size_t same = SIZE_MAX, any = SIZE_MAX, idle_small = SIZE_MAX;
+  size_t same = SIZE_MAX, any = SIZE_MAX, idle_small = SIZE_MAX, busy_small = SIZE_MAX;
   for (size_t i = 0; i < c.log_pool.size(); ++i) {
     auto& b = c.log_pool[i];
     if (b.lent) continue;
     const bool finished = hipEventQuery(b.ev) == hipSuccess;
     if (b.bytes < bytes) {
-      if (finished) idle_small = i;
+      if (finished)
+        idle_small = i;
+      else
+        busy_small = i;
       continue;
     }
     if (finished) {
@@ -396,7 +404,8 @@ hipError_t log_scratch_acquire(DeviceCtx& c, hipStream_t stream, size_t bytes, v
     if (b.stream == stream) same = i;
     any = i;
   }
-  size_t pick = same != SIZE_MAX ? same : (c.log_pool.size() >= kPoolMax ? any : SIZE_MAX);
+  const bool full = c.log_pool.size() >= kPoolMax;
+  size_t pick = same != SIZE_MAX ? same : (full ? any : SIZE_MAX);
   if (pick != SIZE_MAX) {
     auto& b = c.log_pool[pick];
     if ((e = hipStreamWaitEvent(stream, b.ev, 0)) != hipSuccess) return e;
@@ -406,6 +415,9 @@ hipError_t log_scratch_acquire(DeviceCtx& c, hipStream_t stream, size_t bytes, v
     *slot = pick;
     return hipSuccess;
   }
+  // nothing big enough: regrow an idle buffer (a busy one once its call has
+  // ended) when the pool is full, else add one
+  if (idle_small == SIZE_MAX && full) idle_small = busy_small;
   if (idle_small == SIZE_MAX) {
     DeviceCtx::Scratch n;
     if ((e = hipEventCreateWithFlags(&n.ev, hipEventDisableTiming)) != hipSuccess) return e;
@@ -413,7 +425,10 @@ hipError_t log_scratch_acquire(DeviceCtx& c, hipStream_t stream, size_t bytes, v
     idle_small = c.log_pool.size() - 1;
   }
   auto& b = c.log_pool[idle_small];
-  if (b.p != nullptr && (e = hipFree(b.p)) != hipSuccess) return e;
+  if (b.p != nullptr) {
+    if ((e = hipEventSynchronize(b.ev)) != hipSuccess) return e;
+    if ((e = hipFree(b.p)) != hipSuccess) return e;
+  }
   b.p = nullptr;
   b.bytes = 0;
   const size_t cap = std::max<size_t>(bytes, size_t{1} << 16);
@@ -759,7 +774,7 @@ int lvkv_log_gather_device(const void* d_file, const uint64_t* d_hdr_offsets, si
   e = launch_log_gather(static_cast<const uint8_t*>(d_file), d_hdr_offsets, capacity, d_report,
                         d_records, static_cast<uint32_t>(record_capacity), d_read,
                         static_cast<uint8_t*>(d_payload), payload_capacity, d_record_pos,
-                        static_cast<uint8_t*>(scratch) + 32, tag, hs);
+                        static_cast<uint8_t*>(scratch) + 32, tag, c->groups, hs);
   const hipError_t e2 = log_scratch_release(*c, slot, hs);
   if (e == hipSuccess) e = e2;
   return e == hipSuccess ? LVKV_OK : hip_fail(e);

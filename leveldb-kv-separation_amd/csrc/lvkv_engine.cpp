@@ -72,19 +72,33 @@ struct EngineKernel {
   uint32_t waves = 8, chains = 5, per_cu = 1;  // shape; per_cu = workgroups per CU
 };
 
-// The engine's kernels (lvkv_engine_kernels.hip): symbol, timestamp build,
-// shape. [0] is the production schedule.
+// Kernel-argument layouts of the engine's kernels.
+enum ArgKind : uint32_t { kArgsUniform = 0, kArgsRagged = 1 };
+
+// The engine's kernels (lvkv_engine_kernels.hip): symbol, timestamp build
+// (nullptr: none), shape, argument layout. [0] is the production schedule of
+// overlapped uniform batches, [1] of ordered ones; [2] and [3] walk
+// general-layout batches.
 struct KernelSpec {
   const char* name;
   const char* stamps;
   uint32_t waves, chains, per_cu;
+  ArgKind kind;
 };
 constexpr KernelSpec kSpecs[] = {
-    {"lvkv_ek_uniform.kd", "lvkv_ek_uniform_stamps.kd", 8, 5, 1},
-    {"lvkv_ek_uniform_pair.kd", "lvkv_ek_uniform_pair_stamps.kd", 8, 3,
-     2},
+    {"lvkv_ek_uniform.kd", "lvkv_ek_uniform_stamps.kd", 8, 5, 1, kArgsUniform},
+    {"lvkv_ek_uniform_pair.kd", "lvkv_ek_uniform_pair_stamps.kd", 8, 3, 2, kArgsUniform},
+    {"lvkv_ek_ragged.kd", nullptr, 8, 2, 2, kArgsRagged},
+    {"lvkv_ek_ragged_small.kd", nullptr, 8, 4, 2, kArgsRagged},
 };
 constexpr int kNumSpecs = static_cast<int>(sizeof(kSpecs) / sizeof(kSpecs[0]));
+constexpr int kNumUniformSpecs = 2;  // lvkv_engine_set_variant's choices
+constexpr int kRaggedSpec = 2, kRaggedSmallSpec = 3;
+static_assert(sizeof(EngineRaggedArgs) <= 256 && sizeof(UniformArgs) <= 256, "kernarg slot");
+
+constexpr size_t args_size(ArgKind k) {
+  return k == kArgsUniform ? sizeof(UniformArgs) : sizeof(EngineRaggedArgs);
+}
 
 struct AgentMatch {
   uint32_t domain, bdfid;
@@ -237,7 +251,8 @@ void drop_probe(Engine& e) {
   e.probe_exe_ok = e.probe_reader_ok = e.probe_on = false;
 }
 
-int load_kernel(Engine& e, hsa_executable_t exe, const char* name, EngineKernel* k) {
+int load_kernel(Engine& e, hsa_executable_t exe, const char* name, EngineKernel* k,
+                size_t want_args = sizeof(UniformArgs)) {
   hsa_executable_symbol_t sym;
   if (hsa_executable_get_symbol_by_name(exe, name, &e.agent, &sym) != HSA_STATUS_SUCCESS)
     return LVKV_ERR_HIP;
@@ -252,7 +267,7 @@ int load_kernel(Engine& e, hsa_executable_t exe, const char* name, EngineKernel*
     return LVKV_ERR_HIP;
   // The kernarg segment must be exactly the argument struct: no hidden
   // arguments the engine would have to fill.
-  if (k->kernarg_size != sizeof(UniformArgs) || k->kernarg_size > kSlotBytes)
+  if (k->kernarg_size != want_args || k->kernarg_size > kSlotBytes)
     return LVKV_ERR_HIP;
   return LVKV_OK;
 }
@@ -358,8 +373,10 @@ int create(int device, Engine** out) {
                                                    nullptr) == HSA_STATUS_SUCCESS;
   ok = ok && hsa_executable_freeze(e->exe, nullptr) == HSA_STATUS_SUCCESS;
   for (int i = 0; ok && i < kNumSpecs; ++i) {
-    ok = load_kernel(*e, e->exe, kSpecs[i].name, &e->kern[i]) == LVKV_OK &&
-         load_kernel(*e, e->exe, kSpecs[i].stamps, &e->kern_stamps[i]) == LVKV_OK;
+    const size_t want = args_size(kSpecs[i].kind);
+    ok = load_kernel(*e, e->exe, kSpecs[i].name, &e->kern[i], want) == LVKV_OK &&
+         load_kernel(*e, e->exe, kSpecs[i].stamps ? kSpecs[i].stamps : kSpecs[i].name,
+                     &e->kern_stamps[i], want) == LVKV_OK;
     for (EngineKernel* k : {&e->kern[i], &e->kern_stamps[i]}) {
       k->waves = kSpecs[i].waves;
       k->chains = kSpecs[i].chains;
@@ -407,13 +424,18 @@ bool wait_signal(Engine& e, hsa_signal_t sig) {
   // the error flag and the deadline are re-checked
   const uint64_t hint = e.tick_us > 0 ? static_cast<uint64_t>(1000.0 / e.tick_us) : 1000000;
   double deadline = 0;
+  hsa_signal_value_t seen = 0;
   for (;;) {
-    if (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, hint, HSA_WAIT_STATE_ACTIVE) < 1)
-      return true;
+    const hsa_signal_value_t v =
+        hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, hint, HSA_WAIT_STATE_ACTIVE);
+    if (v < 1) return true;
     if (e.queue_error) return false;
     const double t = now_s();
-    if (deadline == 0) {
+    // the cutoff counts from the last progress: a fence over many queues
+    // decrements its signal once per queue, and each decrement restarts it
+    if (deadline == 0 || v != seen) {
       deadline = t + e.stuck_s;
+      seen = v;
     } else if (t > deadline) {
       e.queue_error = kStuck;
       return false;
@@ -427,12 +449,15 @@ void* packet_slot(Engine& e, uint64_t* idx) {
   hsa_queue_t* q = e.queues[e.cur];
   *idx = hsa_queue_add_write_index_screlease(q, 1);
   double deadline = 0;
+  uint64_t seen = 0;
   for (uint64_t spin = 0; *idx - hsa_queue_load_read_index_scacquire(q) >= q->size; ++spin) {
     if (e.queue_error) return nullptr;
     if ((spin & 1023u) == 1023u) {
       const double t = now_s();
-      if (deadline == 0) {
+      const uint64_t rd = hsa_queue_load_read_index_relaxed(q);
+      if (deadline == 0 || rd != seen) {  // the queue still advances: restart the cutoff
         deadline = t + e.stuck_s;
+        seen = rd;
       } else if (t > deadline) {
         e.queue_error = kStuck;
         return nullptr;
@@ -504,14 +529,16 @@ int fence(Engine& e) {
   return e.queue_error ? LVKV_ERR_HIP : LVKV_OK;
 }
 
-// One kernel-dispatch packet; the caller holds e.mu.
-int dispatch(Engine& e, const EngineKernel& k, const UniformArgs& args, bool acquire,
-             bool barrier, bool system_acquire) {
+// One kernel-dispatch packet of `ngroups` workgroups whose kernel arguments
+// are args[0, size); the caller holds e.mu. queue < 0: dispatch n goes to
+// queue n % nq (consecutive dispatches side by side); else that queue.
+int dispatch(Engine& e, const EngineKernel& k, const void* args, size_t size, uint32_t ngroups,
+             bool acquire, bool barrier, bool system_acquire, int queue = -1) {
   if (e.queue_error) return LVKV_ERR_HIP;
   const uint64_t n = e.next;
   // Kernarg slot n % kSlots was last used by dispatch n - kSlots.
   if (n - e.fenced >= kSlots && fence(e) != LVKV_OK) return LVKV_ERR_HIP;
-  e.cur = static_cast<int>(n % static_cast<uint64_t>(e.nq));
+  e.cur = queue >= 0 ? queue : static_cast<int>(n % static_cast<uint64_t>(e.nq));
   hsa_signal_t done{};
   if (e.profiling) {
     const uint32_t s = static_cast<uint32_t>(n % kProfSlots);
@@ -521,7 +548,7 @@ int dispatch(Engine& e, const EngineKernel& k, const UniformArgs& args, bool acq
     done = e.prof_sig[s];
   }
   uint8_t* ka = e.kernarg + static_cast<size_t>(n % kSlots) * kSlotBytes;
-  memcpy(ka, &args, sizeof(args));
+  memcpy(ka, args, size);
   if (e.kernarg_vram) {
     // BAR writes are write-combined and may sit in the HDP write cache: fence
     // them, flush the HDP and read the register back (the read completes
@@ -538,7 +565,7 @@ int dispatch(Engine& e, const EngineKernel& k, const UniformArgs& args, bool acq
   p->workgroup_size_y = 1;
   p->workgroup_size_z = 1;
   p->reserved0 = 0;
-  p->grid_size_x = args.ngroups * wg;
+  p->grid_size_x = ngroups * wg;
   p->grid_size_y = 1;
   p->grid_size_z = 1;
   p->private_segment_size = k.private_size;
@@ -557,6 +584,52 @@ int dispatch(Engine& e, const EngineKernel& k, const UniformArgs& args, bool acq
        << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
   publish(e, p, header, 1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS, idx);
   e.next = n + 1;
+  return LVKV_OK;
+}
+
+// A general-layout batch (KernelArgs as the HIP path builds it: offsets or
+// the uniform stride, a mode) through the engine's ragged kernels; the
+// same ordering and acquire rules as the uniform submit.
+int submit_general(Engine& eng, KernelArgs a, size_t nblocks, uint32_t flags) {
+  Engine* e = &eng;
+  if (nblocks == 0) return LVKV_OK;
+  const bool log = a.mode == kModeLogVerify || a.mode == kModeLogFill;
+  a.long_split = log ? kLogLongBytes : kLongBytes;
+  a.row_tab = e->d_tables;
+  a.lane_tab = e->d_tables + kRowTabDwords;
+  std::lock_guard<std::mutex> lk(e->mu);
+  const bool ordered = (flags & LVKV_FLAG_ORDERED) != 0;
+  if (ordered && e->nq > 1 && e->fenced != e->next && fence(*e) != LVKV_OK) return LVKV_ERR_HIP;
+  const int queue = ordered ? static_cast<int>(e->next % static_cast<uint64_t>(e->nq)) : -1;
+  const int spec = log ? kRaggedSmallSpec : kRaggedSpec;
+  const EngineKernel& k = e->kern[spec];
+  const uint64_t per_round = uint64_t{k.waves} * k.chains;
+  const uint64_t max_groups = static_cast<uint64_t>(e->cus) * k.per_cu;
+  // the kernel indexes blocks with u32
+  constexpr uint64_t kMaxPerDispatch = uint64_t{1} << 30;
+  for (uint64_t done = 0; done < nblocks;) {
+    const uint64_t n = std::min<uint64_t>(nblocks - done, kMaxPerDispatch);
+    EngineRaggedArgs r;
+    memset(&r, 0, sizeof(r));
+    r.k = a;
+    r.k.nblocks = static_cast<uint32_t>(n);
+    if (a.offsets != nullptr) {
+      r.k.offsets = a.offsets + done;
+      if (a.lengths != nullptr) r.k.lengths = a.lengths + done;
+    } else {
+      r.k.base = a.base + done * a.stride;
+    }
+    if (a.inits != nullptr) r.k.inits = a.inits + done;
+    if (a.out_crc != nullptr) r.k.out_crc = a.out_crc + done;
+    if (a.out_status != nullptr) r.k.out_status = a.out_status + done;
+    r.zpow = e->d_tables + kZPowOffset;
+    r.lane_cols = e->d_tables + kRowTabDwords + kLaneTabDwords;
+    r.ngroups = static_cast<uint32_t>(std::min(max_groups, (n + per_round - 1) / per_round));
+    const int rc = dispatch(*e, k, &r, sizeof(r), r.ngroups, /*acquire=*/true,
+                            /*barrier=*/ordered, (flags & LVKV_FLAG_SYSTEM_ACQUIRE) != 0, queue);
+    if (rc != LVKV_OK) return rc;
+    done += n;
+  }
   return LVKV_OK;
 }
 
@@ -586,16 +659,31 @@ int lvkv_engine_crc32c_uniform(lvkv_engine* eng, const void* d_base, uint64_t st
                                uint32_t flags) {
   if (eng == nullptr) return LVKV_ERR_INVALID;
   if (nblocks == 0) return LVKV_OK;
-  if (!d_base || !d_out || length < 4 || length > kRowsPerChunk * kRowBytes || stride % 4 != 0 ||
-      (reinterpret_cast<uintptr_t>(d_base) + length) % 4 != 0 || nblocks > (size_t{1} << 40))
-    return LVKV_ERR_INVALID;
+  if (!d_base || !d_out || nblocks > (size_t{1} << 40)) return LVKV_ERR_INVALID;
   Engine* e = reinterpret_cast<Engine*>(eng);
+  if (length < 4 || length > kRowsPerChunk * kRowBytes || stride % 4 != 0 ||
+      (reinterpret_cast<uintptr_t>(d_base) + length) % 4 != 0) {
+    // beyond the burst kernel (> 16 rows, < 4 bytes, block ends not 4-byte
+    // aligned): the general walk in its uniform layout
+    KernelArgs a;
+    memset(&a, 0, sizeof(a));
+    a.base = static_cast<const uint8_t*>(d_base);
+    a.stride = stride;
+    a.length = length;
+    a.init = init;
+    a.out_crc = d_out;
+    a.mode = kModeCompute;
+    a.mask = (flags & LVKV_FLAG_MASK) ? 1u : 0u;
+    return submit_general(*e, a, nblocks, flags);
+  }
   std::lock_guard<std::mutex> lk(e->mu);
   const bool ordered = (flags & LVKV_FLAG_ORDERED) != 0;
   // An ordered batch runs alone: the other queues drain first (the barrier
-  // bit orders a packet only within its own queue), and it gets the kernel
-  // shaped for the whole chip.
+  // bit orders a packet only within its own queue), all of its dispatches go
+  // to ONE queue with the barrier bit, so they run one after another, and it
+  // gets the kernel shaped for the whole chip.
   if (ordered && e->nq > 1 && e->fenced != e->next && fence(*e) != LVKV_OK) return LVKV_ERR_HIP;
+  const int queue = ordered ? static_cast<int>(e->next % static_cast<uint64_t>(e->nq)) : -1;
   const int v = ordered ? e->ordered_variant : e->variant;
   const EngineKernel& k = (e->probe_on && ordered != e->probe_overlapped) ? e->probe
                           : e->stamps                ? e->kern_stamps[v]
@@ -628,10 +716,11 @@ int lvkv_engine_crc32c_uniform(lvkv_engine* eng, const void* d_base, uint64_t st
       const uint64_t area = groups * k.waves * 8;
       a.stamps = e->stamps + (e->stamp_next++ % e->stamp_areas) * area;
     }
-    // every dispatch acquires: they rotate over queues, so dispatch i > 0
-    // may start before (or during) dispatch 0's acquire on another queue
-    const int rc = dispatch(*e, k, a, /*acquire=*/true, /*barrier=*/ordered,
-                            (flags & LVKV_FLAG_SYSTEM_ACQUIRE) != 0);
+    // every dispatch acquires: overlapped ones rotate over queues, so
+    // dispatch i > 0 may start before (or during) dispatch 0's acquire on
+    // another queue
+    const int rc = dispatch(*e, k, &a, sizeof(a), a.ngroups, /*acquire=*/true,
+                            /*barrier=*/ordered, (flags & LVKV_FLAG_SYSTEM_ACQUIRE) != 0, queue);
     if (rc != LVKV_OK) return rc;
     done += n;
   }
@@ -644,6 +733,88 @@ int lvkv_engine_wait(lvkv_engine* eng) {
   std::lock_guard<std::mutex> lk(e->mu);
   if (e->fenced != e->next && fence(*e) != LVKV_OK) return LVKV_ERR_HIP;
   return e->queue_error ? LVKV_ERR_HIP : LVKV_OK;
+}
+
+int lvkv_engine_crc32c_batch(lvkv_engine* eng, const void* d_base, const uint64_t* d_offsets,
+                             const uint32_t* d_lengths, const uint32_t* d_init, uint32_t init,
+                             uint32_t* d_out, size_t nblocks, uint32_t flags) {
+  if (eng == nullptr) return LVKV_ERR_INVALID;
+  if (nblocks == 0) return LVKV_OK;
+  if (!d_base || !d_offsets || !d_lengths || !d_out) return LVKV_ERR_INVALID;
+  KernelArgs a;
+  memset(&a, 0, sizeof(a));
+  a.base = static_cast<const uint8_t*>(d_base);
+  a.offsets = d_offsets;
+  a.lengths = d_lengths;
+  a.inits = d_init;
+  a.init = init;
+  a.out_crc = d_out;
+  a.mode = kModeCompute;
+  a.mask = (flags & LVKV_FLAG_MASK) ? 1u : 0u;
+  return submit_general(*reinterpret_cast<Engine*>(eng), a, nblocks, flags);
+}
+
+int lvkv_engine_sst_verify(lvkv_engine* eng, const void* d_file, const uint64_t* d_offsets,
+                           const uint32_t* d_sizes, uint32_t* d_actual, uint8_t* d_status,
+                           size_t nblocks, uint32_t flags) {
+  if (eng == nullptr) return LVKV_ERR_INVALID;
+  if (nblocks == 0) return LVKV_OK;
+  if (!d_file || !d_offsets || !d_sizes || !d_actual || !d_status) return LVKV_ERR_INVALID;
+  KernelArgs a;
+  memset(&a, 0, sizeof(a));
+  a.base = static_cast<const uint8_t*>(d_file);
+  a.offsets = d_offsets;
+  a.lengths = d_sizes;
+  a.out_crc = d_actual;
+  a.out_status = d_status;
+  a.mode = kModeSstVerify;
+  return submit_general(*reinterpret_cast<Engine*>(eng), a, nblocks, flags);
+}
+
+int lvkv_engine_log_verify(lvkv_engine* eng, const void* d_file, const uint64_t* d_hdr_offsets,
+                           uint32_t* d_actual, uint8_t* d_status, size_t nrecords,
+                           uint32_t flags) {
+  if (eng == nullptr) return LVKV_ERR_INVALID;
+  if (nrecords == 0) return LVKV_OK;
+  if (!d_file || !d_hdr_offsets || !d_actual || !d_status) return LVKV_ERR_INVALID;
+  KernelArgs a;
+  memset(&a, 0, sizeof(a));
+  a.base = static_cast<const uint8_t*>(d_file);
+  a.offsets = d_hdr_offsets;
+  a.out_crc = d_actual;
+  a.out_status = d_status;
+  a.mode = kModeLogVerify;
+  return submit_general(*reinterpret_cast<Engine*>(eng), a, nrecords, flags);
+}
+
+int lvkv_engine_sst_fill_trailers(lvkv_engine* eng, void* d_file, const uint64_t* d_offsets,
+                                  const uint32_t* d_sizes, uint32_t* d_crc, size_t nblocks,
+                                  uint32_t flags) {
+  if (eng == nullptr) return LVKV_ERR_INVALID;
+  if (nblocks == 0) return LVKV_OK;
+  if (!d_file || !d_offsets || !d_sizes) return LVKV_ERR_INVALID;
+  KernelArgs a;
+  memset(&a, 0, sizeof(a));
+  a.base = static_cast<const uint8_t*>(d_file);
+  a.offsets = d_offsets;
+  a.lengths = d_sizes;
+  a.out_crc = d_crc;
+  a.mode = kModeSstFill;
+  return submit_general(*reinterpret_cast<Engine*>(eng), a, nblocks, flags);
+}
+
+int lvkv_engine_log_fill_headers(lvkv_engine* eng, void* d_file, const uint64_t* d_hdr_offsets,
+                                 uint32_t* d_crc, size_t nrecords, uint32_t flags) {
+  if (eng == nullptr) return LVKV_ERR_INVALID;
+  if (nrecords == 0) return LVKV_OK;
+  if (!d_file || !d_hdr_offsets) return LVKV_ERR_INVALID;
+  KernelArgs a;
+  memset(&a, 0, sizeof(a));
+  a.base = static_cast<const uint8_t*>(d_file);
+  a.offsets = d_hdr_offsets;
+  a.out_crc = d_crc;
+  a.mode = kModeLogFill;
+  return submit_general(*reinterpret_cast<Engine*>(eng), a, nrecords, flags);
 }
 
 int lvkv_engine_queues(lvkv_engine* eng, int nq) {
@@ -695,8 +866,8 @@ int lvkv_engine_set_stamps(lvkv_engine* eng, uint64_t* d_stamps, uint64_t areas)
 }
 
 int lvkv_engine_set_variant(lvkv_engine* eng, int variant, int ordered_variant) {
-  if (eng == nullptr || variant < 0 || variant >= kNumSpecs || ordered_variant < 0 ||
-      ordered_variant >= kNumSpecs)
+  if (eng == nullptr || variant < 0 || variant >= kNumUniformSpecs || ordered_variant < 0 ||
+      ordered_variant >= kNumUniformSpecs)
     return LVKV_ERR_INVALID;
   Engine* e = reinterpret_cast<Engine*>(eng);
   std::lock_guard<std::mutex> lk(e->mu);

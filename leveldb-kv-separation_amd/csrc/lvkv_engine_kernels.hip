@@ -11,6 +11,7 @@
 #include <stdint.h>
 
 #include "crc32c_burst.h"
+#include "crc32c_ragged_body.h"
 #include "lvkv_kernel_args.h"
 
 namespace {
@@ -48,4 +49,22 @@ extern "C" __global__ void __launch_bounds__(512, 2)
     lvkv_ek_uniform_pair_stamps(lvkv::UniformArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLds];
   lvkv::burst_kernel_body<lvkv::kBurstPipe1 | lvkv::kBurstStamps, 8, 3>(a, lds, a.ngroups);
+}
+
+// General-layout batches (lvkv_engine_crc32c_batch, the verify and fill
+// submits, uniform blocks beyond the burst kernel's 16 rows): the HIP path's
+// ragged walk (crc32c_ragged_body.h, ragged_run) over a.k.nblocks blocks,
+// two 512-thread workgroups per CU. 8 waves x 2 chains x 24-row chunks for
+// SST blocks and compute batches; 8 x 4 x 8 for WAL records (mostly short).
+extern "C" __global__ void __launch_bounds__(512, 2)
+    lvkv_ek_ragged(lvkv::EngineRaggedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::RagLds<8>::kDwords];
+  lvkv::ragged_run<8, 2, 24>(a.k, a.zpow, a.lane_cols, lds, blockIdx.x, a.ngroups, a.k.nblocks,
+                             false);
+}
+extern "C" __global__ void __launch_bounds__(512, 2)
+    lvkv_ek_ragged_small(lvkv::EngineRaggedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::RagLds<8>::kDwords];
+  lvkv::ragged_run<8, 4, 8>(a.k, a.zpow, a.lane_cols, lds, blockIdx.x, a.ngroups, a.k.nblocks,
+                            false);
 }

@@ -133,6 +133,18 @@ struct UniformArgs {
                               // generated in-kernel from these columns
 };
 
+// Arguments of the engine's general-layout kernels (lvkv_ek_ragged*,
+// lvkv_engine_kernels.hip): the HIP path's KernelArgs plus what
+// launch_crc32c_ragged passes beside it, and the grid size (the engine's
+// dispatches read no hidden kernel arguments).
+struct EngineRaggedArgs {
+  KernelArgs k;
+  const uint32_t* zpow;
+  const uint32_t* lane_cols;
+  uint32_t ngroups;
+  uint32_t pad_;
+};
+
 }  // namespace lvkv
 
 #endif  // LVKV_KERNEL_ARGS_H_

@@ -725,6 +725,7 @@ struct GatherArgs {
   const lvkv_log_record* recs;
   const lvkv_log_read_report* read;
   uint32_t rec_cap;
+  uint32_t cap;           // candidates the scratch holds (the read call's capacity)
   uint8_t* out;
   uint64_t out_cap;
   uint64_t* rec_pos;      // nullable
@@ -762,7 +763,7 @@ __global__ void __launch_bounds__(kGatherT) log_gather_own_kernel(GatherArgs a) 
   __shared__ unsigned long long wsum[kGatherT / 64];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u, wave = tid >> 6;
-  const uint32_t N = a.phys->status == LVKV_OK ? a.phys->count_ : 0u;
+  const uint32_t N = a.phys->status == LVKV_OK ? min(a.phys->count_, a.cap) : 0u;
   const uint32_t R = a.phys->status == LVKV_OK ? min(a.read->nrecords, a.rec_cap) : 0u;
   const uint32_t g = blockIdx.x;
   if (g * kGatherPer >= N) return;
@@ -804,7 +805,7 @@ __global__ void __launch_bounds__(kGatherT) log_gather_kernel(GatherArgs a) {
   __shared__ unsigned long long base_s;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u, wave = tid >> 6;
-  const uint32_t N = a.phys->status == LVKV_OK ? a.phys->count_ : 0u;
+  const uint32_t N = a.phys->status == LVKV_OK ? min(a.phys->count_, a.cap) : 0u;
   const uint32_t g = blockIdx.x;
   if (g * kGatherPer >= N) return;
   const uint32_t j0 = g * kGatherPer + tid * kGatherItems;
@@ -845,52 +846,115 @@ __global__ void __launch_bounds__(kGatherT) log_gather_kernel(GatherArgs a) {
   }
 }
 
-// The owned fragments' payloads to their places, one wave per candidate (a
-// grid of N waves: the copies are latency-bound, so as many as the chip
-// holds are in flight; with the copy inside the scan's 61 workgroups it
-// took 680 us for a 66 MB log). Each output word is rebuilt from two aligned
-// source dwords (a buffer resource over the payload's aligned dwords: a
-// dword past them reads as 0; one partly past a range's end would read as 0
-// whole); the 0-3 bytes before the output's first 4-byte boundary and after
-// its last go bytewise.
-__global__ void __launch_bounds__(256) log_gather_copy_kernel(GatherArgs a) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t j = blockIdx.x * 4u + (threadIdx.x >> 6);
-  const uint32_t N = a.phys->status == LVKV_OK ? a.phys->count_ : 0u;
-  if (j >= N) return;
-  const ulonglong2 de = a.dst[j];
+// The owned fragments' payloads to their places. A bounded grid (a few
+// workgroups per CU, whatever the capacity); wave v takes candidates v, v + W,
+// ... and walks them as a stream of 1 KiB units (candidate, round): the next
+// unit's loads are issued before the current unit's stores, and each
+// candidate's place is fetched one candidate ahead, so two units of every wave
+// are in flight. Each output word is rebuilt from two aligned source dwords
+// (a buffer resource over the payload's aligned dwords: a dword past them
+// reads as 0; one partly past a range's end would read as 0 whole); the 0-3
+// bytes before the output's first 4-byte boundary and after its last go
+// bytewise. (One wave per candidate over a grid of N waves: 50 us for the
+// 62k-record log, and a grid sized by the capacity that passed 2^32
+// work-items above ~470 MB images.)
+struct CopyJob {
+  const uint8_t* src;  // payload start
+  uint8_t* dst;        // its place
+  uint32_t l;          // bytes (0: nothing to copy)
+  uint32_t rounds;     // 1 KiB rounds of whole output words (at least 1)
+};
+
+__device__ __forceinline__ CopyJob copy_job(const GatherArgs& a, ulonglong2 de) {
+  CopyJob c;
   const uint64_t d = de.x;
-  if (d == ~0ull) return;
-  const uint8_t* src = a.file + (de.y & ((uint64_t{1} << 48) - 1));
-  const uint32_t l = static_cast<uint32_t>(de.y >> 48);
-  if (d + l > a.out_cap) return;
-  const uint32_t hb = min(l, (4u - static_cast<uint32_t>(d & 3u)) & 3u);
-  if (lane < hb) a.out[d + lane] = src[lane];
-  const uint64_t s0 = reinterpret_cast<uint64_t>(src);
+  c.l = static_cast<uint32_t>(de.y >> 48);
+  c.src = a.file + (de.y & ((uint64_t{1} << 48) - 1));
+  if (d == ~0ull || d + c.l > a.out_cap) c.l = 0;
+  c.dst = a.out + (c.l ? d : 0);
+  const uint32_t hb = min(c.l, (4u - static_cast<uint32_t>(reinterpret_cast<uint64_t>(c.dst) & 3u)) & 3u);
+  const uint32_t nw = (c.l - hb) >> 2;
+  c.rounds = max(1u, (nw + 255u) >> 8);
+  return c;
+}
+
+struct CopyRegs {
+  uint32_t lo[4], hi[4];
+};
+
+// Loads of round r of job c (lane's words w0 + lane + 64u).
+__device__ __forceinline__ CopyRegs copy_load(const CopyJob& c, uint32_t r, uint32_t lane) {
+  CopyRegs x;
+  const uint64_t s0 = reinterpret_cast<uint64_t>(c.src);
   const uint64_t sa = s0 & ~uint64_t{3};
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void*>(sa), 0, static_cast<int>((s0 + l - sa + 3u) & ~uint64_t{3}),
+      reinterpret_cast<void*>(sa), 0, static_cast<int>((s0 + c.l - sa + 3u) & ~uint64_t{3}),
       kBufferDword3);
-  const uint32_t nw = (l - hb) >> 2;
-  uint32_t* dw = reinterpret_cast<uint32_t*>(a.out + d + hb);
+  const uint32_t hb = min(c.l, (4u - static_cast<uint32_t>(reinterpret_cast<uint64_t>(c.dst) & 3u)) & 3u);
   const uint32_t sb = static_cast<uint32_t>(s0 - sa) + hb;
-  // four words a lane in flight per round
-  for (uint32_t w0 = 0; w0 < nw; w0 += 256) {
-    uint32_t lo[4], hi[4];
 #pragma unroll
-    for (uint32_t u = 0; u < 4; ++u) {
-      const uint32_t so = sb + 4u * (w0 + 64u * u + lane);
-      lo[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(so & ~3u), 0, 0);
-      hi[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>((so & ~3u) + 4u), 0, 0);
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < 4; ++u) {
-      const uint32_t w = w0 + 64u * u + lane;
-      if (w < nw) dw[w] = __builtin_amdgcn_alignbyte(hi[u], lo[u], sb & 3u);
-    }
+  for (uint32_t u = 0; u < 4; ++u) {
+    const uint32_t so = (sb + 4u * (256u * r + 64u * u + lane)) & ~3u;
+    x.lo[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(so), 0, 0);
+    x.hi[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(so + 4u), 0, 0);
   }
-  const uint32_t tb = (l - hb) & 3u;
-  if (lane < tb) a.out[d + hb + 4u * nw + lane] = src[hb + 4u * nw + lane];
+  return x;
+}
+
+// Stores of round r of job c (the head and tail bytes with round 0).
+__device__ __forceinline__ void copy_store(const CopyJob& c, uint32_t r, uint32_t lane,
+                                           const CopyRegs& x) {
+  if (c.l == 0) return;
+  const uint32_t hb = min(c.l, (4u - static_cast<uint32_t>(reinterpret_cast<uint64_t>(c.dst) & 3u)) & 3u);
+  const uint32_t nw = (c.l - hb) >> 2;
+  const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uint64_t>(c.src) + hb) & 3u;
+  uint32_t* dw = reinterpret_cast<uint32_t*>(c.dst + hb);
+#pragma unroll
+  for (uint32_t u = 0; u < 4; ++u) {
+    const uint32_t w = 256u * r + 64u * u + lane;
+    if (w < nw) dw[w] = __builtin_amdgcn_alignbyte(x.hi[u], x.lo[u], sh);
+  }
+  if (r == 0) {
+    if (lane < hb) c.dst[lane] = c.src[lane];
+    const uint32_t tb = (c.l - hb) & 3u;
+    if (lane < tb) c.dst[hb + 4u * nw + lane] = c.src[hb + 4u * nw + lane];
+  }
+}
+
+__global__ void __launch_bounds__(256) log_gather_copy_kernel(GatherArgs a) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t W = gridDim.x * 4u;
+  const uint32_t N = a.phys->status == LVKV_OK ? min(a.phys->count_, a.cap) : 0u;
+  uint32_t j = blockIdx.x * 4u + wave;
+  if (j >= N) return;
+  CopyJob c = copy_job(a, a.dst[j]);
+  ulonglong2 de_next = j + W < N ? a.dst[j + W] : make_ulonglong2(~0ull, 0);
+  uint32_t r = 0;
+  CopyRegs x = copy_load(c, 0, lane);
+  for (;;) {
+    // the next unit: the job's next round, or the next candidate's round 0
+    CopyJob cn = c;
+    uint32_t rn = r + 1;
+    uint32_t jn = j;
+    if (rn == c.rounds) {
+      jn = j + W;
+      rn = 0;
+      if (jn < N) {
+        cn = copy_job(a, de_next);
+        de_next = jn + W < N ? a.dst[jn + W] : make_ulonglong2(~0ull, 0);
+      }
+    }
+    const bool more = jn < N;
+    CopyRegs xn;
+    if (more) xn = copy_load(cn, rn, lane);
+    copy_store(c, r, lane, x);
+    if (!more) break;
+    c = cn;
+    r = rn;
+    j = jn;
+    x = xn;
+  }
 }
 
 }  // namespace
@@ -967,7 +1031,7 @@ hipError_t launch_log_gather(const uint8_t* file, const uint64_t* hdr_off, size_
                              const lvkv_log_report* phys, const lvkv_log_record* recs,
                              uint32_t rec_cap, const lvkv_log_read_report* read, uint8_t* out,
                              uint64_t out_cap, uint64_t* rec_pos, void* look, uint32_t tag,
-                             hipStream_t stream) {
+                             int cus, hipStream_t stream) {
   GatherArgs a;
   a.file = file;
   a.hdr_off = hdr_off;
@@ -975,6 +1039,7 @@ hipError_t launch_log_gather(const uint8_t* file, const uint64_t* hdr_off, size_
   a.recs = recs;
   a.read = read;
   a.rec_cap = rec_cap;
+  a.cap = static_cast<uint32_t>(capacity);
   (void)tag;
   a.out = out;
   a.out_cap = out_cap;
@@ -987,8 +1052,12 @@ hipError_t launch_log_gather(const uint8_t* file, const uint64_t* hdr_off, size_
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(log_gather_kernel, dim3(groups), dim3(kGatherT), 0, stream, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(log_gather_copy_kernel, dim3(static_cast<uint32_t>((capacity + 3) / 4)),
-                     dim3(256), 0, stream, a);
+  // the copy: a bounded grid (8 workgroups of 4 waves per CU), grid-stride
+  // over the candidates the device counted
+  const uint32_t copy_groups = static_cast<uint32_t>(
+      std::min<uint64_t>((capacity + 3) / 4, uint64_t{8} * static_cast<uint64_t>(cus)));
+  hipLaunchKernelGGL(log_gather_copy_kernel, dim3(std::max(1u, copy_groups)), dim3(256), 0,
+                     stream, a);
   return hipGetLastError();
 }
 

@@ -114,7 +114,10 @@ def _device_log_records(img, records, hdrs, gathered):
     record, the contents taken from the device's own gather
     (lvkv_log_gather_device: the records end to end); the CRC is the
     checker's (oracle). The fragment list is cross-checked against the
-    image."""
+    image, and the gathered bytes byte for byte against the fragments'
+    payloads sliced from the image (ReadRecord's scratch->append of each
+    fragment, db/log_reader.cc:92-137), so the CRC comparison with the
+    reference rides on top of an exact one."""
     import oracle
     payload, pos = gathered
     pl = payload.cpu().numpy().tobytes()
@@ -122,8 +125,10 @@ def _device_log_records(img, records, hdrs, gathered):
     assert len(pos) == len(records)
     out, at = [], 0
     for (off, length, first, nfrags), p in zip(records, pos):
-        frag_bytes = sum(img[h + 4] | img[h + 5] << 8 for h in hdrs[first: first + nfrags])
-        assert hdrs[first] == off and frag_bytes == length and p == at
+        frags = hdrs[first: first + nfrags]
+        want = b"".join(img[h + 7: h + 7 + (img[h + 4] | img[h + 5] << 8)] for h in frags)
+        assert hdrs[first] == off and len(want) == length and p == at
+        assert pl[p: p + length] == want, ("gathered bytes differ", off)
         at += length
         out.append((off, length, oracle.value(pl[p: p + length])))
     return out
@@ -203,3 +208,47 @@ def test_device_log_read_large_and_capacity(lvkv, gpu):
     assert rd["nreports"] == len(want_reps) and len(records) == 5
     # the first five records' bytes are still gathered
     assert _device_log_records(img, records, hdrs, gathered) == want_recs[:5]
+
+
+@pytest.mark.gpu
+def test_device_log_gather_large_image_default_capacity(lvkv, gpu):
+    """A ~650 MB log (a clean 20k-record, 40 MB log padded to whole 32 KiB blocks
+    with zeros — zero-type zero-length trailers, skipped silently, as
+    log_reader.cc:234-240 has them — tiled 16 times) read and gathered with
+    the default capacities (size // 7 + blocks candidates): the gather's copy
+    grid is bounded (a grid sized by that capacity passed 2^32 work-items
+    above ~470 MB), and every record's bytes are exact."""
+    import torch
+    import log_synth
+    base = log_synth.build_log(20000, seed=23, max_len=2000, big_every=97)
+    base += bytes(-len(base) % 32768)
+    b_recs, b_reps = lw.read_records(base)
+    assert not b_reps
+    hdrs_b = lw.block_verdicts(base).hdrs
+    at = {h: k for k, h in enumerate(hdrs_b)}
+    tiles = 16
+    img = base * tiles
+    payload_b = []
+    for (off, length, _crc) in b_recs:
+        # a record's fragments: consecutive headers from its first one
+        k = at[off]
+        got, parts = 0, []
+        while got < length:
+            h = hdrs_b[k]
+            n = base[h + 4] | base[h + 5] << 8
+            parts.append(base[h + 7: h + 7 + n])
+            got += n
+            k += 1
+        payload_b.append(b"".join(parts))
+    want_payload = b"".join(payload_b) * tiles
+    buf = torch.from_numpy(np.frombuffer(img, dtype=np.uint8)).to(gpu)
+    rd, records, reports, _, (payload, pos) = lvkv.log_read(buf, gather=True)
+    torch.cuda.synchronize()
+    assert rd["status"] == 0 and not reports
+    assert rd["nrecords"] == len(b_recs) * tiles
+    assert rd["bytes"] == len(want_payload)
+    want_offs = [t * len(base) + r[0] for t in range(tiles) for r in b_recs]
+    assert [r[0] for r in records] == want_offs
+    assert payload[:len(want_payload)].cpu().numpy().tobytes() == want_payload
+    starts = np.cumsum([0] + [len(p) for p in payload_b] * tiles)[:-1]
+    assert np.array_equal(pos.cpu().numpy(), starts)

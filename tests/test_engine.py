@@ -94,15 +94,23 @@ def test_engine_queues_and_profile(oracle, eng, gpu):
     assert eng.profile_read() == []
 
 
-def test_engine_rejects_bad_shapes(lvkv, eng, gpu):
+def test_engine_rejects_bad_arguments(lvkv, eng, gpu):
+    """Null pointers are LVKV_ERR_INVALID; an empty batch is a no-op. (Every
+    block shape is accepted: the burst kernel's 16-row, end-aligned blocks go
+    to it, the rest to the general walk, tests/test_engine_general.py.)"""
+    import ctypes
+
     import torch
     buf = _data(torch, gpu, 1 << 16, 1)
-    with pytest.raises(lvkv.LvkvError):
-        eng.crc32c_uniform(buf, 2, 8192)      # beyond the kernel's 16 rows
-    with pytest.raises(lvkv.LvkvError):
-        eng.crc32c_uniform(buf, 2, 3)         # < 4 bytes
-    with pytest.raises(lvkv.LvkvError):
-        eng.crc32c_uniform(buf[1:], 2, 8, 8)  # end not 4-byte aligned
+    L = lvkv.lib
+    vp = ctypes.c_void_p
+    assert L.lvkv_engine_crc32c_uniform(eng.handle, vp(buf.data_ptr()), 4096, 4096, 0, None,
+                                        2, 0) == -1
+    assert L.lvkv_engine_crc32c_uniform(eng.handle, None, 4096, 4096, 0, vp(buf.data_ptr()),
+                                        2, 0) == -1
+    assert L.lvkv_engine_crc32c_batch(eng.handle, vp(buf.data_ptr()), None, None, None, 0,
+                                      vp(buf.data_ptr()), 2, 0) == -1
+    assert L.lvkv_engine_sst_verify(None, None, None, None, None, None, 1, 0) == -1
     out = eng.crc32c_uniform(buf, 0, 4096)
     assert out.numel() == 0
 
@@ -151,3 +159,78 @@ def test_engine_wait_gives_up_on_a_stuck_queue(lvkv, gpu):
         time.sleep(0.2)
         e._inflight.clear()
         e.close()
+
+
+# ---- config 4 / 5 scale (db_bench_new.cc:782-799 as a
+# batch): the paths behind bench.py's `split` figure, checked block for block
+
+def _oracle_threads():
+    import os
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def test_engine_1m_blocks_overlapped_and_ordered(lvkv, oracle, eng, gpu):
+    """Config 4: ONE submit of 1M x 4 KiB (4.1 GB, ~98 dispatches rotating
+    over the queues), overlapped and then LVKV_FLAG_ORDERED; every block
+    against the oracle. Ordered: all of the batch's dispatches on one queue,
+    one after another (profiled start/end never overlap)."""
+    import torch
+    nb, L = 1_000_000, 4096
+    buf = _data(torch, gpu, nb * L, 0x1EDC6F41 + 4)
+    host = buf.cpu().numpy()
+    want = oracle.uniform(host, nb, L, threads=_oracle_threads())
+    del host
+    _, chains, groups = eng.shape()
+    over = eng.crc32c_uniform(buf, nb, L, fresh=False)
+    eng.wait()
+    assert np.array_equal(over.cpu().numpy().view(np.uint32), want)
+    eng.profile(True)
+    ordered = eng.crc32c_uniform(buf, nb, L, fresh=False, ordered=True)
+    eng.wait()
+    spans = eng.profile_read()
+    eng.profile(False)
+    assert np.array_equal(ordered.cpu().numpy().view(np.uint32), want)
+    assert len(spans) > 1  # several dispatches
+    for (a, b), (c, _) in zip(spans, spans[1:]):
+        assert c >= b - 1e-3, "dispatches of one ordered batch overlapped"
+
+
+def test_engine_config5_slice_as_bench_builds_it(lvkv, oracle, eng, gpu):
+    """Config 5: rank 3 of 8's slice of the 1M-block batch (125,000 blocks
+    at a non-zero start), built by bench.py's own _split_runner (which checks
+    window 0 block for block), then every rotation window stepped through the
+    engine and compared in full."""
+    import torch
+
+    import bench
+    shard = bench._load_shard()
+    start, count = shard.shard_range(bench.SPLIT_TOTAL, 3, 8)
+    assert start > 0 and count == 125_000
+    r = bench._split_runner(torch, lvkv, eng, gpu, 3, start, count)
+    assert r.nrot >= 2
+    for i in range(1, r.nrot + 1):
+        r.step(i)
+        r.finish()
+        r.sync()
+        w = i % r.nrot
+        host = r.buf[w * count * 4096:(w + 1) * count * 4096].cpu().numpy()
+        want = oracle.uniform(host, count, 4096, threads=_oracle_threads())
+        got = r.outs_t[i % len(r.outs_t)].cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, want), i
+    del r
+
+
+def test_bench_parity_check_catches_a_wrong_block(lvkv, oracle, gpu):
+    """bench.parity_check compares every block, not a prefix: a wrong CRC at
+    the last block of a slice fails it."""
+    import torch
+
+    import bench
+    nb, L = 50_000, 4096
+    buf = _data(torch, gpu, nb * L, 77)
+    out = lvkv.crc32c_uniform(buf, nb, L)
+    torch.cuda.synchronize()
+    assert bench.parity_check(buf, out, nb, L, L, 0, 0, "test", chunk=8192) == nb
+    out[nb - 1] ^= 1
+    with pytest.raises(SystemExit, match="block 49999"):
+        bench.parity_check(buf, out, nb, L, L, 0, 0, "test", chunk=8192)
