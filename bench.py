@@ -141,8 +141,12 @@ def timed_region(runner, comm: Comm, steps: int, warmup: int, warmup_s: float,
     comm.barrier()
     runner.sync()
     t0 = time.perf_counter()
+    fw = getattr(runner, "final_window", 0)
     for k in range(steps):
-        runner.step(i + k)
+        if k >= steps - fw:
+            runner.step(i + k, final=True)
+        else:
+            runner.step(i + k)
     runner.finish()
     runner.sync()
     elapsed = time.perf_counter() - t0
@@ -191,9 +195,15 @@ class EngineRunner:
         self.nrot = nrot
         self.flags = 0
 
-    def step(self, i):
+    # the last submits before a wait, one per queue, carry LVKV_FLAG_FINAL
+    # (their completion releases the results, so the wait needs no barrier
+    # packets); the engine's default is three queues
+    final_window = 3
+
+    def step(self, i, final=False):
         rc = self.submit(self.h, self.bases[i % self.nrot], self.stride, self.L, 0,
-                         self.outs[i % len(self.outs)], self.nb, self.flags)
+                         self.outs[i % len(self.outs)], self.nb,
+                         self.flags | (8 if final else 0))  # LVKV_FLAG_FINAL
         if rc != 0:
             raise SystemExit(f"bench: lvkv_engine_crc32c_uniform failed ({rc})")
 

@@ -49,6 +49,16 @@ extern "C" {
  * device do not need it. Costs about 2.5 us per submission. */
 #define LVKV_FLAG_SYSTEM_ACQUIRE 4u
 
+/* Engine submits only: a wait will follow soon. The batch's last dispatch
+ * starts after every earlier one of its queue and, when it completes,
+ * releases its results at system scope into a completion signal, so the next
+ * lvkv_engine_wait needs no barrier packet on that queue (the packet
+ * processor's barrier costs several microseconds after the last kernel). Give
+ * it to the last submit on each queue before a wait: with the default three
+ * queues, the last three submits. Any mix is correct; other queues are fenced
+ * as before. Ignored while profiling. */
+#define LVKV_FLAG_FINAL 8u
+
 /* ---- per-call, host CPU: the drop-in for the reference's own symbols ---- */
 
 /* Replaces leveldb::crc32c::Extend (util/crc32c.h:17, util/crc32c.cc:276).

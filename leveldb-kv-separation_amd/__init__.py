@@ -32,6 +32,7 @@ LVKV_ERR_INVALID = -1
 LVKV_FLAG_MASK = 1
 LVKV_FLAG_ORDERED = 2
 LVKV_FLAG_SYSTEM_ACQUIRE = 4
+LVKV_FLAG_FINAL = 8
 
 
 class LvkvError(RuntimeError):
@@ -649,16 +650,17 @@ class Engine:
 
     def crc32c_uniform(self, buf, nblocks: int, length: int, stride: Optional[int] = None, *,
                        init: int = 0, mask: bool = False, ordered: bool = False,
-                       fresh: bool = True, out=None):
+                       fresh: bool = True, final: bool = False, out=None):
         """fresh: the input may have been written by a copy engine or the host
-        (LVKV_FLAG_SYSTEM_ACQUIRE); False when a kernel on this device wrote it."""
+        (LVKV_FLAG_SYSTEM_ACQUIRE); False when a kernel on this device wrote it.
+        final: a wait follows (LVKV_FLAG_FINAL)."""
         torch = _torch()
         stride = length if stride is None else stride
         if nblocks and (nblocks - 1) * stride + length > buf.numel():
             raise ValueError("blocks exceed the buffer")
         out = _u32_out(torch, nblocks, buf.device, out)
         flags = ((LVKV_FLAG_MASK if mask else 0) | (LVKV_FLAG_ORDERED if ordered else 0) |
-                 (LVKV_FLAG_SYSTEM_ACQUIRE if fresh else 0))
+                 (LVKV_FLAG_SYSTEM_ACQUIRE if fresh else 0) | (LVKV_FLAG_FINAL if final else 0))
         # the engine does not follow HIP streams: the inputs must be complete
         torch.cuda.current_stream(buf.device).synchronize()
         rc = _lib.lvkv_engine_crc32c_uniform(

@@ -30,8 +30,10 @@
 //     submit's dispatches rotate over queues and run side by side; no
 //     dispatch releases;
 //   * lvkv_engine_wait (and the slot-reuse fence) puts a barrier-AND packet on
-//     every queue in use, acquire and release at system scope: results are
-//     visible to the host, to HIP streams and to copy engines after it.
+//     every queue with dispatches since the last fence, release at system
+//     scope (none on a queue whose last dispatch was LVKV_FLAG_FINAL: that
+//     one released at system scope itself): results are visible to the host,
+//     to HIP streams and to copy engines after it.
 // Engine dispatches are not ordered with HIP streams: synchronise the stream
 // that produced the input before submitting.
 #include <hip/hip_runtime.h>
@@ -216,6 +218,13 @@ struct Engine {
   uint32_t* hdp_flush = nullptr;  // HDP_MEM_FLUSH_CNTL
   hsa_signal_t fence_sig{};       // barrier-AND fences, one decrement per queue
   bool fence_ok = false;
+  // LVKV_FLAG_FINAL dispatches: each carries this completion signal (one
+  // decrement) with a system-scope release, and the next fence needs no
+  // barrier packet on a queue whose last dispatch is one of them
+  hsa_signal_t fin_sig{};
+  bool fin_ok = false;
+  uint64_t q_last[kQueues] = {};   // 1 + index of the queue's last dispatch since the fence
+  uint64_t q_final[kQueues] = {};  // 1 + index of its last FINAL dispatch
 
   uint64_t next = 0;    // dispatches submitted
   uint64_t fenced = 0;  // every dispatch before this index is known complete
@@ -277,6 +286,7 @@ void destroy(Engine* e) {
     if (q) hsa_queue_destroy(q);
   for (uint32_t i = 0; i < e->nprof_sig; ++i) hsa_signal_destroy(e->prof_sig[i]);
   if (e->fence_ok) hsa_signal_destroy(e->fence_sig);
+  if (e->fin_ok) hsa_signal_destroy(e->fin_sig);
   if (e->hold_ok) hsa_signal_destroy(e->hold_sig);
   if (e->kernarg) {
     if (e->kernarg_vram)
@@ -386,6 +396,8 @@ int create(int device, Engine** out) {
   ok = ok && alloc_kernargs(*e);
   ok = ok && hsa_signal_create(0, 0, nullptr, &e->fence_sig) == HSA_STATUS_SUCCESS;
   e->fence_ok = ok;
+  ok = ok && hsa_signal_create(0, 0, nullptr, &e->fin_sig) == HSA_STATUS_SUCCESS;
+  e->fin_ok = ok;
   for (uint32_t i = 0; ok && i < kProfSlots; ++i) {
     ok = hsa_signal_create(0, 0, nullptr, &e->prof_sig[i]) == HSA_STATUS_SUCCESS;
     if (ok) e->nprof_sig = i + 1;
@@ -491,16 +503,24 @@ void collect_profile(Engine& e, uint32_t s) {
   e.prof_pending[s] = false;
 }
 
-// A barrier-AND packet with the barrier bit on every queue in use: each
-// completes after every earlier packet of its queue and releases at system
-// scope (the results visible to the host and to copy engines); then wait for
-// all of them. Caller holds e.mu. LVKV_ERR_HIP if a queue faulted or the
-// device stopped (the wait ends instead of spinning forever).
+// Every dispatch so far complete and its results visible to the host and to
+// copy engines. A queue whose last dispatch since the previous fence was a
+// LVKV_FLAG_FINAL one needs nothing more (that dispatch starts after the
+// queue's earlier ones end and releases at system scope into fin_sig); every
+// other queue with dispatches since then gets a barrier-AND packet with the
+// barrier bit (it completes after every earlier packet of its queue and
+// releases at system scope into fence_sig). Then the host spins on both.
+// Caller holds e.mu. LVKV_ERR_HIP if a queue faulted or the device stopped
+// (the wait ends instead of spinning forever).
 int fence(Engine& e) {
   if (e.queue_error) return LVKV_ERR_HIP;
-  hsa_signal_store_relaxed(e.fence_sig, e.nq);
+  int need = 0;
+  for (int q = 0; q < kQueues; ++q)
+    if (e.q_last[q] != 0 && e.q_final[q] != e.q_last[q]) ++need;
+  hsa_signal_store_relaxed(e.fence_sig, need);
   const int keep = e.cur;
-  for (int q = 0; q < e.nq; ++q) {
+  for (int q = 0; q < kQueues; ++q) {
+    if (e.q_last[q] == 0 || e.q_final[q] == e.q_last[q]) continue;
     e.cur = q;
     uint64_t idx;
     hsa_barrier_and_packet_t* p = static_cast<hsa_barrier_and_packet_t*>(packet_slot(e, &idx));
@@ -521,7 +541,9 @@ int fence(Engine& e) {
     publish(e, p, header, 0, idx);
   }
   e.cur = keep;
-  if (!wait_signal(e, e.fence_sig)) return LVKV_ERR_HIP;
+  if (need && !wait_signal(e, e.fence_sig)) return LVKV_ERR_HIP;
+  if (!wait_signal(e, e.fin_sig)) return LVKV_ERR_HIP;
+  for (int q = 0; q < kQueues; ++q) e.q_last[q] = e.q_final[q] = 0;
   e.fenced = e.next;
   // oldest first: dispatch n used slot n % kProfSlots
   for (uint32_t i = 0; i < kProfSlots; ++i)
@@ -533,13 +555,21 @@ int fence(Engine& e) {
 // are args[0, size); the caller holds e.mu. queue < 0: dispatch n goes to
 // queue n % nq (consecutive dispatches side by side); else that queue.
 int dispatch(Engine& e, const EngineKernel& k, const void* args, size_t size, uint32_t ngroups,
-             bool acquire, bool barrier, bool system_acquire, int queue = -1) {
+             bool acquire, bool barrier, bool system_acquire, int queue = -1,
+             bool final = false) {
   if (e.queue_error) return LVKV_ERR_HIP;
   const uint64_t n = e.next;
   // Kernarg slot n % kSlots was last used by dispatch n - kSlots.
   if (n - e.fenced >= kSlots && fence(e) != LVKV_OK) return LVKV_ERR_HIP;
   e.cur = queue >= 0 ? queue : static_cast<int>(n % static_cast<uint64_t>(e.nq));
   hsa_signal_t done{};
+  // (profiled dispatches carry their own signals: FINAL is ignored then)
+  final = final && !e.profiling;
+  if (final) {
+    hsa_signal_add_relaxed(e.fin_sig, 1);
+    done = e.fin_sig;
+    barrier = true;
+  }
   if (e.profiling) {
     const uint32_t s = static_cast<uint32_t>(n % kProfSlots);
     collect_profile(e, s);
@@ -580,9 +610,11 @@ int dispatch(Engine& e, const EngineKernel& k, const void* args, size_t size, ui
       ((acquire ? (system_acquire ? HSA_FENCE_SCOPE_SYSTEM : e.dispatch_acq)
                  : HSA_FENCE_SCOPE_NONE)
        << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-      (HSA_FENCE_SCOPE_NONE
+      ((final ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_NONE)
        << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
   publish(e, p, header, 1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS, idx);
+  e.q_last[e.cur] = n + 1;
+  if (final) e.q_final[e.cur] = n + 1;
   e.next = n + 1;
   return LVKV_OK;
 }
@@ -626,7 +658,8 @@ int submit_general(Engine& eng, KernelArgs a, size_t nblocks, uint32_t flags) {
     r.lane_cols = e->d_tables + kRowTabDwords + kLaneTabDwords;
     r.ngroups = static_cast<uint32_t>(std::min(max_groups, (n + per_round - 1) / per_round));
     const int rc = dispatch(*e, k, &r, sizeof(r), r.ngroups, /*acquire=*/true,
-                            /*barrier=*/ordered, (flags & LVKV_FLAG_SYSTEM_ACQUIRE) != 0, queue);
+                            /*barrier=*/ordered, (flags & LVKV_FLAG_SYSTEM_ACQUIRE) != 0, queue,
+                            (flags & LVKV_FLAG_FINAL) != 0 && done + n == nblocks);
     if (rc != LVKV_OK) return rc;
     done += n;
   }
@@ -720,7 +753,8 @@ int lvkv_engine_crc32c_uniform(lvkv_engine* eng, const void* d_base, uint64_t st
     // dispatch i > 0 may start before (or during) dispatch 0's acquire on
     // another queue
     const int rc = dispatch(*e, k, &a, sizeof(a), a.ngroups, /*acquire=*/true,
-                            /*barrier=*/ordered, (flags & LVKV_FLAG_SYSTEM_ACQUIRE) != 0, queue);
+                            /*barrier=*/ordered, (flags & LVKV_FLAG_SYSTEM_ACQUIRE) != 0, queue,
+                            (flags & LVKV_FLAG_FINAL) != 0 && i + 1 == nd);
     if (rc != LVKV_OK) return rc;
     done += n;
   }

@@ -234,3 +234,30 @@ def test_bench_parity_check_catches_a_wrong_block(lvkv, oracle, gpu):
     out[nb - 1] ^= 1
     with pytest.raises(SystemExit, match="block 49999"):
         bench.parity_check(buf, out, nb, L, L, 0, 0, "test", chunk=8192)
+
+
+@pytest.mark.parametrize("nq,finals", [(3, 3), (3, 1), (1, 1), (4, 2)])
+def test_engine_final_flag_fence(lvkv, oracle, eng, gpu, nq, finals):
+    """LVKV_FLAG_FINAL on the last `finals` submits before a wait: queues
+    whose last dispatch is FINAL are fenced by its own completion (system
+    release), the others by barrier packets; every result is intact and
+    visible after wait(), for any mix, over several rounds."""
+    import torch
+    nb, L, K = 3000, 4096, 12
+    buf = _data(torch, gpu, 6 * nb * L, 31)
+    host = buf.cpu().numpy()
+    want = [oracle.uniform(host[w * nb * L:(w + 1) * nb * L], nb, L, threads=8) for w in range(6)]
+    assert eng.queues(nq) == nq
+    try:
+        for rnd in range(3):
+            outs = torch.zeros(K, nb, dtype=torch.int32, device=gpu)
+            for k in range(K):
+                w = (k + rnd) % 6
+                eng.crc32c_uniform(buf[w * nb * L:], nb, L, out=outs[k], fresh=False,
+                                   final=k >= K - finals)
+            eng.wait()
+            got = outs.cpu().numpy().view(np.uint32)
+            for k in range(K):
+                assert np.array_equal(got[k], want[(k + rnd) % 6]), (rnd, k)
+    finally:
+        eng.queues(3)
