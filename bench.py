@@ -194,6 +194,9 @@ class EngineRunner:
         self.outs_t = outs
         self.nrot = nrot
         self.flags = 0
+        # the engine does not follow HIP streams: the kernels that wrote the
+        # blocks (torch.randint) must be complete before the first submit
+        torch.cuda.synchronize()
 
     # the last submits before a wait, one per queue, carry LVKV_FLAG_FINAL
     # (their completion releases the results, so the wait needs no barrier
