@@ -416,7 +416,7 @@ int lvkv_log_read_device(const void* d_file, uint64_t file_size, uint64_t* d_hdr
  * stream after it). payload_capacity >= d_read->bytes is needed for every
  * record to be written (file_size always suffices); a fragment that does
  * not fit is skipped. d_record_pos (record_capacity u64, nullable) gets
- * every returned record's offset in d_payload. Three launches, asynchronous. */
+ * every returned record's offset in d_payload. Four launches, asynchronous. */
 int lvkv_log_gather_device(const void* d_file, const uint64_t* d_hdr_offsets, size_t capacity,
                            const lvkv_log_report* d_report, const lvkv_log_record* d_records,
                            size_t record_capacity, const lvkv_log_read_report* d_read,

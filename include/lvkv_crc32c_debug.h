@@ -67,6 +67,12 @@ int lvkv_engine_set_stamps(struct lvkv_engine* engine, uint64_t* d_stamps, uint6
  * up after stuck_seconds without progress (default 60) and returns
  * LVKV_ERR_HIP, after which the engine refuses work. */
 int lvkv_debug_engine_stall(struct lvkv_engine* engine, int stall, double stuck_seconds);
+/* The engine's general-layout kernel for every later submit (A/B timing,
+ * tools/probe/engine_shapes.py): 2 = persistent 8 x 2 x 24, 3 = persistent
+ * 8 x 4 x 8, 4 = one-round 8 x 4 x 17, 5 = one-round 8 x 6 x 8, 6 = pipelined
+ * persistent 8 x 2 x 17, 7 = pipelined persistent 8 x 4 x 8; -1 = chosen by
+ * the batch's layout (the default). */
+int lvkv_debug_engine_ragged_spec(struct lvkv_engine* engine, int spec);
 
 #ifdef __cplusplus
 }

@@ -92,10 +92,17 @@ constexpr KernelSpec kSpecs[] = {
     {"lvkv_ek_uniform_pair.kd", "lvkv_ek_uniform_pair_stamps.kd", 8, 3, 2, kArgsUniform},
     {"lvkv_ek_ragged.kd", nullptr, 8, 2, 2, kArgsRagged},
     {"lvkv_ek_ragged_small.kd", nullptr, 8, 4, 2, kArgsRagged},
+    {"lvkv_ek_ragged_burst.kd", nullptr, 8, 4, 1, kArgsRagged},
+    {"lvkv_ek_ragged_burst_small.kd", nullptr, 8, 6, 1, kArgsRagged},
+    {"lvkv_ek_ragged_pipe.kd", nullptr, 8, 2, 2, kArgsRagged},
+    {"lvkv_ek_ragged_pipe_small.kd", nullptr, 8, 4, 2, kArgsRagged},
 };
 constexpr int kNumSpecs = static_cast<int>(sizeof(kSpecs) / sizeof(kSpecs[0]));
 constexpr int kNumUniformSpecs = 2;  // lvkv_engine_set_variant's choices
-constexpr int kRaggedSpec = 2, kRaggedSmallSpec = 3;
+// general-layout kernels: persistent runs (two workgroups per CU, rounds of
+// 16 / 32 blocks), and one round per dispatch (one workgroup per CU)
+constexpr int kRaggedSpec = 2, kRaggedSmallSpec = 3, kBurstSpec = 4, kBurstSmallSpec = 5;
+constexpr uint32_t kBurstRows = 17, kBurstSmallRows = 8;  // their chunk rows
 static_assert(sizeof(EngineRaggedArgs) <= 256 && sizeof(UniformArgs) <= 256, "kernarg slot");
 
 constexpr size_t args_size(ArgKind k) {
@@ -242,6 +249,7 @@ struct Engine {
   uint32_t* d_tables = nullptr;
   uint32_t zcol[32];
   std::mutex mu;
+  int ragged_spec = -1;     // lvkv_debug_engine_ragged_spec: -1 = by layout
   volatile int queue_error = 0;
   double stuck_s = 60.0;     // a wait gives up after this long without progress
   hsa_signal_t hold_sig{};   // lvkv_debug_engine_stall: queues blocked on it
@@ -621,7 +629,16 @@ int dispatch(Engine& e, const EngineKernel& k, const void* args, size_t size, ui
 
 // A general-layout batch (KernelArgs as the HIP path builds it: offsets or
 // the uniform stride, a mode) through the engine's ragged kernels; the
-// same ordering and acquire rules as the uniform submit.
+// same ordering and acquire rules as the uniform submit. The kernel:
+//   * uniform layouts (the host knows the length): blocks of more than 17
+//     rows (config 3's 32 KiB WAL blocks) the persistent 8 x 2 x 24 walk
+//     (measured 0.76 of 8 TB/s overlapped on 16,384 x 32 KiB), up to 8 rows
+//     the 8 x 6 x 8 burst, else the 8 x 4 x 17 burst;
+//   * descriptor batches: WAL records (log verify / fill) the 8 x 6 x 8 burst,
+//     everything else the 8 x 4 x 17 burst (SST blocks, ~4.1 KiB).
+// A burst kernel's batch is cut into dispatches of one round (cus x 8 x NCH
+// blocks, one workgroup per CU) rotating over the queues like separate
+// batches, so consecutive rounds overlap on the device.
 int submit_general(Engine& eng, KernelArgs a, size_t nblocks, uint32_t flags) {
   Engine* e = &eng;
   if (nblocks == 0) return LVKV_OK;
@@ -633,14 +650,22 @@ int submit_general(Engine& eng, KernelArgs a, size_t nblocks, uint32_t flags) {
   const bool ordered = (flags & LVKV_FLAG_ORDERED) != 0;
   if (ordered && e->nq > 1 && e->fenced != e->next && fence(*e) != LVKV_OK) return LVKV_ERR_HIP;
   const int queue = ordered ? static_cast<int>(e->next % static_cast<uint64_t>(e->nq)) : -1;
-  const int spec = log ? kRaggedSmallSpec : kRaggedSpec;
+  int spec;
+  if (a.offsets == nullptr) {
+    const uint64_t rows = (uint64_t{a.length} + 3u + 255u) / 256u;  // upper bound, any alignment
+    spec = rows > kBurstRows ? kRaggedSpec : rows <= kBurstSmallRows ? kBurstSmallSpec : kBurstSpec;
+  } else {
+    spec = log ? kBurstSmallSpec : kBurstSpec;
+  }
+  if (e->ragged_spec >= 0) spec = e->ragged_spec;
   const EngineKernel& k = e->kern[spec];
   const uint64_t per_round = uint64_t{k.waves} * k.chains;
   const uint64_t max_groups = static_cast<uint64_t>(e->cus) * k.per_cu;
-  // the kernel indexes blocks with u32
-  constexpr uint64_t kMaxPerDispatch = uint64_t{1} << 30;
+  const bool burst = spec == kBurstSpec || spec == kBurstSmallSpec;
+  // the kernel indexes blocks with u32; a burst dispatch holds one round
+  const uint64_t max_per = burst ? max_groups * per_round : uint64_t{1} << 30;
   for (uint64_t done = 0; done < nblocks;) {
-    const uint64_t n = std::min<uint64_t>(nblocks - done, kMaxPerDispatch);
+    const uint64_t n = std::min<uint64_t>(nblocks - done, max_per);
     EngineRaggedArgs r;
     memset(&r, 0, sizeof(r));
     r.k = a;
@@ -1007,6 +1032,15 @@ int lvkv_debug_engine_stall(lvkv_engine* eng, int stall, double stuck_seconds) {
             0, idx);
   }
   e->cur = keep;
+  return LVKV_OK;
+}
+
+int lvkv_debug_engine_ragged_spec(lvkv_engine* eng, int spec) {
+  if (eng == nullptr || spec < -1 || spec >= kNumSpecs || (spec >= 0 && spec < kRaggedSpec))
+    return LVKV_ERR_INVALID;
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  std::lock_guard<std::mutex> lk(e->mu);
+  e->ragged_spec = spec;
   return LVKV_OK;
 }
 

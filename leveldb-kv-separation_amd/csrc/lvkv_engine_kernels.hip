@@ -68,3 +68,36 @@ extern "C" __global__ void __launch_bounds__(512, 2)
   lvkv::ragged_run<8, 4, 8>(a.k, a.zpow, a.lane_cols, lds, blockIdx.x, a.ngroups, a.k.nblocks,
                             false);
 }
+
+// One round per workgroup, one workgroup per CU per dispatch (the engine cuts
+// a batch into dispatches of cus x 8 x NCH blocks and rotates them over its
+// queues, so the next dispatch's workgroup runs beside this one, as the
+// uniform burst kernel's): every chain's rows are requested before any walk.
+// 8 waves x 4 chains x 17 rows (SST blocks up to 4352 B in one chunk) and
+// 8 x 6 x 8 (records up to 2 KiB: WAL records, small values).
+extern "C" __global__ void __launch_bounds__(512, 2)
+    lvkv_ek_ragged_burst(lvkv::EngineRaggedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::RagLds<8>::kDwords];
+  lvkv::ragged_run<8, 4, 17>(a.k, a.zpow, a.lane_cols, lds, blockIdx.x, a.ngroups, a.k.nblocks,
+                             false);
+}
+extern "C" __global__ void __launch_bounds__(512, 2)
+    lvkv_ek_ragged_burst_small(lvkv::EngineRaggedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::RagLds<8>::kDwords];
+  lvkv::ragged_run<8, 6, 8>(a.k, a.zpow, a.lane_cols, lds, blockIdx.x, a.ngroups, a.k.nblocks,
+                            false);
+}
+
+// The persistent walk software-pipelined (ragged_pipe: the next chunk's rows
+// in flight while one is walked), two workgroups per CU: 8 waves x 2 chains x
+// 17 rows, and 8 x 4 x 8 for small records.
+extern "C" __global__ void __launch_bounds__(512, 2)
+    lvkv_ek_ragged_pipe(lvkv::EngineRaggedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::RagLds<8>::kDwords];
+  lvkv::ragged_pipe<8, 2, 17>(a.k, a.zpow, a.lane_cols, lds, blockIdx.x, a.ngroups, a.k.nblocks);
+}
+extern "C" __global__ void __launch_bounds__(512, 2)
+    lvkv_ek_ragged_pipe_small(lvkv::EngineRaggedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::RagLds<8>::kDwords];
+  lvkv::ragged_pipe<8, 4, 8>(a.k, a.zpow, a.lane_cols, lds, blockIdx.x, a.ngroups, a.k.nblocks);
+}

@@ -699,17 +699,19 @@ __global__ void __launch_bounds__(kGT) log_asm_emit(AsmArgs a) {
 //
 // ReadRecord hands back each record as one buffer (scratch->assign/append,
 // *record = Slice(*scratch), db/log_reader.cc:92-137). Here every record is
-// written end to end into one output: physical candidate j belongs to a
-// returned record iff the last record whose first fragment is <= j also
-// spans j (records are in order and their fragments disjoint, a binary
-// search over their `first`); its payload goes to dest[j] = the payloads of
-// the returned fragments before it (a scan over candidates), so record i
-// starts at dest[first_i]. Three launches: each candidate's owner and
-// length (1024 candidates a workgroup) with the workgroup's sum; the places
-// (each workgroup folds the sums before it, 64 per wave step, and scans its
-// own); the copies, one wave per candidate. (With the scan across
+// written end to end into one output: physical candidate j belongs to
+// returned record i iff first_i <= j < first_i + nfrags_i (records are in
+// order and their fragments disjoint); its payload goes to dest[j] = the
+// payloads of the returned fragments before it (a scan over candidates), so
+// record i starts at dest[first_i]. Four launches: each record marks its
+// fragments with its index (tagged with the call, so nothing is cleared);
+// each candidate's owner and length (1024 candidates a workgroup) with the
+// workgroup's sum; the places (each workgroup folds the sums before it, 64
+// per wave step, and scans its own); the copies. (A binary search over the
+// records' `first` per thread, the round-3 owner launch, took 12.7 us on
+// the 62k-record log: 16 dependent loads a thread. With the scan across
 // workgroups as a decoupled look-back in one launch, the first two took
-// 22-28 us on the 62k-record log: waits on other XCDs' flags.)
+// 22-28 us: waits on other XCDs' flags.)
 
 constexpr uint32_t kGatherT = 256, kGatherItems = 4, kGatherPer = kGatherT * kGatherItems;
 
@@ -730,9 +732,11 @@ struct GatherArgs {
   uint64_t out_cap;
   uint64_t* rec_pos;      // nullable
   struct LookSlot* look;  // per workgroup
-  ulonglong2* dst;  // per candidate: {its owner record (launch 1), then its payload's
-                   //  place in `out` (launch 2); ~0: not returned,
-                   //  payload file offset | length << 48}
+  ulonglong2* dst;  // per candidate: .x = {the marking record, tagged (launch 1); its owner
+                    //  (launch 2), then its payload's place in `out` (launch 3); ~0: not
+                    //  returned}, .y = payload file offset | length << 48
+  uint32_t tag;     // this call's mark tag: bit 31 set, bit 30 clear (never ~0's high
+                    //  word nor a place's, < 2^14)
 };
 
 // The u16 at p (any alignment) from the aligned dword(s) holding it: no
@@ -746,43 +750,55 @@ __device__ __forceinline__ uint32_t ld_u16_any(const uint8_t* p) {
   return __builtin_amdgcn_alignbyte(hi, lo, sh) & 0xffffu;
 }
 
-// Index of the last record whose first fragment is <= j (or -1).
-__device__ __forceinline__ int32_t owner_of(const lvkv_log_record* recs, uint32_t n, uint32_t j) {
-  uint32_t lo = 0, hi = n;  // first record with first > j
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (recs[mid].first <= j) lo = mid + 1; else hi = mid;
-  }
-  return static_cast<int32_t>(lo) - 1;
+// Launch 1: record i marks its fragments' entries with (tag << 32) | i.
+__global__ void __launch_bounds__(256) log_gather_mark_kernel(GatherArgs a) {
+  const uint32_t N = a.phys->status == LVKV_OK ? min(a.phys->count_, a.cap) : 0u;
+  const uint32_t R = a.phys->status == LVKV_OK ? min(a.read->nrecords, a.rec_cap) : 0u;
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= R) return;
+  const lvkv_log_record r = a.recs[i];
+  const unsigned long long m = (static_cast<unsigned long long>(a.tag) << 32) | i;
+  const uint32_t end = static_cast<uint32_t>(min<uint64_t>(N, uint64_t{r.first} + r.nfrags));
+  for (uint32_t f = r.first; f < end; ++f) a.dst[f].x = m;
 }
 
-// Launch 1: each candidate's owner record and payload length into dst, and
-// the workgroup's sum of owned lengths. A thread's four candidates are
-// consecutive: one binary search, then forward steps.
+// Launch 2: each candidate's owner record (its mark, if this call's) and
+// payload length into dst, and the workgroup's sum of owned lengths.
 __global__ void __launch_bounds__(kGatherT) log_gather_own_kernel(GatherArgs a) {
   __shared__ unsigned long long wsum[kGatherT / 64];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u, wave = tid >> 6;
   const uint32_t N = a.phys->status == LVKV_OK ? min(a.phys->count_, a.cap) : 0u;
-  const uint32_t R = a.phys->status == LVKV_OK ? min(a.read->nrecords, a.rec_cap) : 0u;
   const uint32_t g = blockIdx.x;
   if (g * kGatherPer >= N) return;
   const uint32_t j0 = g * kGatherPer + tid * kGatherItems;
   uint64_t mine = 0;
-  int32_t i = j0 < N && R != 0 ? owner_of(a.recs, R, j0) : -1;
+  unsigned long long mk[kGatherItems];
+  uint64_t ho[kGatherItems];
+#pragma unroll
+  for (uint32_t t = 0; t < kGatherItems; ++t) {
+    const uint32_t j = j0 + t;
+    mk[t] = j < N ? a.dst[j].x : ~0ull;
+    ho[t] = j < N ? a.hdr_off[j] : 0;
+  }
+  const uint32_t R = a.phys->status == LVKV_OK ? min(a.read->nrecords, a.rec_cap) : 0u;
 #pragma unroll
   for (uint32_t t = 0; t < kGatherItems; ++t) {
     const uint32_t j = j0 + t;
     if (j >= N) break;
-    while (static_cast<uint32_t>(i + 1) < R && a.recs[i + 1].first <= j) ++i;
-    uint32_t len = 0;
-    bool owned = false;
-    if (i >= 0 && j < a.recs[i].first + a.recs[i].nfrags) {
-      len = ld_u16_any(a.file + a.hdr_off[j] + 4);
-      owned = true;
+    // this call's mark, naming a record that spans j: the tag alone could be
+    // matched by stale scratch bytes (the buffer is pooled with other
+    // calls'), the span check cannot (fragments of returned records are
+    // disjoint, and every fragment of one was marked by it)
+    const uint32_t i = static_cast<uint32_t>(mk[t]);
+    bool owned = static_cast<uint32_t>(mk[t] >> 32) == a.tag && i < R;
+    if (owned) {
+      const lvkv_log_record r = a.recs[i];
+      owned = r.first <= j && j - r.first < r.nfrags;
     }
-    a.dst[j] = make_ulonglong2(owned ? static_cast<unsigned long long>(i) : ~0ull,
-                               (a.hdr_off[j] + 7) | (uint64_t{len} << 48));
+    const uint32_t len = owned ? ld_u16_any(a.file + ho[t] + 4) : 0u;
+    a.dst[j] = make_ulonglong2(owned ? (mk[t] & 0xffffffffull) : ~0ull,
+                               (ho[t] + 7) | (uint64_t{len} << 48));
     mine += len;
   }
   const uint64_t w = wave_sum64(mine);
@@ -796,7 +812,7 @@ __global__ void __launch_bounds__(kGatherT) log_gather_own_kernel(GatherArgs a) 
   }
 }
 
-// Launch 2: the places. Wave 0 sums the workgroups before this one while
+// Launch 3: the places. Wave 0 sums the workgroups before this one while
 // every thread reads its candidates' lengths; a workgroup scan; dst[j].x
 // becomes the payload's place (~0: not returned), and each record's first
 // fragment gives its position.
@@ -1020,9 +1036,10 @@ hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
   return hipGetLastError();
 }
 
-// lvkv_log_gather_device: three launches; `look`: 16 bytes per workgroup of
-// ceil(capacity / 1024), then 16 bytes per candidate (any contents); `tag`
-// is unused (the launches exchange through kernel boundaries).
+// lvkv_log_gather_device: four launches; `look`: 16 bytes per workgroup of
+// ceil(capacity / 1024), then 16 bytes per candidate (any contents: the
+// marks carry `tag`, a per-call value, so stale entries are never taken for
+// this call's).
 size_t log_gather_scratch_bytes(size_t capacity) {
   return ((capacity + kGatherPer - 1) / kGatherPer) * sizeof(LookSlot) + capacity * 16;
 }
@@ -1040,16 +1057,19 @@ hipError_t launch_log_gather(const uint8_t* file, const uint64_t* hdr_off, size_
   a.read = read;
   a.rec_cap = rec_cap;
   a.cap = static_cast<uint32_t>(capacity);
-  (void)tag;
   a.out = out;
   a.out_cap = out_cap;
   a.rec_pos = rec_pos;
   a.look = static_cast<LookSlot*>(look);
+  a.tag = (tag & 0x3fffffffu) | 0x80000000u;
   const uint32_t groups = static_cast<uint32_t>((capacity + kGatherPer - 1) / kGatherPer);
   a.dst = reinterpret_cast<ulonglong2*>(a.look + groups);
-  hipLaunchKernelGGL(log_gather_own_kernel, dim3(groups), dim3(kGatherT), 0, stream, a);
+  hipLaunchKernelGGL(log_gather_mark_kernel, dim3(std::max(1u, (rec_cap + 255u) / 256u)),
+                     dim3(256), 0, stream, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(log_gather_own_kernel, dim3(groups), dim3(kGatherT), 0, stream, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(log_gather_kernel, dim3(groups), dim3(kGatherT), 0, stream, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // the copy: a bounded grid (8 workgroups of 4 waves per CU), grid-stride

@@ -48,9 +48,12 @@ def main():
     sub, h = eng.submit_ptr, eng.handle
     rot = [0]
 
-    def step(n=nb):
+    fin = [0]
+
+    def step(n=nb, final=False):
         rot[0] += 1
-        sub(h, buf.data_ptr() + (rot[0] % nrot) * win, Lb, Lb, 0, out.data_ptr(), n, 0)
+        sub(h, buf.data_ptr() + (rot[0] % nrot) * win, Lb, Lb, 0, out.data_ptr(), n,
+            8 if (final and fin[0]) else 0)  # LVKV_FLAG_FINAL on the last submit per queue
 
     res = {}
     lvkv.lib.lvkv_engine_set_scopes.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
@@ -61,7 +64,9 @@ def main():
     for sc in scopes:
         assert lvkv.lib.lvkv_engine_set_priority(h, sc[3] if len(sc) > 3 else 1) == 0
         assert lvkv.lib.lvkv_engine_set_scopes(h, *sc[:3]) == 0
-        res[f"scopes_{sc}"] = run_set(eng, step, sc)
+        for f in (0, 1):
+            fin[0] = f
+            res[f"scopes_{sc}_final{f}"] = run_set(eng, step, (sc, f"final={f}"))
     (REPO / "gpurun_out").mkdir(exist_ok=True)
     (REPO / "gpurun_out" / "edges.json").write_text(json.dumps(res, indent=1))
 
@@ -97,8 +102,8 @@ def run_set(eng, step, sc):
             eng.profile(True)
             torch.cuda.synchronize()
             t0 = now_us()
-            for _ in range(K):
-                step()
+            for k in range(K):
+                step(final=k >= K - 3)
             t_sub = now_us()
             eng.wait()
             t_wait = now_us()
@@ -123,8 +128,8 @@ def run_set(eng, step, sc):
             eng.wait()
             torch.cuda.synchronize()
             t0 = now_us()
-            for _ in range(K):
-                step()
+            for k in range(K):
+                step(final=k >= K - 3)
             eng.wait()
             torch.cuda.synchronize()
             ts.append((now_us() - t0) / K)
