@@ -23,7 +23,32 @@ __global__ void __launch_bounds__(64 * W, 2)
   ragged_run<W, NCH, R>(a, zpow, lane_cols, lds, blockIdx.x, gridDim.x, total, false);
 }
 
+// The software-pipelined walk (ragged_pipe: a chunk's rows in flight while
+// the previous one is walked), two workgroups per CU; the block count may
+// come from the device (a.count, written by an earlier launch).
+template <int W, int NCH, int R>
+__global__ void __launch_bounds__(64 * W, 2)
+    crc32c_ragged_pipe_kernel(KernelArgs a, const uint32_t* zpow, const uint32_t* lane_cols) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[RagLds<W>::kDwords];
+  const uint32_t total = a.count != nullptr ? min(a.nblocks, sload_u32(a.count, 0)) : a.nblocks;
+  ragged_pipe<W, NCH, R>(a, zpow, lane_cols, lds, blockIdx.x, gridDim.x, total);
+}
+
 }  // namespace
+
+// small: 8 waves x 4 chains x 8 rows (records up to 2 KiB: WAL records),
+// else 8 x 2 x 17 (SST-sized blocks).
+hipError_t launch_crc32c_ragged_pipe(const KernelArgs& a, const uint32_t* zpow,
+                                     const uint32_t* lane_cols, bool small, int num_groups,
+                                     hipStream_t stream) {
+  if (small)
+    hipLaunchKernelGGL((crc32c_ragged_pipe_kernel<8, 4, 8>), dim3(num_groups), dim3(512), 0,
+                       stream, a, zpow, lane_cols);
+  else
+    hipLaunchKernelGGL((crc32c_ragged_pipe_kernel<8, 2, 17>), dim3(num_groups), dim3(512), 0,
+                       stream, a, zpow, lane_cols);
+  return hipGetLastError();
+}
 
 // cfg: shape = cfg & 3, or cfg >> 3 for the small-record shapes (1: 8 waves
 // x 4 chains x 8 rows; 2: 8 x 6 x 8; 3: 8 x 8 x 4); the large-record shapes

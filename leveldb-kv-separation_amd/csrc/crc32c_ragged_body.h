@@ -110,12 +110,12 @@ __device__ __forceinline__ RagBlock rag_block(const KernelArgs& a, uint32_t b, b
   const uint64_t base = reinterpret_cast<uint64_t>(a.base);
   uint64_t off;
   uint32_t len, init = a.init, expected = 0;
-  if (a.mode == kModeLogVerify || a.mode == kModeLogFill) {
+  if (a.mode == kModeLogVerify || a.mode == kModeLogFill || a.mode == kModeLogStaged) {
     // [masked crc u32][len u16][type u8]; the CRC covers type + payload
     // (db/log_reader.cc:217-221, 243-247).
     const uint64_t hoff = desc_u64(a, b);
     const uint32_t len_type = sload_le(base + hoff + 4, 3);
-    if (a.mode == kModeLogVerify) expected = crc_unmask(sload_le(base + hoff, 4));
+    if (a.mode != kModeLogFill) expected = crc_unmask(sload_le(base + hoff, 4));
     off = hoff + 6;
     len = 1u + (len_type & 0xffffu);
     init = 0;
@@ -224,6 +224,11 @@ __device__ __forceinline__ void rag_store(const KernelArgs& a, uint32_t b, const
   } else {
     a.out_crc[b] = crc;
     if (a.out_status != nullptr) a.out_status[b] = crc != g.expected ? 1 : 0;
+    if (a.mode == kModeLogStaged && crc != g.expected) {
+      // the block's first mismatch (its records are staged in file order)
+      const uint64_t hoff = g.ptr() - 6u - reinterpret_cast<uint64_t>(a.base);
+      atomicMin(a.log_first_bad + (hoff >> 15), b);
+    }
   }
 }
 
@@ -323,7 +328,7 @@ __device__ __forceinline__ void ragged_long_pass(const KernelArgs& a, const uint
   __syncthreads();
   if (lds[kFlag] == 0) return;
   const bool sst = a.mode == kModeSstVerify || a.mode == kModeSstFill || a.mode == kModeSstTable;
-  const bool log = a.mode == kModeLogVerify || a.mode == kModeLogFill;
+  const bool log = a.mode == kModeLogVerify || a.mode == kModeLogFill || a.mode == kModeLogStaged;
   for (uint32_t slice = 0; slice < n; slice += 64 * W) {
     if (tid == 0) lds[kCount] = 0;
     __syncthreads();

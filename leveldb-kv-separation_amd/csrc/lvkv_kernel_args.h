@@ -62,6 +62,10 @@ enum : uint32_t {
   kModeSstTable = 5,   // kModeSstVerify whose store also merges the index
                        // parse status (out_status in), the type byte and
                        // the per-table totals (sst_reports)
+  kModeLogStaged = 6,  // kModeLogVerify over the WAL walk's staged headers
+                       // (lvkv_log_blocks.hip): out_crc, out_status (1 =
+                       // mismatch), and on a mismatch the lowest staged
+                       // index per 32 KiB block into log_first_bad[hdr >> 15]
 };
 
 struct KernelArgs {
@@ -99,6 +103,7 @@ struct KernelArgs {
                               //   block counts per workgroup
   uint32_t fresh_desc;        // 1: offsets/lengths were written by this same
                               //   launch (vector loads after an acquire)
+  uint32_t* log_first_bad;    // kModeLogStaged: per 32 KiB block (atomicMin)
   int32_t general_cfg;        // host side: kernel of general-layout batches
   int32_t log_cfg;            //   and of WAL records (launch_crc32c_general);
                               //   the device context's choice, never read

@@ -22,14 +22,18 @@ if want bench; then
   cat gpurun_out/bench_k20.json
 fi
 if want logprof; then
-  rm -rf gpurun_out/r04_logread_prof
-  timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r04_logread_prof -o run -- python3 tools/probe/log_probe.py 60000 --read > gpurun_out/r04_logread_prof.log 2>&1 \
-    || { echo "log prof failed"; tail -20 gpurun_out/r04_logread_prof.log; exit 1; }
-  grep -v amdgpu.ids gpurun_out/r04_logread_prof.log | tail -4
-  python3 -c "
-import csv,glob
-for f in glob.glob('gpurun_out/r04_logread_prof/**/run_kernel_stats.csv', recursive=True):
+  for P in ${LOGPATHS:-0 1}; do
+    D=gpurun_out/r04_logread_prof_p$P
+    rm -rf $D
+    timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 tools/probe/log_probe.py 60000 --read --path=$P > $D.log 2>&1 \
+      || { echo "log prof failed"; tail -20 $D.log; exit 1; }
+    grep -v amdgpu.ids $D.log | grep "log_" | tail -4
+    python3 -c "
+import csv,glob,sys
+for f in glob.glob(sys.argv[1] + '/**/run_kernel_stats.csv', recursive=True):
     for r in csv.DictReader(open(f)):
-        print(r['Name'].split('(')[0][-40:], r['Calls'], r['AverageNs'], r['MinNs'], r['MaxNs'])
-"
+        n = r['Name'].split('(')[0] if '(anonymous' not in r['Name'] else r['Name'].split('::')[2].split('(')[0]
+        print('  ', n[-44:], r['Calls'], r['AverageNs'], r['MinNs'], r['MaxNs'])
+" $D
+  done
 fi
