@@ -25,7 +25,8 @@ uint32_t lvkv_debug_extend_portable(uint32_t crc, const uint8_t* data, size_t n)
 
 /* Kernel choices of the current device (per device, not process globals;
  * timing and A/B tests): general-layout batches (-1 crc32c_kernel.hip's
- * persistent kernel, 0..31 ragged cfgs), WAL records (ragged cfg), and the
+ * persistent kernel, 0..31 ragged cfgs, 32 / 33 the pipelined walk 8 x 2 x 17 /
+ * 8 x 4 x 8), WAL records (ragged cfg), and the
  * whole-SSTable verify form (0 by size, 1 one fused launch, 2 two launches). */
 int lvkv_debug_set_general_kernel(int cfg);
 int lvkv_debug_set_log_kernel(int cfg);

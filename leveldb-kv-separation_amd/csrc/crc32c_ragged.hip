@@ -118,6 +118,13 @@ hipError_t launch_crc32c_general(const KernelArgs& a, int cus, hipStream_t strea
                              b.row_tab + kRowTabDwords + kLaneTabDwords, cus, stream);
     return e;
   }
+  if (cfg >= 32) {  // the pipelined walk: 32 = 8 x 2 x 17, 33 = 8 x 4 x 8
+    const uint32_t per = cfg == 33 ? 32u : 16u;
+    const uint32_t groups = min(2u * static_cast<uint32_t>(cus), (n + per - 1) / per);
+    return launch_crc32c_ragged_pipe(a, a.row_tab + kZPowOffset,
+                                     a.row_tab + kRowTabDwords + kLaneTabDwords, cfg == 33,
+                                     static_cast<int>(max(1u, groups)), stream);
+  }
   const uint32_t per = static_cast<uint32_t>(ragged_blocks_per_round(cfg));
   const uint32_t rounds1 = (n + per - 1) / per;
   const uint32_t groups =
