@@ -372,8 +372,7 @@ __device__ __forceinline__ void ragged_run(const KernelArgs& a, const uint32_t* 
                                            const uint32_t* lane_cols, uint32_t* lds,
                                            uint32_t grp, uint32_t G, uint32_t total,
                                            bool image_ready) {
-  constexpr uint32_t kAcc = RagLds<W>::kAcc, kFlag = RagLds<W>::kFlag,
-                     kList = RagLds<W>::kList, kCount = RagLds<W>::kCount;
+  constexpr uint32_t kFlag = RagLds<W>::kFlag;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = lane_id();
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);

@@ -306,6 +306,22 @@ __device__ __forceinline__ void event_counts(uint32_t ev, uint32_t (&cnt)[kScena
   }
 }
 
+// One event's returned bytes for each entering scenario (step()'s records):
+// a FULL record its payload in any live state, a LAST its payload plus the
+// open fragment's bytes (`uses`) when the reader is in a fragment.
+__device__ __forceinline__ void event_bytes(uint32_t ev, uint32_t (&eb)[kScenarios],
+                                            uint32_t (&eu)[kScenarios]) {
+  const uint32_t kind = ev & 15u, type = (ev >> 8) & 255u, n = ev >> 16;
+  const bool rec = kind == kEvRec;
+#pragma unroll
+  for (uint32_t sc = 0; sc < kScenarios; ++sc) {
+    const bool in = sc == kScFrag || sc == kScEmpty;
+    const bool full = rec && type == 1, last = rec && type == 4 && in;
+    eb[sc] = (full || last) ? n : 0u;
+    eu[sc] = last ? 1u : 0u;
+  }
+}
+
 // A run of events (a chunk, a workgroup, a run of workgroups) as a map of
 // the reader's state: its composed summary and its record / report counts
 // for each state the reader may enter it in. Runs of them compose
@@ -313,6 +329,11 @@ __device__ __forceinline__ void event_counts(uint32_t ev, uint32_t (&cnt)[kScena
 struct Agg {
   Summ s;
   uint32_t nrec[kScenarios], nrep[kScenarios];
+  // bytes of the records the run returns, entered in each scenario with an
+  // empty fragment; uses[sc]: a LAST before the run's first reset also
+  // returns the entering fragment's bytes (add them when they are not 0)
+  unsigned long long nbytes[kScenarios];
+  uint32_t uses[kScenarios];
 };
 
 struct AsmArgs {
@@ -325,8 +346,6 @@ struct AsmArgs {
   uint32_t init_st; // the reader's first state: kIdle, or kResync with an offset
   Seek seek;
   uint32_t* lohi;   // log_asm_seek's output (seek.lohi)
-  uint32_t* done;   // workgroups finished (left at 0 by the last one)
-  unsigned long long* wg_bytes;  // per workgroup: its records' bytes
   lvkv_log_record* recs;
   lvkv_log_corruption* reps;
   lvkv_log_read_report* out;
@@ -383,16 +402,21 @@ __global__ void __launch_bounds__(64) log_asm_seek(AsmArgs a) {
 __device__ __forceinline__ Agg agg_compose(const Agg& x, const Agg& y) {
   Agg r;
   r.s = compose(x.s, y.s);
+  // the fragment bytes y is entered with, beyond x's entering ones
+  const uint64_t carried = x.s.pass ? x.s.len : (x.s.c == kInFrag ? x.s.scratch : 0u);
 #pragma unroll
   for (uint32_t sc = 0; sc < kScenarios; ++sc) {
     const uint32_t after = chunk_scenario(sc, x.s);  // kScStopped: pick gives 0
     r.nrec[sc] = x.nrec[sc] + pick(y.nrec, after);
     r.nrep[sc] = x.nrep[sc] + pick(y.nrep, after);
+    const uint32_t yu = pick(y.uses, after);
+    r.nbytes[sc] = x.nbytes[sc] + pick(y.nbytes, after) + (yu ? carried : 0u);
+    r.uses[sc] = x.uses[sc] | (x.s.pass ? yu : 0u);
   }
   return r;
 }
 
-constexpr Agg kAggIdentity = {kIdentity, {0, 0, 0, 0}, {0, 0, 0, 0}};
+constexpr Agg kAggIdentity = {kIdentity, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
 
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 #pragma unroll
@@ -438,38 +462,30 @@ __device__ __forceinline__ Agg window_fold(const Agg& A, uint32_t lane) {
   const uint64_t between = Lm & below & ~((uint64_t{2} << rl) - 1u);  // lanes in (rl, l)
   const uint32_t fixed = (Sm & below) ? kScStopped : scenario(rc, rs | (between ? 1u : 0u));
   const bool len_below = (Lm & below) != 0;
+  // MIDDLE bytes of the lanes below l (exclusive scan), and those after the
+  // last reset below l: the fragment bytes lane l is entered with, beyond
+  // the window's own
+  uint64_t incl = A.s.pass ? A.s.len : 0u;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint64_t o = __shfl_up(static_cast<unsigned long long>(incl), d, 64);
+    if (lane >= d) incl += o;
+  }
+  const uint64_t excl = incl - (A.s.pass ? A.s.len : 0u);
+  const uint64_t at_r = __shfl(static_cast<unsigned long long>(incl), rl, 64);
+  const uint64_t carried = rb ? (rc == kInFrag ? rs + (excl - at_r) : 0u) : excl;
 #pragma unroll
   for (uint32_t sw = 0; sw < kScenarios; ++sw) {
     const uint32_t sc = rb ? fixed : (sw == kScEmpty && len_below ? kScFrag : sw);
     const uint64_t t = wave_sum64(pick(A.nrec, sc) | (uint64_t{pick(A.nrep, sc)} << 32));
     r.nrec[sw] = static_cast<uint32_t>(t);
     r.nrep[sw] = static_cast<uint32_t>(t >> 32);
+    const uint32_t u = pick(A.uses, sc);
+    r.nbytes[sw] = wave_sum64(pick(A.nbytes, sc) + (u ? carried : 0u));
+    r.uses[sw] = __ballot(!rb && u) ? 1u : 0u;
   }
   return r;
 }
-
-// Counters shared by every workgroup of a launch move as agent-scope atomic
-// read-modify-writes (a fetch-add of 0 reads, an exchange writes): those are
-// performed at the device's coherence point, past every XCD's L2, so no L2
-// writeback or invalidate is needed.
-template <typename T>
-__device__ __forceinline__ T co_ld(const T* p) {
-  // a zero the compiler cannot see: an atomic add of a known 0 is folded
-  // into a plain load
-  uint32_t z;
-  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-  return __hip_atomic_fetch_add(const_cast<T*>(p), static_cast<T>(z), __ATOMIC_RELAXED,
-                                __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename T>
-__device__ __forceinline__ void co_st(T* p, T v) {
-  (void)__hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// Every earlier memory operation of the wave has completed (and the compiler
-// moves none across).
-__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-
 
 // The items of workgroup g: the event of each thread's item, its counts
 // for each entering scenario, its summary's exclusive scan in the workgroup
@@ -549,31 +565,48 @@ __device__ __forceinline__ void wg_items(const AsmArgs& a, uint32_t K, uint32_t 
   it.agg.s = tot;
   it.x = compose(pre, xw);
   // output positions for each entering scenario: per item at most one
-  // record and two reports, so the wave's prefix counts are ballots
-  uint32_t cnt[kScenarios];
+  // record and two reports, so the wave's prefix counts are ballots; and the
+  // returned bytes (Agg::nbytes / uses)
+  __shared__ unsigned long long wbytes[kGT / 64][kScenarios];
+  __shared__ uint32_t wuses[kGT / 64][kScenarios];
+  uint32_t cnt[kScenarios], eb[kScenarios], eu[kScenarios];
   event_counts(it.ev, cnt);
+  event_bytes(it.ev, eb, eu);
+  const uint64_t carried = it.x.pass ? it.x.len : (it.x.c == kInFrag ? it.x.scratch : 0u);
 #pragma unroll
   for (uint32_t sw = 0; sw < kScenarios; ++sw) {
-    const uint32_t c = pick(cnt, chunk_scenario(sw, it.x));
+    const uint32_t isc = chunk_scenario(sw, it.x);
+    const uint32_t c = pick(cnt, isc);
     const uint64_t br = __ballot(c & 1u), b0 = __ballot((c >> 16) & 1u), b1 = __ballot((c >> 17) & 1u);
     it.v[sw] = static_cast<uint32_t>(__popcll(br & below)) |
                static_cast<uint32_t>(__popcll(b0 & below) + 2 * __popcll(b1 & below)) << 16;
-    if (lane == 0)
+    const uint32_t u = pick(eu, isc);
+    const uint64_t nb = wave_sum64(pick(eb, isc) + (u ? carried : 0u));
+    const uint64_t bu = __ballot(it.x.pass && u);
+    if (lane == 0) {
       wsum[w][sw] = static_cast<uint32_t>(__popcll(br)) |
                     static_cast<uint32_t>(__popcll(b0) + 2 * __popcll(b1)) << 16;
+      wbytes[w][sw] = nb;
+      wuses[w][sw] = bu ? 1u : 0u;
+    }
   }
   __syncthreads();
 #pragma unroll
   for (uint32_t sw = 0; sw < kScenarios; ++sw) {
-    uint32_t before = 0, all = 0;
+    uint32_t before = 0, all = 0, uses = 0;
+    unsigned long long bytes = 0;
 #pragma unroll
     for (uint32_t v = 0; v < kGT / 64; ++v) {
       before += v < w ? wsum[v][sw] : 0u;
       all += wsum[v][sw];
+      bytes += wbytes[v][sw];
+      uses |= wuses[v][sw];
     }
     it.v[sw] += before;
     it.agg.nrec[sw] = all & 0xffffu;
     it.agg.nrep[sw] = all >> 16;
+    it.agg.nbytes[sw] = bytes;
+    it.agg.uses[sw] = uses;
   }
 }
 
@@ -597,15 +630,14 @@ __global__ void __launch_bounds__(kGT) log_asm_reduce(AsmArgs a) {
 // workgroups before this one (64 at a time, window_fold; each wave a
 // contiguous share) into its entering state and output positions, and the
 // items are rescanned; then each item goes
-// through step() once. Workgroup G - 1 writes the report's counts; the last
-// workgroup to finish (a completion counter it leaves at 0) writes the
-// records' bytes.
+// through step() once. Workgroup G - 1 writes the report: counts and the
+// records' bytes both come from the composed aggregates (Agg::nbytes), so no
+// workgroup waits for or counts the others (round 3's completion counter, one
+// device-scope atomic per workgroup on one address, cost ~5 us).
 __global__ void __launch_bounds__(kGT) log_asm_emit(AsmArgs a) {
   __shared__ Summ wagg[kGT / 64];
   __shared__ uint32_t wsum[kGT / 64][kScenarios];
   __shared__ Agg part_s[kGT / 64];
-  __shared__ unsigned long long wbytes_s[kGT / 64];
-  __shared__ uint32_t last_s;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
   const uint32_t K = asm_items(a);
@@ -657,7 +689,8 @@ __global__ void __launch_bounds__(kGT) log_asm_emit(AsmArgs a) {
   Sink out = {true, 0, 0, 0, a.recs + rb, a.rec_cap > rb ? a.rec_cap - rb : 0u, a.reps + pb,
               a.rep_cap > pb ? a.rep_cap - pb : 0u};
   step<true>(r, ev, j, hoff, out);
-  // the report's counts: the last workgroup's prefix and its own aggregate
+  // the report: the last workgroup's prefix composed with its own aggregate
+  // (counts and returned bytes, from the reader's first state)
   if (g == G - 1 && tid == 0) {
     const Agg tot = agg_compose(p, it.agg);
     const uint32_t r0 = pick(tot.nrec, init_sc), r1 = pick(tot.nrep, init_sc);
@@ -667,32 +700,9 @@ __global__ void __launch_bounds__(kGT) log_asm_emit(AsmArgs a) {
     a.out->nrecords = r0;
     a.out->nreports = r1;
     a.out->stopped = (!tot.s.pass && tot.s.c == kStopped) ? tot.s.stop5 : 0u;
+    a.out->bytes = pick(tot.nbytes, init_sc);
   }
-  // the records' bytes: the workgroup's sum into its slot (a device-scope
-  // exchange: no contended atomic); the last workgroup to finish sums the
-  // slots (one atomic per workgroup on the completion counter)
-  const uint64_t wb = wave_sum64(out.bytes);
-  if (lane == 0) wbytes_s[tid >> 6] = wb;
-  __syncthreads();
-  if (tid == 0) {
-    uint64_t t = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < kGT / 64; ++w) t += wbytes_s[w];
-    co_st(&a.wg_bytes[g], static_cast<unsigned long long>(t));
-    asm_stamp(a, 5);
-    vm_drain();  // the slot's exchange has landed
-    const uint32_t n = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last_s = n == G - 1 ? 1u : 0u;
-  }
-  __syncthreads();
-  if (!last_s || tid >= 64) return;
-  uint64_t t = 0;
-  for (uint32_t i = lane; i < G; i += 64) t += co_ld(&a.wg_bytes[i]);
-  t = wave_sum64(t);
-  if (lane == 0) {
-    a.out->bytes = t;
-    co_st(a.done, 0u);  // the next call with this scratch reuses the counter
-  }
+  if (tid == 0) asm_stamp(a, 5);
 }
 
 // ---- the records' bytes ---------------------------------------------------
@@ -981,7 +991,7 @@ uint64_t* g_asm_stamps = nullptr;  // lvkv_debug_asm_stamps
 
 size_t log_asm_scratch_bytes(size_t max_items) {
   const size_t groups = (max_items + kGT - 1) / kGT;
-  return groups * (sizeof(Agg) + 8) + 16;  // + the byte slots, log_asm_seek's two words
+  return groups * sizeof(Agg) + 16;  // + log_asm_seek's two words
 }
 
 // `scratch`: log_asm_scratch_bytes(capacity + nblocks) bytes, 16-byte aligned
@@ -1013,9 +1023,8 @@ hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
   a.stamps = nullptr;
 #endif
   a.lohi = reinterpret_cast<uint32_t*>(a.aggs + a.groups);
-  a.wg_bytes = reinterpret_cast<unsigned long long*>(a.lohi + 4);
   (void)tag;
-  a.done = done;
+  (void)done;
   (void)bytes;
   a.init_st = initial_offset ? kResync : kIdle;
   a.seek.offset = initial_offset;
