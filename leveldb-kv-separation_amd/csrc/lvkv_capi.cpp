@@ -1006,7 +1006,7 @@ int lvkv_debug_read_bw(const void* d_data, uint64_t bytes, uint32_t* d_scratch,
 // -1: crc32c_kernel.hip's persistent kernel for general-layout batches;
 // 0..31: crc32c_ragged.hip cfgs (launch_crc32c_ragged). Timing only.
 int lvkv_debug_set_general_kernel(int k) {
-  if (k < -1 || k > 33) return LVKV_ERR_INVALID;
+  if (k < -1 || k > 34) return LVKV_ERR_INVALID;
   int rc = LVKV_OK;
   DeviceCtx* c = current_ctx(&rc);
   if (c == nullptr) return rc;
@@ -1016,7 +1016,7 @@ int lvkv_debug_set_general_kernel(int k) {
 
 // The ragged cfg used for WAL records (8, 16, 24: small-record shapes).
 int lvkv_debug_set_log_kernel(int k) {
-  if (k < 0 || k > 33) return LVKV_ERR_INVALID;
+  if (k < 0 || k > 34) return LVKV_ERR_INVALID;
   int rc = LVKV_OK;
   DeviceCtx* c = current_ctx(&rc);
   if (c == nullptr) return rc;

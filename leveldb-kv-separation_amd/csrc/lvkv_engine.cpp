@@ -96,12 +96,14 @@ constexpr KernelSpec kSpecs[] = {
     {"lvkv_ek_ragged_burst_small.kd", nullptr, 8, 6, 1, kArgsRagged},
     {"lvkv_ek_ragged_pipe.kd", nullptr, 8, 2, 2, kArgsRagged},
     {"lvkv_ek_ragged_pipe_small.kd", nullptr, 8, 4, 2, kArgsRagged},
+    {"lvkv_ek_lanes.kd", nullptr, 8, 64, 2, kArgsRagged},
 };
 constexpr int kNumSpecs = static_cast<int>(sizeof(kSpecs) / sizeof(kSpecs[0]));
 constexpr int kNumUniformSpecs = 2;  // lvkv_engine_set_variant's choices
 // general-layout kernels: persistent runs (two workgroups per CU, rounds of
 // 16 / 32 blocks), and one round per dispatch (one workgroup per CU)
-constexpr int kRaggedSpec = 2, kRaggedSmallSpec = 3, kBurstSpec = 4, kBurstSmallSpec = 5;
+constexpr int kRaggedSpec = 2, kBurstSpec = 4, kBurstSmallSpec = 5, kLanesSpec = 8;
+constexpr uint32_t kLanesLong = 4096;  // the lane walk's longest block (crc32c_lanes.h)
 constexpr uint32_t kBurstRows = 17, kBurstSmallRows = 8;  // their chunk rows
 static_assert(sizeof(EngineRaggedArgs) <= 256 && sizeof(UniformArgs) <= 256, "kernarg slot");
 
@@ -659,6 +661,8 @@ int submit_general(Engine& eng, KernelArgs a, size_t nblocks, uint32_t flags) {
   }
   if (e->ragged_spec >= 0) spec = e->ragged_spec;
   const EngineKernel& k = e->kern[spec];
+  if (spec == kLanesSpec && (a.long_split == 0 || a.long_split > kLanesLong))
+    a.long_split = kLanesLong;
   const uint64_t per_round = uint64_t{k.waves} * k.chains;
   const uint64_t max_groups = static_cast<uint64_t>(e->cus) * k.per_cu;
   const bool burst = spec == kBurstSpec || spec == kBurstSmallSpec;

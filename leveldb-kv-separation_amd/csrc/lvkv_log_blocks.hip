@@ -1193,9 +1193,10 @@ size_t log_scratch_bytes(uint64_t size, uint32_t capacity, int cus) {
 // `scratch`: log_scratch_bytes(size, capacity, cus) bytes, 16-byte aligned,
 // its counters 0 (zeroed when allocated; every call leaves them at 0), used
 // by one call at a time. Two launches: the verify, then the emit.
-hipError_t launch_crc32c_ragged_pipe(const KernelArgs& a, const uint32_t* zpow,
-                                     const uint32_t* lane_cols, bool small, int num_groups,
-                                     hipStream_t stream);
+hipError_t launch_crc32c_lanes(const KernelArgs& a, const uint32_t* zpow,
+                               const uint32_t* lane_cols, int num_groups, hipStream_t stream);
+// WAL records the lane walk leaves to its workgroup (crc32c_lanes.h)
+constexpr uint32_t kLanesLogLong = 4096;
 
 hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_off,
                              uint32_t* actual, uint8_t* rec_status, uint32_t capacity,
@@ -1253,8 +1254,8 @@ hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_o
       k.mode = kModeLogStaged;
       k.long_split = kLogLongBytes;
       k.log_first_bad = a.first_bad;
-      if ((e = launch_crc32c_ragged_pipe(k, zpow, lane_cols, true, 2 * cus, stream)) != hipSuccess)
-        return e;
+      k.long_split = kLanesLogLong;
+      if ((e = launch_crc32c_lanes(k, zpow, lane_cols, 2 * cus, stream)) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(log_emit2_kernel, dim3(std::max<uint32_t>(1, (nblocks + 15) / 16)),
                        dim3(64 * 16), 0, stream, a);

@@ -156,3 +156,52 @@ def test_engine_general_many_in_flight(oracle, eng, gpu):
     got = outs.cpu().numpy().view(np.uint32)
     for k in range(K):
         assert np.array_equal(got[k], want[k % 8]), k
+
+
+@pytest.mark.parametrize("spec", [2, 3, 4, 5, 6, 7, 8])
+def test_engine_every_general_kernel(lvkv, oracle, eng, gpu, spec):
+    """Each of the engine's general-layout kernels forced in turn
+    (lvkv_debug_engine_ragged_spec): persistent, one-round burst, pipelined
+    and one-block-per-lane walks, on blocks of every start alignment and
+    lengths 0..12,000 (some over the lane walk's 4 KiB and over 64 KiB), with
+    per-block inits; compute, masked compute, SST verify and WAL verify."""
+    import ctypes
+
+    import torch
+    lvkv.lib.lvkv_debug_engine_ragged_spec.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    assert lvkv.lib.lvkv_debug_engine_ragged_spec(eng.handle, spec) == 0
+    try:
+        rng = np.random.default_rng(100 + spec)
+        data = rng.integers(0, 256, 24 << 20, dtype=np.uint8)
+        n = 6000
+        L = rng.integers(0, 2500, n).astype(np.uint32)
+        L[::53] = rng.integers(2500, 12000, L[::53].size)
+        L[:12] = [0, 1, 2, 3, 4, 15, 16, 17, 4095, 4096, 4097, 70000]
+        offs = rng.integers(0, data.size - 70008, n).astype(np.uint64)
+        inits = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        d = _dev(torch, data, gpu)
+        do, dl = _dev(torch, offs.astype(np.int64), gpu), _dev(torch, L.view(np.int32), gpu)
+        got = eng.crc32c_batch(d, do, dl, inits=_dev(torch, inits.view(np.int32), gpu))
+        gm = eng.crc32c_batch(d, do, dl, init=0x0BADF00D, mask=True, ordered=True)
+        eng.wait()
+        assert np.array_equal(_u32(got), oracle.batch(data, offs, L, inits, threads=8))
+        want_m = oracle.batch(data, offs, L, np.full(n, 0x0BADF00D, np.uint32), mask=True,
+                              threads=8)
+        assert np.array_equal(_u32(gm), want_m)
+        # SST verify: trailers written from the oracle, some corrupted
+        host = data.copy()
+        so = (np.arange(800, dtype=np.uint64) * 7001 + rng.integers(0, 4, 800)).astype(np.uint64)
+        ss = rng.integers(0, 6000, 800).astype(np.uint32)
+        crc = oracle.batch(host, so, ss + 1, threads=8)
+        for i in range(800):
+            o = int(so[i]) + int(ss[i]) + 1
+            host[o:o + 4] = np.frombuffer(np.uint32(oracle.mask(int(crc[i]))).tobytes(), np.uint8)
+        bad = rng.choice(800, 40, replace=False)
+        for i in bad:
+            host[int(so[i]) + int(ss[i]) // 2] ^= 0x10
+        act, st = eng.sst_verify(_dev(torch, host, gpu), _dev(torch, so.astype(np.int64), gpu),
+                                 _dev(torch, ss.view(np.int32), gpu))
+        eng.wait()
+        assert sorted(np.nonzero(st.cpu().numpy())[0].tolist()) == sorted(bad.tolist())
+    finally:
+        lvkv.lib.lvkv_debug_engine_ragged_spec(eng.handle, -1)
