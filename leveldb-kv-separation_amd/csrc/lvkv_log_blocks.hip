@@ -782,7 +782,7 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
 // ---- the walk path: walk, then one ragged CRC launch, then the merge -------
 //
 // log_walk_kernel: one wave per workgroup and one 32 KiB slot each (four
-// workgroups per CU). A wave claims a block by ticket, pulls it into its
+// workgroups per CU). Wave g takes blocks g, g + G, ..., pulls each into its
 // slot by LDS-DMA, walks its headers (the same chain of LDS reads as
 // walk_block, nothing else on the CU's LDS but the other walkers), reserves
 // the block's run of the staging array (an atomic bump) and writes the
@@ -854,11 +854,9 @@ __global__ void __launch_bounds__(64) log_walk_kernel(LogArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[kBufBytes];
   const uint32_t lane = lane_id();
   uint16_t* over = a.over16 + static_cast<uint64_t>(blockIdx.x) * kMaxRecs;
-  uint32_t tk = 0;
-  if (lane == 0) tk = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (;;) {
-    const uint32_t b = __builtin_amdgcn_readfirstlane(tk);
-    if (b >= a.nblocks) break;
+  // blocks g, g + G, ...: no ticket (a thousand walkers claiming from one
+  // counter at once serialise on it)
+  for (uint32_t b = blockIdx.x; b < a.nblocks; b += gridDim.x) {
     const uint64_t start = uint64_t{b} * kLogBlock;
     const uint64_t end = min(a.size, start + kLogBlock);
     const uint32_t n = static_cast<uint32_t>(end - start);
@@ -881,8 +879,6 @@ __global__ void __launch_bounds__(64) log_walk_kernel(LogArgs a) {
       if (lane < (nbytes & 15u)) buf[16u * lines + lane] = (src - shift)[16u * lines + lane];
       __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) lgkmcnt(0): the DMA and the tail have landed
     }
-    // the next block's ticket: its round trip overlaps the walk
-    if (lane == 0) tk = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t held, c, stop_at;
     const uint8_t walked = walk_only(buf + shift, n, eof, over, &held, &c, &stop_at);
     uint32_t off = 0;
