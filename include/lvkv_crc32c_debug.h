@@ -25,16 +25,16 @@ uint32_t lvkv_debug_extend_portable(uint32_t crc, const uint8_t* data, size_t n)
 
 /* Kernel choices of the current device (per device, not process globals;
  * timing and A/B tests): general-layout batches (-1 crc32c_kernel.hip's
- * persistent kernel, 0..31 ragged cfgs, 32 / 33 the pipelined walk 8 x 2 x 17 /
- * 8 x 4 x 8, 34 one block per lane), WAL records (ragged cfg), and the
+ * persistent kernel, 0..31 ragged cfgs), WAL records (ragged cfg), and the
  * whole-SSTable verify form (0 by size, 1 one fused launch, 2 two launches). */
 int lvkv_debug_set_general_kernel(int cfg);
 int lvkv_debug_set_log_kernel(int cfg);
 int lvkv_debug_set_sst_form(int form);
 /* WAL verify (lvkv_log_verify_blocks_device, lvkv_log_read_device) on the
  * current device: 0 = two LDS slots per CU, each block walked and its records
- * checksummed in one launch; 1 = a walk launch (four one-wave walkers per CU),
- * one general-layout CRC launch over the staged headers, a merge launch. */
+ * checksummed in one launch; 1 = walk first (a launch of one-wave walkers,
+ * four per CU), then the slots load the walked positions instead of
+ * walking. */
 int lvkv_debug_set_log_path(int path);
 
 /* The kernel-variant, timestamp and read-bandwidth probes live in the probe
@@ -75,9 +75,8 @@ int lvkv_engine_set_stamps(struct lvkv_engine* engine, uint64_t* d_stamps, uint6
 int lvkv_debug_engine_stall(struct lvkv_engine* engine, int stall, double stuck_seconds);
 /* The engine's general-layout kernel for every later submit (A/B timing,
  * tools/probe/engine_shapes.py): 2 = persistent 8 x 2 x 24, 3 = persistent
- * 8 x 4 x 8, 4 = one-round 8 x 4 x 17, 5 = one-round 8 x 6 x 8, 6 = pipelined
- * persistent 8 x 2 x 17, 7 = pipelined persistent 8 x 4 x 8, 8 = one block per
- * lane (crc32c_lanes.h); -1 = chosen by the batch's layout (the default). */
+ * 8 x 4 x 8, 4 = one-round 8 x 4 x 17, 5 = one-round 8 x 6 x 8; -1 = chosen by
+ * the batch's layout (the default). */
 int lvkv_debug_engine_ragged_spec(struct lvkv_engine* engine, int spec);
 
 #ifdef __cplusplus

@@ -8,7 +8,6 @@
 
 #include "crc32c_compact_common.h"
 #include "crc32c_device_common.h"
-#include "crc32c_lanes.h"
 #include "crc32c_ragged_body.h"
 #include "lvkv_crc32c.h"
 #include "lvkv_kernel_args.h"
@@ -24,50 +23,7 @@ __global__ void __launch_bounds__(64 * W, 2)
   ragged_run<W, NCH, R>(a, zpow, lane_cols, lds, blockIdx.x, gridDim.x, total, false);
 }
 
-// The software-pipelined walk (ragged_pipe: a chunk's rows in flight while
-// the previous one is walked), two workgroups per CU; the block count may
-// come from the device (a.count, written by an earlier launch).
-template <int W, int NCH, int R>
-__global__ void __launch_bounds__(64 * W, 2)
-    crc32c_ragged_pipe_kernel(KernelArgs a, const uint32_t* zpow, const uint32_t* lane_cols) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[RagLds<W>::kDwords];
-  const uint32_t total = a.count != nullptr ? min(a.nblocks, sload_u32(a.count, 0)) : a.nblocks;
-  ragged_pipe<W, NCH, R>(a, zpow, lane_cols, lds, blockIdx.x, gridDim.x, total);
-}
-
-// The lane-serial walk (crc32c_lanes.h: a block per lane), two workgroups
-// per CU; the count may come from the device.
-__global__ void __launch_bounds__(512, 2)
-    crc32c_lanes_kernel(KernelArgs a, const uint32_t* zpow, const uint32_t* lane_cols) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[lanes_lds_bytes<8>() / 4];
-  const uint32_t total = a.count != nullptr ? min(a.nblocks, sload_u32(a.count, 0)) : a.nblocks;
-  lanes_run<8>(a, zpow, lane_cols, lds, blockIdx.x, gridDim.x, total);
-}
-
 }  // namespace
-
-// Short blocks, one per lane (crc32c_lanes.h); blocks over a.long_split go
-// to the workgroup at the end of its run.
-hipError_t launch_crc32c_lanes(const KernelArgs& a, const uint32_t* zpow,
-                               const uint32_t* lane_cols, int num_groups, hipStream_t stream) {
-  hipLaunchKernelGGL(crc32c_lanes_kernel, dim3(num_groups), dim3(512), 0, stream, a, zpow,
-                     lane_cols);
-  return hipGetLastError();
-}
-
-// small: 8 waves x 4 chains x 8 rows (records up to 2 KiB: WAL records),
-// else 8 x 2 x 17 (SST-sized blocks).
-hipError_t launch_crc32c_ragged_pipe(const KernelArgs& a, const uint32_t* zpow,
-                                     const uint32_t* lane_cols, bool small, int num_groups,
-                                     hipStream_t stream) {
-  if (small)
-    hipLaunchKernelGGL((crc32c_ragged_pipe_kernel<8, 4, 8>), dim3(num_groups), dim3(512), 0,
-                       stream, a, zpow, lane_cols);
-  else
-    hipLaunchKernelGGL((crc32c_ragged_pipe_kernel<8, 2, 17>), dim3(num_groups), dim3(512), 0,
-                       stream, a, zpow, lane_cols);
-  return hipGetLastError();
-}
 
 // cfg: shape = cfg & 3, or cfg >> 3 for the small-record shapes (1: 8 waves
 // x 4 chains x 8 rows; 2: 8 x 6 x 8; 3: 8 x 8 x 4); the large-record shapes
@@ -136,22 +92,6 @@ hipError_t launch_crc32c_general(const KernelArgs& a, int cus, hipStream_t strea
       e = launch_crc32c_long(b, b.row_tab + kZPowOffset,
                              b.row_tab + kRowTabDwords + kLaneTabDwords, cus, stream);
     return e;
-  }
-  if (cfg == 34 && a.mode != kModeSstTable) {  // one block per lane, 512 blocks a round
-    KernelArgs b = a;
-    // blocks over 4 KiB (the lane walk's serial length) to the workgroup
-    if (b.long_split == 0 || b.long_split > kLaneLongBytes) b.long_split = kLaneLongBytes;
-    const uint32_t groups = min(2u * static_cast<uint32_t>(cus), (n + 511u) / 512u);
-    return launch_crc32c_lanes(b, a.row_tab + kZPowOffset,
-                               a.row_tab + kRowTabDwords + kLaneTabDwords,
-                               static_cast<int>(max(1u, groups)), stream);
-  }
-  if (cfg >= 32) {  // the pipelined walk: 32 = 8 x 2 x 17, 33 = 8 x 4 x 8
-    const uint32_t per = cfg == 33 ? 32u : 16u;
-    const uint32_t groups = min(2u * static_cast<uint32_t>(cus), (n + per - 1) / per);
-    return launch_crc32c_ragged_pipe(a, a.row_tab + kZPowOffset,
-                                     a.row_tab + kRowTabDwords + kLaneTabDwords, cfg == 33,
-                                     static_cast<int>(max(1u, groups)), stream);
   }
   const uint32_t per = static_cast<uint32_t>(ragged_blocks_per_round(cfg));
   const uint32_t rounds1 = (n + per - 1) / per;

@@ -501,167 +501,6 @@ __device__ __forceinline__ void ragged_run(const KernelArgs& a, const uint32_t* 
   ragged_long_pass<W>(a, zpow, lds, start, n, keys, lane_base);
 }
 
-// One unit of ragged_pipe's stream: chunk k of the round rd holds (its rows
-// have been issued), walked into the chains' states st; a chain whose last
-// chunk this is is reduced and stored; at the round's last chunk its tiny
-// blocks are computed and long ones flagged.
-template <int W, int NCH, int R>
-__device__ __forceinline__ void rag_walk_unit(const KernelArgs& a, uint32_t* lds,
-                                              RagRound<NCH, R>& rd, uint32_t k,
-                                              uint32_t (&st)[NCH], const LaneKeys& keys,
-                                              uint32_t lane, uint32_t lane_base) {
-  constexpr uint32_t kFlag = RagLds<W>::kFlag;
-#pragma unroll
-  for (int c = 0; c < NCH; ++c)
-    if (rd.g[c].e() != 0) rd.realign(c, lane);
-  if (k == 0) {
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const uint32_t s0l = rd.g[c].s0l(), sh = 8u * rd.g[c].delta();
-      uint32_t x = rd.w[c][0];
-      x = lane < s0l ? 0u : x;
-      x = lane == s0l ? (x & (0xffffffffu << sh)) ^ (rd.g[c].s0 << sh) : x;
-      x = lane == s0l + 1u ? x ^ rd.g[c].spill() : x;
-      st[c] = x;
-      rd.w[c][1] = (s0l == 63u && lane == 0) ? rd.w[c][1] ^ rd.g[c].spill() : rd.w[c][1];
-    }
-  } else {
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) st[c] = row_step_c(lds, st[c], rd.w[c][0], keys);
-  }
-  uint32_t nrow[NCH];
-  uint32_t nab = R;
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const uint32_t rows = rd.g[c].kind == kRagRows ? rd.g[c].rows() : 0u;
-    nrow[c] = rows > k * R ? min(static_cast<uint32_t>(R), rows - k * R) : 0u;
-    nab = min(nab, nrow[c]);
-  }
-#pragma unroll
-  for (int j = 1; j < R; ++j) {
-    if (static_cast<uint32_t>(j) < nab) {
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) st[c] = row_step_c(lds, st[c], rd.w[c][j], keys);
-    }
-  }
-#pragma unroll
-  for (int j = 1; j < R; ++j) {
-    const uint32_t u = static_cast<uint32_t>(j);
-    if (u >= nab) {
-#pragma unroll
-      for (int c = 0; c < NCH; ++c)
-        if (u < nrow[c]) st[c] = row_step_c(lds, st[c], rd.w[c][j], keys);
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    if (nrow[c] > 0 && rd.g[c].rows() <= (k + 1) * R) {
-      const uint32_t crc = wave_xor_dpp(lane_end_shift_c(lds, st[c], lane_base)) ^ 0xffffffffu;
-      rag_store(a, rd.blk[c], rd.g[c], crc);
-    }
-  }
-  if (k + 1 == rd.nchunks) {
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      if (rd.g[c].kind == kRagTiny) rag_store(a, rd.blk[c], rd.g[c], rag_tiny(rd.g[c]));
-      if (rd.g[c].kind == kRagSkip && lane == 0) lds[kFlag] = 1;
-    }
-  }
-}
-
-// ragged_run's walk, software-pipelined: the run is a stream of units
-// (round, chunk), and the next unit's rows are issued into the second of two
-// register buffers BEFORE the current unit is walked, so a wave always has a
-// unit's loads in flight while it walks (ragged_run issues them after the
-// walk: its rounds alternate between waiting on HBM and walking). The next
-// round's descriptors are fetched one round ahead, as there. Loads are
-// issued unconditionally (past the run: empty windows, no memory access), so
-// the compiler's vmcnt waits stay counted. Registers: 2 x NCH x (R + 1) for
-// the rows. Every thread of the workgroup calls it; it builds the image.
-template <int W, int NCH, int R>
-__device__ __forceinline__ void ragged_pipe(const KernelArgs& a, const uint32_t* zpow,
-                                            const uint32_t* lane_cols, uint32_t* lds,
-                                            uint32_t grp, uint32_t G, uint32_t total) {
-  constexpr uint32_t kFlag = RagLds<W>::kFlag;
-  constexpr uint32_t kRound = W * NCH;
-  const uint32_t tid = threadIdx.x;
-  const uint32_t lane = lane_id();
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  uint32_t start, n;
-  if (a.run_base != nullptr) {  // runs of whole units (bytes balanced)
-    const uint32_t U = a.run_units;
-    const uint32_t u0 = static_cast<uint32_t>(static_cast<uint64_t>(grp) * U / G);
-    const uint32_t u1 = static_cast<uint32_t>(static_cast<uint64_t>(grp + 1) * U / G);
-    start = min(total, sload_u32(a.run_base, u0));
-    const uint32_t end = u1 < U ? min(total, sload_u32(a.run_base, u1)) : total;
-    n = end > start ? end - start : 0u;
-  } else {
-    const uint32_t per = total / G, extra = total % G;
-    n = per + (grp < extra ? 1u : 0u);
-    start = grp * per + min(grp, extra);
-  }
-  if (n == 0) return;  // the whole workgroup: no barrier is left waiting
-
-  RagRound<NCH, R> A, B;
-  RagBlock gn[NCH];  // descriptors of the round after the last one adopted
-  {
-    RowTabStage<64 * W> rt;
-    LaneTabGen<W> lg;
-    rt.load(zpow, tid);
-    lg.load(lane_cols, wave, lane);
-    {
-      RagBlock g0[NCH];
-      RagRound<NCH, R>::fetch(g0, a, start, n, 0, wave, W);
-      A.adopt(g0, start, 0, wave, W);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    A.issue(0, lane);
-    __builtin_amdgcn_sched_barrier(0);
-    RagRound<NCH, R>::fetch(gn, a, start, n, kRound, wave, W);
-    rt.store(lds, tid);
-    lg.store(lds, wave, lane);
-    if (tid == 0) lds[kFlag] = 0;
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  const LaneKeys keys = lane_keys(lane);
-  const uint32_t lane_base = compact_lane_base(lane);
-  uint32_t st[NCH];
-
-  // one phase: the unit after cur's goes into nxt (its rows issued), then
-  // cur's unit is walked; false when cur's was the run's last unit
-  auto phase = [&](RagRound<NCH, R>& cur, uint32_t& kc, uint32_t& rc, RagRound<NCH, R>& nxt,
-                   uint32_t& kn, uint32_t& rn) -> bool {
-    if (kc + 1 < cur.nchunks) {  // the same round's next chunk
-      nxt.nchunks = cur.nchunks;
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        nxt.g[c] = cur.g[c];
-        nxt.blk[c] = cur.blk[c];
-      }
-      kn = kc + 1;
-      rn = rc;
-    } else {  // the next round (empty past the run)
-      kn = 0;
-      rn = rc + kRound;
-      nxt.adopt(gn, start, rn, wave, W);
-      RagRound<NCH, R>::fetch(gn, a, start, n, rn + kRound, wave, W);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    nxt.issue(kn, lane);
-    __builtin_amdgcn_sched_barrier(0);
-    rag_walk_unit<W, NCH, R>(a, lds, cur, kc, st, keys, lane, lane_base);
-    return rn < n;
-  };
-  uint32_t kA = 0, rA = 0, kB = 0, rB = 0;
-  for (;;) {
-    if (!phase(A, kA, rA, B, kB, rB)) break;
-    if (!phase(B, kB, rB, A, kA, rA)) break;
-  }
-
-  ragged_long_pass<W>(a, zpow, lds, start, n, keys, lane_base);
-}
-
 }  // namespace
 }  // namespace lvkv
 

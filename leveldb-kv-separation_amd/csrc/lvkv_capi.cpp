@@ -122,7 +122,7 @@ struct DeviceCtx {
   // (lvkv_debug_set_sst_form)
   std::atomic<int> sst_form{0};
   // WAL verify: 0 two LDS slots per CU walked and checksummed in one launch,
-  // 1 walk launch + ragged CRC launch + merge (lvkv_debug_set_log_path)
+  // 1 a walk launch first, the slots load its positions (lvkv_debug_set_log_path)
   std::atomic<int> log_path{0};
   std::mutex host_mu;  // serialises lvkv_crc32c_batch_host per device
   // WAL verify scratch: a pool of buffers, each lent to one call at a time
@@ -1006,7 +1006,7 @@ int lvkv_debug_read_bw(const void* d_data, uint64_t bytes, uint32_t* d_scratch,
 // -1: crc32c_kernel.hip's persistent kernel for general-layout batches;
 // 0..31: crc32c_ragged.hip cfgs (launch_crc32c_ragged). Timing only.
 int lvkv_debug_set_general_kernel(int k) {
-  if (k < -1 || k > 34) return LVKV_ERR_INVALID;
+  if (k < -1 || k > 31) return LVKV_ERR_INVALID;
   int rc = LVKV_OK;
   DeviceCtx* c = current_ctx(&rc);
   if (c == nullptr) return rc;
@@ -1016,7 +1016,7 @@ int lvkv_debug_set_general_kernel(int k) {
 
 // The ragged cfg used for WAL records (8, 16, 24: small-record shapes).
 int lvkv_debug_set_log_kernel(int k) {
-  if (k < 0 || k > 34) return LVKV_ERR_INVALID;
+  if (k < 0 || k > 31) return LVKV_ERR_INVALID;
   int rc = LVKV_OK;
   DeviceCtx* c = current_ctx(&rc);
   if (c == nullptr) return rc;

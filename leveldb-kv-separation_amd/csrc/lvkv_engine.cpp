@@ -94,17 +94,13 @@ constexpr KernelSpec kSpecs[] = {
     {"lvkv_ek_ragged_small.kd", nullptr, 8, 4, 2, kArgsRagged},
     {"lvkv_ek_ragged_burst.kd", nullptr, 8, 4, 1, kArgsRagged},
     {"lvkv_ek_ragged_burst_small.kd", nullptr, 8, 6, 1, kArgsRagged},
-    {"lvkv_ek_ragged_pipe.kd", nullptr, 8, 2, 2, kArgsRagged},
-    {"lvkv_ek_ragged_pipe_small.kd", nullptr, 8, 4, 2, kArgsRagged},
-    {"lvkv_ek_lanes.kd", nullptr, 8, 64, 2, kArgsRagged},
 };
 constexpr int kNumSpecs = static_cast<int>(sizeof(kSpecs) / sizeof(kSpecs[0]));
 constexpr int kNumUniformSpecs = 2;  // lvkv_engine_set_variant's choices
 // general-layout kernels: persistent runs (two workgroups per CU, rounds of
 // 16 / 32 blocks), and one round per dispatch (one workgroup per CU)
-constexpr int kRaggedSpec = 2, kBurstSpec = 4, kBurstSmallSpec = 5, kLanesSpec = 8;
-constexpr uint32_t kLanesLong = 4096;  // the lane walk's longest block (crc32c_lanes.h)
-constexpr uint32_t kBurstRows = 17, kBurstSmallRows = 8;  // their chunk rows
+constexpr int kRaggedSpec = 2, kRaggedSmallSpec = 3, kBurstSpec = 4, kBurstSmallSpec = 5;
+constexpr uint32_t kBurstRows = 17, kBurstSmallRows = 8;  // chunk rows of the SST / small shapes
 static_assert(sizeof(EngineRaggedArgs) <= 256 && sizeof(UniformArgs) <= 256, "kernarg slot");
 
 constexpr size_t args_size(ArgKind k) {
@@ -631,16 +627,19 @@ int dispatch(Engine& e, const EngineKernel& k, const void* args, size_t size, ui
 
 // A general-layout batch (KernelArgs as the HIP path builds it: offsets or
 // the uniform stride, a mode) through the engine's ragged kernels; the
-// same ordering and acquire rules as the uniform submit. The kernel:
-//   * uniform layouts (the host knows the length): blocks of more than 17
-//     rows (config 3's 32 KiB WAL blocks) the persistent 8 x 2 x 24 walk
-//     (measured 0.76 of 8 TB/s overlapped on 16,384 x 32 KiB), up to 8 rows
-//     the 8 x 6 x 8 burst, else the 8 x 4 x 17 burst;
-//   * descriptor batches: WAL records (log verify / fill) the 8 x 6 x 8 burst,
-//     everything else the 8 x 4 x 17 burst (SST blocks, ~4.1 KiB).
-// A burst kernel's batch is cut into dispatches of one round (cus x 8 x NCH
-// blocks, one workgroup per CU) rotating over the queues like separate
-// batches, so consecutive rounds overlap on the device.
+// same ordering and acquire rules as the uniform submit. The kernel, by the
+// measurements of tools/probe/engine_shapes.py:
+//   * blocks of more than 17 rows in a uniform layout (config 3's 32 KiB WAL
+//     blocks): the persistent 8 x 2 x 24 walk (0.77 of 8 TB/s overlapped on
+//     16,384 x 32 KiB);
+//   * WAL records (log verify / fill) and uniform blocks of up to 8 rows: the
+//     persistent 8 x 4 x 8 walk (0.29 overlapped on 62,000 x 0-2000 B, the
+//     one-round 8 x 6 x 8 burst 0.23);
+//   * everything else (SST blocks, ~4.1 KiB): the 8 x 4 x 17 burst, whose
+//     batch is cut into dispatches of one round (cus x 32 blocks, one
+//     workgroup per CU) rotating over the queues like separate batches, so
+//     consecutive rounds overlap on the device (0.62-0.64 overlapped on
+//     16,384 x 4271 B, the persistent walk 0.53).
 int submit_general(Engine& eng, KernelArgs a, size_t nblocks, uint32_t flags) {
   Engine* e = &eng;
   if (nblocks == 0) return LVKV_OK;
@@ -655,14 +654,12 @@ int submit_general(Engine& eng, KernelArgs a, size_t nblocks, uint32_t flags) {
   int spec;
   if (a.offsets == nullptr) {
     const uint64_t rows = (uint64_t{a.length} + 3u + 255u) / 256u;  // upper bound, any alignment
-    spec = rows > kBurstRows ? kRaggedSpec : rows <= kBurstSmallRows ? kBurstSmallSpec : kBurstSpec;
+    spec = rows > kBurstRows ? kRaggedSpec : rows <= kBurstSmallRows ? kRaggedSmallSpec : kBurstSpec;
   } else {
-    spec = log ? kBurstSmallSpec : kBurstSpec;
+    spec = log ? kRaggedSmallSpec : kBurstSpec;
   }
   if (e->ragged_spec >= 0) spec = e->ragged_spec;
   const EngineKernel& k = e->kern[spec];
-  if (spec == kLanesSpec && (a.long_split == 0 || a.long_split > kLanesLong))
-    a.long_split = kLanesLong;
   const uint64_t per_round = uint64_t{k.waves} * k.chains;
   const uint64_t max_groups = static_cast<uint64_t>(e->cus) * k.per_cu;
   const bool burst = spec == kBurstSpec || spec == kBurstSmallSpec;

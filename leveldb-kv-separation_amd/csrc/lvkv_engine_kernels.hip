@@ -11,7 +11,6 @@
 #include <stdint.h>
 
 #include "crc32c_burst.h"
-#include "crc32c_lanes.h"
 #include "crc32c_ragged_body.h"
 #include "lvkv_kernel_args.h"
 
@@ -87,27 +86,4 @@ extern "C" __global__ void __launch_bounds__(512, 2)
   __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::RagLds<8>::kDwords];
   lvkv::ragged_run<8, 6, 8>(a.k, a.zpow, a.lane_cols, lds, blockIdx.x, a.ngroups, a.k.nblocks,
                             false);
-}
-
-// The persistent walk software-pipelined (ragged_pipe: the next chunk's rows
-// in flight while one is walked), two workgroups per CU: 8 waves x 2 chains x
-// 17 rows, and 8 x 4 x 8 for small records.
-extern "C" __global__ void __launch_bounds__(512, 2)
-    lvkv_ek_ragged_pipe(lvkv::EngineRaggedArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::RagLds<8>::kDwords];
-  lvkv::ragged_pipe<8, 2, 17>(a.k, a.zpow, a.lane_cols, lds, blockIdx.x, a.ngroups, a.k.nblocks);
-}
-extern "C" __global__ void __launch_bounds__(512, 2)
-    lvkv_ek_ragged_pipe_small(lvkv::EngineRaggedArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::RagLds<8>::kDwords];
-  lvkv::ragged_pipe<8, 4, 8>(a.k, a.zpow, a.lane_cols, lds, blockIdx.x, a.ngroups, a.k.nblocks);
-}
-
-// Short blocks, one per lane (crc32c_lanes.h: the four-stream swath walk),
-// two workgroups per CU, 512 blocks a round; blocks over a.k.long_split to
-// the workgroup at the end of its run.
-extern "C" __global__ void __launch_bounds__(512, 2)
-    lvkv_ek_lanes(lvkv::EngineRaggedArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::lanes_lds_bytes<8>() / 4];
-  lvkv::lanes_run<8>(a.k, a.zpow, a.lane_cols, lds, blockIdx.x, a.ngroups, a.k.nblocks);
 }

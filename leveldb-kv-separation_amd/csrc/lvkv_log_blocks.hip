@@ -97,12 +97,14 @@ struct LogArgs {
   const uint32_t* zpow;
   const uint32_t* lane_cols;
   uint32_t* events;  // nullable: the ReadRecord event stream (lvkv_log_events.h)
-  // the walk path (log_walk_kernel -> the ragged CRC launch -> log_emit2_kernel)
-  uint64_t* stg_hdr;     // capacity: staged header offsets, each block's run in file order
-  uint32_t* stg_actual;  // capacity: their CRCs (the CRC launch)
-  uint8_t* stg_status;   // capacity: 1 = mismatch (the CRC launch)
-  uint32_t* first_bad;   // nblocks: the block's lowest mismatching staged index, or ~0
-  uint16_t* over16;      // walkers x kMaxRecs: positions of records 64 and on
+  // the walk-first path (log_walk_kernel, then log_verify_kernel with the
+  // positions precomputed, then log_emit_kernel)
+  uint32_t pre;          // 1: log_verify_kernel reads the walk's results
+  ulonglong2* winfo;     // nblocks: {count | verdict << 32, bad-length drop | overflow run << 32}
+  uint16_t* wpos;        // nblocks x kWalkSlot: the records' positions in their block
+  uint16_t* wover;       // positions past kWalkSlot (runs reserved by an atomic bump)
+  uint32_t* wover_top;   // entries of wover reserved (left at 0 by the emit launch)
+  uint16_t* over16;      // walkers x kMaxRecs: the walk's positions of records 64 and on
   uint64_t* stamps;  // probe build only: 8 u64 per (workgroup, slot, block)
   uint32_t knobs;    // probe build only: bit 0 = workers idle, no CRCs (timing)
 };
@@ -420,6 +422,186 @@ __device__ __forceinline__ void record_done(const uint8_t* blk, uint32_t p, uint
   hb[3] = static_cast<uint8_t>(crc >> 24);
 }
 
+// ---- the walk-first path --------------------------------------------------
+//
+// What bounds log_verify_kernel is each slot's serial chain: DMA, the walk
+// of ~31 headers (a chain of LDS round trips slowed by the record waves'
+// traffic), the last records' CRCs. This path takes the walk out of it:
+//   log_walk_kernel   one wave per workgroup and one 32 KiB slot each (four
+//                     per CU, nothing else on their LDS); wave g walks blocks
+//                     g, g + G, ... (static: no ticket, no per-block atomic:
+//                     a thousand walkers bumping one counter at once
+//                     serialise on it) and writes each block's count, verdict
+//                     and drop and its records' positions into a fixed slot of
+//                     kWalkSlot entries (positions past it, rare, into a run
+//                     reserved by an atomic bump);
+//   log_verify_kernel with a.pre: each slot's manager pulls its block in and
+//                     loads the walked positions instead of walking, so the
+//                     workers start on every record at once;
+//   log_emit_kernel   as before.
+// The image is read twice (both DMAs).
+
+constexpr uint32_t kWalkPerCu = 4;   // walker workgroups per CU
+constexpr uint32_t kWalkSlot = 512;  // positions per block in its fixed slot
+
+// Walks blk[0, n) like walk_block (ReadPhysicalRecord's header loop,
+// db/log_reader.cc:189-247, to the first stop), keeping record k's position
+// in lane k % 64 of `held` and writing each full 64 to over[]. Returns the
+// verdict; *count, *stop = records and the block offset after the last one.
+__device__ __forceinline__ uint8_t walk_only(const uint8_t* blk, uint32_t n, bool eof,
+                                             uint16_t* over, uint32_t* held_out,
+                                             uint32_t* count, uint32_t* stop) {
+  const uint32_t lane = lane_id();
+  const uint32_t base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(blk));
+  const uint32_t end = base + n;
+  uint32_t k = 0, bp = base, len = 0, typ = 0;
+  uint32_t held = 0;
+  if (n >= kLogHeader) {
+    uint32_t nlen, ntyp;
+    asm volatile("ds_read_u16 %0, %2 offset:4\n\tds_read_u8 %1, %2 offset:6\n\ts_waitcnt lgkmcnt(0)"
+                 : "=v"(len), "=v"(typ)
+                 : "v"(bp));
+    for (;;) {
+      const uint32_t nbp = bp + kLogHeader + len;
+      asm volatile("ds_read_u16 %0, %2 offset:4\n\tds_read_u8 %1, %2 offset:6"
+                   : "=v"(nlen), "=v"(ntyp)
+                   : "v"(nbp));
+      __builtin_amdgcn_sched_barrier(0);  // the reads issue before the tests below
+      const uint32_t f = __builtin_amdgcn_readfirstlane(
+          (nbp > end || (len | typ) == 0 ? 1u : 0u) | (end - nbp < kLogHeader ? 2u : 0u));
+      if (f & 1u) break;
+      held = lane == (k & 63u) ? bp - base : held;
+      ++k;
+      if ((k & 63u) == 0) over[k - 64u + lane] = static_cast<uint16_t>(held);
+      bp = nbp;
+      if (f & 2u) break;
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nlen), "+v"(ntyp));
+      len = nlen;
+      typ = ntyp;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nlen), "+v"(ntyp));
+  }
+  const uint32_t p = __builtin_amdgcn_readfirstlane(bp - base);
+  len = __builtin_amdgcn_readfirstlane(len);
+  uint8_t v;
+  if (n - p < kLogHeader)
+    v = (eof && p < n) ? LVKV_LOGBLK_EOF : LVKV_LOGBLK_OK;  // :206-213
+  else if (kLogHeader + len > n - p)
+    v = eof ? LVKV_LOGBLK_EOF : LVKV_LOGBLK_BAD_LENGTH;
+  else
+    v = LVKV_LOGBLK_ZERO;
+  *held_out = held;
+  *count = k;
+  *stop = p;
+  return v;
+}
+
+// The block at file offset `start` (n bytes) into buf by LDS-DMA from its
+// 16-byte aligned start: full 16-byte lines as dwordx4, the last 0-15 bytes
+// by plain loads; returns the block's offset in buf (its misalignment).
+__device__ __forceinline__ uint32_t dma_block(const uint8_t* file, uint64_t start, uint32_t n,
+                                              uint8_t* buf, uint32_t lane) {
+  const uint8_t* src = file + start;
+  const uint32_t shift = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src) & 15u);
+  const uint32_t nbytes = shift + n;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(src - shift), 0, static_cast<int>(nbytes), kBufferDword3);
+  const uint32_t lines = nbytes >> 4;
+  for (uint32_t i = 0; i * 64u < lines; ++i) {
+    const uint32_t line = i * 64u + lane;
+    if (line < lines)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          r, (__attribute__((address_space(3))) void*)(buf + 1024u * i), 16, 16u * line, 0, 0, 0);
+  }
+  // (a sub-dword LDS-DMA does not land one byte per lane: plain loads)
+  if (lane < (nbytes & 15u)) buf[16u * lines + lane] = (src - shift)[16u * lines + lane];
+  __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) lgkmcnt(0): the DMA and the tail have landed
+  return shift;
+}
+
+__global__ void __launch_bounds__(64) log_walk_kernel(LogArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kBufBytes];
+  const uint32_t lane = lane_id();
+  uint16_t* over = a.over16 + static_cast<uint64_t>(blockIdx.x) * kMaxRecs;
+  for (uint32_t b = blockIdx.x; b < a.nblocks; b += gridDim.x) {
+    const uint64_t start = uint64_t{b} * kLogBlock;
+    const uint64_t end = min(a.size, start + kLogBlock);
+    const uint32_t n = static_cast<uint32_t>(end - start);
+    const uint32_t shift = dma_block(a.file, start, n, buf, lane);
+    uint32_t held, c, stop_at;
+    const uint8_t walked = walk_only(buf + shift, n, n < kLogBlock, over, &held, &c, &stop_at);
+    // positions past the fixed slot: a run of wover (rare: > kWalkSlot records)
+    uint32_t oo = 0;
+    if (c > kWalkSlot && lane == 0)
+      oo = __hip_atomic_fetch_add(a.wover_top, c - kWalkSlot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    oo = __builtin_amdgcn_readfirstlane(oo);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's over[] stores have landed
+    const uint32_t full = c & ~63u;
+    uint16_t* slot = a.wpos + static_cast<uint64_t>(b) * kWalkSlot;
+    for (uint32_t j = lane; j < c; j += 64) {
+      const uint16_t p = j < full ? over[j] : static_cast<uint16_t>(held);
+      if (j < kWalkSlot)
+        slot[j] = p;
+      else if (oo + (j - kWalkSlot) < a.capacity)
+        a.wover[oo + (j - kWalkSlot)] = p;
+    }
+    if (lane == 0)
+      a.winfo[b] = make_ulonglong2(uint64_t{c} | (uint64_t{walked} << 32),
+                                   uint64_t{walked == LVKV_LOGBLK_BAD_LENGTH ? n - stop_at : 0u} |
+                                       (uint64_t{oo} << 32));
+  }
+}
+
+// log_verify_kernel's walk replaced (a.pre): block b's walked positions into
+// the slot (LDS, the overflow past kPosLds in scratch), its long records
+// registered for segmented CRCs in order, then published as walked to its
+// end. Called by the slot's manager wave with uniform arguments.
+__device__ __forceinline__ uint8_t load_walk(const LogArgs& a, uint32_t b, const uint8_t* blk,
+                                             uint32_t n, uint16_t* pos, uint32_t* over, Slot& S,
+                                             uint32_t gen, uint32_t* count, uint32_t* stop) {
+  const uint32_t lane = lane_id();
+  const ulonglong2 wi = a.winfo[b];
+  const uint32_t c = static_cast<uint32_t>(wi.x);
+  const uint8_t walked = static_cast<uint8_t>(wi.x >> 32);
+  const uint32_t drop = static_cast<uint32_t>(wi.y), oo = static_cast<uint32_t>(wi.y >> 32);
+  const uint16_t* slot = a.wpos + static_cast<uint64_t>(b) * kWalkSlot;
+  uint32_t nseg = 0;
+  for (uint32_t j0 = 0; j0 < c; j0 += 64) {
+    const uint32_t j = j0 + lane;
+    uint32_t p = 0, len = 0;
+    if (j < c) {
+      p = j < kWalkSlot ? slot[j] : a.wover[oo + (j - kWalkSlot)];
+      put_pos(pos, over, j, p);
+      len = static_cast<uint32_t>(blk[p + 4]) | (static_cast<uint32_t>(blk[p + 5]) << 8);
+    }
+    // records longer than kSegBytes: segmented, in file order
+    uint64_t lm = __ballot(j < c && len + 1u > kSegBytes);
+    while (lm) {
+      const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(lm));
+      lm &= lm - 1;
+      const uint32_t lp = __shfl(p, l, 64), ll = __shfl(len, l, 64);
+      const uint32_t m = (ll + 1u + kSegBytes - 1u) / kSegBytes;
+      if (lane == 0) {
+        const uint32_t e = S.nlong++;
+        S.lj[e] = static_cast<uint16_t>(j0 + l);
+        S.lp[e] = static_cast<uint16_t>(lp);
+        S.lseg[e] = static_cast<uint8_t>(m);
+        S.lfirst[e] = static_cast<uint8_t>(nseg);
+        S.lacc[e] = 0;
+        S.lrem[e] = m;
+      }
+      nseg += m;
+    }
+  }
+  if (lane == 0) {
+    lds_store_rel(&S.lavail, (gen << 16) | nseg);
+    lds_store_rel(&S.prog, (gen << kGenShift) | kDoneBit | c);
+  }
+  *count = c;
+  *stop = walked == LVKV_LOGBLK_BAD_LENGTH ? n - drop : 0u;
+  return walked;
+}
+
 // ---- the kernel ------------------------------------------------------------
 
 __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
@@ -495,7 +677,8 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
       log_stamp(a, m, k, 1);
       const uint8_t* blk = sbuf + S.shift;
       uint32_t c, stop_at;
-      const uint8_t walked = walk_block(blk, n, eof, spos, sover, S, gen, &c, &stop_at, a, m, k);
+      const uint8_t walked = a.pre ? load_walk(a, b, blk, n, spos, sover, S, gen, &c, &stop_at)
+                                   : walk_block(blk, n, eof, spos, sover, S, gen, &c, &stop_at, a, m, k);
       // the block's run of staging entries (the atomic's round trip overlaps
       // the CRCs: its value is first used by the staging stores)
       uint32_t off = 0;
@@ -779,255 +962,6 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
   // so no workgroup here waits for the last one to finish.
 }
 
-// ---- the walk path: walk, then one ragged CRC launch, then the merge -------
-//
-// log_walk_kernel: one wave per workgroup and one 32 KiB slot each (four
-// workgroups per CU). Wave g takes blocks g, g + G, ..., pulls each into its
-// slot by LDS-DMA, walks its headers (the same chain of LDS reads as
-// walk_block, nothing else on the CU's LDS but the other walkers), reserves
-// the block's run of the staging array (an atomic bump) and writes the
-// records' header offsets there, in file order within the run; per block:
-// the count, the walk's verdict and drop, its run. The records' CRCs are then
-// one general-layout launch over the staged headers (kModeLogStaged: the
-// ragged walk, count read on the device; a mismatch lowers the block's
-// first_bad), and log_emit2_kernel merges (first mismatch drops the rest of
-// the block, db/log_reader.cc:248-255) and places everything in file order.
-// The image is read twice (the walk's DMA, the CRCs' loads); in exchange no
-// slot waits for a block's CRCs and the CRCs run at the batch kernel's rate.
-
-constexpr uint32_t kWalkPerCu = 4;  // walker workgroups per CU
-
-// Walks blk[0, n) like walk_block (ReadPhysicalRecord's header loop,
-// db/log_reader.cc:189-247, to the first stop), keeping record k's position
-// in lane k % 64 of `held` and writing each full 64 to over[]. Returns the
-// verdict; *count, *stop, *last_len = records, block offset after the last
-// one, and the length field of the header the walk stopped on.
-__device__ __forceinline__ uint8_t walk_only(const uint8_t* blk, uint32_t n, bool eof,
-                                             uint16_t* over, uint32_t* held_out,
-                                             uint32_t* count, uint32_t* stop) {
-  const uint32_t lane = lane_id();
-  const uint32_t base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(blk));
-  const uint32_t end = base + n;
-  uint32_t k = 0, bp = base, len = 0, typ = 0;
-  uint32_t held = 0;
-  if (n >= kLogHeader) {
-    uint32_t nlen, ntyp;
-    asm volatile("ds_read_u16 %0, %2 offset:4\n\tds_read_u8 %1, %2 offset:6\n\ts_waitcnt lgkmcnt(0)"
-                 : "=v"(len), "=v"(typ)
-                 : "v"(bp));
-    for (;;) {
-      const uint32_t nbp = bp + kLogHeader + len;
-      asm volatile("ds_read_u16 %0, %2 offset:4\n\tds_read_u8 %1, %2 offset:6"
-                   : "=v"(nlen), "=v"(ntyp)
-                   : "v"(nbp));
-      __builtin_amdgcn_sched_barrier(0);  // the reads issue before the tests below
-      const uint32_t f = __builtin_amdgcn_readfirstlane(
-          (nbp > end || (len | typ) == 0 ? 1u : 0u) | (end - nbp < kLogHeader ? 2u : 0u));
-      if (f & 1u) break;
-      held = lane == (k & 63u) ? bp - base : held;
-      ++k;
-      if ((k & 63u) == 0) over[k - 64u + lane] = static_cast<uint16_t>(held);
-      bp = nbp;
-      if (f & 2u) break;
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nlen), "+v"(ntyp));
-      len = nlen;
-      typ = ntyp;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nlen), "+v"(ntyp));
-  }
-  const uint32_t p = __builtin_amdgcn_readfirstlane(bp - base);
-  len = __builtin_amdgcn_readfirstlane(len);
-  uint8_t v;
-  if (n - p < kLogHeader)
-    v = (eof && p < n) ? LVKV_LOGBLK_EOF : LVKV_LOGBLK_OK;  // :206-213
-  else if (kLogHeader + len > n - p)
-    v = eof ? LVKV_LOGBLK_EOF : LVKV_LOGBLK_BAD_LENGTH;
-  else
-    v = LVKV_LOGBLK_ZERO;
-  *held_out = held;
-  *count = k;
-  *stop = p;
-  return v;
-}
-
-__global__ void __launch_bounds__(64) log_walk_kernel(LogArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t buf[kBufBytes];
-  const uint32_t lane = lane_id();
-  uint16_t* over = a.over16 + static_cast<uint64_t>(blockIdx.x) * kMaxRecs;
-  // blocks g, g + G, ...: no ticket (a thousand walkers claiming from one
-  // counter at once serialise on it)
-  for (uint32_t b = blockIdx.x; b < a.nblocks; b += gridDim.x) {
-    const uint64_t start = uint64_t{b} * kLogBlock;
-    const uint64_t end = min(a.size, start + kLogBlock);
-    const uint32_t n = static_cast<uint32_t>(end - start);
-    const bool eof = n < kLogBlock;
-    uint32_t shift;
-    {
-      const uint8_t* src = a.file + start;
-      shift = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src) & 15u);
-      const uint32_t nbytes = shift + n;
-      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<uint8_t*>(src - shift), 0, static_cast<int>(nbytes), kBufferDword3);
-      const uint32_t lines = nbytes >> 4;
-      for (uint32_t i = 0; i * 64u < lines; ++i) {
-        const uint32_t line = i * 64u + lane;
-        if (line < lines)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              r, (__attribute__((address_space(3))) void*)(buf + 1024u * i), 16, 16u * line, 0, 0,
-              0);
-      }
-      if (lane < (nbytes & 15u)) buf[16u * lines + lane] = (src - shift)[16u * lines + lane];
-      __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) lgkmcnt(0): the DMA and the tail have landed
-    }
-    uint32_t held, c, stop_at;
-    const uint8_t walked = walk_only(buf + shift, n, eof, over, &held, &c, &stop_at);
-    uint32_t off = 0;
-    if (lane == 0) off = __hip_atomic_fetch_add(a.stg_top, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    off = __builtin_amdgcn_readfirstlane(off);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the overflow positions have landed
-    const uint32_t full = c & ~63u;
-    for (uint32_t j = lane; j < c && off + j < a.capacity; j += 64) {
-      const uint32_t p = j < full ? static_cast<uint32_t>(over[j]) : held;
-      a.stg_hdr[off + j] = start + p;
-    }
-    if (lane == 0) {
-      a.first_bad[b] = 0xffffffffu;
-      a.info[b] = make_ulonglong2(uint64_t{c} | (uint64_t{walked} << 32),
-                                  uint64_t{walked == LVKV_LOGBLK_BAD_LENGTH ? n - stop_at : 0u} |
-                                      (uint64_t{off} << 32));
-    }
-  }
-}
-
-// The merge, one wave per block: the block's first mismatch (the CRC launch's
-// first_bad) drops the rest of the block (:248-255); records placed in file
-// order (the counts of the blocks before it, summed by each workgroup), with
-// their ReadRecord events; the last workgroup writes the report; workgroup 0
-// leaves the counters at 0 for the next call.
-__global__ void __launch_bounds__(64 * 16) log_emit2_kernel(LogArgs a) {
-  constexpr uint32_t kW = 16;
-  __shared__ unsigned long long s_cnt[kW], s_good[kW], s_drop[kW];
-  __shared__ uint32_t s_corrupt[kW], s_first[kW];
-  const uint32_t tid = threadIdx.x;
-  const uint32_t lane = lane_id();
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t b0 = blockIdx.x * kW;
-  const bool last = blockIdx.x + 1 == gridDim.x;
-  if (blockIdx.x == 0 && tid == 0) {
-    *a.ticket = 0;
-    *a.stg_top = 0;
-  }
-  const uint32_t upto = last ? a.nblocks : min(b0, a.nblocks);
-  unsigned long long cnt = 0, good = 0, drop = 0;
-  uint32_t corrupt = 0, fb = 0xffffffffu;
-  for (uint32_t b = tid; b < upto; b += 64 * kW) {
-    const ulonglong2 v = a.info[b];
-    const uint32_t c = static_cast<uint32_t>(v.x);
-    if (b < b0) cnt += c;
-    if (last) {
-      const uint32_t fbad = a.first_bad[b];
-      const uint32_t off = static_cast<uint32_t>(v.y >> 32);
-      const uint32_t walked = static_cast<uint32_t>(v.x >> 32);
-      if (fbad != 0xffffffffu) {
-        good += fbad - off;
-        ++corrupt;
-        drop += min(a.size, (uint64_t{b} + 1) * kLogBlock) - a.stg_hdr[fbad];
-        fb = min(fb, b);
-      } else {
-        good += c;
-        if (walked == LVKV_LOGBLK_BAD_LENGTH) {
-          ++corrupt;
-          drop += static_cast<uint32_t>(v.y);
-          fb = min(fb, b);
-        }
-      }
-      if (b >= b0) cnt += uint64_t{c} << 32;
-    }
-  }
-#pragma unroll
-  for (uint32_t dd = 32; dd >= 1; dd >>= 1) {
-    cnt += __shfl_xor(cnt, dd, 64);
-    good += __shfl_xor(good, dd, 64);
-    drop += __shfl_xor(drop, dd, 64);
-    corrupt += __shfl_xor(corrupt, dd, 64);
-    fb = min(fb, static_cast<uint32_t>(__shfl_xor(fb, dd, 64)));
-  }
-  if (lane == 0) {
-    s_cnt[wave] = cnt;
-    s_good[wave] = good;
-    s_drop[wave] = drop;
-    s_corrupt[wave] = corrupt;
-    s_first[wave] = fb;
-  }
-  __syncthreads();
-  unsigned long long before = 0, mine_all = 0;
-#pragma unroll
-  for (uint32_t w = 0; w < kW; ++w) {
-    before += s_cnt[w] & 0xffffffffull;
-    mine_all += s_cnt[w] >> 32;
-  }
-  if (last && tid == 0) {
-    unsigned long long g = 0, d = 0;
-    uint32_t nc = 0, f = 0xffffffffu;
-#pragma unroll
-    for (uint32_t w = 0; w < kW; ++w) {
-      g += s_good[w];
-      d += s_drop[w];
-      nc += s_corrupt[w];
-      f = min(f, s_first[w]);
-    }
-    const uint64_t total = before + mine_all;
-    lvkv_log_report* r = a.r;
-    r->status = total > a.capacity ? LVKV_LOG_CAPACITY : LVKV_OK;
-    r->nblocks = a.nblocks;
-    r->nrecords = static_cast<uint32_t>(total);
-    r->ngood = static_cast<uint32_t>(g);
-    r->ncorrupt = nc;
-    r->first_bad_block = f;
-    r->dropped_bytes = d;
-    r->count_ = total > a.capacity ? 0u : static_cast<uint32_t>(total);
-    r->reserved_ = 0;
-  }
-  const uint32_t b = b0 + wave;
-  if (b >= a.nblocks) return;
-  uint32_t pre = lane < wave ? static_cast<uint32_t>(a.info[b0 + lane].x) : 0u;
-#pragma unroll
-  for (uint32_t dd = 32; dd >= 1; dd >>= 1) pre += __shfl_xor(pre, dd, 64);
-  const uint64_t base = before + pre;
-  const ulonglong2 v = a.info[b];
-  const uint32_t c = static_cast<uint32_t>(v.x);
-  const uint32_t off = static_cast<uint32_t>(v.y >> 32);
-  const uint32_t fbad = a.first_bad[b];
-  const uint32_t bad = fbad != 0xffffffffu ? fbad - off : 0xffffffffu;
-  const uint64_t bend = min(a.size, (uint64_t{b} + 1) * kLogBlock);
-  uint8_t status = static_cast<uint8_t>(v.x >> 32);
-  uint32_t bdrop = static_cast<uint32_t>(v.y);
-  if (bad != 0xffffffffu) {
-    status = LVKV_LOGBLK_CHECKSUM;
-    bdrop = static_cast<uint32_t>(bend - a.stg_hdr[fbad]);
-  }
-  for (uint32_t j = lane; j < c; j += 64) {
-    const uint64_t gi = base + j;
-    if (gi >= a.capacity || off + j >= a.capacity) break;
-    const uint64_t h = a.stg_hdr[off + j];
-    const uint8_t rs = j < bad ? LVKV_REC_OK : j == bad ? LVKV_REC_CHECKSUM : LVKV_REC_DROPPED;
-    a.hdr_off[gi] = h;
-    a.actual[gi] = a.stg_actual[off + j];
-    a.rec_status[gi] = rs;
-    if (a.events != nullptr) {
-      const uint32_t len = static_cast<uint32_t>(a.file[h + 4]) | (static_cast<uint32_t>(a.file[h + 5]) << 8);
-      a.events[gi + b] = rs == LVKV_REC_OK ? log_event(kEvRec, a.file[h + 6], len)
-                                          : log_event(kEvSkip, 0, 0);
-    }
-  }
-  if (lane == 0) {
-    a.block_status[b] = status;
-    a.block_drop[b] = bdrop;
-    if (a.events != nullptr && base + c <= a.capacity)
-      a.events[base + c + b] = log_block_event(status, bdrop);
-  }
-}
-
 constexpr uint32_t kEmitWaves = 16;  // blocks per emit workgroup (one wave each)
 
 // The staged results to their places, one wave per block: record j of block
@@ -1050,6 +984,7 @@ __global__ void __launch_bounds__(64 * kEmitWaves) log_emit_kernel(LogArgs a) {
   if (blockIdx.x == 0 && tid == 0) {
     *a.ticket = 0;
     *a.stg_top = 0;
+    if (a.wover_top != nullptr) *a.wover_top = 0;
   }
   // counts before b0 (and, in the last workgroup, every block's totals)
   const uint32_t upto = last ? a.nblocks : min(b0, a.nblocks);
@@ -1141,7 +1076,8 @@ __global__ void __launch_bounds__(64 * kEmitWaves) log_emit_kernel(LogArgs a) {
 }
 
 // Scratch: [0, 8) unused, [8, 16) the logical layer's counter (not touched
-// here), [16, 20) ticket counter, [20, 24) staging counter, then from byte
+// here), [16, 20) ticket counter, [20, 24) staging counter, [24, 28) the
+// walk-first path's overflow counter, then from byte
 // 32 info (16 B per block), stg_off (u32 per block) and 4 unused bytes per block,
 // the staging array (16 B per record, `capacity` of them) and the slots'
 // overflow positions (u32, kPosOver per slot of each of the grid's
@@ -1164,35 +1100,32 @@ uint64_t* g_log_stamps = nullptr;  // lvkv_debug_log_stamps
 uint32_t g_log_knobs = 0;          // lvkv_debug_log_knobs (LogArgs::knobs)
 #endif
 
-// Walkers of the walk path.
+// Walkers of the walk-first path.
 uint32_t walk_groups(uint64_t nblocks, int cus) {
   return static_cast<uint32_t>(std::max<uint64_t>(
       1, std::min<uint64_t>(nblocks, uint64_t{kWalkPerCu} * static_cast<uint64_t>(cus))));
 }
 
-// The walk path's layout after the head: first_bad (u32 per block), then
-// 16-aligned stg_hdr (u64), stg_actual (u32), stg_status (u8) per staged
-// record, then each walker's overflow positions (u16 x kMaxRecs).
+// The slot path's layout (head, staging, the slots' overflow positions),
+// then the walk-first path's: winfo (16 B per block), wpos (kWalkSlot u16
+// per block), wover (u16 per record), the walkers' scratch (u16 x kMaxRecs
+// each); offsets 16-aligned.
+size_t slot_scratch_bytes(uint64_t nblocks, uint32_t capacity, int cus) {
+  return log_scratch_head(nblocks) + size_t{capacity} * 16 +
+         size_t{log_groups(nblocks, cus)} * kSlots * kPosOver * 4;
+}
 size_t walk_scratch_bytes(uint64_t nblocks, uint32_t capacity, int cus) {
-  size_t at = log_scratch_head(nblocks) + ((static_cast<size_t>(nblocks) * 4 + 15) & ~size_t{15});
-  at += size_t{capacity} * 8 + ((size_t{capacity} * 5 + 15) & ~size_t{15});
+  size_t at = (slot_scratch_bytes(nblocks, capacity, cus) + 15) & ~size_t{15};
+  at += static_cast<size_t>(nblocks) * 16;
+  at += (static_cast<size_t>(nblocks) * kWalkSlot * 2 + 15) & ~size_t{15};
+  at += (size_t{capacity} * 2 + 15) & ~size_t{15};
   return at + size_t{walk_groups(nblocks, cus)} * kMaxRecs * 2;
 }
 
 size_t log_scratch_bytes(uint64_t size, uint32_t capacity, int cus) {
   const uint64_t nblocks = (size + kLogBlock - 1) / kLogBlock;
-  const size_t slots = log_scratch_head(nblocks) + size_t{capacity} * 16 +
-                       size_t{log_groups(nblocks, cus)} * kSlots * kPosOver * 4;
-  return std::max(slots, walk_scratch_bytes(nblocks, capacity, cus));
+  return walk_scratch_bytes(nblocks, capacity, cus);
 }
-
-// `scratch`: log_scratch_bytes(size, capacity, cus) bytes, 16-byte aligned,
-// its counters 0 (zeroed when allocated; every call leaves them at 0), used
-// by one call at a time. Two launches: the verify, then the emit.
-hipError_t launch_crc32c_lanes(const KernelArgs& a, const uint32_t* zpow,
-                               const uint32_t* lane_cols, int num_groups, hipStream_t stream);
-// WAL records the lane walk leaves to its workgroup (crc32c_lanes.h)
-constexpr uint32_t kLanesLogLong = 4096;
 
 hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_off,
                              uint32_t* actual, uint8_t* rec_status, uint32_t capacity,
@@ -1226,36 +1159,22 @@ hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_o
   a.stamps = g_log_stamps;
   a.knobs = g_log_knobs;
 #endif
-  if (path == 1) {  // walk, ragged CRC launch, merge
-    uint8_t* w = sb + log_scratch_head(nblocks);
-    a.first_bad = reinterpret_cast<uint32_t*>(w);
-    w += (static_cast<size_t>(nblocks) * 4 + 15) & ~size_t{15};
-    a.stg_hdr = reinterpret_cast<uint64_t*>(w);
-    a.stg_actual = reinterpret_cast<uint32_t*>(w + size_t{capacity} * 8);
-    a.stg_status = w + size_t{capacity} * 12;
-    w += size_t{capacity} * 8 + ((size_t{capacity} * 5 + 15) & ~size_t{15});
+  if (path == 1) {  // walk first: the verify loads the walked positions
+    uint8_t* w = sb + ((slot_scratch_bytes(nblocks, capacity, cus) + 15) & ~size_t{15});
+    a.winfo = reinterpret_cast<ulonglong2*>(w);
+    w += static_cast<size_t>(nblocks) * 16;
+    a.wpos = reinterpret_cast<uint16_t*>(w);
+    w += (static_cast<size_t>(nblocks) * kWalkSlot * 2 + 15) & ~size_t{15};
+    a.wover = reinterpret_cast<uint16_t*>(w);
+    w += (size_t{capacity} * 2 + 15) & ~size_t{15};
     a.over16 = reinterpret_cast<uint16_t*>(w);
-    hipError_t e;
+    a.wover_top = reinterpret_cast<uint32_t*>(sb + 24);
+    a.pre = 1;
     if (nblocks != 0) {
       hipLaunchKernelGGL(log_walk_kernel, dim3(walk_groups(nblocks, cus)), dim3(64), 0, stream, a);
-      if ((e = hipGetLastError()) != hipSuccess) return e;
-      KernelArgs k;
-      memset(&k, 0, sizeof(k));
-      k.base = file;
-      k.offsets = a.stg_hdr;
-      k.out_crc = a.stg_actual;
-      k.out_status = a.stg_status;
-      k.nblocks = capacity;
-      k.count = a.stg_top;
-      k.mode = kModeLogStaged;
-      k.long_split = kLogLongBytes;
-      k.log_first_bad = a.first_bad;
-      k.long_split = kLanesLogLong;
-      if ((e = launch_crc32c_lanes(k, zpow, lane_cols, 2 * cus, stream)) != hipSuccess) return e;
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(log_emit2_kernel, dim3(std::max<uint32_t>(1, (nblocks + 15) / 16)),
-                       dim3(64 * 16), 0, stream, a);
-    return hipGetLastError();
   }
   if (nblocks != 0) {
     hipLaunchKernelGGL(log_verify_kernel, dim3(log_groups(nblocks, cus)), dim3(kVThreads), 0,

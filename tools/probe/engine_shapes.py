@@ -42,7 +42,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", default=",".join(CASES))
     ap.add_argument("--reps", type=int, default=40)
-    ap.add_argument("--specs", default="-1,2,3,4,5,6,7,8",
+    ap.add_argument("--specs", default="-1,2,3,4,5",
                     help="lvkv_debug_engine_ragged_spec values (-1: the engine's choice)")
     args = ap.parse_args()
     lvkv = g.load_package()
