@@ -661,8 +661,7 @@ class Engine:
         if nblocks and (nblocks - 1) * stride + length > buf.numel():
             raise ValueError("blocks exceed the buffer")
         out = _u32_out(torch, nblocks, buf.device, out)
-        flags = ((LVKV_FLAG_MASK if mask else 0) | (LVKV_FLAG_ORDERED if ordered else 0) |
-                 (LVKV_FLAG_SYSTEM_ACQUIRE if fresh else 0) | (LVKV_FLAG_FINAL if final else 0))
+        flags = self._flags(mask, ordered, fresh, final)
         # the engine does not follow HIP streams: the inputs must be complete
         torch.cuda.current_stream(buf.device).synchronize()
         rc = _lib.lvkv_engine_crc32c_uniform(
@@ -672,12 +671,13 @@ class Engine:
         self._inflight.append((buf, out))
         return out
 
-    def _flags(self, mask=False, ordered=False, fresh=True):
+    def _flags(self, mask=False, ordered=False, fresh=True, final=False):
         return ((LVKV_FLAG_MASK if mask else 0) | (LVKV_FLAG_ORDERED if ordered else 0) |
-                (LVKV_FLAG_SYSTEM_ACQUIRE if fresh else 0))
+                (LVKV_FLAG_SYSTEM_ACQUIRE if fresh else 0) | (LVKV_FLAG_FINAL if final else 0))
 
     def crc32c_batch(self, buf, offsets, lengths, *, init: int = 0, inits=None,
-                     mask: bool = False, ordered: bool = False, fresh: bool = True, out=None):
+                     mask: bool = False, ordered: bool = False, fresh: bool = True,
+                     final: bool = False, out=None):
         """lvkv_engine_crc32c_batch: crc32c_batch's contract on the engine."""
         torch = _torch()
         n = offsets.numel()
@@ -691,12 +691,12 @@ class Engine:
             _dev_ptr(lengths, "lengths", (torch.int32,)),
             _dev_ptr(inits, "inits", (torch.int32,), n) if inits is not None else None,
             init & 0xFFFFFFFF, _dev_ptr(out, "out", (torch.int32,), n), n,
-            self._flags(mask, ordered, fresh))
+            self._flags(mask, ordered, fresh, final))
         _check("lvkv_engine_crc32c_batch", rc)
         self._inflight.append((buf, offsets, lengths, inits, out))
         return out
 
-    def sst_verify(self, file_buf, offsets, sizes, *, ordered=False, fresh=True):
+    def sst_verify(self, file_buf, offsets, sizes, *, ordered=False, fresh=True, final=False):
         """lvkv_engine_sst_verify: (actual int32, status uint8) as sst_verify."""
         torch = _torch()
         n = offsets.numel()
@@ -707,12 +707,12 @@ class Engine:
             self.handle, _dev_ptr(file_buf, "file_buf", (torch.uint8, torch.int8)),
             _dev_ptr(offsets, "offsets", (torch.int64,)), _dev_ptr(sizes, "sizes", (torch.int32,), n),
             _dev_ptr(actual, "actual"), _dev_ptr(status, "status"), n,
-            self._flags(False, ordered, fresh))
+            self._flags(False, ordered, fresh, final))
         _check("lvkv_engine_sst_verify", rc)
         self._inflight.append((file_buf, offsets, sizes, actual, status))
         return actual, status
 
-    def log_verify(self, file_buf, hdr_offsets, *, ordered=False, fresh=True):
+    def log_verify(self, file_buf, hdr_offsets, *, ordered=False, fresh=True, final=False):
         """lvkv_engine_log_verify: (actual int32, status uint8) as log_verify."""
         torch = _torch()
         n = hdr_offsets.numel()
@@ -722,12 +722,12 @@ class Engine:
         rc = _lib.lvkv_engine_log_verify(
             self.handle, _dev_ptr(file_buf, "file_buf", (torch.uint8, torch.int8)),
             _dev_ptr(hdr_offsets, "hdr_offsets", (torch.int64,)), _dev_ptr(actual, "actual"),
-            _dev_ptr(status, "status"), n, self._flags(False, ordered, fresh))
+            _dev_ptr(status, "status"), n, self._flags(False, ordered, fresh, final))
         _check("lvkv_engine_log_verify", rc)
         self._inflight.append((file_buf, hdr_offsets, actual, status))
         return actual, status
 
-    def sst_fill_trailers(self, file_buf, offsets, sizes, *, ordered=False, fresh=True):
+    def sst_fill_trailers(self, file_buf, offsets, sizes, *, ordered=False, fresh=True, final=False):
         """lvkv_engine_sst_fill_trailers: sst_fill_trailers on the engine."""
         torch = _torch()
         n = offsets.numel()
@@ -736,12 +736,12 @@ class Engine:
         rc = _lib.lvkv_engine_sst_fill_trailers(
             self.handle, _dev_ptr(file_buf, "file_buf", (torch.uint8, torch.int8)),
             _dev_ptr(offsets, "offsets", (torch.int64,)), _dev_ptr(sizes, "sizes", (torch.int32,), n),
-            _dev_ptr(crc, "crc"), n, self._flags(False, ordered, fresh))
+            _dev_ptr(crc, "crc"), n, self._flags(False, ordered, fresh, final))
         _check("lvkv_engine_sst_fill_trailers", rc)
         self._inflight.append((file_buf, offsets, sizes, crc))
         return crc
 
-    def log_fill_headers(self, file_buf, hdr_offsets, *, ordered=False, fresh=True):
+    def log_fill_headers(self, file_buf, hdr_offsets, *, ordered=False, fresh=True, final=False):
         """lvkv_engine_log_fill_headers: log_fill_headers on the engine."""
         torch = _torch()
         n = hdr_offsets.numel()
@@ -750,7 +750,7 @@ class Engine:
         rc = _lib.lvkv_engine_log_fill_headers(
             self.handle, _dev_ptr(file_buf, "file_buf", (torch.uint8, torch.int8)),
             _dev_ptr(hdr_offsets, "hdr_offsets", (torch.int64,)), _dev_ptr(crc, "crc"), n,
-            self._flags(False, ordered, fresh))
+            self._flags(False, ordered, fresh, final))
         _check("lvkv_engine_log_fill_headers", rc)
         self._inflight.append((file_buf, hdr_offsets, crc))
         return crc

@@ -232,6 +232,29 @@ __device__ __forceinline__ void rag_store(const KernelArgs& a, uint32_t b, const
   }
 }
 
+// Where a walk's blocks come from and where its results go: the batch's
+// descriptor arrays and rag_store (ArgsSrc), or a caller's own list (the
+// whole-SSTable verify's entries decoded into LDS, lvkv_sst_table.hip).
+struct ArgsSrc {
+  __device__ __forceinline__ RagBlock block(const KernelArgs& a, uint32_t b, bool live) const {
+    return rag_block(a, b, live);
+  }
+  __device__ __forceinline__ void store(const KernelArgs& a, uint32_t b, const RagBlock& g,
+                                        uint32_t crc) const {
+    rag_store(a, b, g, crc);
+  }
+  // covered length of block b, as rag_block computes it (the long-block scan)
+  __device__ __forceinline__ uint32_t covered(const KernelArgs& a, uint32_t b) const {
+    const bool sst = a.mode == kModeSstVerify || a.mode == kModeSstFill || a.mode == kModeSstTable;
+    const bool log = a.mode == kModeLogVerify || a.mode == kModeLogFill || a.mode == kModeLogStaged;
+    if (log) {
+      const uint8_t* h = a.base + fresh_ld(a, a.offsets + b);
+      return 1u + (static_cast<uint32_t>(h[4]) | (static_cast<uint32_t>(h[5]) << 8));
+    }
+    return (a.offsets == nullptr ? a.length : fresh_ld(a, a.lengths + b)) + (sst ? 1u : 0u);
+  }
+};
+
 // One round of one wave: NCH chains (blocks), chunk k of each in flight.
 template <int NCH, int R>
 struct RagRound {
@@ -241,13 +264,14 @@ struct RagRound {
   uint32_t w[NCH][R + 1];  // row R: the neighbour dwords of row R - 1
 
   // Chain c of round r0 is block start + r0 + c * W + wave.
+  template <class Src>
   __device__ static __forceinline__ void fetch(RagBlock (&out)[NCH], const KernelArgs& a,
-                                               uint32_t start, uint32_t n, uint32_t r0,
-                                               uint32_t wave, uint32_t W) {
+                                               const Src& src, uint32_t start, uint32_t n,
+                                               uint32_t r0, uint32_t wave, uint32_t W) {
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const uint32_t i = r0 + static_cast<uint32_t>(c) * W + wave;
-      out[c] = rag_block(a, start + i, i < n);
+      out[c] = src.block(a, start + i, i < n);
     }
   }
   __device__ __forceinline__ void adopt(const RagBlock (&in)[NCH], uint32_t start, uint32_t r0,
@@ -316,10 +340,11 @@ struct RagLds {
 // instead of a second kernel launch per batch. The run's lengths are scanned
 // 64 * W at a time only when a wave met one (lds[kFlag], set by the walk).
 // Every thread of the workgroup calls it.
-template <int W>
+template <int W, class Src = ArgsSrc>
 __device__ __forceinline__ void ragged_long_pass(const KernelArgs& a, const uint32_t* zpow,
                                                  uint32_t* lds, uint32_t start, uint32_t n,
-                                                 const LaneKeys& keys, uint32_t lane_base) {
+                                                 const LaneKeys& keys, uint32_t lane_base,
+                                                 const Src& src = Src()) {
   constexpr uint32_t kAcc = RagLds<W>::kAcc, kFlag = RagLds<W>::kFlag,
                      kList = RagLds<W>::kList, kCount = RagLds<W>::kCount;
   const uint32_t tid = threadIdx.x;
@@ -327,28 +352,17 @@ __device__ __forceinline__ void ragged_long_pass(const KernelArgs& a, const uint
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   __syncthreads();
   if (lds[kFlag] == 0) return;
-  const bool sst = a.mode == kModeSstVerify || a.mode == kModeSstFill || a.mode == kModeSstTable;
-  const bool log = a.mode == kModeLogVerify || a.mode == kModeLogFill || a.mode == kModeLogStaged;
   for (uint32_t slice = 0; slice < n; slice += 64 * W) {
     if (tid == 0) lds[kCount] = 0;
     __syncthreads();
     const uint32_t i = slice + tid;
-    if (i < n) {
-      uint32_t clen;  // covered length, as rag_block computes it
-      if (log) {
-        const uint8_t* h = a.base + fresh_ld(a, a.offsets + start + i);
-        clen = 1u + (static_cast<uint32_t>(h[4]) | (static_cast<uint32_t>(h[5]) << 8));
-      } else {
-        clen = (a.offsets == nullptr ? a.length : fresh_ld(a, a.lengths + start + i)) +
-               (sst ? 1u : 0u);
-      }
-      if (clen > a.long_split) lds[kList + atomicAdd(&lds[kCount], 1u)] = start + i;
-    }
+    if (i < n && src.covered(a, start + i) > a.long_split)
+      lds[kList + atomicAdd(&lds[kCount], 1u)] = start + i;
     __syncthreads();
     const uint32_t cnt = __builtin_amdgcn_readfirstlane(lds[kCount]);
     for (uint32_t li = 0; li < cnt; ++li) {
       const uint32_t b = __builtin_amdgcn_readfirstlane(lds[kList + li]);
-      const RagBlock g = rag_block(a, b, true);
+      const RagBlock g = src.block(a, b, true);
       // WAL fragments (<= 32 KiB): 4 KiB segments, one per wave; longer
       // blocks: 16 KiB segments
       const uint32_t crc =
@@ -357,7 +371,7 @@ __device__ __forceinline__ void ragged_long_pass(const KernelArgs& a, const uint
                                        g.s0 ^ 0xffffffffu, keys, tid, wave, lane, lane_base, zpow)
               : workgroup_crc<W>(lds, lds + kAcc, g.ptr(), g.ptr() + g.len, g.s0 ^ 0xffffffffu,
                                  keys, tid, wave, lane, lane_base, zpow);
-      if (tid == 0) rag_store(a, b, g, crc);
+      if (tid == 0) src.store(a, b, g, crc);
     }
     __syncthreads();
   }
@@ -367,11 +381,11 @@ __device__ __forceinline__ void ragged_long_pass(const KernelArgs& a, const uint
 // the caller built the compact image in `lds` (and zeroed lds[kFlag]) before
 // a barrier; otherwise it is built here, overlapped with the first loads.
 // Every thread of the workgroup calls it; it returns workgroup-uniformly.
-template <int W, int NCH, int R>
+template <int W, int NCH, int R, class Src = ArgsSrc>
 __device__ __forceinline__ void ragged_run(const KernelArgs& a, const uint32_t* zpow,
                                            const uint32_t* lane_cols, uint32_t* lds,
                                            uint32_t grp, uint32_t G, uint32_t total,
-                                           bool image_ready) {
+                                           bool image_ready, const Src& src = Src()) {
   constexpr uint32_t kFlag = RagLds<W>::kFlag;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = lane_id();
@@ -395,7 +409,7 @@ __device__ __forceinline__ void ragged_run(const KernelArgs& a, const uint32_t* 
   RagRound<NCH, R> rd;
   if (image_ready) {
     RagBlock g0[NCH];
-    RagRound<NCH, R>::fetch(g0, a, start, n, 0, wave, W);
+    RagRound<NCH, R>::fetch(g0, a, src, start, n, 0, wave, W);
     rd.adopt(g0, start, 0, wave, W);
     rd.issue(0, lane);
   } else {
@@ -405,7 +419,7 @@ __device__ __forceinline__ void ragged_run(const KernelArgs& a, const uint32_t* 
     lg.load(lane_cols, wave, lane);
     {
       RagBlock g0[NCH];
-      RagRound<NCH, R>::fetch(g0, a, start, n, 0, wave, W);
+      RagRound<NCH, R>::fetch(g0, a, src, start, n, 0, wave, W);
       rd.adopt(g0, start, 0, wave, W);
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -428,7 +442,7 @@ __device__ __forceinline__ void ragged_run(const KernelArgs& a, const uint32_t* 
     //    dependent scalar loads) fetched while this round's rows are in
     //    flight. Row 0: start every chain (fix-ups) or continue it. Idle
     //    chains walk zeros and store nothing.
-    if (k == 0) RagRound<NCH, R>::fetch(gn, a, start, n, r0 + W * NCH, wave, W);
+    if (k == 0) RagRound<NCH, R>::fetch(gn, a, src, start, n, r0 + W * NCH, wave, W);
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
       if (rd.g[c].e() != 0) rd.realign(c, lane);
@@ -479,14 +493,14 @@ __device__ __forceinline__ void ragged_run(const KernelArgs& a, const uint32_t* 
     for (int c = 0; c < NCH; ++c) {
       if (nrow[c] > 0 && rd.g[c].rows() <= (k + 1) * R) {
         const uint32_t crc = wave_xor_dpp(lane_end_shift_c(lds, st[c], lane_base)) ^ 0xffffffffu;
-        rag_store(a, rd.blk[c], rd.g[c], crc);
+        src.store(a, rd.blk[c], rd.g[c], crc);
       }
     }
     // 5. next chunk of this round, or the next round
     if (++k == rd.nchunks) {
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
-        if (rd.g[c].kind == kRagTiny) rag_store(a, rd.blk[c], rd.g[c], rag_tiny(rd.g[c]));
+        if (rd.g[c].kind == kRagTiny) src.store(a, rd.blk[c], rd.g[c], rag_tiny(rd.g[c]));
         if (rd.g[c].kind == kRagSkip && lane == 0) lds[kFlag] = 1;
       }
       r0 += W * NCH;
@@ -498,7 +512,7 @@ __device__ __forceinline__ void ragged_run(const KernelArgs& a, const uint32_t* 
   }
 
   // 6. Blocks over kLongBytes in this run (rare)
-  ragged_long_pass<W>(a, zpow, lds, start, n, keys, lane_base);
+  ragged_long_pass<W>(a, zpow, lds, start, n, keys, lane_base, src);
 }
 
 }  // namespace

@@ -56,7 +56,7 @@ hipError_t launch_sst_tables(const uint8_t* file, const uint64_t* toff, const ui
                              uint32_t* d_size, uint32_t* d_actual, uint8_t* d_status,
                              uint32_t capacity, lvkv_sst_report* reports, const FilterKey& fk,
                              uint32_t gen, const KernelArgs& verify, const uint32_t* zpow,
-                             const uint32_t* lane_cols, int groups, bool fused,
+                             const uint32_t* lane_cols, int groups, int form,
                              hipStream_t stream);
 hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_off,
                              uint32_t* actual, uint8_t* rec_status, uint32_t capacity,
@@ -118,8 +118,8 @@ struct DeviceCtx {
   // (launch_crc32c_general; lvkv_debug_set_general_kernel/_log_kernel)
   std::atomic<int> general_cfg{0};  // ragged cfg 0: 8 waves x 2 chains x 24 rows
   std::atomic<int> log_cfg{8};      // one workgroup per round of 32 small records
-  // whole-SSTable verify form: 0 by size, 1 fused, 2 two launches
-  // (lvkv_debug_set_sst_form)
+  // whole-SSTable verify form: 0 by size, 1 fused, 2 two launches,
+  // 3 speculative (lvkv_debug_set_sst_form)
   std::atomic<int> sst_form{0};
   // WAL verify: 0 two LDS slots per CU walked and checksummed in one launch,
   // 1 a walk launch first, the slots load its positions (lvkv_debug_set_log_path)
@@ -314,17 +314,26 @@ bool filter_key(const char* policy, FilterKey* fk) {
   return true;
 }
 
-// The fused one-launch SST verify for one table up to this size (larger
-// indexes are faster on the two-launch form's 16-wave heads). Multi-table
-// calls take the two launches by default (measured faster: 41.6 against
-// 48.1 us for 32 x 2 MiB); lvkv_debug_set_sst_form(1) fuses them too, up to
-// kFusedMaxTables (every CRC workgroup polls every head).
+// The one-launch SST verify forms for one table up to this size (larger
+// indexes are faster on the two-launch form's 16-wave heads and its wide
+// index launch). Multi-table calls take the speculative form (each CRC
+// workgroup decodes its own share of one table's index) up to half as many
+// tables as CUs, the two launches beyond.
 constexpr uint64_t kFusedTableBytes = uint64_t{32} << 20;
 constexpr size_t kFusedMaxTables = 256;
 
-bool sst_fused(const DeviceCtx& c, bool by_size, size_t ntables = 1) {
+// kSstForm* for a call: lvkv_debug_set_sst_form's 1 (fused), 2 (two
+// launches), 3 (speculative), or by size (0). The speculative form needs
+// fewer tables than half its grid.
+int sst_form(const DeviceCtx& c, bool by_size, size_t ntables = 1) {
   const int mode = c.sst_form.load(std::memory_order_relaxed);
-  return ntables <= kFusedMaxTables && (mode == 0 ? by_size : mode == 1);
+  const bool spec_ok = ntables * 2 <= static_cast<size_t>(c.groups);
+  switch (mode) {
+    case 1: return ntables <= kFusedMaxTables ? kSstFormFused : kSstFormTwo;
+    case 2: return kSstFormTwo;
+    case 3: return spec_ok ? kSstFormSpec : kSstFormTwo;
+  }
+  return by_size && spec_ok ? kSstFormSpec : kSstFormTwo;
 }
 
 // Per-call tag of the multi-table placement words (never 0: fresh report
@@ -373,7 +382,7 @@ KernelArgs ctx_args(const DeviceCtx& c) {
 // buffer is regrown in place (after its last call has ended: its event is
 // synchronised before the free) or, below four buffers, one is added; the
 // pool exceeds four only while every buffer is lent to a call in progress on
-// another thread. A new buffer's counters (bytes [0, 24)) are zeroed on
+// another thread. A new buffer's counters (bytes [0, 32)) are zeroed on
 // `stream`; every call leaves them at 0. Not capturable: a graph would replay
 // the counters unzeroed. The buffers live as long as the process (the HIP
 // runtime may be gone by the time static destructors run).
@@ -436,7 +445,7 @@ hipError_t log_scratch_acquire(DeviceCtx& c, hipStream_t stream, size_t bytes, v
   b.bytes = 0;
   const size_t cap = std::max<size_t>(bytes, size_t{1} << 16);
   if ((e = hipMalloc(&b.p, cap)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(b.p, 0, 24, stream)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(b.p, 0, 32, stream)) != hipSuccess) return e;
   b.bytes = cap;
   b.lent = true;
   b.stream = stream;
@@ -636,7 +645,7 @@ int lvkv_sst_verify_table_device(const void* d_file, uint64_t file_size,
       static_cast<const uint8_t*>(d_file), nullptr, nullptr, file_size, 1, d_offsets, d_sizes,
       d_actual, d_status, static_cast<uint32_t>(capacity), d_report, fk, next_sst_generation(), a,
       c->d_tables + kZPowOffset, c->d_tables + kRowTabDwords + kLaneTabDwords, c->groups,
-      sst_fused(*c, file_size <= kFusedTableBytes), static_cast<hipStream_t>(stream));
+      sst_form(*c, file_size <= kFusedTableBytes), static_cast<hipStream_t>(stream));
   return e == hipSuccess ? LVKV_OK : hip_fail(e);
 }
 
@@ -662,7 +671,7 @@ int lvkv_sst_verify_tables_device(const void* d_file, const uint64_t* d_table_of
       static_cast<uint32_t>(capacity), d_reports, fk, next_sst_generation(), a,
       c->d_tables + kZPowOffset,
       c->d_tables + kRowTabDwords + kLaneTabDwords, c->groups,
-      sst_fused(*c, false, ntables), static_cast<hipStream_t>(stream));
+      sst_form(*c, true, ntables), static_cast<hipStream_t>(stream));
   return e == hipSuccess ? LVKV_OK : hip_fail(e);
 }
 
@@ -1025,9 +1034,10 @@ int lvkv_debug_set_log_kernel(int k) {
 }
 
 // Whole-SSTable verify form: 0 by size (default), 1 always the fused launch,
-// 2 always the two launches. Timing and tests.
+// 2 always the two launches, 3 the speculative launch where it applies.
+// Timing and tests.
 int lvkv_debug_set_sst_form(int form) {
-  if (form < 0 || form > 2) return LVKV_ERR_INVALID;
+  if (form < 0 || form > 3) return LVKV_ERR_INVALID;
   int rc = LVKV_OK;
   DeviceCtx* c = current_ctx(&rc);
   if (c == nullptr) return rc;

@@ -110,6 +110,9 @@ struct KernelArgs {
                               //   by a kernel
 };
 
+// Whole-SSTable verify forms (launch_sst_tables, lvkv_sst_table.hip).
+enum : int { kSstFormTwo = 0, kSstFormFused = 1, kSstFormSpec = 2 };
+
 // "filter." + FilterPolicy::Name() (table/table.cc:100-101), the metaindex
 // key the whole-SSTable verify looks for; len 0: no filter policy.
 constexpr uint32_t kMaxFilterKey = 7 + LVKV_SST_MAX_POLICY_NAME;

@@ -350,6 +350,8 @@ struct AsmArgs {
   lvkv_log_corruption* reps;
   lvkv_log_read_report* out;
   Agg* aggs;        // per workgroup (log_asm_reduce)
+  Agg* pref;        // many workgroups: per 64-workgroup window, the windows
+                    // before it composed (log_asm_scan); else nullptr
   uint64_t* stamps;  // probe build only: 8 u64 per workgroup
 };
 
@@ -626,6 +628,42 @@ __global__ void __launch_bounds__(kGT) log_asm_reduce(AsmArgs a) {
   if (threadIdx.x == 0) a.aggs[blockIdx.x] = it.agg;
 }
 
+// Past this many workgroups the emit no longer folds every aggregate before
+// its own (a quadratic total): log_asm_scan composes the 64-workgroup
+// windows' prefixes first, and each emit workgroup folds one window. (The
+// scan is launched when the host's bound, from the capacity, passes it, and
+// does nothing when the items on the device do not.)
+constexpr uint32_t kAsmFoldMax = 1024;
+
+// ReadRecord, between the two launches when there are many workgroups: the
+// exclusive prefix of every 64-workgroup window (pref[k] = windows 0..k-1
+// composed). One workgroup; each wave folds a contiguous share of the windows
+// (window_fold), the shares' totals are composed in LDS, and each wave walks
+// its share again writing the running prefix. Linear in the workgroups.
+__global__ void __launch_bounds__(kGT) log_asm_scan(AsmArgs a) {
+  __shared__ Agg wtot[kGT / 64];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63u, w = tid >> 6;
+  const uint32_t G = asm_groups(a, asm_items(a));
+  if (G <= kAsmFoldMax) return;  // the emit folds (the host knew only a bound)
+  const uint32_t nwin = (G + 63) / 64;
+  const uint32_t k0 = w * nwin / (kGT / 64), k1 = (w + 1) * nwin / (kGT / 64);
+  Agg part = kAggIdentity;
+  for (uint32_t k = k0; k < k1; ++k) {
+    const uint32_t idx = k * 64 + lane;
+    part = agg_compose(part, window_fold(idx < G ? a.aggs[idx] : kAggIdentity, lane));
+  }
+  if (lane == 0) wtot[w] = part;
+  __syncthreads();
+  Agg run = kAggIdentity;
+  for (uint32_t v = 0; v < w; ++v) run = agg_compose(run, wtot[v]);
+  for (uint32_t k = k0; k < k1; ++k) {
+    if (lane == 0) a.pref[k] = run;
+    const uint32_t idx = k * 64 + lane;
+    run = agg_compose(run, window_fold(idx < G ? a.aggs[idx] : kAggIdentity, lane));
+  }
+}
+
 // ReadRecord, launch 2 of 2: the waves fold the aggregates of the
 // workgroups before this one (64 at a time, window_fold; each wave a
 // contiguous share) into its entering state and output positions, and the
@@ -647,12 +685,21 @@ __global__ void __launch_bounds__(kGT) log_asm_emit(AsmArgs a) {
   if (tid == 0) asm_stamp(a, 0);
   {
     // the workgroups before g, 64 a window; wave w folds its contiguous
-    // share of the windows, the shares are composed below
+    // share of the windows, the shares are composed below. With the windows'
+    // prefixes scanned (a.pref): wave 0 takes g's window prefix and folds the
+    // workgroups of g's own window before it.
     const uint32_t w = tid >> 6, nwin = (g + 63) / 64;
     Agg part = kAggIdentity;
-    for (uint32_t wi = w * nwin / (kGT / 64); wi < (w + 1) * nwin / (kGT / 64); ++wi) {
-      const uint32_t idx = wi * 64 + lane;
-      part = agg_compose(part, window_fold(idx < g ? a.aggs[idx] : kAggIdentity, lane));
+    if (a.pref != nullptr && G > kAsmFoldMax) {
+      if (w == 0) {
+        const uint32_t idx = (g & ~63u) + lane;
+        part = agg_compose(a.pref[g >> 6], window_fold(idx < g ? a.aggs[idx] : kAggIdentity, lane));
+      }
+    } else {
+      for (uint32_t wi = w * nwin / (kGT / 64); wi < (w + 1) * nwin / (kGT / 64); ++wi) {
+        const uint32_t idx = wi * 64 + lane;
+        part = agg_compose(part, window_fold(idx < g ? a.aggs[idx] : kAggIdentity, lane));
+      }
     }
     if (lane == 0) part_s[w] = part;
     if (tid == 0) asm_stamp(a, 1);
@@ -991,7 +1038,8 @@ uint64_t* g_asm_stamps = nullptr;  // lvkv_debug_asm_stamps
 
 size_t log_asm_scratch_bytes(size_t max_items) {
   const size_t groups = (max_items + kGT - 1) / kGT;
-  return groups * sizeof(Agg) + 16;  // + log_asm_seek's two words
+  // the aggregates, the window prefixes, log_asm_seek's two words
+  return (groups + (groups + 63) / 64) * sizeof(Agg) + 16;
 }
 
 // `scratch`: log_asm_scratch_bytes(capacity + nblocks) bytes, 16-byte aligned
@@ -1022,7 +1070,9 @@ hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
 #else
   a.stamps = nullptr;
 #endif
-  a.lohi = reinterpret_cast<uint32_t*>(a.aggs + a.groups);
+  const uint32_t nwin = (a.groups + 63) / 64;
+  a.pref = a.groups > kAsmFoldMax ? a.aggs + a.groups : nullptr;
+  a.lohi = reinterpret_cast<uint32_t*>(a.aggs + a.groups + nwin);
   (void)tag;
   (void)done;
   (void)bytes;
@@ -1041,6 +1091,10 @@ hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
   }
   hipLaunchKernelGGL(log_asm_reduce, dim3(a.groups), dim3(kGT), 0, stream, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (a.pref != nullptr) {
+    hipLaunchKernelGGL(log_asm_scan, dim3(1), dim3(kGT), 0, stream, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(log_asm_emit, dim3(a.groups), dim3(kGT), 0, stream, a);
   return hipGetLastError();
 }

@@ -105,6 +105,9 @@ struct LogArgs {
   uint16_t* wover;       // positions past kWalkSlot (runs reserved by an atomic bump)
   uint32_t* wover_top;   // entries of wover reserved (left at 0 by the emit launch)
   uint16_t* over16;      // walkers x kMaxRecs: the walk's positions of records 64 and on
+  // many blocks: the records before each block (nblocks + 1 entries), scanned
+  // by log_scan_kernel for the emit; else nullptr
+  unsigned long long* first_of;
   uint64_t* stamps;  // probe build only: 8 u64 per (workgroup, slot, block)
   uint32_t knobs;    // probe build only: bit 0 = workers idle, no CRCs (timing)
 };
@@ -552,6 +555,15 @@ __global__ void __launch_bounds__(64) log_walk_kernel(LogArgs a) {
   }
 }
 
+// Whether the walk launch kept all of block b's positions: those past the
+// fixed slot go to wover, which holds `capacity` of them; a block whose
+// overflow did not fit is walked by its manager as on the slot path.
+__device__ __forceinline__ bool walk_kept(const LogArgs& a, uint32_t b) {
+  const ulonglong2 wi = a.winfo[b];
+  const uint32_t c = static_cast<uint32_t>(wi.x), oo = static_cast<uint32_t>(wi.y >> 32);
+  return c <= kWalkSlot || uint64_t{oo} + (c - kWalkSlot) <= a.capacity;
+}
+
 // log_verify_kernel's walk replaced (a.pre): block b's walked positions into
 // the slot (LDS, the overflow past kPosLds in scratch), its long records
 // registered for segmented CRCs in order, then published as walked to its
@@ -677,7 +689,8 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
       log_stamp(a, m, k, 1);
       const uint8_t* blk = sbuf + S.shift;
       uint32_t c, stop_at;
-      const uint8_t walked = a.pre ? load_walk(a, b, blk, n, spos, sover, S, gen, &c, &stop_at)
+      const uint8_t walked = a.pre && walk_kept(a, b)
+                                 ? load_walk(a, b, blk, n, spos, sover, S, gen, &c, &stop_at)
                                    : walk_block(blk, n, eof, spos, sover, S, gen, &c, &stop_at, a, m, k);
       // the block's run of staging entries (the atomic's round trip overlaps
       // the CRCs: its value is first used by the staging stores)
@@ -963,6 +976,38 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
 }
 
 constexpr uint32_t kEmitWaves = 16;  // blocks per emit workgroup (one wave each)
+// Past this many blocks the emit workgroups no longer sum every count before
+// their own (a quadratic total): log_scan_kernel scans them first.
+constexpr uint32_t kEmitFoldMax = 4096;
+constexpr uint32_t kScanThreads = 1024;
+
+// first_of[b] = the records of the blocks before b, first_of[nblocks] = all
+// of them. One workgroup; each thread a contiguous run of blocks.
+__global__ void __launch_bounds__(kScanThreads) log_scan_kernel(LogArgs a) {
+  __shared__ unsigned long long wtot[kScanThreads / 64];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = lane_id(), wave = tid >> 6;
+  const uint32_t n = a.nblocks;
+  const uint32_t per = (n + kScanThreads - 1) / kScanThreads;
+  const uint32_t b0 = min(n, tid * per), b1 = min(n, b0 + per);
+  unsigned long long mine = 0;
+  for (uint32_t b = b0; b < b1; ++b) mine += static_cast<uint32_t>(a.info[b].x);
+  unsigned long long inc = mine;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long o = __shfl_up(inc, d, 64);
+    if (lane >= static_cast<uint32_t>(d)) inc += o;
+  }
+  if (lane == 63) wtot[wave] = inc;
+  __syncthreads();
+  unsigned long long run = inc - mine;
+  for (uint32_t v = 0; v < wave; ++v) run += wtot[v];
+  for (uint32_t b = b0; b < b1; ++b) {
+    a.first_of[b] = run;
+    run += static_cast<uint32_t>(a.info[b].x);
+  }
+  if (tid == kScanThreads - 1) a.first_of[n] = run;
+}
 
 // The staged results to their places, one wave per block: record j of block
 // b is record first[b] + j in file order, first[b] = the counts of the
@@ -986,8 +1031,10 @@ __global__ void __launch_bounds__(64 * kEmitWaves) log_emit_kernel(LogArgs a) {
     *a.stg_top = 0;
     if (a.wover_top != nullptr) *a.wover_top = 0;
   }
-  // counts before b0 (and, in the last workgroup, every block's totals)
-  const uint32_t upto = last ? a.nblocks : min(b0, a.nblocks);
+  // counts before b0 (and, in the last workgroup, every block's totals);
+  // scanned already when there are many blocks
+  const bool scanned = a.first_of != nullptr;
+  const uint32_t upto = last ? a.nblocks : scanned ? 0u : min(b0, a.nblocks);
   unsigned long long cnt = 0, good = 0, drop = 0;
   uint32_t corrupt = 0, fb = 0xffffffffu;
   for (uint32_t b = tid; b < upto; b += 64 * kEmitWaves) {
@@ -1027,6 +1074,7 @@ __global__ void __launch_bounds__(64 * kEmitWaves) log_emit_kernel(LogArgs a) {
     before += s_cnt[w] & 0xffffffffull;
     mine_all += s_cnt[w] >> 32;
   }
+  if (scanned && !last) before = a.first_of[b0];
   // (a count is at most kMaxRecs and a log at most 2^32 records: the low
   // halves do not carry into the high ones)
   if (last && tid == 0) {
@@ -1082,8 +1130,10 @@ __global__ void __launch_bounds__(64 * kEmitWaves) log_emit_kernel(LogArgs a) {
 // the staging array (16 B per record, `capacity` of them) and the slots'
 // overflow positions (u32, kPosOver per slot of each of the grid's
 // workgroups).
+// The counters, info (16 B a block), stg_off (4 B a block, 8 reserved),
+// first_of (8 B a block, and one).
 size_t log_scratch_head(uint64_t nblocks) {
-  return (32 + static_cast<size_t>(nblocks) * 24 + 15) & ~size_t{15};
+  return (32 + static_cast<size_t>(nblocks) * 32 + 8 + 15) & ~size_t{15};
 }
 
 // One workgroup per CU at most (each takes most of a CU's LDS); blocks are
@@ -1150,6 +1200,9 @@ hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_o
   a.stg_top = reinterpret_cast<uint32_t*>(sb + 20);
   a.info = reinterpret_cast<ulonglong2*>(sb + 32);
   a.stg_off = reinterpret_cast<uint32_t*>(a.info + nblocks);
+  a.first_of = nblocks > kEmitFoldMax
+                   ? reinterpret_cast<unsigned long long*>(sb + 32 + size_t{nblocks} * 24)
+                   : nullptr;
   a.stg = reinterpret_cast<uint4*>(sb + log_scratch_head(nblocks));
   a.over = reinterpret_cast<uint32_t*>(a.stg + capacity);
   a.zpow = zpow;
@@ -1179,6 +1232,11 @@ hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_o
   if (nblocks != 0) {
     hipLaunchKernelGGL(log_verify_kernel, dim3(log_groups(nblocks, cus)), dim3(kVThreads), 0,
                        stream, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (a.first_of != nullptr) {
+    hipLaunchKernelGGL(log_scan_kernel, dim3(1), dim3(kScanThreads), 0, stream, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

@@ -318,18 +318,21 @@ __device__ uint32_t place_table(lvkv_sst_report* reports, uint32_t t, uint32_t n
   return static_cast<uint32_t>(min<uint64_t>(run, capacity));
 }
 
-// Index entry i (restart point i, block_restart_interval = 1) -> its data
-// block handle and status in the shared arrays at first + i. The entry bytes
-// are read from `w` (a copy of index bytes [wlo, whi)) when they lie inside
-// it, else from the index `idx` itself; `ro` is the restart array's offset.
-__device__ __forceinline__ void emit_entry(const uint8_t* idx, uint64_t ro, uint64_t nr, uint32_t i,
-                           const uint8_t* w, uint64_t wlo, uint64_t whi, const Table& tb,
-                           uint32_t first, uint64_t* out_off, uint32_t* out_size,
-                           uint8_t* out_status) {
+struct Entry {
+  uint64_t off, size;  // the handle (0/0 unless st is LVKV_BLOCK_OK)
+  uint8_t st;          // LVKV_BLOCK_* of the parse
+};
+
+// The index entry at restart offset rs, ending at `end` (the next restart
+// offset, or ro for the last): its data block handle and parse status. The
+// entry bytes are read from `w` (a copy of index bytes [wlo, whi)) when they
+// lie inside it, else from the index `idx` itself; `ro` is the restart
+// array's offset.
+__device__ __forceinline__ Entry decode_index_entry(const uint8_t* idx, uint64_t ro, uint32_t rs,
+                                                    uint64_t end, const uint8_t* w, uint64_t wlo,
+                                                    uint64_t whi, const Table& tb) {
   uint8_t st = LVKV_BLOCK_BAD_ENTRY;
   uint64_t off = 0, size = 0;
-  const uint32_t rs = ld_le32(idx + ro + 4ull * i);
-  const uint64_t end = i + 1 < nr ? ld_le32(idx + ro + 4ull * (i + 1)) : ro;
   if (rs < ro && end <= ro) {
     // DecodeEntry's limit is the restart array (block.cc:55-75, :181-195)
     // (pointers formed only inside their buffer: no out-of-range base)
@@ -356,10 +359,22 @@ __device__ __forceinline__ void emit_entry(const uint8_t* idx, uint64_t ro, uint
     }
   }
   if (st != LVKV_BLOCK_OK) off = size = 0;
+  return Entry{off, size, st};
+}
+
+// Index entry i (restart point i, block_restart_interval = 1) -> its handle
+// and status in the shared arrays at first + i.
+__device__ __forceinline__ void emit_entry(const uint8_t* idx, uint64_t ro, uint64_t nr, uint32_t i,
+                           const uint8_t* w, uint64_t wlo, uint64_t whi, const Table& tb,
+                           uint32_t first, uint64_t* out_off, uint32_t* out_size,
+                           uint8_t* out_status) {
+  const uint32_t rs = ld_le32(idx + ro + 4ull * i);
+  const uint64_t end = i + 1 < nr ? ld_le32(idx + ro + 4ull * (i + 1)) : ro;
+  const Entry x = decode_index_entry(idx, ro, rs, end, w, wlo, whi, tb);
   const uint32_t e = first + i;
-  out_off[e] = tb.base + off;  // into d_file
-  out_size[e] = static_cast<uint32_t>(size);
-  out_status[e] = st;
+  out_off[e] = tb.base + x.off;  // into d_file
+  out_size[e] = static_cast<uint32_t>(x.size);
+  out_status[e] = x.st;
 }
 
 // What a table's workgroup keeps in LDS after the 64 KiB CRC image.
@@ -401,8 +416,12 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
                          uint32_t ntables, uint32_t capacity, uint32_t gen, const FilterKey& fk,
                          lvkv_sst_report* reports, uint64_t* out_off, uint32_t* out_size,
                          uint8_t* out_status, const uint32_t* zpow, const uint32_t* lane_cols,
-                         uint64_t* stamps, bool wide) {
+                         uint64_t* stamps, bool wide, uint32_t* spec_crc = nullptr) {
   constexpr uint32_t kT = 64 * W;
+  // spec_crc set: the speculative form (sst_spec_kernel). The data entries
+  // are decoded and checksummed by the CRC workgroups; the head checksums the
+  // filter block itself (beside the placement) and writes its whole entry.
+  const bool spec = spec_crc != nullptr;
   SstHeadLds& L = *reinterpret_cast<SstHeadLds*>(lds + kCompactLdsBytes / 4);
   Head& h = L.h;
   const uint32_t tid = threadIdx.x;
@@ -469,7 +488,7 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
   // only when that is inside the image)
   const uint64_t ia4 = istart & ~uint64_t{3};
   const uint32_t ind = static_cast<uint32_t>((istart + h.is + 3 - ia4) >> 2);
-  const bool ipf = ifit && ind <= kT * kIndexPf && ia4 >= reinterpret_cast<uint64_t>(tb.img);
+  const bool ipf = !spec && ifit && ind <= kT * kIndexPf && ia4 >= reinterpret_cast<uint64_t>(tb.img);
   uint32_t pf[kIndexPf];
   if (ipf) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(ia4);
@@ -543,7 +562,7 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
   const bool index_read = footer_ok && h.index_status == LVKV_BLOCK_OK;
   const bool index_usable = h.status == LVKV_SST_OK;
   const bool stage_meta = index_read && h.meta_status == LVKV_BLOCK_OK && h.ms < kMetaStage;
-  const bool stage_index = index_usable && h.is <= kIndexStage;
+  const bool stage_index = !spec && index_usable && h.is <= kIndexStage;
   uint8_t* ibuf = reinterpret_cast<uint8_t*>(lds);  // the CRC image is spent
   if (stage_index) {
     if (ipf) {
@@ -569,7 +588,18 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
   __syncthreads();
 
   sst_stamp(stamps, t, 5);
-  // 5. Place this table's entries in the shared arrays.
+  // 5. Place this table's entries in the shared arrays (wave 0); in the
+  //    speculative form the other waves checksum the filter block meanwhile
+  //    (the CRC image is intact: nothing was staged over it).
+  const bool fcrc = spec && h.has_filter && h.filter_status == LVKV_BLOCK_OK;
+  const uint64_t fstart = reinterpret_cast<uint64_t>(tb.img) + h.fo, fend = fstart + h.fs + 1;
+  if (wave != 0) {
+    uint32_t fpart = 0;
+    if (fcrc)
+      fpart = group_crc_part(lds, fstart, fend, 0u, wave - 1u, W - 1u,
+                             group_log2seg(h.fs + 1, W - 1u), keys, lane, lane_base, zpow);
+    if (lane == 0) L.acc[wave] = fpart;
+  }
   if (wave == 0) {
     uint32_t total = 0, first = 0;
     if (ntables == 1) {
@@ -613,12 +643,30 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
   const uint64_t nr = index_usable ? h.nr : 0u;
   if (tid == 0 && h.has_filter) {
     const uint32_t e = h.first + static_cast<uint32_t>(nr);
-    const uint8_t st = h.filter_status;
+    uint8_t st = h.filter_status;
     out_off[e] = tb.base + (st == LVKV_BLOCK_OK ? h.fo : 0);
     out_size[e] = static_cast<uint32_t>(st == LVKV_BLOCK_OK ? h.fs : 0);
+    if (spec) {
+      // ReadBlock's verdict on the filter block (format.cc:92-158), as the
+      // CRC store merges it for the data blocks
+      uint32_t crc = 0;
+      if (fcrc) {
+        uint32_t fp = 0;
+#pragma unroll
+        for (int w = 1; w < W; ++w) fp ^= L.acc[w];
+        crc = group_crc_finish(fp, fstart, fend, 0u, group_crc_tail(fstart, fend));
+        const uint8_t* fe = tb.img + h.fo + h.fs;
+        st = read_status(crc == crc_unmask(ld_le32(fe + 1)), fe[0]);
+      }
+      spec_crc[e] = crc;
+      if (st != LVKV_BLOCK_OK) {
+        r->nbad = 1;
+        r->first_bad = static_cast<uint32_t>(nr);
+      }
+    }
     out_status[e] = st;
   }
-  if (nr == 0 || defer) return;
+  if (nr == 0 || defer || spec) return;
   const uint64_t ro = h.is - (1 + nr) * 4;
   if (stage_index) {
     for (uint32_t i = tid; i < nr; i += kT)
@@ -838,6 +886,298 @@ __global__ void __launch_bounds__(64 * kFW, 2)
   if (probe) sst_stamp(stamps, 0, 9);
 }
 
+// ---- Speculative form, ONE launch (sst_spec_kernel) ----------------------
+// The heads' chain (footer, index and metaindex CRCs, verdicts, the filter
+// lookup, the placement) no longer stands before the data CRCs: each CRC
+// workgroup takes a share of one table's index entries, reads the footer and
+// the index itself, decodes its entries (restart point i is entry i), walks
+// their blocks, and only then waits for its table's head to publish the
+// verdict and the table's place; the results are written there, or dropped
+// when the head found the index unusable (Table::Open failed) or the arrays
+// full. Decoding the same index bytes as the head would gives the same
+// entries, so the outputs are the two-launch form's.
+constexpr uint32_t kSpecPass = 256;    // entries decoded and walked per pass
+constexpr uint32_t kSpecTail = 4096;   // index tail staged: restart arrays of <= 1023 entries
+constexpr uint32_t kSpecWindow = 6144; // entry bytes staged per pass
+
+struct SpecLds {
+  uint64_t off[kSpecPass];       // handle offset in the table (0 unless parsed)
+  uint32_t size[kSpecPass];      // contents bytes
+  uint32_t rst[kSpecPass + 1];   // the pass's restart offsets, then its end
+  uint8_t st[kSpecPass];         // parse status, then ReadBlock's verdict
+  union {
+    uint32_t tail[kSpecTail / 4 + 1];   // the index's last bytes (aligned dwords)
+    uint32_t win[kSpecWindow / 4 + 1];  // the pass's entry bytes (aligned dwords)
+    uint32_t crc[kSpecPass];            // computed CRCs (after the decode)
+  };
+  uint64_t wsum[kFW];            // size scan: per-wave totals
+  Head h;
+  uint8_t foot[kFooterLen];
+  uint64_t wlo, whi;
+  uint32_t slot_t, slot_k, slot_c;
+  uint32_t nr_raw;
+  uint32_t first, nblocks, ndata;
+  uint32_t nbad, minbad;
+};
+
+// The walk's blocks: the pass's decoded entries in LDS; its results go back
+// there (CRC, ReadBlock's verdict merged as rag_store's kModeSstTable does).
+struct SpecSrc {
+  SpecLds* L;
+  uint64_t img;  // the table image's address
+  __device__ __forceinline__ RagBlock block(const KernelArgs& a, uint32_t b, bool live) const {
+    RagBlock g;
+    g.ptr_lo = g.ptr_hi = g.len = g.s0 = g.expected = 0;
+    g.kind = kRagNone;
+    if (!live) return g;
+    if (__builtin_amdgcn_readfirstlane(L->st[b]) != LVKV_BLOCK_OK) return g;
+    const uint64_t o = L->off[b];
+    const uint64_t ptr = img + ((static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(
+                                     static_cast<uint32_t>(o >> 32))) << 32) |
+                                __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(o)));
+    const uint32_t len = __builtin_amdgcn_readfirstlane(L->size[b]) + 1u;  // + the type byte
+    g.ptr_lo = static_cast<uint32_t>(ptr);
+    g.ptr_hi = static_cast<uint32_t>(ptr >> 32);
+    g.len = len;
+    g.s0 = 0xffffffffu;  // init 0
+    g.expected = crc_unmask(sload_le(ptr + len, 4));
+    g.kind = len > a.long_split ? kRagSkip : len < 4 ? kRagTiny : kRagRows;
+    return g;
+  }
+  __device__ __forceinline__ void store(const KernelArgs&, uint32_t b, const RagBlock& g,
+                                        uint32_t crc) const {
+    if (lane_id() != 0) return;
+    const uint8_t type = *reinterpret_cast<const uint8_t*>(g.ptr() + g.len - 1);
+    L->crc[b] = crc;
+    L->st[b] = read_status(crc == g.expected, type);
+  }
+  __device__ __forceinline__ uint32_t covered(const KernelArgs&, uint32_t b) const {
+    return L->st[b] == LVKV_BLOCK_OK ? L->size[b] + 1u : 0u;
+  }
+};
+
+constexpr uint32_t kSpecLdsDwords =
+    RagLds<kFW>::kDwords + static_cast<uint32_t>((sizeof(SpecLds) + 3) / 4);
+constexpr uint32_t kSpecKernelLdsDwords =
+    kSpecLdsDwords > kHeadLdsDwords ? kSpecLdsDwords : kHeadLdsDwords;
+
+// CRC workgroup j of G (G > ntables): its table t and share k of c. Table t
+// owns the workgroups [ceil(P_t G / P), ceil(P_{t+1} G / P)), P_t the prefix of
+// (size + U) over the tables before t and U > T / (G - ntables) (T the
+// tables' bytes), so every table has at least one and large tables more.
+template <int W>
+__device__ __forceinline__ void spec_crc_group(const KernelArgs& a, const uint8_t* file,
+                                               const uint64_t* toff, const uint64_t* tsize,
+                                               uint64_t single_size, uint32_t ntables,
+                                               uint32_t gen, lvkv_sst_report* reports,
+                                               const uint32_t* zpow, const uint32_t* lane_cols,
+                                               uint32_t* lds, uint32_t j, uint32_t G,
+                                               uint64_t* stamps) {
+  constexpr uint32_t kT = 64 * W;
+  SpecLds& L = *reinterpret_cast<SpecLds*>(lds + RagLds<W>::kDwords);
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  // 1. The share, the sizes' load beside the CRC image.
+  const uint64_t mysz = (ntables > 1 && tid < ntables) ? tsize[tid] : 0u;
+  build_compact_image<W>(lds, zpow, lane_cols, tid, wave, lane);  // ends with a barrier
+  if (ntables == 1) {
+    if (tid == 0) {
+      L.slot_t = 0;
+      L.slot_k = j;
+      L.slot_c = G;
+    }
+  } else {
+    uint64_t inc = mysz;  // inclusive prefix within the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t o = __shfl_up(static_cast<unsigned long long>(inc), d, 64);
+      if (lane >= static_cast<uint32_t>(d)) inc += o;
+    }
+    if (lane == 63) L.wsum[wave] = inc;
+    __syncthreads();
+    uint64_t before = 0, T = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < W; ++w) {
+      const uint64_t v = L.wsum[w];
+      before += w < wave ? v : 0u;
+      T += v;
+    }
+    if (tid < ntables) {
+      const uint64_t U = T / (G - ntables) + 1u;
+      const uint64_t P = T + uint64_t{ntables} * U;
+      const uint64_t p0 = before + inc - mysz + uint64_t{tid} * U;
+      const uint64_t p1 = before + inc + uint64_t{tid + 1} * U;
+      const uint64_t lo = (p0 * G + P - 1) / P, hi = (p1 * G + P - 1) / P;
+      if (lo <= j && j < hi) {
+        L.slot_t = tid;
+        L.slot_k = j - static_cast<uint32_t>(lo);
+        L.slot_c = static_cast<uint32_t>(hi - lo);
+      }
+    }
+  }
+  __syncthreads();
+  const uint32_t t = __builtin_amdgcn_readfirstlane(L.slot_t);
+  const uint32_t k = __builtin_amdgcn_readfirstlane(L.slot_k);
+  const uint32_t c = __builtin_amdgcn_readfirstlane(L.slot_c);
+  const Table tb = table_of(file, toff, tsize, single_size, t);
+  lvkv_sst_report* r = reports + t;
+  // probe stamps of the table's first CRC workgroup: 8 share known, 9 entries
+  // decoded, 10 walked, 11 head seen, 12 stored (first pass)
+  uint64_t* st = k == 0 ? stamps : nullptr;
+  sst_stamp(st, t, 8);
+
+  // 2. The footer (format.cc:43-67); a table whose index cannot be read or
+  //    has no usable restart array has no data entries (its head reports why).
+  if (tid < kFooterLen && tb.size >= kFooterLen) L.foot[tid] = tb.img[tb.size - kFooterLen + tid];
+  __syncthreads();
+  if (tid == 0) parse_footer(L.h, L.foot, tb.size);
+  __syncthreads();
+  if (L.h.status != LVKV_SST_OK || L.h.ifit != kFitOk || L.h.is < 4) return;
+  const uint64_t io = L.h.io, is = L.h.is;
+  const uint8_t* idx = tb.img + io;
+  const uint64_t istart = reinterpret_cast<uint64_t>(idx), iend = istart + is;
+
+  // 3. The index's last bytes (the restart array), staged as aligned dwords.
+  const uint64_t tlo = iend - min<uint64_t>(is, kSpecTail);
+  const uint64_t t4 = tlo & ~uint64_t{3};
+  const bool tail_ok = t4 >= reinterpret_cast<uint64_t>(tb.img);
+  if (tail_ok) {
+    const uint32_t ndw = static_cast<uint32_t>((iend - t4 + 3) >> 2);
+    for (uint32_t i = tid; i < ndw; i += kT)
+      L.tail[i] = *reinterpret_cast<const uint32_t*>(t4 + 4u * i);
+  }
+  __syncthreads();
+  const uint8_t* tb8 = reinterpret_cast<const uint8_t*>(L.tail);
+  auto le32_at = [&](uint64_t addr) -> uint32_t {  // index bytes, staged when possible
+    if (tail_ok && addr >= tlo) {
+      const uint8_t* q = tb8 + (addr - t4);
+      return static_cast<uint32_t>(q[0]) | (static_cast<uint32_t>(q[1]) << 8) |
+             (static_cast<uint32_t>(q[2]) << 16) | (static_cast<uint32_t>(q[3]) << 24);
+    }
+    return ld_le32(reinterpret_cast<const uint8_t*>(addr));
+  };
+  const uint32_t nr = le32_at(iend - 4);
+  if (nr > (is - 4) / 4 || nr == 0) return;  // Block::Block (block.cc:28-37)
+  const uint64_t ro = is - (1 + uint64_t{nr}) * 4;
+  const uint32_t i0 = static_cast<uint32_t>(uint64_t{k} * nr / c);
+  const uint32_t i1 = static_cast<uint32_t>(uint64_t{k + 1} * nr / c);
+  const SpecSrc src{&L, reinterpret_cast<uint64_t>(tb.img)};
+
+  bool waited = false;
+  for (uint32_t p0 = i0; p0 < i1; p0 += kSpecPass) {
+    const uint32_t n = min(kSpecPass, i1 - p0);
+    // 4. The pass's restart offsets, then its entry bytes [rst[0], rst[n]).
+    for (uint32_t i = tid; i <= n; i += kT) {
+      const uint32_t q = p0 + i;
+      L.rst[i] = q == nr ? static_cast<uint32_t>(ro) : le32_at(istart + ro + 4ull * q);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      // restart offsets ascend in a well-formed index; a pass whose bytes do
+      // not (or are too many) is decoded from the index itself
+      const uint64_t lo = L.rst[0], hi = L.rst[n];
+      const bool ok = lo <= hi && hi <= ro && hi - lo <= kSpecWindow - 8 &&
+                      ((istart + lo) & ~uint64_t{3}) >= reinterpret_cast<uint64_t>(tb.img);
+      L.wlo = ok ? lo : 0;
+      L.whi = ok ? hi : 0;
+    }
+    __syncthreads();  // the tail is read: the window may overwrite it
+    const uint64_t wlo = L.wlo, whi = L.whi;
+    const uint64_t w4 = (istart + wlo) & ~uint64_t{3};
+    const uint32_t wsh = static_cast<uint32_t>((istart + wlo) & 3u);
+    if (whi > wlo) {
+      const uint32_t ndw = static_cast<uint32_t>((whi - wlo + wsh + 3) >> 2);
+      for (uint32_t i = tid; i < ndw; i += kT)
+        L.win[i] = *reinterpret_cast<const uint32_t*>(w4 + 4u * i);
+    }
+    __syncthreads();
+    Entry x{0, 0, LVKV_BLOCK_OK};
+    if (tid < n)
+      x = decode_index_entry(idx, ro, L.rst[tid], L.rst[tid + 1],
+                             reinterpret_cast<const uint8_t*>(L.win) + wsh, wlo, whi, tb);
+    __syncthreads();  // the window is read: the CRCs overlay it
+    if (tid < n) {
+      L.off[tid] = x.off;
+      L.size[tid] = static_cast<uint32_t>(x.size);
+      L.st[tid] = x.st;
+      L.crc[tid] = 0;
+    }
+    if (tid == 0) lds[RagLds<W>::kFlag] = 0;
+    __syncthreads();
+    if (p0 == i0) sst_stamp(st, t, 9);
+    // 5. The walk (ragged_run over the LDS list, long blocks by the group).
+    ragged_run<W, 2, 24>(a, zpow, lane_cols, lds, 0, 1, n, true, src);
+    __syncthreads();
+    if (p0 == i0) sst_stamp(st, t, 10);
+    // 6. The head's verdict and the table's place (agent-scope loads of what
+    //    it released with done_), then this pass's entries.
+    if (!waited) {
+      if (tid == 0) {
+        while (__hip_atomic_load(&r->done_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen)
+          __builtin_amdgcn_s_sleep(8);
+        L.first = __hip_atomic_load(&r->first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        L.nblocks = __hip_atomic_load(&r->nblocks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        L.ndata = __hip_atomic_load(&r->ndata, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      waited = true;
+      sst_stamp(st, t, 11);
+    }
+    const uint32_t first = L.first, nblocks = L.nblocks, ndata = L.ndata;
+    if (tid == 0) {
+      L.nbad = 0;
+      L.minbad = 0xffffffffu;
+    }
+    __syncthreads();
+    if (tid < n && nblocks != 0 && p0 + tid < ndata) {
+      const uint32_t e = first + p0 + tid;
+      const uint8_t st = L.st[tid];
+      const_cast<uint64_t*>(a.offsets)[e] = tb.base + L.off[tid];
+      const_cast<uint32_t*>(a.lengths)[e] = L.size[tid];
+      a.out_crc[e] = L.crc[tid];
+      a.out_status[e] = st;
+      if (st != LVKV_BLOCK_OK) {
+        atomicAdd(&L.nbad, 1u);
+        atomicMin(&L.minbad, p0 + tid);
+      }
+    }
+    __syncthreads();
+    if (tid == 0 && L.nbad) {
+      atomicAdd(&r->nbad, L.nbad);
+      atomicMin(&r->first_bad, L.minbad);
+    }
+    if (p0 == i0) sst_stamp(st, t, 12);
+  }
+}
+
+// The speculative form: workgroups [0, ntables) are the heads (the filter
+// block checksummed by the head, no data entries), each releasing its report
+// with done_ = this call's generation; the others are CRC workgroups
+// (spec_crc_group). Heads have the lower ids and never wait on a CRC
+// workgroup, so every wait ends.
+__global__ void __launch_bounds__(64 * kFW, 4)
+    sst_spec_kernel(KernelArgs a, const uint8_t* file, const uint64_t* toff,
+                    const uint64_t* tsize, uint64_t single_size, uint32_t ntables,
+                    uint32_t capacity, uint32_t gen, FilterKey fk, lvkv_sst_report* reports,
+                    const uint32_t* zpow, const uint32_t* lane_cols, uint64_t* stamps) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kSpecKernelLdsDwords];
+  if (blockIdx.x < ntables) {
+    sst_head<kFW>(lds, file, toff, tsize, single_size, blockIdx.x, ntables, capacity, gen, fk,
+                  reports, const_cast<uint64_t*>(a.offsets), const_cast<uint32_t*>(a.lengths),
+                  a.out_status, zpow, lane_cols, stamps, false, a.out_crc);
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_store(&reports[blockIdx.x].done_, gen, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    sst_stamp(stamps, blockIdx.x, 7);
+    return;
+  }
+  spec_crc_group<kFW>(a, file, toff, tsize, single_size, ntables, gen, reports, zpow, lane_cols,
+                      lds, blockIdx.x - ntables, gridDim.x - ntables, stamps);
+}
+
 }  // namespace
 
 hipError_t launch_crc32c_general(const KernelArgs& a, int cus, hipStream_t stream);
@@ -851,15 +1191,16 @@ static uint64_t* sst_stamps() { return nullptr; }
 
 // Whole-table verify of `ntables` images (toff/tsize device arrays, or
 // nullptr and `single_size` for one image at d_file); `verify` carries the
-// KernelArgs template (tables) the caller filled. `fused`: one launch
-// (sst_fused_kernel, for tables whose index the 8-wave head handles well);
-// else the two-launch form (16-wave heads, then the ragged kernel).
+// KernelArgs template (tables) the caller filled. `form`: kSstFormSpec one
+// launch (sst_spec_kernel; ntables < groups), kSstFormFused one launch
+// (sst_fused_kernel), kSstFormTwo the two-launch form (16-wave heads, then
+// the ragged kernel).
 hipError_t launch_sst_tables(const uint8_t* file, const uint64_t* toff, const uint64_t* tsize,
                              uint64_t single_size, uint32_t ntables, uint64_t* d_off,
                              uint32_t* d_size, uint32_t* d_actual, uint8_t* d_status,
                              uint32_t capacity, lvkv_sst_report* reports, const FilterKey& fk,
                              uint32_t gen, const KernelArgs& verify, const uint32_t* zpow,
-                             const uint32_t* lane_cols, int groups, bool fused,
+                             const uint32_t* lane_cols, int groups, int form,
                              hipStream_t stream) {
   // every data and filter block of every table: CRC, then the merge into
   // LVKV_BLOCK_* and the per-table totals in the kernel's store
@@ -876,7 +1217,17 @@ hipError_t launch_sst_tables(const uint8_t* file, const uint64_t* toff, const ui
   a.long_split = kLongBytes;  // large data/filter blocks: one workgroup each
   a.sst_reports = reports;
   a.sst_ntables = ntables;
-  if (fused) {
+  if (form == kSstFormSpec && ntables < static_cast<uint32_t>(groups)) {
+    a.run_base = nullptr;
+    // two workgroups per CU resident: the heads, then 2 * groups - ntables
+    // CRC workgroups (more than ntables)
+    const uint32_t grid = 2u * static_cast<uint32_t>(groups);
+    hipLaunchKernelGGL(sst_spec_kernel, dim3(grid), dim3(64 * kFW), 0, stream, a, file, toff,
+                       tsize, single_size, ntables, capacity, gen, fk, reports, zpow, lane_cols,
+                       sst_stamps());
+    return hipGetLastError();
+  }
+  if (form == kSstFormFused) {
     a.fresh_desc = 1;
     // two workgroups per CU resident; the heads come first
     const uint32_t grid = max(2u * static_cast<uint32_t>(groups), ntables + static_cast<uint32_t>(groups));

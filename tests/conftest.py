@@ -63,10 +63,11 @@ def gpu():
     return torch.device("cuda:0")
 
 
-@pytest.fixture(params=[1, 2], ids=["fused", "two_launch"])
+@pytest.fixture(params=[1, 2, 3], ids=["fused", "two_launch", "spec"])
 def sst_form(request, lvkv, gpu):
     """Whole-SSTable verify form under test: 1 = one fused launch, 2 = the
-    two-launch form (lvkv_debug_set_sst_form); back to by-size afterwards."""
+    two-launch form, 3 = the speculative launch (CRC workgroups decode their
+    own index entries; lvkv_debug_set_sst_form); back to by-size afterwards."""
     assert lvkv.lib.lvkv_debug_set_sst_form(request.param) == 0
     yield request.param
     lvkv.lib.lvkv_debug_set_sst_form(0)

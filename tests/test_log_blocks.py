@@ -244,6 +244,40 @@ def test_device_log_large_and_capacity(lvkv, gpu, log_path):
 
 
 @pytest.mark.gpu
+def test_device_log_many_blocks_tiled(lvkv, gpu, log_path):
+    """Past 4096 blocks the emit launch takes every block's first record from
+    log_scan_kernel instead of summing the counts before it. A damaged ~1 MB
+    log padded to whole 32 KiB blocks (zero trailers, skipped silently) and
+    tiled: each block's verdict depends on that block alone, so the oracle's
+    answer for the base tiles too."""
+    import oracle
+    base = bytearray(log_synth.build_log(1500, seed=41, max_len=1200, big_every=89))
+    base += bytes(-len(base) % 32768)
+    for p in (5000, 200_001, len(base) // 2 + 7):
+        base[p] ^= 0x20
+    base = bytes(base)
+    nb = len(base) // 32768
+    tiles = 4096 // nb + 2
+    v = lw.block_verdicts(base)
+    img = base * tiles
+    rep, hdr, actual, rst, bst, bdrop = _device(lvkv, img, gpu)
+    assert rep["status"] == 0 and rep["nblocks"] == nb * tiles > 4096
+    assert rep["nrecords"] == len(v.hdrs) * tiles
+    assert np.array_equal(hdr, np.array([t * len(base) + h for t in range(tiles) for h in v.hdrs]))
+    assert list(rst) == v.rec_status * tiles
+    assert list(bst) == v.block_status * tiles and list(bdrop) == v.block_drop * tiles
+    bad = [i for i, s in enumerate(v.block_status) if s in (lw.BLK_CHECKSUM, lw.BLK_BAD_LENGTH)]
+    assert bad and rep["first_bad_block"] == bad[0]
+    assert rep["ncorrupt"] == len(bad) * tiles
+    assert rep["ngood"] == v.rec_status.count(lw.REC_OK) * tiles
+    assert rep["dropped_bytes"] == sum(v.block_drop[i] for i in bad) * tiles
+    want = np.array([oracle.value(base[h + 6: h + 7 + (base[h + 4] | base[h + 5] << 8)])
+                     for h in v.hdrs], dtype=np.uint32)
+    keep = np.tile(np.array(v.rec_status) != lw.REC_DROPPED, tiles)
+    assert np.array_equal(actual[keep], np.tile(want, tiles)[keep])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("source", ["golden", "synthetic"])
 def test_device_fill_headers_rebuilds_the_log(lvkv, gpu, source):
     # log::Writer::EmitPhysicalRecord (log_writer.cc:82-108) wrote these

@@ -67,6 +67,48 @@ def multi(nblocks, k):
     us = (time.perf_counter() - t0) / 50 * 1e6
     print(f"sst_verify_tables form {opt('form', 0)}, {k} x {nblocks} blocks, {len(raw)} bytes: "
           f"{us:.1f} us/call", flush=True)
+    if "--stamps" in sys.argv:
+        P = probe_lib(opt("form", 0))
+        P.lvkv_sst_verify_tables_device.argtypes = L_TABLES_ARGS
+        stz = torch.zeros(16 * k, dtype=torch.int64, device=dev)
+        P.lvkv_debug_sst_stamps(vp(stz.data_ptr()))
+        rows = []
+        for _ in range(8):
+            stz.zero_()
+            torch.cuda.synchronize()
+            assert P.lvkv_sst_verify_tables_device(
+                vp(buf.data_ptr()), vp(toff.data_ptr()), vp(tsz.data_ptr()), k, vp(o.data_ptr()),
+                vp(sz.data_ptr()), vp(ac.data_ptr()), vp(st.data_ptr()), cap, pol,
+                vp(rp.data_ptr()), h) == 0
+            torch.cuda.synchronize()
+            x = stz.cpu().numpy().astype(np.int64).reshape(k, 16)
+            t0 = x[:, 0][x[:, 0] > 0].min()
+            rows.append(np.where(x > 0, (x - t0) / 100.0, np.nan))
+        r = np.array(rows)  # runs x tables x slots
+        med0 = np.nanmedian(r[:, 0, :], axis=0)
+        print("  table 0: " + "  ".join(f"{n} {v:.2f}" for n, v in zip(STAMP_NAMES, med0)
+                                         if not np.isnan(v)), flush=True)
+        mx = np.nanmedian(np.nanmax(r, axis=1), axis=0)
+        print("  max over tables: " + "  ".join(f"{n} {v:.2f}" for n, v in zip(STAMP_NAMES, mx)
+                                                 if not np.isnan(v)), flush=True)
+        P.lvkv_debug_sst_stamps(None)
+
+
+# phase stamps (tools/probe build): head slots 0-7; the CRC workgroups' 8-12
+# (speculative form: table t's first CRC workgroup; fused: the first one)
+STAMP_NAMES = ["start", "footer", "crcs", "verdicts", "staged", "filter", "placed", "done",
+               "crc_share", "crc_decoded", "crc_walked", "crc_head_seen", "crc_stored"]
+L_TABLES_ARGS = [ctypes.c_void_p] * 3 + [ctypes.c_size_t] + [ctypes.c_void_p] * 4 + [
+    ctypes.c_size_t, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p]
+
+
+def probe_lib(form):
+    vp = ctypes.c_void_p
+    P = ctypes.CDLL(str(HERE / "liblvkv_probe.so"))
+    P.lvkv_debug_sst_stamps.argtypes = [vp]
+    P.lvkv_debug_set_sst_form.argtypes = [ctypes.c_int]
+    P.lvkv_debug_set_sst_form(form)
+    return P
 
 
 def main():
@@ -107,10 +149,7 @@ def main():
           flush=True)
     if "--stamps" in sys.argv:
         # phase stamps from the probe build (10 ns units -> us from the head's start)
-        P = ctypes.CDLL(str(HERE / "liblvkv_probe.so"))
-        P.lvkv_debug_sst_stamps.argtypes = [vp]
-        P.lvkv_debug_set_sst_form.argtypes = [ctypes.c_int]
-        P.lvkv_debug_set_sst_form(form)
+        P = probe_lib(form)
         P.lvkv_sst_verify_table_device.argtypes = [vp, ctypes.c_uint64, vp, vp, vp, vp,
                                                    ctypes.c_size_t, ctypes.c_char_p, vp, vp]
         stz = torch.zeros(16, dtype=torch.int64, device=dev)
@@ -125,11 +164,12 @@ def main():
             assert rc == 0
             torch.cuda.synchronize()
             x = stz.cpu().numpy().astype(np.int64)
-            rows.append([(v - x[0]) / 100.0 if v else float("nan") for v in x[:11]])
+            rows.append([(v - x[0]) / 100.0 if v else float("nan") for v in x[:13]])
         med = np.nanmedian(np.array(rows), axis=0)
-        names = ["start", "footer", "crcs", "verdicts", "staged", "filter", "placed", "done",
-                 "crc_wg_waited", "crc_wg_end", "crc_wg_image"]
-        print("  " + "  ".join(f"{n} {v:.2f}" for n, v in zip(names, med)), flush=True)
+        names = STAMP_NAMES if form == 3 else STAMP_NAMES[:8] + [
+            "crc_wg_waited", "crc_wg_end", "crc_wg_image"]
+        print("  " + "  ".join(f"{n} {v:.2f}" for n, v in zip(names, med) if not np.isnan(v)),
+              flush=True)
         P.lvkv_debug_sst_stamps(None)
 
 
