@@ -30,12 +30,6 @@ uint32_t lvkv_debug_extend_portable(uint32_t crc, const uint8_t* data, size_t n)
 int lvkv_debug_set_general_kernel(int cfg);
 int lvkv_debug_set_log_kernel(int cfg);
 int lvkv_debug_set_sst_form(int form);
-/* WAL verify (lvkv_log_verify_blocks_device, lvkv_log_read_device) on the
- * current device: 0 = two LDS slots per CU, each block walked and its records
- * checksummed in one launch; 1 = walk first (a launch of one-wave walkers,
- * four per CU), then the slots load the walked positions instead of
- * walking. */
-int lvkv_debug_set_log_path(int path);
 
 /* The kernel-variant, timestamp and read-bandwidth probes live in the probe
  * build of the library (tools/probe/liblvkv_probe.so, tools/probe/lvkv_probe.h),

@@ -96,8 +96,6 @@ def _load() -> ctypes.CDLL:
     L.lvkv_log_gather_device.restype = i32
     L.lvkv_debug_set_sst_form.argtypes = [i32]
     L.lvkv_debug_set_sst_form.restype = i32
-    L.lvkv_debug_set_log_path.argtypes = [i32]
-    L.lvkv_debug_set_log_path.restype = i32
     L.lvkv_log_verify_device.argtypes = [vp, vp, vp, vp, sz, vp]
     L.lvkv_log_verify_device.restype = i32
     L.lvkv_crc32c_batch_host.argtypes = [vp, vp, vp, vp, u32, vp, sz, u32]

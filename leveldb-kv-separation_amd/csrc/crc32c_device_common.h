@@ -24,6 +24,13 @@ typedef __attribute__((address_space(4))) const uint64_t ConstU64;
 __device__ __forceinline__ uint32_t sload32(uint64_t addr) {
   return *reinterpret_cast<ConstU32*>(addr);
 }
+typedef __attribute__((address_space(1))) const uint32_t GlobalU32;
+// Dword vector load from global memory (vmcnt only: a flat load would also
+// count in lgkmcnt and hold up the next LDS wait). `addr` must be 4-aligned.
+__device__ __forceinline__ uint32_t gload32(uint64_t addr) {
+  return *reinterpret_cast<GlobalU32*>(addr);
+}
+
 // Wave-uniform element loads of the descriptor arrays (s_load, lgkmcnt).
 __device__ __forceinline__ uint32_t sload_u32(const uint32_t* p, uint32_t i) {
   return reinterpret_cast<ConstU32*>(reinterpret_cast<uint64_t>(p))[i];

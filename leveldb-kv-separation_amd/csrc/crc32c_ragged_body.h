@@ -102,7 +102,12 @@ __device__ __forceinline__ uint32_t desc_u32(const KernelArgs& a, uint32_t b) {
 
 // Block b's covered range and verdict inputs by mode (crc32c_kernel.hip
 // make_geo: log headers, SST trailers, per-block inits).
-__device__ __forceinline__ RagBlock rag_block(const KernelArgs& a, uint32_t b, bool live) {
+// With `defer`, an SST mode's stored trailer is not loaded here: the walk
+// loads it with a vector load when the block's round starts (RagRound::adopt)
+// and reads it at the store, so no scalar load is outstanding while the walk
+// waits on its LDS reads (one lgkmcnt counts both).
+__device__ __forceinline__ RagBlock rag_block(const KernelArgs& a, uint32_t b, bool live,
+                                              bool defer = false) {
   RagBlock g;
   g.ptr_lo = g.ptr_hi = g.len = g.s0 = g.expected = 0;
   g.kind = kRagNone;
@@ -134,7 +139,7 @@ __device__ __forceinline__ RagBlock rag_block(const KernelArgs& a, uint32_t b, b
     // (table/format.cc:92-94, table/table_builder.cc:199-203)
     len += 1;
     init = 0;
-    if (a.mode != kModeSstFill) expected = crc_unmask(sload_le(base + off + len, 4));
+    if (a.mode != kModeSstFill && !defer) expected = crc_unmask(sload_le(base + off + len, 4));
   }
   const uint64_t ptr = base + off;
   g.ptr_lo = static_cast<uint32_t>(ptr);
@@ -236,8 +241,13 @@ __device__ __forceinline__ void rag_store(const KernelArgs& a, uint32_t b, const
 // descriptor arrays and rag_store (ArgsSrc), or a caller's own list (the
 // whole-SSTable verify's entries decoded into LDS, lvkv_sst_table.hip).
 struct ArgsSrc {
+  // the stored CRC follows the covered bytes (SST verify modes): loaded by
+  // the walk (RagRound::adopt), not by block()
+  __device__ __forceinline__ bool trailer(const KernelArgs& a) const {
+    return a.mode == kModeSstVerify || a.mode == kModeSstTable;
+  }
   __device__ __forceinline__ RagBlock block(const KernelArgs& a, uint32_t b, bool live) const {
-    return rag_block(a, b, live);
+    return rag_block(a, b, live, trailer(a));
   }
   __device__ __forceinline__ void store(const KernelArgs& a, uint32_t b, const RagBlock& g,
                                         uint32_t crc) const {
@@ -262,6 +272,7 @@ struct RagRound {
   uint32_t blk[NCH];
   uint32_t nchunks;  // max over the chains, >= 1
   uint32_t w[NCH][R + 1];  // row R: the neighbour dwords of row R - 1
+  uint32_t x0[NCH], x1[NCH];  // the stored trailer's aligned dwords (Src::trailer)
 
   // Chain c of round r0 is block start + r0 + c * W + wave.
   template <class Src>
@@ -274,15 +285,27 @@ struct RagRound {
       out[c] = src.block(a, start + i, i < n);
     }
   }
+  // `trailer`: load each block's stored CRC (the 4 bytes after it) now, as
+  // vector loads issued before the round's rows; expected() reads them.
   __device__ __forceinline__ void adopt(const RagBlock (&in)[NCH], uint32_t start, uint32_t r0,
-                                        uint32_t wave, uint32_t W) {
+                                        uint32_t wave, uint32_t W, bool trailer) {
     nchunks = 1;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       g[c] = in[c];
       blk[c] = start + r0 + static_cast<uint32_t>(c) * W + wave;
       if (g[c].kind == kRagRows) nchunks = max(nchunks, (g[c].rows() + R - 1) / R);
+      x0[c] = x1[c] = 0;
+      if (trailer && (g[c].kind == kRagRows || g[c].kind == kRagTiny)) {
+        const uint64_t t = g[c].ptr() + g[c].len;
+        x0[c] = gload32(t & ~uint64_t{3});
+        x1[c] = (t & 3u) ? gload32((t & ~uint64_t{3}) + 4u) : 0u;
+      }
     }
+  }
+  __device__ __forceinline__ uint32_t expected(int c) const {
+    const uint32_t sh = static_cast<uint32_t>(g[c].ptr_lo + g[c].len) & 3u;
+    return crc_unmask(__builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbyte(x1[c], x0[c], sh)));
   }
 
   // R + 1 loads per chain, unconditional: rows past the block (and every
@@ -362,7 +385,8 @@ __device__ __forceinline__ void ragged_long_pass(const KernelArgs& a, const uint
     const uint32_t cnt = __builtin_amdgcn_readfirstlane(lds[kCount]);
     for (uint32_t li = 0; li < cnt; ++li) {
       const uint32_t b = __builtin_amdgcn_readfirstlane(lds[kList + li]);
-      const RagBlock g = src.block(a, b, true);
+      RagBlock g = src.block(a, b, true);
+      if (src.trailer(a)) g.expected = crc_unmask(sload_le(g.ptr() + g.len, 4));
       // WAL fragments (<= 32 KiB): 4 KiB segments, one per wave; longer
       // blocks: 16 KiB segments
       const uint32_t crc =
@@ -410,7 +434,7 @@ __device__ __forceinline__ void ragged_run(const KernelArgs& a, const uint32_t* 
   if (image_ready) {
     RagBlock g0[NCH];
     RagRound<NCH, R>::fetch(g0, a, src, start, n, 0, wave, W);
-    rd.adopt(g0, start, 0, wave, W);
+    rd.adopt(g0, start, 0, wave, W, src.trailer(a));
     rd.issue(0, lane);
   } else {
     RowTabStage<64 * W> rt;
@@ -420,7 +444,7 @@ __device__ __forceinline__ void ragged_run(const KernelArgs& a, const uint32_t* 
     {
       RagBlock g0[NCH];
       RagRound<NCH, R>::fetch(g0, a, src, start, n, 0, wave, W);
-      rd.adopt(g0, start, 0, wave, W);
+      rd.adopt(g0, start, 0, wave, W, src.trailer(a));
     }
     __builtin_amdgcn_sched_barrier(0);
     rd.issue(0, lane);
@@ -493,6 +517,7 @@ __device__ __forceinline__ void ragged_run(const KernelArgs& a, const uint32_t* 
     for (int c = 0; c < NCH; ++c) {
       if (nrow[c] > 0 && rd.g[c].rows() <= (k + 1) * R) {
         const uint32_t crc = wave_xor_dpp(lane_end_shift_c(lds, st[c], lane_base)) ^ 0xffffffffu;
+        if (src.trailer(a)) rd.g[c].expected = rd.expected(c);
         src.store(a, rd.blk[c], rd.g[c], crc);
       }
     }
@@ -500,12 +525,15 @@ __device__ __forceinline__ void ragged_run(const KernelArgs& a, const uint32_t* 
     if (++k == rd.nchunks) {
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
-        if (rd.g[c].kind == kRagTiny) src.store(a, rd.blk[c], rd.g[c], rag_tiny(rd.g[c]));
+        if (rd.g[c].kind == kRagTiny) {
+          if (src.trailer(a)) rd.g[c].expected = rd.expected(c);
+          src.store(a, rd.blk[c], rd.g[c], rag_tiny(rd.g[c]));
+        }
         if (rd.g[c].kind == kRagSkip && lane == 0) lds[kFlag] = 1;
       }
       r0 += W * NCH;
       if (r0 >= n) break;
-      rd.adopt(gn, start, r0, wave, W);
+      rd.adopt(gn, start, r0, wave, W, src.trailer(a));
       k = 0;
     }
     rd.issue(k, lane);

@@ -62,7 +62,7 @@ hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_o
                              uint32_t* actual, uint8_t* rec_status, uint32_t capacity,
                              uint8_t* block_status, uint32_t* block_drop, lvkv_log_report* r,
                              const uint32_t* zpow, const uint32_t* lane_cols, int cus,
-                             void* scratch, uint32_t* events, int path, hipStream_t stream);
+                             void* scratch, uint32_t* events, hipStream_t stream);
 size_t log_scratch_bytes(uint64_t size, uint32_t capacity, int cus);
 hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
                                const lvkv_log_report* phys, uint64_t size, uint32_t capacity,
@@ -121,9 +121,6 @@ struct DeviceCtx {
   // whole-SSTable verify form: 0 by size, 1 fused, 2 two launches,
   // 3 speculative (lvkv_debug_set_sst_form)
   std::atomic<int> sst_form{0};
-  // WAL verify: 0 two LDS slots per CU walked and checksummed in one launch,
-  // 1 a walk launch first, the slots load its positions (lvkv_debug_set_log_path)
-  std::atomic<int> log_path{0};
   std::mutex host_mu;  // serialises lvkv_crc32c_batch_host per device
   // WAL verify scratch: a pool of buffers, each lent to one call at a time
   // (busy from acquire to the event recorded after the call's launches,
@@ -697,7 +694,7 @@ int lvkv_log_verify_blocks_device(const void* d_file, uint64_t file_size,
                         d_rec_status, static_cast<uint32_t>(capacity), d_block_status,
                         d_block_drop, d_report, c->d_tables + kZPowOffset,
                         c->d_tables + kRowTabDwords + kLaneTabDwords, c->groups, scratch, nullptr,
-                        c->log_path.load(std::memory_order_relaxed), hs);
+                        hs);
   const hipError_t e2 = log_scratch_release(*c, slot, hs);
   if (e == hipSuccess) e = e2;
   return e == hipSuccess ? LVKV_OK : hip_fail(e);
@@ -739,7 +736,7 @@ int lvkv_log_read_device(const void* d_file, uint64_t file_size, uint64_t* d_hdr
                           d_actual, d_rec_status, static_cast<uint32_t>(capacity),
                           d_block_status, d_block_drop, d_report, c->d_tables + kZPowOffset,
                           c->d_tables + kRowTabDwords + kLaneTabDwords, c->groups, scratch,
-                          events, c->log_path.load(std::memory_order_relaxed), hs);
+                          events, hs);
   if (e == hipSuccess)
     e = launch_log_assemble(events, d_hdr_offsets, d_report, file_size,
                             static_cast<uint32_t>(capacity), initial_offset, d_records,
@@ -1042,15 +1039,6 @@ int lvkv_debug_set_sst_form(int form) {
   DeviceCtx* c = current_ctx(&rc);
   if (c == nullptr) return rc;
   c->sst_form.store(form, std::memory_order_relaxed);
-  return LVKV_OK;
-}
-
-int lvkv_debug_set_log_path(int path) {
-  if (path < 0 || path > 1) return LVKV_ERR_INVALID;
-  int rc = LVKV_OK;
-  DeviceCtx* c = current_ctx(&rc);
-  if (c == nullptr) return rc;
-  c->log_path.store(path, std::memory_order_relaxed);
   return LVKV_OK;
 }
 

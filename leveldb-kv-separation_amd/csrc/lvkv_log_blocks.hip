@@ -97,14 +97,6 @@ struct LogArgs {
   const uint32_t* zpow;
   const uint32_t* lane_cols;
   uint32_t* events;  // nullable: the ReadRecord event stream (lvkv_log_events.h)
-  // the walk-first path (log_walk_kernel, then log_verify_kernel with the
-  // positions precomputed, then log_emit_kernel)
-  uint32_t pre;          // 1: log_verify_kernel reads the walk's results
-  ulonglong2* winfo;     // nblocks: {count | verdict << 32, bad-length drop | overflow run << 32}
-  uint16_t* wpos;        // nblocks x kWalkSlot: the records' positions in their block
-  uint16_t* wover;       // positions past kWalkSlot (runs reserved by an atomic bump)
-  uint32_t* wover_top;   // entries of wover reserved (left at 0 by the emit launch)
-  uint16_t* over16;      // walkers x kMaxRecs: the walk's positions of records 64 and on
   // many blocks: the records before each block (nblocks + 1 entries), scanned
   // by log_scan_kernel for the emit; else nullptr
   unsigned long long* first_of;
@@ -425,195 +417,6 @@ __device__ __forceinline__ void record_done(const uint8_t* blk, uint32_t p, uint
   hb[3] = static_cast<uint8_t>(crc >> 24);
 }
 
-// ---- the walk-first path --------------------------------------------------
-//
-// What bounds log_verify_kernel is each slot's serial chain: DMA, the walk
-// of ~31 headers (a chain of LDS round trips slowed by the record waves'
-// traffic), the last records' CRCs. This path takes the walk out of it:
-//   log_walk_kernel   one wave per workgroup and one 32 KiB slot each (four
-//                     per CU, nothing else on their LDS); wave g walks blocks
-//                     g, g + G, ... (static: no ticket, no per-block atomic:
-//                     a thousand walkers bumping one counter at once
-//                     serialise on it) and writes each block's count, verdict
-//                     and drop and its records' positions into a fixed slot of
-//                     kWalkSlot entries (positions past it, rare, into a run
-//                     reserved by an atomic bump);
-//   log_verify_kernel with a.pre: each slot's manager pulls its block in and
-//                     loads the walked positions instead of walking, so the
-//                     workers start on every record at once;
-//   log_emit_kernel   as before.
-// The image is read twice (both DMAs).
-
-constexpr uint32_t kWalkPerCu = 4;   // walker workgroups per CU
-constexpr uint32_t kWalkSlot = 512;  // positions per block in its fixed slot
-
-// Walks blk[0, n) like walk_block (ReadPhysicalRecord's header loop,
-// db/log_reader.cc:189-247, to the first stop), keeping record k's position
-// in lane k % 64 of `held` and writing each full 64 to over[]. Returns the
-// verdict; *count, *stop = records and the block offset after the last one.
-__device__ __forceinline__ uint8_t walk_only(const uint8_t* blk, uint32_t n, bool eof,
-                                             uint16_t* over, uint32_t* held_out,
-                                             uint32_t* count, uint32_t* stop) {
-  const uint32_t lane = lane_id();
-  const uint32_t base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(blk));
-  const uint32_t end = base + n;
-  uint32_t k = 0, bp = base, len = 0, typ = 0;
-  uint32_t held = 0;
-  if (n >= kLogHeader) {
-    uint32_t nlen, ntyp;
-    asm volatile("ds_read_u16 %0, %2 offset:4\n\tds_read_u8 %1, %2 offset:6\n\ts_waitcnt lgkmcnt(0)"
-                 : "=v"(len), "=v"(typ)
-                 : "v"(bp));
-    for (;;) {
-      const uint32_t nbp = bp + kLogHeader + len;
-      asm volatile("ds_read_u16 %0, %2 offset:4\n\tds_read_u8 %1, %2 offset:6"
-                   : "=v"(nlen), "=v"(ntyp)
-                   : "v"(nbp));
-      __builtin_amdgcn_sched_barrier(0);  // the reads issue before the tests below
-      const uint32_t f = __builtin_amdgcn_readfirstlane(
-          (nbp > end || (len | typ) == 0 ? 1u : 0u) | (end - nbp < kLogHeader ? 2u : 0u));
-      if (f & 1u) break;
-      held = lane == (k & 63u) ? bp - base : held;
-      ++k;
-      if ((k & 63u) == 0) over[k - 64u + lane] = static_cast<uint16_t>(held);
-      bp = nbp;
-      if (f & 2u) break;
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nlen), "+v"(ntyp));
-      len = nlen;
-      typ = ntyp;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nlen), "+v"(ntyp));
-  }
-  const uint32_t p = __builtin_amdgcn_readfirstlane(bp - base);
-  len = __builtin_amdgcn_readfirstlane(len);
-  uint8_t v;
-  if (n - p < kLogHeader)
-    v = (eof && p < n) ? LVKV_LOGBLK_EOF : LVKV_LOGBLK_OK;  // :206-213
-  else if (kLogHeader + len > n - p)
-    v = eof ? LVKV_LOGBLK_EOF : LVKV_LOGBLK_BAD_LENGTH;
-  else
-    v = LVKV_LOGBLK_ZERO;
-  *held_out = held;
-  *count = k;
-  *stop = p;
-  return v;
-}
-
-// The block at file offset `start` (n bytes) into buf by LDS-DMA from its
-// 16-byte aligned start: full 16-byte lines as dwordx4, the last 0-15 bytes
-// by plain loads; returns the block's offset in buf (its misalignment).
-__device__ __forceinline__ uint32_t dma_block(const uint8_t* file, uint64_t start, uint32_t n,
-                                              uint8_t* buf, uint32_t lane) {
-  const uint8_t* src = file + start;
-  const uint32_t shift = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src) & 15u);
-  const uint32_t nbytes = shift + n;
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint8_t*>(src - shift), 0, static_cast<int>(nbytes), kBufferDword3);
-  const uint32_t lines = nbytes >> 4;
-  for (uint32_t i = 0; i * 64u < lines; ++i) {
-    const uint32_t line = i * 64u + lane;
-    if (line < lines)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          r, (__attribute__((address_space(3))) void*)(buf + 1024u * i), 16, 16u * line, 0, 0, 0);
-  }
-  // (a sub-dword LDS-DMA does not land one byte per lane: plain loads)
-  if (lane < (nbytes & 15u)) buf[16u * lines + lane] = (src - shift)[16u * lines + lane];
-  __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) lgkmcnt(0): the DMA and the tail have landed
-  return shift;
-}
-
-__global__ void __launch_bounds__(64) log_walk_kernel(LogArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t buf[kBufBytes];
-  const uint32_t lane = lane_id();
-  uint16_t* over = a.over16 + static_cast<uint64_t>(blockIdx.x) * kMaxRecs;
-  for (uint32_t b = blockIdx.x; b < a.nblocks; b += gridDim.x) {
-    const uint64_t start = uint64_t{b} * kLogBlock;
-    const uint64_t end = min(a.size, start + kLogBlock);
-    const uint32_t n = static_cast<uint32_t>(end - start);
-    const uint32_t shift = dma_block(a.file, start, n, buf, lane);
-    uint32_t held, c, stop_at;
-    const uint8_t walked = walk_only(buf + shift, n, n < kLogBlock, over, &held, &c, &stop_at);
-    // positions past the fixed slot: a run of wover (rare: > kWalkSlot records)
-    uint32_t oo = 0;
-    if (c > kWalkSlot && lane == 0)
-      oo = __hip_atomic_fetch_add(a.wover_top, c - kWalkSlot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    oo = __builtin_amdgcn_readfirstlane(oo);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's over[] stores have landed
-    const uint32_t full = c & ~63u;
-    uint16_t* slot = a.wpos + static_cast<uint64_t>(b) * kWalkSlot;
-    for (uint32_t j = lane; j < c; j += 64) {
-      const uint16_t p = j < full ? over[j] : static_cast<uint16_t>(held);
-      if (j < kWalkSlot)
-        slot[j] = p;
-      else if (oo + (j - kWalkSlot) < a.capacity)
-        a.wover[oo + (j - kWalkSlot)] = p;
-    }
-    if (lane == 0)
-      a.winfo[b] = make_ulonglong2(uint64_t{c} | (uint64_t{walked} << 32),
-                                   uint64_t{walked == LVKV_LOGBLK_BAD_LENGTH ? n - stop_at : 0u} |
-                                       (uint64_t{oo} << 32));
-  }
-}
-
-// Whether the walk launch kept all of block b's positions: those past the
-// fixed slot go to wover, which holds `capacity` of them; a block whose
-// overflow did not fit is walked by its manager as on the slot path.
-__device__ __forceinline__ bool walk_kept(const LogArgs& a, uint32_t b) {
-  const ulonglong2 wi = a.winfo[b];
-  const uint32_t c = static_cast<uint32_t>(wi.x), oo = static_cast<uint32_t>(wi.y >> 32);
-  return c <= kWalkSlot || uint64_t{oo} + (c - kWalkSlot) <= a.capacity;
-}
-
-// log_verify_kernel's walk replaced (a.pre): block b's walked positions into
-// the slot (LDS, the overflow past kPosLds in scratch), its long records
-// registered for segmented CRCs in order, then published as walked to its
-// end. Called by the slot's manager wave with uniform arguments.
-__device__ __forceinline__ uint8_t load_walk(const LogArgs& a, uint32_t b, const uint8_t* blk,
-                                             uint32_t n, uint16_t* pos, uint32_t* over, Slot& S,
-                                             uint32_t gen, uint32_t* count, uint32_t* stop) {
-  const uint32_t lane = lane_id();
-  const ulonglong2 wi = a.winfo[b];
-  const uint32_t c = static_cast<uint32_t>(wi.x);
-  const uint8_t walked = static_cast<uint8_t>(wi.x >> 32);
-  const uint32_t drop = static_cast<uint32_t>(wi.y), oo = static_cast<uint32_t>(wi.y >> 32);
-  const uint16_t* slot = a.wpos + static_cast<uint64_t>(b) * kWalkSlot;
-  uint32_t nseg = 0;
-  for (uint32_t j0 = 0; j0 < c; j0 += 64) {
-    const uint32_t j = j0 + lane;
-    uint32_t p = 0, len = 0;
-    if (j < c) {
-      p = j < kWalkSlot ? slot[j] : a.wover[oo + (j - kWalkSlot)];
-      put_pos(pos, over, j, p);
-      len = static_cast<uint32_t>(blk[p + 4]) | (static_cast<uint32_t>(blk[p + 5]) << 8);
-    }
-    // records longer than kSegBytes: segmented, in file order
-    uint64_t lm = __ballot(j < c && len + 1u > kSegBytes);
-    while (lm) {
-      const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(lm));
-      lm &= lm - 1;
-      const uint32_t lp = __shfl(p, l, 64), ll = __shfl(len, l, 64);
-      const uint32_t m = (ll + 1u + kSegBytes - 1u) / kSegBytes;
-      if (lane == 0) {
-        const uint32_t e = S.nlong++;
-        S.lj[e] = static_cast<uint16_t>(j0 + l);
-        S.lp[e] = static_cast<uint16_t>(lp);
-        S.lseg[e] = static_cast<uint8_t>(m);
-        S.lfirst[e] = static_cast<uint8_t>(nseg);
-        S.lacc[e] = 0;
-        S.lrem[e] = m;
-      }
-      nseg += m;
-    }
-  }
-  if (lane == 0) {
-    lds_store_rel(&S.lavail, (gen << 16) | nseg);
-    lds_store_rel(&S.prog, (gen << kGenShift) | kDoneBit | c);
-  }
-  *count = c;
-  *stop = walked == LVKV_LOGBLK_BAD_LENGTH ? n - drop : 0u;
-  return walked;
-}
-
 // ---- the kernel ------------------------------------------------------------
 
 __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
@@ -689,9 +492,7 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
       log_stamp(a, m, k, 1);
       const uint8_t* blk = sbuf + S.shift;
       uint32_t c, stop_at;
-      const uint8_t walked = a.pre && walk_kept(a, b)
-                                 ? load_walk(a, b, blk, n, spos, sover, S, gen, &c, &stop_at)
-                                   : walk_block(blk, n, eof, spos, sover, S, gen, &c, &stop_at, a, m, k);
+      const uint8_t walked = walk_block(blk, n, eof, spos, sover, S, gen, &c, &stop_at, a, m, k);
       // the block's run of staging entries (the atomic's round trip overlaps
       // the CRCs: its value is first used by the staging stores)
       uint32_t off = 0;
@@ -1029,7 +830,6 @@ __global__ void __launch_bounds__(64 * kEmitWaves) log_emit_kernel(LogArgs a) {
   if (blockIdx.x == 0 && tid == 0) {
     *a.ticket = 0;
     *a.stg_top = 0;
-    if (a.wover_top != nullptr) *a.wover_top = 0;
   }
   // counts before b0 (and, in the last workgroup, every block's totals);
   // scanned already when there are many blocks
@@ -1124,14 +924,11 @@ __global__ void __launch_bounds__(64 * kEmitWaves) log_emit_kernel(LogArgs a) {
 }
 
 // Scratch: [0, 8) unused, [8, 16) the logical layer's counter (not touched
-// here), [16, 20) ticket counter, [20, 24) staging counter, [24, 28) the
-// walk-first path's overflow counter, then from byte
-// 32 info (16 B per block), stg_off (u32 per block) and 4 unused bytes per block,
-// the staging array (16 B per record, `capacity` of them) and the slots'
-// overflow positions (u32, kPosOver per slot of each of the grid's
-// workgroups).
-// The counters, info (16 B a block), stg_off (4 B a block, 8 reserved),
-// first_of (8 B a block, and one).
+// here), [16, 20) ticket counter, [20, 24) staging counter, then from byte
+// 32 info (16 B per block), stg_off (u32 per block) and 4 unused bytes per
+// block, first_of (u64 per block, and one), the staging array (16 B per
+// record, `capacity` of them) and the slots' overflow positions (u32,
+// kPosOver per slot of each of the grid's workgroups).
 size_t log_scratch_head(uint64_t nblocks) {
   return (32 + static_cast<size_t>(nblocks) * 32 + 8 + 15) & ~size_t{15};
 }
@@ -1150,38 +947,17 @@ uint64_t* g_log_stamps = nullptr;  // lvkv_debug_log_stamps
 uint32_t g_log_knobs = 0;          // lvkv_debug_log_knobs (LogArgs::knobs)
 #endif
 
-// Walkers of the walk-first path.
-uint32_t walk_groups(uint64_t nblocks, int cus) {
-  return static_cast<uint32_t>(std::max<uint64_t>(
-      1, std::min<uint64_t>(nblocks, uint64_t{kWalkPerCu} * static_cast<uint64_t>(cus))));
-}
-
-// The slot path's layout (head, staging, the slots' overflow positions),
-// then the walk-first path's: winfo (16 B per block), wpos (kWalkSlot u16
-// per block), wover (u16 per record), the walkers' scratch (u16 x kMaxRecs
-// each); offsets 16-aligned.
-size_t slot_scratch_bytes(uint64_t nblocks, uint32_t capacity, int cus) {
-  return log_scratch_head(nblocks) + size_t{capacity} * 16 +
-         size_t{log_groups(nblocks, cus)} * kSlots * kPosOver * 4;
-}
-size_t walk_scratch_bytes(uint64_t nblocks, uint32_t capacity, int cus) {
-  size_t at = (slot_scratch_bytes(nblocks, capacity, cus) + 15) & ~size_t{15};
-  at += static_cast<size_t>(nblocks) * 16;
-  at += (static_cast<size_t>(nblocks) * kWalkSlot * 2 + 15) & ~size_t{15};
-  at += (size_t{capacity} * 2 + 15) & ~size_t{15};
-  return at + size_t{walk_groups(nblocks, cus)} * kMaxRecs * 2;
-}
-
 size_t log_scratch_bytes(uint64_t size, uint32_t capacity, int cus) {
   const uint64_t nblocks = (size + kLogBlock - 1) / kLogBlock;
-  return walk_scratch_bytes(nblocks, capacity, cus);
+  return log_scratch_head(nblocks) + size_t{capacity} * 16 +
+         size_t{log_groups(nblocks, cus)} * kSlots * kPosOver * 4;
 }
 
 hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_off,
                              uint32_t* actual, uint8_t* rec_status, uint32_t capacity,
                              uint8_t* block_status, uint32_t* block_drop, lvkv_log_report* r,
                              const uint32_t* zpow, const uint32_t* lane_cols, int cus,
-                             void* scratch, uint32_t* events, int path, hipStream_t stream) {
+                             void* scratch, uint32_t* events, hipStream_t stream) {
   const uint32_t nblocks = static_cast<uint32_t>((size + kLogBlock - 1) / kLogBlock);
   LogArgs a;
   memset(&a, 0, sizeof(a));
@@ -1212,23 +988,6 @@ hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_o
   a.stamps = g_log_stamps;
   a.knobs = g_log_knobs;
 #endif
-  if (path == 1) {  // walk first: the verify loads the walked positions
-    uint8_t* w = sb + ((slot_scratch_bytes(nblocks, capacity, cus) + 15) & ~size_t{15});
-    a.winfo = reinterpret_cast<ulonglong2*>(w);
-    w += static_cast<size_t>(nblocks) * 16;
-    a.wpos = reinterpret_cast<uint16_t*>(w);
-    w += (static_cast<size_t>(nblocks) * kWalkSlot * 2 + 15) & ~size_t{15};
-    a.wover = reinterpret_cast<uint16_t*>(w);
-    w += (size_t{capacity} * 2 + 15) & ~size_t{15};
-    a.over16 = reinterpret_cast<uint16_t*>(w);
-    a.wover_top = reinterpret_cast<uint32_t*>(sb + 24);
-    a.pre = 1;
-    if (nblocks != 0) {
-      hipLaunchKernelGGL(log_walk_kernel, dim3(walk_groups(nblocks, cus)), dim3(64), 0, stream, a);
-      const hipError_t e = hipGetLastError();
-      if (e != hipSuccess) return e;
-    }
-  }
   if (nblocks != 0) {
     hipLaunchKernelGGL(log_verify_kernel, dim3(log_groups(nblocks, cus)), dim3(kVThreads), 0,
                        stream, a);

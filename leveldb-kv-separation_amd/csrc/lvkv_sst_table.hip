@@ -382,6 +382,7 @@ constexpr uint32_t kFilterKeyWords = (kMaxFilterKey + 4) / 4;
 
 struct SstHeadLds {
   uint32_t acc[16];  // per-wave CRC shares
+  uint32_t ftail, ftrail, ftype;  // the filter block's last bytes (speculative form)
   uint32_t fkey[kFilterKeyWords];  // the metaindex key sought, from the kernel argument
   uint8_t foot[kFooterLen];
   uint8_t mbuf[kMetaStage];
@@ -594,6 +595,12 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
   const bool fcrc = spec && h.has_filter && h.filter_status == LVKV_BLOCK_OK;
   const uint64_t fstart = reinterpret_cast<uint64_t>(tb.img) + h.fo, fend = fstart + h.fs + 1;
   if (wave != 0) {
+    if (fcrc && wave == 1 && lane == 0) {  // the verdict's bytes, loaded beside the walk
+      const uint8_t* fe = tb.img + h.fo + h.fs;
+      L.ftail = group_crc_tail(fstart, fend);
+      L.ftype = fe[0];
+      L.ftrail = ld_le32(fe + 1);
+    }
     uint32_t fpart = 0;
     if (fcrc)
       fpart = group_crc_part(lds, fstart, fend, 0u, wave - 1u, W - 1u,
@@ -626,6 +633,10 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
       r->index_size = h.is;
       r->meta_offset = h.mo;
       r->meta_size = h.ms;
+      // the speculative form's CRC workgroups need only the above: published
+      // now, while the other waves finish the filter block (its entry and
+      // its share of nbad / first_bad follow, atomically)
+      if (spec) __hip_atomic_store(&r->done_, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       if (t == ntables - 1) reports[0].total_ = total;
       if (wide) {
         // sst_index_kernel's tag (this call's generation when it has the
@@ -654,14 +665,13 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
         uint32_t fp = 0;
 #pragma unroll
         for (int w = 1; w < W; ++w) fp ^= L.acc[w];
-        crc = group_crc_finish(fp, fstart, fend, 0u, group_crc_tail(fstart, fend));
-        const uint8_t* fe = tb.img + h.fo + h.fs;
-        st = read_status(crc == crc_unmask(ld_le32(fe + 1)), fe[0]);
+        crc = group_crc_finish(fp, fstart, fend, 0u, L.ftail);
+        st = read_status(crc == crc_unmask(L.ftrail), static_cast<uint8_t>(L.ftype));
       }
       spec_crc[e] = crc;
       if (st != LVKV_BLOCK_OK) {
-        r->nbad = 1;
-        r->first_bad = static_cast<uint32_t>(nr);
+        atomicAdd(&r->nbad, 1u);
+        atomicMin(&r->first_bad, static_cast<uint32_t>(nr));
       }
     }
     out_status[e] = st;
@@ -925,6 +935,8 @@ struct SpecLds {
 struct SpecSrc {
   SpecLds* L;
   uint64_t img;  // the table image's address
+  // the stored CRC after each block: loaded by the walk (RagRound::adopt)
+  __device__ __forceinline__ bool trailer(const KernelArgs&) const { return true; }
   __device__ __forceinline__ RagBlock block(const KernelArgs& a, uint32_t b, bool live) const {
     RagBlock g;
     g.ptr_lo = g.ptr_hi = g.len = g.s0 = g.expected = 0;
@@ -940,7 +952,6 @@ struct SpecSrc {
     g.ptr_hi = static_cast<uint32_t>(ptr >> 32);
     g.len = len;
     g.s0 = 0xffffffffu;  // init 0
-    g.expected = crc_unmask(sload_le(ptr + len, 4));
     g.kind = len > a.long_split ? kRagSkip : len < 4 ? kRagTiny : kRagRows;
     return g;
   }

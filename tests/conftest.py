@@ -73,11 +73,3 @@ def sst_form(request, lvkv, gpu):
     lvkv.lib.lvkv_debug_set_sst_form(0)
 
 
-@pytest.fixture(params=[0, 1], ids=["slots", "walk"])
-def log_path(request, lvkv, gpu):
-    """WAL verify path under test (lvkv_debug_set_log_path): 0 = two LDS
-    slots per CU walked and checksummed in one launch, 1 = walk launch first,
-    the slots load the walked positions; back to the default afterwards."""
-    assert lvkv.lib.lvkv_debug_set_log_path(request.param) == 0
-    yield request.param
-    lvkv.lib.lvkv_debug_set_log_path(0)

@@ -94,7 +94,7 @@ def test_device_sst_matches_reference(lvkv, gpu, sst_form):
 
 
 @pytest.mark.gpu
-def test_device_wal_matches_reference(lvkv, gpu, log_path):
+def test_device_wal_matches_reference(lvkv, gpu):
     import torch
     for case in WAL_CASES:
         if case["initial_offset"]:
@@ -135,7 +135,7 @@ def _device_log_records(img, records, hdrs, gathered):
 
 
 @pytest.mark.gpu
-def test_device_log_read_matches_reference(lvkv, gpu, log_path):
+def test_device_log_read_matches_reference(lvkv, gpu):
     # The logical layer on the device (lvkv_log_read_device): records and
     # every Reporter call, against the reference's own log::Reader run on
     # the same damaged images (oracle/gen_damage.cc), from offset 0 and from
@@ -160,7 +160,7 @@ def test_device_log_read_matches_reference(lvkv, gpu, log_path):
 
 
 @pytest.mark.gpu
-def test_device_log_read_large_and_capacity(lvkv, gpu, log_path):
+def test_device_log_read_large_and_capacity(lvkv, gpu):
     # A synthetic 20k-record log with fragmented records across blocks and
     # random damage: device ReadRecord = the oracle's; too-small capacities
     # are reported with exact counts.

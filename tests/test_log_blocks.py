@@ -193,13 +193,13 @@ def _assert_matches(lvkv, img: bytes, gpu):
 
 
 @pytest.mark.gpu
-def test_device_log_golden(lvkv, gpu, log_path):
+def test_device_log_golden(lvkv, gpu):
     rep = _assert_matches(lvkv, _golden_log(), gpu)
     assert rep["ngood"] == 18 and rep["ncorrupt"] == 0
 
 
 @pytest.mark.gpu
-def test_device_log_reference_cases(lvkv, gpu, log_path):
+def test_device_log_reference_cases(lvkv, gpu):
     def one(payload):
         wr = log_synth.LogWriter()
         wr.add_record(payload)
@@ -218,7 +218,7 @@ def test_device_log_reference_cases(lvkv, gpu, log_path):
 
 
 @pytest.mark.gpu
-def test_device_log_random_damage(lvkv, gpu, log_path):
+def test_device_log_random_damage(lvkv, gpu):
     img = log_synth.build_log(400, seed=9, max_len=5000, big_every=61)
     rng = random.Random(11)
     for _ in range(40):
@@ -235,7 +235,7 @@ def test_device_log_random_damage(lvkv, gpu, log_path):
 
 
 @pytest.mark.gpu
-def test_device_log_large_and_capacity(lvkv, gpu, log_path):
+def test_device_log_large_and_capacity(lvkv, gpu):
     img = log_synth.build_log(20_000, seed=3, max_len=600, big_every=997)  # ~6 MB, ~190 blocks
     rep = _assert_matches(lvkv, img, gpu)
     assert rep["ncorrupt"] == 0 and rep["nblocks"] == (len(img) + 32767) // 32768
@@ -244,7 +244,7 @@ def test_device_log_large_and_capacity(lvkv, gpu, log_path):
 
 
 @pytest.mark.gpu
-def test_device_log_many_blocks_tiled(lvkv, gpu, log_path):
+def test_device_log_many_blocks_tiled(lvkv, gpu):
     """Past 4096 blocks the emit launch takes every block's first record from
     log_scan_kernel instead of summing the counts before it. A damaged ~1 MB
     log padded to whole 32 KiB blocks (zero trailers, skipped silently) and
@@ -299,7 +299,7 @@ def test_device_fill_headers_rebuilds_the_log(lvkv, gpu, source):
 
 
 @pytest.mark.gpu
-def test_device_log_two_streams_at_once(lvkv, gpu, log_path):
+def test_device_log_two_streams_at_once(lvkv, gpu):
     """Two WAL verifies in flight on two streams (and back to back on each):
     blocks are claimed by ticket and each call has its own scratch, so the
     calls neither deadlock nor share counters; every result equals the
@@ -380,7 +380,7 @@ def test_device_log_refuses_stream_capture(lvkv, gpu):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("max_len", [1, 24])
-def test_device_log_dense_blocks(lvkv, gpu, log_path, max_len):
+def test_device_log_dense_blocks(lvkv, gpu, max_len):
     """Blocks of thousands of tiny records (7-30 bytes each: up to 4681 in a
     block), past what a slot keeps in LDS: the positions beyond it go
     through the slot's scratch overflow. Also a few damaged ones."""

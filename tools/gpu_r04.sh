@@ -22,10 +22,10 @@ if want bench; then
   cat gpurun_out/bench_k20.json
 fi
 if want logprof; then
-  for P in ${LOGPATHS:-0 1}; do
-    D=gpurun_out/r04_logread_prof_p$P
+  for P in 0; do
+    D=gpurun_out/r04_logread_prof
     rm -rf $D
-    timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 tools/probe/log_probe.py 60000 --read --path=$P > $D.log 2>&1 \
+    timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 tools/probe/log_probe.py 60000 --read > $D.log 2>&1 \
       || { echo "log prof failed"; tail -20 $D.log; exit 1; }
     grep -v amdgpu.ids $D.log | grep "log_" | tail -4
     python3 -c "

@@ -27,8 +27,6 @@ lvkv = g.load_package()
 
 def main():
     nrec = int(sys.argv[1]) if len(sys.argv) > 1 else 60000
-    path = int(next((x.split("=")[1] for x in sys.argv if x.startswith("--path=")), 0))
-    assert lvkv.lib.lvkv_debug_set_log_path(path) == 0  # WAL verify path (0 slots, 1 walk)
     img = log_synth.build_log(nrec, seed=nrec, max_len=2000, big_every=997)
     dev = torch.device("cuda:0")
     buf = torch.from_numpy(np.frombuffer(img, dtype=np.uint8).copy()).to(dev)
