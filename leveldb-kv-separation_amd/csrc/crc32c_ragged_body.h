@@ -272,7 +272,7 @@ struct RagRound {
   uint32_t blk[NCH];
   uint32_t nchunks;  // max over the chains, >= 1
   uint32_t w[NCH][R + 1];  // row R: the neighbour dwords of row R - 1
-  uint32_t x0[NCH], x1[NCH];  // the stored trailer's aligned dwords (Src::trailer)
+  uint32_t x[NCH];  // the stored trailer's aligned dwords (Src::trailer): lanes 0, 1
 
   // Chain c of round r0 is block start + r0 + c * W + wave.
   template <class Src>
@@ -295,17 +295,21 @@ struct RagRound {
       g[c] = in[c];
       blk[c] = start + r0 + static_cast<uint32_t>(c) * W + wave;
       if (g[c].kind == kRagRows) nchunks = max(nchunks, (g[c].rows() + R - 1) / R);
-      x0[c] = x1[c] = 0;
+      x[c] = 0;
       if (trailer && (g[c].kind == kRagRows || g[c].kind == kRagTiny)) {
+        // lane 0 the dword holding the trailer's first byte, lane 1 the next
+        // (when the trailer straddles two)
         const uint64_t t = g[c].ptr() + g[c].len;
-        x0[c] = gload32(t & ~uint64_t{3});
-        x1[c] = (t & 3u) ? gload32((t & ~uint64_t{3}) + 4u) : 0u;
+        const uint32_t lane = lane_id();
+        if (lane == 0 || (lane == 1 && (t & 3u)))
+          x[c] = gload32((t & ~uint64_t{3}) + 4u * lane);
       }
     }
   }
   __device__ __forceinline__ uint32_t expected(int c) const {
     const uint32_t sh = static_cast<uint32_t>(g[c].ptr_lo + g[c].len) & 3u;
-    return crc_unmask(__builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbyte(x1[c], x0[c], sh)));
+    const uint32_t lo = __builtin_amdgcn_readlane(x[c], 0), hi = __builtin_amdgcn_readlane(x[c], 1);
+    return crc_unmask(__builtin_amdgcn_alignbyte(hi, lo, sh));
   }
 
   // R + 1 loads per chain, unconditional: rows past the block (and every

@@ -916,7 +916,7 @@ struct SpecLds {
   uint32_t rst[kSpecPass + 1];   // the pass's restart offsets, then its end
   uint8_t st[kSpecPass];         // parse status, then ReadBlock's verdict
   union {
-    uint32_t tail[kSpecTail / 4 + 1];   // the index's last bytes (aligned dwords)
+    uint32_t tail[kSpecTail / 4 + 16];  // the table's / index's last bytes (aligned dwords)
     uint32_t win[kSpecWindow / 4 + 1];  // the pass's entry bytes (aligned dwords)
     uint32_t crc[kSpecPass];            // computed CRCs (after the decode)
   };
@@ -929,6 +929,13 @@ struct SpecLds {
   uint32_t first, nblocks, ndata;
   uint32_t nbad, minbad;
 };
+
+// A 64-bit value every lane holds alike, as scalars.
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32)))
+          << 32) |
+         __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+}
 
 // The walk's blocks: the pass's decoded entries in LDS; its results go back
 // there (CRC, ReadBlock's verdict merged as rag_store's kModeSstTable does).
@@ -1039,28 +1046,50 @@ __device__ __forceinline__ void spec_crc_group(const KernelArgs& a, const uint8_
   uint64_t* st = k == 0 ? stamps : nullptr;
   sst_stamp(st, t, 8);
 
-  // 2. The footer (format.cc:43-67); a table whose index cannot be read or
-  //    has no usable restart array has no data entries (its head reports why).
-  if (tid < kFooterLen && tb.size >= kFooterLen) L.foot[tid] = tb.img[tb.size - kFooterLen + tid];
+  // 2. The table's last bytes in one round trip: the footer (format.cc:43-67)
+  //    and, where TableBuilder leaves the index (right before its 5-byte
+  //    trailer and the footer), the index's last kSpecTail bytes with its
+  //    restart array. A table whose index cannot be read or has no usable
+  //    restart array has no data entries (its head reports why).
+  uint8_t* tb8 = reinterpret_cast<uint8_t*>(L.tail);
+  const uint64_t img = reinterpret_cast<uint64_t>(tb.img), tend = img + tb.size;
+  const uint64_t s4 =
+      (tend - min<uint64_t>(tb.size, kSpecTail + kFooterLen + kTrailer)) & ~uint64_t{3};
+  const bool staged = s4 >= img && tb.size >= kFooterLen;
+  if (staged) {
+    const uint64_t e4 = tend & ~uint64_t{3};
+    const uint32_t ndw = static_cast<uint32_t>((e4 - s4) >> 2);
+    for (uint32_t i = tid; i < ndw; i += kT) L.tail[i] = *reinterpret_cast<const uint32_t*>(s4 + 4u * i);
+    if (tid < (tend & 3u)) tb8[e4 - s4 + tid] = *reinterpret_cast<const uint8_t*>(e4 + tid);
+  } else if (tid < kFooterLen && tb.size >= kFooterLen) {
+    L.foot[tid] = tb.img[tb.size - kFooterLen + tid];
+  }
   __syncthreads();
-  if (tid == 0) parse_footer(L.h, L.foot, tb.size);
+  if (tid == 0) parse_footer(L.h, staged ? tb8 + (tend - kFooterLen - s4) : L.foot, tb.size);
   __syncthreads();
   if (L.h.status != LVKV_SST_OK || L.h.ifit != kFitOk || L.h.is < 4) return;
-  const uint64_t io = L.h.io, is = L.h.is;
+  // (LDS values the whole workgroup shares: made scalar, so what derives from
+  // them does not hold vector registers through the walk)
+  const uint64_t io = uni64(L.h.io), is = uni64(L.h.is);
   const uint8_t* idx = tb.img + io;
   const uint64_t istart = reinterpret_cast<uint64_t>(idx), iend = istart + is;
 
-  // 3. The index's last bytes (the restart array), staged as aligned dwords.
+  // 3. The index's last bytes (the restart array): already staged when the
+  //    index ends where TableBuilder puts it, else staged now.
   const uint64_t tlo = iend - min<uint64_t>(is, kSpecTail);
-  const uint64_t t4 = tlo & ~uint64_t{3};
-  const bool tail_ok = t4 >= reinterpret_cast<uint64_t>(tb.img);
-  if (tail_ok) {
-    const uint32_t ndw = static_cast<uint32_t>((iend - t4 + 3) >> 2);
-    for (uint32_t i = tid; i < ndw; i += kT)
-      L.tail[i] = *reinterpret_cast<const uint32_t*>(t4 + 4u * i);
+  bool tail_ok = staged && tlo >= s4;
+  uint64_t t4 = s4;
+  if (!tail_ok) {
+    t4 = tlo & ~uint64_t{3};
+    tail_ok = t4 >= img;
+    __syncthreads();  // the footer's bytes are read
+    if (tail_ok) {
+      const uint32_t ndw = static_cast<uint32_t>((iend - t4 + 3) >> 2);
+      for (uint32_t i = tid; i < ndw; i += kT)
+        L.tail[i] = *reinterpret_cast<const uint32_t*>(t4 + 4u * i);
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  const uint8_t* tb8 = reinterpret_cast<const uint8_t*>(L.tail);
   auto le32_at = [&](uint64_t addr) -> uint32_t {  // index bytes, staged when possible
     if (tail_ok && addr >= tlo) {
       const uint8_t* q = tb8 + (addr - t4);
@@ -1069,7 +1098,7 @@ __device__ __forceinline__ void spec_crc_group(const KernelArgs& a, const uint8_
     }
     return ld_le32(reinterpret_cast<const uint8_t*>(addr));
   };
-  const uint32_t nr = le32_at(iend - 4);
+  const uint32_t nr = __builtin_amdgcn_readfirstlane(le32_at(iend - 4));
   if (nr > (is - 4) / 4 || nr == 0) return;  // Block::Block (block.cc:28-37)
   const uint64_t ro = is - (1 + uint64_t{nr}) * 4;
   const uint32_t i0 = static_cast<uint32_t>(uint64_t{k} * nr / c);
@@ -1095,7 +1124,7 @@ __device__ __forceinline__ void spec_crc_group(const KernelArgs& a, const uint8_
       L.whi = ok ? hi : 0;
     }
     __syncthreads();  // the tail is read: the window may overwrite it
-    const uint64_t wlo = L.wlo, whi = L.whi;
+    const uint64_t wlo = uni64(L.wlo), whi = uni64(L.whi);
     const uint64_t w4 = (istart + wlo) & ~uint64_t{3};
     const uint32_t wsh = static_cast<uint32_t>((istart + wlo) & 3u);
     if (whi > wlo) {
@@ -1119,7 +1148,7 @@ __device__ __forceinline__ void spec_crc_group(const KernelArgs& a, const uint8_
     __syncthreads();
     if (p0 == i0) sst_stamp(st, t, 9);
     // 5. The walk (ragged_run over the LDS list, long blocks by the group).
-    ragged_run<W, 2, 24>(a, zpow, lane_cols, lds, 0, 1, n, true, src);
+    ragged_run<W, 3, 17>(a, zpow, lane_cols, lds, 0, 1, n, true, src);
     __syncthreads();
     if (p0 == i0) sst_stamp(st, t, 10);
     // 6. The head's verdict and the table's place (agent-scope loads of what
@@ -1136,7 +1165,9 @@ __device__ __forceinline__ void spec_crc_group(const KernelArgs& a, const uint8_
       waited = true;
       sst_stamp(st, t, 11);
     }
-    const uint32_t first = L.first, nblocks = L.nblocks, ndata = L.ndata;
+    const uint32_t first = __builtin_amdgcn_readfirstlane(L.first);
+    const uint32_t nblocks = __builtin_amdgcn_readfirstlane(L.nblocks);
+    const uint32_t ndata = __builtin_amdgcn_readfirstlane(L.ndata);
     if (tid == 0) {
       L.nbad = 0;
       L.minbad = 0xffffffffu;
