@@ -72,6 +72,11 @@ int lvkv_debug_engine_stall(struct lvkv_engine* engine, int stall, double stuck_
  * 8 x 4 x 8, 4 = one-round 8 x 4 x 17, 5 = one-round 8 x 6 x 8; -1 = chosen by
  * the batch's layout (the default). */
 int lvkv_debug_engine_ragged_spec(struct lvkv_engine* engine, int spec);
+/* The engine's kernel-argument cache: dispatches whose arguments an earlier
+ * dispatch's cached VRAM copy already held (no BAR write, no HDP flush), and
+ * those written afresh. */
+int lvkv_debug_engine_kernarg_cache(struct lvkv_engine* engine, uint64_t* hits,
+                                    uint64_t* misses);
 
 #ifdef __cplusplus
 }

@@ -123,6 +123,8 @@ def _load() -> ctypes.CDLL:
     L.lvkv_engine_shape.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32),
                                     ctypes.POINTER(u32)]
     L.lvkv_engine_shape.restype = i32
+    L.lvkv_debug_engine_kernarg_cache.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]
+    L.lvkv_debug_engine_kernarg_cache.restype = i32
     L.lvkv_engine_profile.argtypes = [vp, i32]
     L.lvkv_engine_profile.restype = i32
     L.lvkv_engine_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double),
@@ -756,6 +758,13 @@ class Engine:
     def wait(self) -> None:
         _check("lvkv_engine_wait", _lib.lvkv_engine_wait(self.handle))
         self._inflight.clear()
+
+    def kernarg_cache(self) -> Tuple[int, int]:
+        """(hits, misses) of the engine's kernel-argument cache."""
+        h, m = ctypes.c_uint64(), ctypes.c_uint64()
+        _check("lvkv_debug_engine_kernarg_cache",
+               _lib.lvkv_debug_engine_kernarg_cache(self.handle, ctypes.byref(h), ctypes.byref(m)))
+        return int(h.value), int(m.value)
 
     def queues(self, n: int = 0) -> int:
         r = int(_lib.lvkv_engine_queues(self.handle, n))

@@ -62,6 +62,12 @@ namespace {
 
 constexpr uint32_t kSlots = 1024;       // kernarg slots (dispatches between fences)
 constexpr uint32_t kSlotBytes = 256;
+// Kernel-argument cache (VRAM kernargs only): a dispatch whose arguments
+// equal an earlier one's (a service cycling over a fixed set of buffers)
+// points its packet at that earlier copy instead of writing the BAR and
+// flushing the HDP again. kCacheSets sets of kCacheWays slots after the ring.
+constexpr uint32_t kCacheSets = 256, kCacheWays = 4;
+constexpr uint32_t kCacheSlots = kCacheSets * kCacheWays;
 constexpr uint32_t kQueuePackets = 1024;
 constexpr int kQueues = 4;              // hardware queues per engine
 constexpr int kDefaultQueues = 3;       // in use by default (measured best)
@@ -218,8 +224,16 @@ struct Engine {
   int fence_acq = HSA_FENCE_SCOPE_NONE, fence_rel = HSA_FENCE_SCOPE_SYSTEM;
   int variant = 0;          // kernel of overlapped dispatches
   int ordered_variant = 1;  // kernel of ordered dispatches (the whole chip)
-  uint8_t* kernarg = nullptr;     // kSlots x kSlotBytes
+  uint8_t* kernarg = nullptr;     // (kSlots + kCacheSlots) x kSlotBytes
   bool kernarg_vram = false;      // BAR-written VRAM (else system memory)
+  struct CachedArgs {             // host copy of a cached kernarg slot
+    uint64_t hash = 0;
+    uint64_t last = 0;            // 1 + index of the last dispatch that used it (0: empty)
+    uint32_t size = 0;
+    uint8_t bytes[kSlotBytes];
+  };
+  CachedArgs* ka_cache = nullptr;  // kCacheSlots
+  uint64_t ka_hits = 0, ka_misses = 0;
   uint32_t* hdp_flush = nullptr;  // HDP_MEM_FLUSH_CNTL
   hsa_signal_t fence_sig{};       // barrier-AND fences, one decrement per queue
   bool fence_ok = false;
@@ -300,6 +314,7 @@ void destroy(Engine* e) {
     else
       hsa_memory_free(e->kernarg);
   }
+  delete[] e->ka_cache;
   drop_probe(*e);
   if (e->exe_ok) hsa_executable_destroy(e->exe);
   if (e->reader_ok) hsa_code_object_reader_destroy(e->reader);
@@ -319,11 +334,13 @@ bool alloc_kernargs(Engine& e) {
       hsa_agent_get_info(e.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_HDP_FLUSH),
                          &hdp) == HSA_STATUS_SUCCESS &&
       hdp.HDP_MEM_FLUSH_CNTL != nullptr &&
-      hsa_amd_memory_pool_allocate(pf.pool, kSlots * kSlotBytes, 0, &p) == HSA_STATUS_SUCCESS) {
+      hsa_amd_memory_pool_allocate(pf.pool, (kSlots + kCacheSlots) * kSlotBytes, 0, &p) ==
+          HSA_STATUS_SUCCESS) {
     if (hsa_amd_agents_allow_access(1, &cpu, nullptr, p) == HSA_STATUS_SUCCESS) {
       e.kernarg = static_cast<uint8_t*>(p);
       e.kernarg_vram = true;
       e.hdp_flush = hdp.HDP_MEM_FLUSH_CNTL;
+      e.ka_cache = new Engine::CachedArgs[kCacheSlots];
       return true;
     }
     hsa_amd_memory_pool_free(p);
@@ -557,6 +574,52 @@ int fence(Engine& e) {
   return e.queue_error ? LVKV_ERR_HIP : LVKV_OK;
 }
 
+// The kernarg copy dispatch n points at: a cached slot holding exactly
+// args[0, size) (its BAR write and HDP flush done by an earlier dispatch), a
+// cache slot no unfinished dispatch uses (written now), or ring slot
+// n % kSlots (written now). Caller holds e.mu.
+uint8_t* kernarg_slot(Engine& e, uint64_t n, const void* args, size_t size) {
+  uint8_t* ka = e.kernarg + static_cast<size_t>(n % kSlots) * kSlotBytes;
+  if (e.kernarg_vram) {
+    // FNV-1a over the argument bytes picks the set
+    uint64_t h = 1469598103934665603ull;
+    const uint8_t* b = static_cast<const uint8_t*>(args);
+    for (size_t i = 0; i < size; ++i) h = (h ^ b[i]) * 1099511628211ull;
+    const uint32_t set = static_cast<uint32_t>(h % kCacheSets);
+    Engine::CachedArgs* ways = e.ka_cache + static_cast<size_t>(set) * kCacheWays;
+    int victim = -1;
+    for (uint32_t w = 0; w < kCacheWays; ++w) {
+      Engine::CachedArgs& c = ways[w];
+      if (c.last != 0 && c.hash == h && c.size == size && memcmp(c.bytes, args, size) == 0) {
+        c.last = n + 1;
+        ++e.ka_hits;
+        return e.kernarg + (kSlots + static_cast<size_t>(set) * kCacheWays + w) * kSlotBytes;
+      }
+      // a slot no unfinished dispatch reads: the least recently used
+      if (c.last <= e.fenced && (victim < 0 || c.last < ways[victim].last)) victim = static_cast<int>(w);
+    }
+    ++e.ka_misses;
+    if (victim >= 0) {
+      Engine::CachedArgs& c = ways[victim];
+      c.hash = h;
+      c.size = static_cast<uint32_t>(size);
+      c.last = n + 1;
+      memcpy(c.bytes, args, size);
+      ka = e.kernarg + (kSlots + static_cast<size_t>(set) * kCacheWays + victim) * kSlotBytes;
+    }
+  }
+  memcpy(ka, args, size);
+  if (e.kernarg_vram) {
+    // BAR writes are write-combined and may sit in the HDP write cache: fence
+    // them, flush the HDP and read the register back (the read completes
+    // only behind the posted writes) before the packet can be seen.
+    __builtin_ia32_sfence();
+    *reinterpret_cast<volatile uint32_t*>(e.hdp_flush) = 1u;
+    (void)*reinterpret_cast<volatile uint32_t*>(e.hdp_flush);
+  }
+  return ka;
+}
+
 // One kernel-dispatch packet of `ngroups` workgroups whose kernel arguments
 // are args[0, size); the caller holds e.mu. queue < 0: dispatch n goes to
 // queue n % nq (consecutive dispatches side by side); else that queue.
@@ -583,16 +646,7 @@ int dispatch(Engine& e, const EngineKernel& k, const void* args, size_t size, ui
     e.prof_pending[s] = true;
     done = e.prof_sig[s];
   }
-  uint8_t* ka = e.kernarg + static_cast<size_t>(n % kSlots) * kSlotBytes;
-  memcpy(ka, args, size);
-  if (e.kernarg_vram) {
-    // BAR writes are write-combined and may sit in the HDP write cache: fence
-    // them, flush the HDP and read the register back (the read completes
-    // only behind the posted writes) before the packet can be seen.
-    __builtin_ia32_sfence();
-    *reinterpret_cast<volatile uint32_t*>(e.hdp_flush) = 1u;
-    (void)*reinterpret_cast<volatile uint32_t*>(e.hdp_flush);
-  }
+  uint8_t* ka = kernarg_slot(e, n, args, size);
   uint64_t idx;
   hsa_kernel_dispatch_packet_t* p = static_cast<hsa_kernel_dispatch_packet_t*>(packet_slot(e, &idx));
   if (p == nullptr) return LVKV_ERR_HIP;
@@ -1042,6 +1096,15 @@ int lvkv_debug_engine_ragged_spec(lvkv_engine* eng, int spec) {
   Engine* e = reinterpret_cast<Engine*>(eng);
   std::lock_guard<std::mutex> lk(e->mu);
   e->ragged_spec = spec;
+  return LVKV_OK;
+}
+
+int lvkv_debug_engine_kernarg_cache(lvkv_engine* eng, uint64_t* hits, uint64_t* misses) {
+  if (eng == nullptr || hits == nullptr || misses == nullptr) return LVKV_ERR_INVALID;
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  std::lock_guard<std::mutex> lk(e->mu);
+  *hits = e->ka_hits;
+  *misses = e->ka_misses;
   return LVKV_OK;
 }
 
