@@ -924,11 +924,13 @@ __global__ void __launch_bounds__(kGatherT) log_gather_kernel(GatherArgs a) {
 // ... and walks them as a stream of 1 KiB units (candidate, round): the next
 // unit's loads are issued before the current unit's stores, and each
 // candidate's place is fetched one candidate ahead, so two units of every wave
-// are in flight. Each output word is rebuilt from two aligned source dwords
-// (a buffer resource over the payload's aligned dwords: a dword past them
-// reads as 0; one partly past a range's end would read as 0 whole); the 0-3
-// bytes before the output's first 4-byte boundary and after its last go
-// bytewise. (One wave per candidate over a grid of N waves: 50 us for the
+// are in flight. A lane moves 16 consecutive output bytes a round, each word
+// rebuilt from two aligned source dwords (one 16-byte and one 4-byte buffer
+// load over the payload's aligned dwords: a dword past them reads as 0, one
+// partly past a range's end would read as 0 whole; eight 4-byte loads and
+// four 4-byte stores a lane, this round's first form, took 35 us on the
+// 62k-record log); the 0-3 bytes before the
+// output's first 4-byte boundary and after its last go bytewise. (One wave per candidate over a grid of N waves: 50 us for the
 // 62k-record log, and a grid sized by the capacity that passed 2^32
 // work-items above ~470 MB images.)
 struct CopyJob {
@@ -951,11 +953,16 @@ __device__ __forceinline__ CopyJob copy_job(const GatherArgs& a, ulonglong2 de) 
   return c;
 }
 
+typedef uint32_t CopyV4 __attribute__((ext_vector_type(4)));
+
+// A lane's part of a round: output words w0 .. w0 + 3 (w0 = 256 r + 4 lane)
+// from the five aligned source dwords holding them.
 struct CopyRegs {
-  uint32_t lo[4], hi[4];
+  CopyV4 d;    // source dwords k0 .. k0 + 3
+  uint32_t e;  // source dword k0 + 4
 };
 
-// Loads of round r of job c (lane's words w0 + lane + 64u).
+// Loads of round r of job c: one 16-byte and one 4-byte buffer load a lane.
 __device__ __forceinline__ CopyRegs copy_load(const CopyJob& c, uint32_t r, uint32_t lane) {
   CopyRegs x;
   const uint64_t s0 = reinterpret_cast<uint64_t>(c.src);
@@ -965,16 +972,14 @@ __device__ __forceinline__ CopyRegs copy_load(const CopyJob& c, uint32_t r, uint
       kBufferDword3);
   const uint32_t hb = min(c.l, (4u - static_cast<uint32_t>(reinterpret_cast<uint64_t>(c.dst) & 3u)) & 3u);
   const uint32_t sb = static_cast<uint32_t>(s0 - sa) + hb;
-#pragma unroll
-  for (uint32_t u = 0; u < 4; ++u) {
-    const uint32_t so = (sb + 4u * (256u * r + 64u * u + lane)) & ~3u;
-    x.lo[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(so), 0, 0);
-    x.hi[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(so + 4u), 0, 0);
-  }
+  const int off = static_cast<int>((sb & ~3u) + 4u * (256u * r + 4u * lane));
+  x.d = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+  x.e = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 16, 0, 0);
   return x;
 }
 
-// Stores of round r of job c (the head and tail bytes with round 0).
+// Stores of round r of job c (the head and tail bytes with round 0): one
+// 16-byte store a lane where its four words are all inside the payload.
 __device__ __forceinline__ void copy_store(const CopyJob& c, uint32_t r, uint32_t lane,
                                            const CopyRegs& x) {
   if (c.l == 0) return;
@@ -982,10 +987,18 @@ __device__ __forceinline__ void copy_store(const CopyJob& c, uint32_t r, uint32_
   const uint32_t nw = (c.l - hb) >> 2;
   const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uint64_t>(c.src) + hb) & 3u;
   uint32_t* dw = reinterpret_cast<uint32_t*>(c.dst + hb);
-#pragma unroll
-  for (uint32_t u = 0; u < 4; ++u) {
-    const uint32_t w = 256u * r + 64u * u + lane;
-    if (w < nw) dw[w] = __builtin_amdgcn_alignbyte(x.hi[u], x.lo[u], sh);
+  const uint32_t w0 = 256u * r + 4u * lane;
+  CopyV4 o;
+  o.x = __builtin_amdgcn_alignbyte(x.d.y, x.d.x, sh);
+  o.y = __builtin_amdgcn_alignbyte(x.d.z, x.d.y, sh);
+  o.z = __builtin_amdgcn_alignbyte(x.d.w, x.d.z, sh);
+  o.w = __builtin_amdgcn_alignbyte(x.e, x.d.w, sh);
+  if (w0 + 4u <= nw) {
+    __builtin_memcpy(dw + w0, &o, 16);  // (4-byte aligned: one dwordx4 store on gfx950)
+  } else {
+    if (w0 < nw) dw[w0] = o.x;
+    if (w0 + 1u < nw) dw[w0 + 1u] = o.y;
+    if (w0 + 2u < nw) dw[w0 + 2u] = o.z;
   }
   if (r == 0) {
     if (lane < hb) c.dst[lane] = c.src[lane];
