@@ -267,11 +267,12 @@ typedef struct lvkv_sst_report {
  * ReadBlock on every block (table/format.cc:69-160) would with
  * verify_checksums: footer and magic, index and metaindex checksums and type
  * bytes, then every data block the index lists and the filter block, all on
- * the device in two launches (three when a single table's index is wide, its
- * CRC and entries then spread over 64 workgroups) (a per-table workgroup for the footer, index and
- * metaindex CRCs, the filter lookup and the index parse, one entry per
- * restart point as table_builder.cc:35 writes it; then one batched verify
- * with the merge). filter_policy = FilterPolicy::Name() of the reader's
+ * the device: for a table up to 32 MiB one launch (a workgroup for the
+ * footer, index and metaindex CRCs, the filter lookup and the placement,
+ * while the other workgroups each decode a share of the index entries, one
+ * entry per restart point as table_builder.cc:35 writes it, and checksum
+ * their blocks), else two launches (three when the index is wide, its CRC
+ * and entries then spread over 64 workgroups). filter_policy = FilterPolicy::Name() of the reader's
  * Options (e.g. "leveldb.BuiltinBloomFilter2" for NewBloomFilterPolicy,
  * util/bloom.cc): the filter block is the metaindex entry whose key is
  * exactly "filter." + filter_policy (table.cc:100-102); NULL = no policy
@@ -293,9 +294,10 @@ int lvkv_sst_verify_table_device(const void* d_file, uint64_t file_size,
                                  void* stream);
 
 /* Many SSTables at once: compaction inputs (paranoid checks), a repair scan.
- * Table t is d_file[d_table_off[t], + d_table_size[t]) (device arrays). The
- * same two launches as one table serve all of them (one workgroup per
- * table); table t's entries go to the shared per-block arrays from
+ * Table t is d_file[d_table_off[t], + d_table_size[t]) (device arrays). One
+ * launch serves up to half as many tables as the device has CUs (a head
+ * workgroup per table, the CRC workgroups shared out by table size), two
+ * launches more; table t's entries go to the shared per-block arrays from
  * d_reports[t].first on, in table order. d_offsets are offsets into d_file
  * (table offset + BlockHandle offset). A table whose entries do not fit in
  * `capacity` gets LVKV_SST_CAPACITY (with ndata set); so do the tables after

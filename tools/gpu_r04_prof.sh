@@ -1,0 +1,61 @@
+#!/bin/bash
+# Round-4 evidence on one GPU: every GPU test, smoke, the driver's bench
+# command and the default bench, kernel traces (isolated headline launches,
+# the SST forms, the engine's general shapes, the WAL read path), the edges
+# probe. Every GPU step has its own time limit; the first failure ends it.
+#   bash tools/gpu_r04_prof.sh [tests|bench|prof|shapes]...
+set -o pipefail
+cd ${GRAFT_REPO_ROOT:-/root/repo} && mkdir -p gpurun_out && export TMPDIR=/tmp
+steps=${*:-tests bench prof shapes}
+want() { [[ " $steps " == *" $1 "* ]]; }
+O=gpurun_out/r04
+mkdir -p $O
+stats() {  # kernel stats of a rocprofv3 csv output dir, short names
+  python3 -c "
+import csv,glob,sys
+for f in glob.glob(sys.argv[1] + '/**/*kernel_stats.csv', recursive=True):
+    for r in csv.DictReader(open(f)):
+        n = r['Name'].split('(')[0] if '(anonymous' not in r['Name'] else r['Name'].split('::')[2].split('(')[0]
+        print('  ', n[-44:], r['Calls'], r['AverageNs'], r['MinNs'], r['MaxNs'])
+" $1
+}
+if want tests; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 \
+    || { echo "gpu tests failed"; tail -40 $O/pytest_gpu.log; exit 1; }
+  tail -2 $O/pytest_gpu.log
+  timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 \
+    || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
+  tail -1 $O/smoke.log
+fi
+if want bench; then
+  timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_k20.json 2> $O/bench_k20.err \
+    || { echo "bench failed"; tail -20 $O/bench_k20.err; exit 1; }
+  cat $O/bench_k20.json
+  timeout -k 10 400 python bench.py > $O/bench_default.json 2> $O/bench_default.err \
+    || { echo "bench failed"; tail -20 $O/bench_default.err; exit 1; }
+  cat $O/bench_default.json
+  timeout -k 10 200 python tools/probe/edges.py > $O/edges.log 2>&1 || { tail -20 $O/edges.log; exit 1; }
+  cp gpurun_out/edges.json $O/edges.json
+  grep -v amdgpu.ids $O/edges.log | tail -12
+fi
+if want prof; then
+  D=$O/iso_prof; rm -rf $D
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 bench.py --isolated 200 --no-cpu-baseline --no-split --no-pmc > $D.log 2>&1 \
+    || { echo "iso prof failed"; tail -20 $D.log; exit 1; }
+  stats $D
+  for A in "512 --form=3" "512 --form=3 --tables=32" "512 --form=2 --tables=32" "16384 --form=0"; do
+    N=$(echo "$A" | tr -d ' =-' ); D=$O/sst_$N; rm -rf $D
+    timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 tools/probe/sst_probe.py $A > $D.log 2>&1 \
+      || { echo "sst prof failed"; tail -20 $D.log; exit 1; }
+    grep "us/call" $D.log; stats $D
+  done
+  D=$O/logread_prof; rm -rf $D
+  timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 tools/probe/log_probe.py 60000 --read > $D.log 2>&1 \
+    || { echo "log prof failed"; tail -20 $D.log; exit 1; }
+  grep "us/call" $D.log; stats $D
+fi
+if want shapes; then
+  timeout -k 10 400 python tools/probe/engine_shapes.py > $O/engine_shapes.log 2>&1 || { echo shapes failed; tail -20 $O/engine_shapes.log; exit 1; }
+  cp gpurun_out/engine_shapes.json $O/engine_shapes.json 2>/dev/null
+  grep -v amdgpu.ids $O/engine_shapes.log | tail -40
+fi
