@@ -33,6 +33,7 @@ LVKV_FLAG_MASK = 1
 LVKV_FLAG_ORDERED = 2
 LVKV_FLAG_SYSTEM_ACQUIRE = 4
 LVKV_FLAG_FINAL = 8
+LVKV_FLAG_SMALL_BLOCKS = 16
 
 
 class LvkvError(RuntimeError):
@@ -677,8 +678,9 @@ class Engine:
 
     def crc32c_batch(self, buf, offsets, lengths, *, init: int = 0, inits=None,
                      mask: bool = False, ordered: bool = False, fresh: bool = True,
-                     final: bool = False, out=None):
-        """lvkv_engine_crc32c_batch: crc32c_batch's contract on the engine."""
+                     final: bool = False, small: bool = False, out=None):
+        """lvkv_engine_crc32c_batch: crc32c_batch's contract on the engine.
+        small: the blocks are mostly under ~2 KiB (LVKV_FLAG_SMALL_BLOCKS)."""
         torch = _torch()
         n = offsets.numel()
         if lengths.numel() != n:
@@ -691,7 +693,7 @@ class Engine:
             _dev_ptr(lengths, "lengths", (torch.int32,)),
             _dev_ptr(inits, "inits", (torch.int32,), n) if inits is not None else None,
             init & 0xFFFFFFFF, _dev_ptr(out, "out", (torch.int32,), n), n,
-            self._flags(mask, ordered, fresh, final))
+            self._flags(mask, ordered, fresh, final) | (LVKV_FLAG_SMALL_BLOCKS if small else 0))
         _check("lvkv_engine_crc32c_batch", rc)
         self._inflight.append((buf, offsets, lengths, inits, out))
         return out

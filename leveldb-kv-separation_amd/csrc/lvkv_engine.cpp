@@ -686,10 +686,13 @@ int dispatch(Engine& e, const EngineKernel& k, const void* args, size_t size, ui
 //   * blocks of more than 17 rows in a uniform layout (config 3's 32 KiB WAL
 //     blocks): the persistent 8 x 2 x 24 walk (0.77 of 8 TB/s overlapped on
 //     16,384 x 32 KiB);
-//   * WAL records (log verify / fill) and uniform blocks of up to 8 rows: the
-//     persistent 8 x 4 x 8 walk (0.29 overlapped on 62,000 x 0-2000 B, the
-//     one-round 8 x 6 x 8 burst 0.23);
-//   * everything else (SST blocks, ~4.1 KiB): the 8 x 4 x 17 burst, whose
+//   * WAL records (log verify / fill), uniform blocks of up to 8 rows and
+//     ragged batches submitted with LVKV_FLAG_SMALL_BLOCKS (the caller knows
+//     its blocks are small: log::Writer's records): the persistent 8 x 4 x 8
+//     walk (0.29 overlapped on 62,000 x 0-2000 B where the burst gets 0.21;
+//     on SST-sized blocks it gets 0.50 against the burst's 0.63);
+//   * other ragged batches (SST blocks, ~4.1 KiB, the sizes being unknown to
+//     the host) and uniform blocks of 9-17 rows: the 8 x 4 x 17 burst, whose
 //     batch is cut into dispatches of one round (cus x 32 blocks, one
 //     workgroup per CU) rotating over the queues like separate batches, so
 //     consecutive rounds overlap on the device (0.62-0.64 overlapped on
@@ -710,7 +713,7 @@ int submit_general(Engine& eng, KernelArgs a, size_t nblocks, uint32_t flags) {
     const uint64_t rows = (uint64_t{a.length} + 3u + 255u) / 256u;  // upper bound, any alignment
     spec = rows > kBurstRows ? kRaggedSpec : rows <= kBurstSmallRows ? kRaggedSmallSpec : kBurstSpec;
   } else {
-    spec = log ? kRaggedSmallSpec : kBurstSpec;
+    spec = log || (flags & LVKV_FLAG_SMALL_BLOCKS) ? kRaggedSmallSpec : kBurstSpec;
   }
   if (e->ragged_spec >= 0) spec = e->ragged_spec;
   const EngineKernel& k = e->kern[spec];

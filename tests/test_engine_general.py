@@ -28,11 +28,12 @@ def _u32(t):
     return t.cpu().numpy().view(np.uint32)
 
 
-@pytest.mark.parametrize("ordered", [False, True])
-def test_engine_batch_ragged_random(lvkv, oracle, eng, gpu, ordered):
+@pytest.mark.parametrize("ordered,small", [(False, False), (True, False), (False, True)])
+def test_engine_batch_ragged_random(lvkv, oracle, eng, gpu, ordered, small):
     """Random offsets (every alignment), lengths 0..70,000 (blocks over
     64 KiB walked by a whole workgroup in the same dispatch, tiny blocks
-    bitwise), per-block inits; then uniform init with Mask."""
+    bitwise), per-block inits; then uniform init with Mask. `small`: the
+    LVKV_FLAG_SMALL_BLOCKS hint (another walk, the same results)."""
     import torch
     rng = np.random.default_rng(41)
     data = rng.integers(0, 256, 48 << 20, dtype=np.uint8)
@@ -45,8 +46,8 @@ def test_engine_batch_ragged_random(lvkv, oracle, eng, gpu, ordered):
     d = _dev(torch, data, gpu)
     do, dl = _dev(torch, offs.astype(np.int64), gpu), _dev(torch, L.view(np.int32), gpu)
     di = _dev(torch, inits.view(np.int32), gpu)
-    got = eng.crc32c_batch(d, do, dl, inits=di, ordered=ordered)
-    gm = eng.crc32c_batch(d, do, dl, init=0x12345678, mask=True, ordered=ordered)
+    got = eng.crc32c_batch(d, do, dl, inits=di, ordered=ordered, small=small)
+    gm = eng.crc32c_batch(d, do, dl, init=0x12345678, mask=True, ordered=ordered, small=small)
     eng.wait()
     assert np.array_equal(_u32(got), oracle.batch(data, offs, L, inits, threads=8))
     want_m = oracle.batch(data, offs, L, np.full(n, 0x12345678, np.uint32), mask=True, threads=8)

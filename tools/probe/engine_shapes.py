@@ -31,7 +31,7 @@ import __graft_entry__ as g  # noqa: E402
 CASES = {
     "sst4271_16k": (16384, 4271, 4272, 0, False),     # SST-sized, ends unaligned
     "sst4106_16k": (16384, 4106, 4106, 3, False),     # 4105 B + type byte, any alignment
-    "rand2000_62k": (62000, 2000, 0, 7, False),       # WAL-record-sized, packed
+    "rand2000_62k": (62000, 2000, 0, 7, False),       # WAL-record-sized, packed (LVKV_FLAG_SMALL_BLOCKS)
     "wal32k_16k": (16384, 32762, 32768, 6, True),     # config 3 (512 MiB)
     "wal32k_2k": (2048, 32762, 32768, 6, True),
     "u4096_65k": (65536, 4096, 4096, 0, False),
@@ -75,7 +75,9 @@ def main():
                 eng.crc32c_uniform(buf[first:], n, length, stride, ordered=ordered, fresh=False,
                                    out=out)
             else:
-                eng.crc32c_batch(buf, d_off, d_len, ordered=ordered, fresh=False, out=out)
+                # (the small-record case passes the caller's hint)
+                eng.crc32c_batch(buf, d_off, d_len, ordered=ordered, fresh=False, out=out,
+                                 small=name.startswith("rand"))
         want = (oracle.uniform(host[first:], n, length, stride, threads=16) if uniform else
                 oracle.batch(host, offs, lens, threads=16))
         algo = int(lens.sum()) + 4 * n
