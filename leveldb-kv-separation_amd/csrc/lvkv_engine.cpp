@@ -682,7 +682,7 @@ int dispatch(Engine& e, const EngineKernel& k, const void* args, size_t size, ui
 // A general-layout batch (KernelArgs as the HIP path builds it: offsets or
 // the uniform stride, a mode) through the engine's ragged kernels; the
 // same ordering and acquire rules as the uniform submit. The kernel, by the
-// measurements of tools/probe/engine_shapes.py (DESIGN.md §13):
+// measurements of tools/probe/engine_shapes.py (DESIGN.md §12):
 //   * blocks of more than 17 rows in a uniform layout (config 3's 32 KiB WAL
 //     blocks): the persistent 8 x 2 x 24 walk (0.77 of 8 TB/s overlapped on
 //     16,384 x 32 KiB);
@@ -715,6 +715,10 @@ int submit_general(Engine& eng, KernelArgs a, size_t nblocks, uint32_t flags) {
   } else {
     spec = log || (flags & LVKV_FLAG_SMALL_BLOCKS) ? kRaggedSmallSpec : kBurstSpec;
   }
+  // An ordered batch runs alone: the burst's one-round dispatches would run
+  // one after another (16k SST-sized blocks: 0.31 of 8 TB/s, against 0.44
+  // for the persistent 8 x 2 x 24 walk in one dispatch)
+  if (ordered && spec == kBurstSpec) spec = kRaggedSpec;
   if (e->ragged_spec >= 0) spec = e->ragged_spec;
   const EngineKernel& k = e->kern[spec];
   const uint64_t per_round = uint64_t{k.waves} * k.chains;
