@@ -153,9 +153,8 @@ def main():
         us2 = (time.perf_counter() - t0) / 50 * 1e6
         print(f"log_read {nrec} records: {us2:.1f} us/call (verify + ReadRecord)", flush=True)
         if "--asm-stamps" in sys.argv:
-            # log_asm_onepass phases per workgroup (probe build; s_memrealtime,
-            # 100 MHz): 0 start, 1 scanned, 2 published, 3 looked back,
-            # 4 prefix published, 5 written; 6 windows walked
+            # log_asm_emit phases per workgroup (probe build; s_memrealtime,
+            # 100 MHz): 0 start, 1 prefix folded, 3 items scanned, 5 written
             P = ctypes.CDLL(str(HERE / "liblvkv_probe.so"))
             P.lvkv_debug_asm_stamps.argtypes = [vp]
             P.lvkv_log_read_device.argtypes = L.lvkv_log_read_device.argtypes
@@ -175,16 +174,11 @@ def main():
             x = st.cpu().numpy().reshape(-1, 8)
             x = x[x[:, 0] > 0]
             t0s = x[:, 0].min()
-            rel = (x[:, :6] - t0s) / 100.0
-            print(f"asm workgroups {len(x)}: start max {rel[:, 0].max():.2f}; med phases "
-                  f"scan {np.median(rel[:, 1] - rel[:, 0]):.2f} pub {np.median(rel[:, 2] - rel[:, 1]):.2f} "
-                  f"look {np.median(rel[:, 3] - rel[:, 2]):.2f} incl {np.median(rel[:, 4] - rel[:, 3]):.2f} "
-                  f"emit {np.median(rel[:, 5] - rel[:, 4]):.2f}; end max {rel[:, 5].max():.2f}; "
-                  f"windows max {x[:, 6].max()}", flush=True)
-            for gi in sorted({0, 1, 2, 10, 50, 100, 150, 200, len(x) - 1}):
-                if gi < len(x):
-                    print(f"  wg {gi}: " + " ".join(f"{v:.2f}" for v in rel[gi]) +
-                          f" windows {x[gi, 6]}", flush=True)
+            rel = (x - t0s) / 100.0
+            print(f"asm emit workgroups {len(x)}: start max {rel[:, 0].max():.2f}; med phases "
+                  f"fold {np.median(rel[:, 1] - rel[:, 0]):.2f} scan {np.median(rel[:, 3] - rel[:, 1]):.2f} "
+                  f"step+write {np.median(rel[:, 5] - rel[:, 3]):.2f}; end max {rel[:, 5].max():.2f}",
+                  flush=True)
         # + the records' bytes laid end to end (lvkv_log_gather_device)
         payload = torch.empty(len(img), dtype=torch.uint8, device=dev)
         rpos = torch.empty(cap, dtype=torch.int64, device=dev)
