@@ -533,6 +533,12 @@ __device__ __forceinline__ void wg_items(const AsmArgs& a, uint32_t K, uint32_t 
   const uint32_t lane = tid & 63u, w = tid >> 6;
   const uint32_t k = g * kGT + tid;
   it.ev = k < K ? seek_event(a.seek, a.hdr_off, k, a.events[k]) : log_event(kEvNone, 0, 0);
+#ifdef LVKV_PROBE_BUILD
+  if (tid == 0) {
+    asm volatile("" ::"v"(it.ev));
+    asm_stamp(a, 2);
+  }
+#endif
   const Summ e = event_summ(it.ev);
   // the wave's exclusive scan of summaries, from ballots
   const uint64_t below = (uint64_t{1} << lane) - 1u;
@@ -558,6 +564,7 @@ __device__ __forceinline__ void wg_items(const AsmArgs& a, uint32_t K, uint32_t 
   const uint32_t sc_rt = __shfl(sc, rt, 64), p_rt = __shfl(inc, rt, 64);
   if (lane == 0) wagg[w] = prefix_summ(~uint64_t{0}, C, R, S, p_all, rt, c_rt, sc_rt, p_rt, stop5_0);
   __syncthreads();
+  if (tid == 0) asm_stamp(a, 4);
   Summ pre = kIdentity, tot = kIdentity;
 #pragma unroll
   for (uint32_t v = 0; v < kGT / 64; ++v) {
@@ -593,6 +600,7 @@ __device__ __forceinline__ void wg_items(const AsmArgs& a, uint32_t K, uint32_t 
     }
   }
   __syncthreads();
+  if (tid == 0) asm_stamp(a, 6);
 #pragma unroll
   for (uint32_t sw = 0; sw < kScenarios; ++sw) {
     uint32_t before = 0, all = 0, uses = 0;

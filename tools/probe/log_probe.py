@@ -177,6 +177,9 @@ def main():
             rel = (x - t0s) / 100.0
             print(f"asm emit workgroups {len(x)}: start max {rel[:, 0].max():.2f}; med phases "
                   f"fold {np.median(rel[:, 1] - rel[:, 0]):.2f} scan {np.median(rel[:, 3] - rel[:, 1]):.2f} "
+                  f"(event loaded +{np.median(rel[:, 2] - rel[:, 1]):.2f}, barrier 1 "
+                  f"+{np.median(rel[:, 4] - rel[:, 2]):.2f}, barrier 2 +{np.median(rel[:, 6] - rel[:, 4]):.2f}, "
+                  f"rest +{np.median(rel[:, 3] - rel[:, 6]):.2f}) "
                   f"step+write {np.median(rel[:, 5] - rel[:, 3]):.2f}; end max {rel[:, 5].max():.2f}",
                   flush=True)
         # + the records' bytes laid end to end (lvkv_log_gather_device)
