@@ -308,6 +308,36 @@ def test_device_table_with_long_blocks(lvkv, gpu, sst_form):
 
 
 @pytest.mark.gpu
+def test_device_many_small_tables(lvkv, gpu, sst_form):
+    # 120 tables of 1-40 blocks in one call (the speculative form shares its
+    # CRC workgroups out by table size, at least one per table; 120 is under
+    # half the CUs), two of them damaged: each exactly as the oracle says.
+    import torch
+    rng = np.random.default_rng(77)
+    imgs = []
+    for t in range(120):
+        im = bytearray(sst_synth.build_sst(int(rng.integers(1, 41)), int(rng.integers(64, 5000)),
+                                           seed=1000 + t, with_filter=bool(t % 3)))
+        if t in (17, 90):
+            im[int(rng.integers(0, len(im) // 2))] ^= 0x20
+        imgs.append(bytes(im))
+    offs, pos = [], 0
+    for im in imgs:
+        offs.append(pos)
+        pos += len(im) + 7
+    buf = bytearray(pos)
+    for o_, im in zip(offs, imgs):
+        buf[o_: o_ + len(im)] = im
+    dbuf = torch.from_numpy(np.frombuffer(bytes(buf), dtype=np.uint8).copy()).to(gpu)
+    res = lvkv.sst_verify_tables(dbuf, offs, [len(im) for im in imgs])
+    torch.cuda.synchronize()
+    for o_, im, (rep, off, size, actual, status) in zip(offs, imgs, res):
+        got = (rep, off.cpu().numpy(), size.cpu().numpy().view(np.uint32),
+               actual.cpu().numpy().view(np.uint32), status.cpu().numpy())
+        _assert_matches_oracle(lvkv, im, gpu, got=got, base=o_)
+
+
+@pytest.mark.gpu
 def test_device_multi_table_verify(lvkv, gpu, sst_form):
     # Compaction-input shape: many tables in one buffer, each checked exactly
     # as the single-table call would (lvkv_sst_verify_tables_device).
