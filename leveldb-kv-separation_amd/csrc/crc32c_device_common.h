@@ -124,6 +124,83 @@ __device__ __forceinline__ uint32_t wave_xor_dpp(uint32_t v) {
          __builtin_amdgcn_readlane(v, 32) ^ __builtin_amdgcn_readlane(v, 48);
 }
 
+// Integer sums and scans over a wave with every lane active, the same way:
+// DPP row ops (a few VALU cycles each) and v_readlane for the four rows,
+// where __shfl_xor / __shfl_up are ds_bpermute round trips through the LDS
+// unit (~100 cycles, six of them in a row for a 64-lane sum).
+template <int Ctrl>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+  return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), Ctrl, 0xF, 0xF, false));
+}
+// row_shr:n with the lanes that have no source reading 0
+template <int N>
+__device__ __forceinline__ uint32_t dpp_shr0(uint32_t v) {
+  return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x110 + N, 0xF, 0xF, false));
+}
+__device__ __forceinline__ uint32_t lane_u32(uint32_t v, uint32_t l) {
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(l)));
+}
+__device__ __forceinline__ uint64_t lane_u64(uint64_t v, uint32_t l) {
+  return uint64_t{lane_u32(static_cast<uint32_t>(v), l)} |
+         uint64_t{lane_u32(static_cast<uint32_t>(v >> 32), l)} << 32;
+}
+template <int Ctrl, typename T>
+__device__ __forceinline__ T dpp_any(T v) {
+  if constexpr (sizeof(T) == 8) {
+    return static_cast<T>(uint64_t{dpp32<Ctrl>(static_cast<uint32_t>(v))} |
+                          uint64_t{dpp32<Ctrl>(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32))} << 32);
+  } else {
+    return static_cast<T>(dpp32<Ctrl>(static_cast<uint32_t>(v)));
+  }
+}
+template <int N, typename T>
+__device__ __forceinline__ T dpp_shr0_any(T v) {
+  if constexpr (sizeof(T) == 8) {
+    return static_cast<T>(uint64_t{dpp_shr0<N>(static_cast<uint32_t>(v))} |
+                          uint64_t{dpp_shr0<N>(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32))} << 32);
+  } else {
+    return static_cast<T>(dpp_shr0<N>(static_cast<uint32_t>(v)));
+  }
+}
+template <typename T>
+__device__ __forceinline__ T lane_any(T v, uint32_t l) {
+  if constexpr (sizeof(T) == 8) return static_cast<T>(lane_u64(static_cast<uint64_t>(v), l));
+  else return static_cast<T>(lane_u32(static_cast<uint32_t>(v), l));
+}
+
+// The sum over the 64 lanes, wave-uniform.
+template <typename T>
+__device__ __forceinline__ T wave_sum_dpp(T v) {
+  v += dpp_any<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_any<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_any<0x141>(v);  // row_half_mirror
+  v += dpp_any<0x140>(v);  // row_mirror
+  return lane_any(v, 0) + lane_any(v, 16) + lane_any(v, 32) + lane_any(v, 48);
+}
+
+// The minimum over the 64 lanes, wave-uniform.
+__device__ __forceinline__ uint32_t wave_min_dpp(uint32_t v) {
+  v = min(v, dpp32<0xB1>(v));
+  v = min(v, dpp32<0x4E>(v));
+  v = min(v, dpp32<0x141>(v));
+  v = min(v, dpp32<0x140>(v));
+  return min(min(lane_u32(v, 0), lane_u32(v, 16)), min(lane_u32(v, 32), lane_u32(v, 48)));
+}
+
+// The inclusive prefix sum over lanes 0..lane: the 16-lane rows scanned by
+// row_shr 1, 2, 4, 8, then each row adds the totals of the rows below it.
+template <typename T>
+__device__ __forceinline__ T wave_scan_dpp(T v, uint32_t lane) {
+  v += dpp_shr0_any<1>(v);
+  v += dpp_shr0_any<2>(v);
+  v += dpp_shr0_any<4>(v);
+  v += dpp_shr0_any<8>(v);
+  const T r0 = lane_any(v, 15), r1 = lane_any(v, 31), r2 = lane_any(v, 47);
+  const uint32_t row = lane >> 4;
+  const T add = row == 0 ? T(0) : row == 1 ? r0 : row == 2 ? T(r0 + r1) : T(r0 + r1 + r2);
+  return v + add;
+}
+
 // Same reduction through ds_bpermute shuffles (probe variant kProbeShflReduce).
 __device__ __forceinline__ uint32_t wave_xor_shfl(uint32_t v) {
 #pragma unroll

@@ -62,14 +62,15 @@ hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_o
                              uint32_t* actual, uint8_t* rec_status, uint32_t capacity,
                              uint8_t* block_status, uint32_t* block_drop, lvkv_log_report* r,
                              const uint32_t* zpow, const uint32_t* lane_cols, int cus,
-                             void* scratch, uint32_t* events, hipStream_t stream);
+                             void* scratch, uint32_t* events, uint64_t* item_off,
+                             hipStream_t stream);
 size_t log_scratch_bytes(uint64_t size, uint32_t capacity, int cus);
-hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
-                               const lvkv_log_report* phys, uint64_t size, uint32_t capacity,
-                               uint64_t initial_offset, lvkv_log_record* recs, uint32_t rec_cap,
+hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* item_off,
+                               const uint64_t* hdr_off, const lvkv_log_report* phys,
+                               uint64_t size, uint32_t capacity, uint64_t initial_offset,
+                               lvkv_log_record* recs, uint32_t rec_cap,
                                lvkv_log_corruption* reps, uint32_t rep_cap,
-                               lvkv_log_read_report* out, void* scratch, uint32_t* done,
-                               unsigned long long* bytes, uint32_t tag, hipStream_t stream);
+                               lvkv_log_read_report* out, void* scratch, hipStream_t stream);
 size_t log_asm_scratch_bytes(size_t max_items);
 hipError_t launch_crc32c_long(const KernelArgs& args, const uint32_t* zpow,
                               const uint32_t* lane_cols, int num_groups, hipStream_t stream);
@@ -340,16 +341,6 @@ uint32_t next_sst_generation() {
   uint32_t v;
   do {
     v = g.fetch_add(1, std::memory_order_relaxed) + 1;
-  } while (v == 0);
-  return v;
-}
-
-// Per-call tag of the logical layer's look-back slots: 30 bits, never 0.
-uint32_t next_asm_tag() {
-  static std::atomic<uint32_t> t{0};
-  uint32_t v;
-  do {
-    v = (t.fetch_add(1, std::memory_order_relaxed) + 1) & 0x3fffffffu;
   } while (v == 0);
   return v;
 }
@@ -694,7 +685,7 @@ int lvkv_log_verify_blocks_device(const void* d_file, uint64_t file_size,
                         d_rec_status, static_cast<uint32_t>(capacity), d_block_status,
                         d_block_drop, d_report, c->d_tables + kZPowOffset,
                         c->d_tables + kRowTabDwords + kLaneTabDwords, c->groups, scratch, nullptr,
-                        hs);
+                        nullptr, hs);
   const hipError_t e2 = log_scratch_release(*c, slot, hs);
   if (e == hipSuccess) e = e2;
   return e == hipSuccess ? LVKV_OK : hip_fail(e);
@@ -718,11 +709,13 @@ int lvkv_log_read_device(const void* d_file, uint64_t file_size, uint64_t* d_hdr
   if (c == nullptr) return rc;
   const hipStream_t hs = static_cast<hipStream_t>(stream);
   // scratch: the verify's counters, the event stream (one u32 per candidate
-  // record and per block), then the logical layer's per-chunk state
+  // record and per block) and the items' header offsets (u64 each), then the
+  // logical layer's per-workgroup state
   const size_t nblocks = static_cast<size_t>((file_size + 32767) / 32768);
   const size_t ev_at =
       (log_scratch_bytes(file_size, static_cast<uint32_t>(capacity), c->groups) + 15) & ~size_t{15};
-  const size_t asm_at = (ev_at + (capacity + nblocks) * 4 + 15) & ~size_t{15};
+  const size_t off_at = (ev_at + (capacity + nblocks) * 4 + 15) & ~size_t{15};
+  const size_t asm_at = (off_at + (capacity + nblocks) * 8 + 15) & ~size_t{15};
   void* scratch = nullptr;
   size_t slot = 0;
   hipError_t e = log_scratch_acquire(*c, hs, asm_at + log_asm_scratch_bytes(capacity + nblocks),
@@ -731,22 +724,18 @@ int lvkv_log_read_device(const void* d_file, uint64_t file_size, uint64_t* d_hdr
   if (e != hipSuccess) return hip_fail(e);
   uint8_t* sb = static_cast<uint8_t*>(scratch);
   uint32_t* events = reinterpret_cast<uint32_t*>(sb + ev_at);
+  uint64_t* item_off = reinterpret_cast<uint64_t*>(sb + off_at);
   if (e == hipSuccess)
     e = launch_log_blocks(static_cast<const uint8_t*>(d_file), file_size, d_hdr_offsets,
                           d_actual, d_rec_status, static_cast<uint32_t>(capacity),
                           d_block_status, d_block_drop, d_report, c->d_tables + kZPowOffset,
                           c->d_tables + kRowTabDwords + kLaneTabDwords, c->groups, scratch,
-                          events, hs);
+                          events, item_off, hs);
   if (e == hipSuccess)
-    e = launch_log_assemble(events, d_hdr_offsets, d_report, file_size,
+    e = launch_log_assemble(events, item_off, d_hdr_offsets, d_report, file_size,
                             static_cast<uint32_t>(capacity), initial_offset, d_records,
                             static_cast<uint32_t>(record_capacity), d_reports,
-                            static_cast<uint32_t>(report_capacity), d_read, sb + asm_at,
-                            // the verify leaves scratch bytes 0-15 alone (zeroed
-                            // when allocated): the assembly's byte sum and
-                            // completion counter
-                            reinterpret_cast<uint32_t*>(sb + 8),
-                            reinterpret_cast<unsigned long long*>(sb), next_asm_tag(), hs);
+                            static_cast<uint32_t>(report_capacity), d_read, sb + asm_at, hs);
   const hipError_t e2 = log_scratch_release(*c, slot, hs);
   if (e == hipSuccess) e = e2;
   return e == hipSuccess ? LVKV_OK : hip_fail(e);

@@ -16,11 +16,12 @@
 // entered in (Agg, agg_compose). Two launches, one item per thread, each
 // item's summary and its counts for each entering state computed
 // straight-line: log_asm_reduce scans each workgroup's items and writes the
-// workgroup's aggregate; log_asm_emit folds the aggregates before its
-// workgroup (64 per wave step, by ballots and wave sums: window_fold) into
-// its starting state and output positions, rescans its items and puts each
-// through step() once, writing records (LastRecordOffset from the verify's
-// header offsets) and reports. Round 3 measured the alternatives on the
+// workgroup's aggregate; log_asm_emit composes the summaries of the
+// aggregates before its workgroup (64 per wave step, by ballots and wave
+// sums: window_summ) into its starting state, counts them for that one state
+// (window_counts_sc), rescans its items and puts each through step() once,
+// writing records (LastRecordOffset from the header offsets carried with the
+// events and in the summaries) and reports. Round 3 measured the alternatives on the
 // 62k-record log: chunks of four items replayed through step() five times
 // in one launch with a decoupled look-back, 29.7 us; one item per thread
 // with the look-back, 34 us (release / acquire flags) and 41 us (flags and
@@ -59,6 +60,7 @@ struct Summ {
   uint32_t first;    // !pass, c == kInFrag: its FIRST, candidates from the run's start
   uint32_t nrec;     // candidate records in the run (additive)
   uint32_t stop5;    // c == kStopped because of a header of type 5
+  uint64_t first_off;  // !pass, c == kInFrag: its FIRST's header offset
 };
 
 __device__ __forceinline__ Summ compose(const Summ& x, const Summ& y) {
@@ -208,8 +210,9 @@ struct Seek {
   const uint32_t* lohi;
 };
 
-// Item k (event ev) as a reader with an initial offset sees it.
-__device__ __forceinline__ uint32_t seek_event(const Seek& sk, const uint64_t* hdr_off, uint32_t k,
+// Item k (event ev, header offset off) as a reader with an initial offset
+// sees it.
+__device__ __forceinline__ uint32_t seek_event(const Seek& sk, uint64_t off, uint32_t k,
                                                uint32_t ev) {
   if (sk.offset == 0) return ev;
   const uint32_t kind = ev & 15u;
@@ -217,7 +220,7 @@ __device__ __forceinline__ uint32_t seek_event(const Seek& sk, const uint64_t* h
   const uint64_t lo = sk.lohi[0] + sk.b0, hi = sk.lohi[1] + sk.b0;
   if (k < lo) return cand ? log_event(kEvSkip, 0, 0) : log_event(kEvNone, 0, 0);
   if (k < hi) {  // b0's candidates: those before the offset are skipped silently
-    return kind == kEvRec && hdr_off[k - sk.b0] < sk.offset ? log_event(kEvPre, 0, 0) : ev;
+    return kind == kEvRec && off < sk.offset ? log_event(kEvPre, 0, 0) : ev;
   }
   if (k == hi && (kind == kEvChecksum || kind == kEvBadLength) &&
       sk.b0_end - (ev >> 16) < sk.offset)  // ReportDrop's filter: header before the offset
@@ -235,7 +238,7 @@ __device__ __forceinline__ T pick(const T (&v)[N], uint32_t i) {
   return r;
 }
 
-constexpr Summ kIdentity = {1, kIdle, 0, 0, 0, 0, 0};  // no events
+constexpr Summ kIdentity = {1, kIdle, 0, 0, 0, 0, 0, 0};  // no events
 
 // A starting state as the counts see it: idle, in a fragment with bytes,
 // in an empty fragment, resyncing, stopped.
@@ -259,9 +262,9 @@ __device__ __forceinline__ uint32_t chunk_scenario(uint32_t sw, const Summ& x) {
   return sw;
 }
 
-// One event as a run: the state it leaves the reader in (step() from an
-// unknown state, straight-line).
-__device__ __forceinline__ Summ event_summ(uint32_t ev) {
+// One event (its header at `off`) as a run: the state it leaves the reader
+// in (step() from an unknown state, straight-line).
+__device__ __forceinline__ Summ event_summ(uint32_t ev, uint64_t off) {
   const uint32_t kind = ev & 15u, type = (ev >> 8) & 255u, n = ev >> 16;
   Summ s = kIdentity;
   s.nrec = is_candidate(ev) ? 1u : 0u;
@@ -277,6 +280,7 @@ __device__ __forceinline__ Summ event_summ(uint32_t ev) {
   s.c = stop ? kStopped : first ? kInFrag : kIdle;
   s.stop5 = rec && type == 5 ? 1u : 0u;
   s.scratch = first ? n : 0u;
+  s.first_off = first ? off : 0u;
   return s;
 }
 
@@ -338,6 +342,7 @@ struct Agg {
 
 struct AsmArgs {
   const uint32_t* events;
+  const uint64_t* item_off;  // each item's header offset (lvkv_log_events.h)
   const uint64_t* hdr_off;
   const lvkv_log_report* phys;
   uint32_t nblocks;
@@ -355,8 +360,8 @@ struct AsmArgs {
   uint64_t* stamps;  // probe build only: 8 u64 per workgroup
 };
 
-// Phase stamps of log_asm_emit (probe build): 0 start, 1 prefix folded,
-// 3 scanned, 5 items written.
+// Phase stamps of log_asm_emit (probe build): 0 start, 1 shares and items
+// summarised, 2 past barrier 1, 3 counted (past barrier 2), 5 items written.
 __device__ __forceinline__ void asm_stamp(const AsmArgs& a, uint32_t slot) {
 #ifdef LVKV_PROBE_BUILD
   if (a.stamps != nullptr) a.stamps[blockIdx.x * 8u + slot] = __builtin_amdgcn_s_memrealtime();
@@ -420,71 +425,107 @@ __device__ __forceinline__ Agg agg_compose(const Agg& x, const Agg& y) {
 
 constexpr Agg kAggIdentity = {kIdentity, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
 
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
-#pragma unroll
-  for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(static_cast<unsigned long long>(v), d, 64);
-  return v;
-}
+// (every lane active; DPP, crc32c_device_common.h)
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) { return wave_sum_dpp<uint64_t>(v); }
 
-// The 64 lanes' aggregates composed in lane order (the look-back window; all
-// 64 lanes active), by ballots and sums instead of a tree of agg_compose:
-// the window's state is the one its last reset lane leaves (plus the MIDDLE
-// bytes after it), or stopped from its first stop lane on; lane l is entered
-// in the state of the last reset lane below it, or in the window's own
-// entering state when there is none.
-__device__ __forceinline__ Agg window_fold(const Agg& A, uint32_t lane) {
-  const bool reset = !A.s.pass;
-  const uint64_t Rm = __ballot(reset);
-  const uint64_t Sm = __ballot(reset && A.s.c == kStopped);
-  const uint64_t Lm = __ballot(A.s.pass && A.s.len != 0);
-  const uint64_t below = (uint64_t{1} << lane) - 1u;
-  Agg r;
-  r.s = kIdentity;
-  r.s.nrec = static_cast<uint32_t>(wave_sum64(A.s.nrec));
+// The 64 lanes' summaries composed in lane order (a window of aggregates;
+// all lanes active), by ballots and sums instead of a tree of compose: the
+// state the window's last reset lane leaves (plus the MIDDLE bytes after
+// it), or stopped from its first stop lane on.
+__device__ __forceinline__ Summ window_summ(const Summ& s, uint32_t lane) {
+  const uint64_t Rm = __ballot(!s.pass);
+  const uint64_t Sm = __ballot(!s.pass && s.c == kStopped);
+  Summ r = kIdentity;
+  r.nrec = wave_sum_dpp<uint32_t>(s.nrec);
   if (Sm) {
-    r.s.pass = 0;
-    r.s.c = kStopped;
-    r.s.stop5 = __shfl(A.s.stop5, static_cast<uint32_t>(__builtin_ctzll(Sm)), 64);
+    r.pass = 0;
+    r.c = kStopped;
+    r.stop5 = lane_u32(s.stop5, static_cast<uint32_t>(__builtin_ctzll(Sm)));
   } else if (Rm) {
     const uint32_t r0 = 63u - static_cast<uint32_t>(__builtin_clzll(Rm));
-    const uint32_t c = __shfl(A.s.c, r0, 64);
-    const uint64_t tail = wave_sum64(lane > r0 ? A.s.len : 0u);
-    r.s.pass = 0;
-    r.s.c = c;
-    r.s.scratch = __shfl(static_cast<unsigned long long>(A.s.scratch), r0, 64) + (c == kInFrag ? tail : 0u);
-    r.s.first = __shfl(A.s.first, r0, 64) + static_cast<uint32_t>(wave_sum64(lane < r0 ? A.s.nrec : 0u));
+    const uint32_t c = lane_u32(s.c, r0);
+    const uint64_t tail = wave_sum64(lane > r0 ? s.len : 0u);
+    r.pass = 0;
+    r.c = c;
+    r.scratch = lane_u64(s.scratch, r0) + (c == kInFrag ? tail : 0u);
+    r.first = lane_u32(s.first, r0) + wave_sum_dpp<uint32_t>(lane < r0 ? s.nrec : 0u);
+    r.first_off = lane_u64(s.first_off, r0);
   } else {
-    r.s.len = wave_sum64(A.s.len);
+    r.len = wave_sum64(s.len);
   }
-  // lane l's entering scenario: fixed by the last reset below it, if any
-  const uint64_t rb = Rm & below;
-  const uint32_t rl = rb ? 63u - static_cast<uint32_t>(__builtin_clzll(rb)) : 0u;
-  const uint32_t rc = __shfl(A.s.c, rl, 64);
-  const uint64_t rs = __shfl(static_cast<unsigned long long>(A.s.scratch), rl, 64);
+  return r;
+}
+
+// Lane l of a window is entered in the state of the last reset lane below it
+// (rb != 0: scenario `fixed`, whatever the window's), else in the window's own
+// entering state (an empty fragment turning non-empty when MIDDLE bytes lie
+// below: len_below); `carried`: the fragment bytes it is entered with beyond
+// the window's own.
+struct WinLane {
+  uint64_t rb;
+  uint32_t fixed;
+  bool len_below;
+  uint64_t carried;
+};
+
+__device__ __forceinline__ WinLane window_lane(const Summ& s, uint32_t lane) {
+  const uint64_t Rm = __ballot(!s.pass);
+  const uint64_t Sm = __ballot(!s.pass && s.c == kStopped);
+  const uint64_t Lm = __ballot(s.pass && s.len != 0);
+  const uint64_t below = (uint64_t{1} << lane) - 1u;
+  WinLane L;
+  L.rb = Rm & below;
+  const uint32_t rl = L.rb ? 63u - static_cast<uint32_t>(__builtin_clzll(L.rb)) : 0u;
+  const uint32_t rc = __shfl(s.c, rl, 64);
+  const uint64_t rs = __shfl(static_cast<unsigned long long>(s.scratch), rl, 64);
   const uint64_t between = Lm & below & ~((uint64_t{2} << rl) - 1u);  // lanes in (rl, l)
-  const uint32_t fixed = (Sm & below) ? kScStopped : scenario(rc, rs | (between ? 1u : 0u));
-  const bool len_below = (Lm & below) != 0;
+  L.fixed = (Sm & below) ? kScStopped : scenario(rc, rs | (between ? 1u : 0u));
+  L.len_below = (Lm & below) != 0;
   // MIDDLE bytes of the lanes below l (exclusive scan), and those after the
-  // last reset below l: the fragment bytes lane l is entered with, beyond
-  // the window's own
-  uint64_t incl = A.s.pass ? A.s.len : 0u;
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint64_t o = __shfl_up(static_cast<unsigned long long>(incl), d, 64);
-    if (lane >= d) incl += o;
-  }
-  const uint64_t excl = incl - (A.s.pass ? A.s.len : 0u);
+  // last reset below l
+  const uint64_t incl = wave_scan_dpp<uint64_t>(s.pass ? s.len : 0u, lane);
+  const uint64_t excl = incl - (s.pass ? s.len : 0u);
   const uint64_t at_r = __shfl(static_cast<unsigned long long>(incl), rl, 64);
-  const uint64_t carried = rb ? (rc == kInFrag ? rs + (excl - at_r) : 0u) : excl;
+  L.carried = L.rb ? (rc == kInFrag ? rs + (excl - at_r) : 0u) : excl;
+  return L;
+}
+
+__device__ __forceinline__ uint32_t window_lane_sc(const WinLane& L, uint32_t sw) {
+  return L.rb ? L.fixed : (sw == kScEmpty && L.len_below ? kScFrag : sw);
+}
+
+// A run's returned records, reports and bytes from one entering scenario.
+struct Counts {
+  uint32_t nrec, nrep;
+  uint64_t nbytes;  // entered with an empty fragment; add its bytes when `uses`
+  uint32_t uses;
+};
+
+__device__ __forceinline__ Counts window_counts_sc(const Agg& A, const WinLane& L, uint32_t sw) {
+  const uint32_t sc = window_lane_sc(L, sw);
+  const uint64_t t = wave_sum64(pick(A.nrec, sc) | (uint64_t{pick(A.nrep, sc)} << 32));
+  const uint32_t u = pick(A.uses, sc);
+  Counts c;
+  c.nrec = static_cast<uint32_t>(t);
+  c.nrep = static_cast<uint32_t>(t >> 32);
+  c.nbytes = wave_sum64(pick(A.nbytes, sc) + (u ? L.carried : 0u));
+  c.uses = __ballot(!L.rb && u) ? 1u : 0u;
+  return c;
+}
+
+// The 64 lanes' aggregates composed in lane order, for every entering
+// scenario (log_asm_scan).
+__device__ __forceinline__ Agg window_fold(const Agg& A, uint32_t lane) {
+  Agg r;
+  r.s = window_summ(A.s, lane);
+  const WinLane L = window_lane(A.s, lane);
 #pragma unroll
   for (uint32_t sw = 0; sw < kScenarios; ++sw) {
-    const uint32_t sc = rb ? fixed : (sw == kScEmpty && len_below ? kScFrag : sw);
-    const uint64_t t = wave_sum64(pick(A.nrec, sc) | (uint64_t{pick(A.nrep, sc)} << 32));
-    r.nrec[sw] = static_cast<uint32_t>(t);
-    r.nrep[sw] = static_cast<uint32_t>(t >> 32);
-    const uint32_t u = pick(A.uses, sc);
-    r.nbytes[sw] = wave_sum64(pick(A.nbytes, sc) + (u ? carried : 0u));
-    r.uses[sw] = __ballot(!rb && u) ? 1u : 0u;
+    const Counts c = window_counts_sc(A, L, sw);
+    r.nrec[sw] = c.nrec;
+    r.nrep[sw] = c.nrep;
+    r.nbytes[sw] = c.nbytes;
+    r.uses[sw] = c.uses;
   }
   return r;
 }
@@ -496,6 +537,7 @@ __device__ __forceinline__ Agg window_fold(const Agg& A, uint32_t lane) {
 // the workgroup's aggregate.
 struct Items {
   uint32_t ev;
+  uint64_t off;  // the item's header offset (a candidate's)
   Summ x;
   uint32_t v[kScenarios];
   Agg agg;
@@ -506,10 +548,11 @@ struct Items {
 // MIDDLE bytes after it), or stopped from its first stop lane. C / R / S:
 // the candidate / reset / stop lanes; P: MIDDLE bytes of the lanes in
 // `below`; r: the last reset lane in `below` and its state (c_r, sc_r) and
-// inclusive MIDDLE bytes p_r; stop5_0: the first stop lane's stop5.
+// inclusive MIDDLE bytes p_r and header offset off_r; stop5_0: the first
+// stop lane's stop5.
 __device__ __forceinline__ Summ prefix_summ(uint64_t below, uint64_t C, uint64_t R, uint64_t S,
                                             uint32_t P, uint32_t r, uint32_t c_r, uint32_t sc_r,
-                                            uint32_t p_r, uint32_t stop5_0) {
+                                            uint32_t p_r, uint64_t off_r, uint32_t stop5_0) {
   Summ x = kIdentity;
   x.nrec = static_cast<uint32_t>(__popcll(C & below));
   if (S & below) {
@@ -521,50 +564,63 @@ __device__ __forceinline__ Summ prefix_summ(uint64_t below, uint64_t C, uint64_t
     x.c = c_r;
     x.scratch = sc_r + (c_r == kInFrag ? P - p_r : 0u);
     x.first = static_cast<uint32_t>(__popcll(C & ((uint64_t{1} << r) - 1u)));
+    x.first_off = off_r;
   } else {
     x.len = P;
   }
   return x;
 }
 
-__device__ __forceinline__ void wg_items(const AsmArgs& a, uint32_t K, uint32_t g, uint32_t tid,
-                                         Summ (&wagg)[kGT / 64],
-                                         uint32_t (&wsum)[kGT / 64][kScenarios], Items& it) {
+// Item k's event and header offset as loaded (issued before anything that
+// waits, so their latency overlaps the emit's fold).
+struct ItemIn {
+  uint32_t ev;
+  uint64_t off;
+};
+__device__ __forceinline__ ItemIn load_item(const AsmArgs& a, uint32_t K, uint32_t k) {
+  ItemIn in;
+  in.ev = k < K ? a.events[k] : log_event(kEvNone, 0, 0);
+  in.off = k < K ? a.item_off[k] : 0u;
+  return in;
+}
+
+// The wave's share of workgroup g's items, before the workgroup's barrier:
+// each item's event (seek applied) and summary, its exclusive summary within
+// the wave (it.x), and the wave's total into wagg[w].
+__device__ __forceinline__ void wave_items(const AsmArgs& a, uint32_t g, uint32_t tid,
+                                           const ItemIn& in, Summ (&wagg)[kGT / 64], Items& it) {
   const uint32_t lane = tid & 63u, w = tid >> 6;
   const uint32_t k = g * kGT + tid;
-  it.ev = k < K ? seek_event(a.seek, a.hdr_off, k, a.events[k]) : log_event(kEvNone, 0, 0);
-#ifdef LVKV_PROBE_BUILD
-  if (tid == 0) {
-    asm volatile("" ::"v"(it.ev));
-    asm_stamp(a, 2);
-  }
-#endif
-  const Summ e = event_summ(it.ev);
+  it.ev = seek_event(a.seek, in.off, k, in.ev);
+  it.off = in.off;
+  const Summ e = event_summ(it.ev, it.off);
   // the wave's exclusive scan of summaries, from ballots
   const uint64_t below = (uint64_t{1} << lane) - 1u;
   const uint64_t C = __ballot(e.nrec != 0);
   const uint64_t R = __ballot(!e.pass);
   const uint64_t S = __ballot(!e.pass && e.c == kStopped);
   const uint32_t len = e.pass ? static_cast<uint32_t>(e.len) : 0u;  // < 2^16 an item
-  uint32_t inc = len;
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(inc, d, 64);
-    if (lane >= d) inc += o;
-  }
+  const uint32_t inc = wave_scan_dpp<uint32_t>(len, lane);
   const uint64_t rb = R & below;
   const uint32_t r = rb ? 63u - static_cast<uint32_t>(__builtin_clzll(rb)) : 0u;
   const uint32_t sc = static_cast<uint32_t>(e.scratch);
-  const uint32_t stop5_0 = __shfl(e.stop5, S ? static_cast<uint32_t>(__builtin_ctzll(S)) : 0u, 64);
+  const uint32_t stop5_0 = lane_u32(e.stop5, S ? static_cast<uint32_t>(__builtin_ctzll(S)) : 0u);
   const Summ xw = prefix_summ(below, C, R, S, inc - len, r, __shfl(e.c, r, 64), __shfl(sc, r, 64),
-                              __shfl(inc, r, 64), stop5_0);
+                              __shfl(inc, r, 64),
+                              __shfl(static_cast<unsigned long long>(it.off), r, 64), stop5_0);
   // the wave's total (shuffles on every lane, then lane 0 writes it)
   const uint32_t rt = R ? 63u - static_cast<uint32_t>(__builtin_clzll(R)) : 0u;
-  const uint32_t p_all = __shfl(inc, 63, 64), c_rt = __shfl(e.c, rt, 64);
-  const uint32_t sc_rt = __shfl(sc, rt, 64), p_rt = __shfl(inc, rt, 64);
-  if (lane == 0) wagg[w] = prefix_summ(~uint64_t{0}, C, R, S, p_all, rt, c_rt, sc_rt, p_rt, stop5_0);
-  __syncthreads();
-  if (tid == 0) asm_stamp(a, 4);
+  const uint32_t p_all = lane_u32(inc, 63), c_rt = lane_u32(e.c, rt);
+  const uint32_t sc_rt = lane_u32(sc, rt), p_rt = lane_u32(inc, rt);
+  const uint64_t off_rt = lane_u64(it.off, rt);
+  if (lane == 0)
+    wagg[w] = prefix_summ(~uint64_t{0}, C, R, S, p_all, rt, c_rt, sc_rt, p_rt, off_rt, stop5_0);
+  it.x = xw;
+}
+
+// After the barrier: the waves before this one composed into it.x, and the
+// workgroup's summary (it.agg.s).
+__device__ __forceinline__ void items_compose(const Summ (&wagg)[kGT / 64], uint32_t w, Items& it) {
   Summ pre = kIdentity, tot = kIdentity;
 #pragma unroll
   for (uint32_t v = 0; v < kGT / 64; ++v) {
@@ -572,7 +628,19 @@ __device__ __forceinline__ void wg_items(const AsmArgs& a, uint32_t K, uint32_t 
     tot = compose(tot, wagg[v]);
   }
   it.agg.s = tot;
-  it.x = compose(pre, xw);
+  it.x = compose(pre, it.x);
+}
+
+// The reduce's items: summaries, then the positions and counts for every
+// scenario the workgroup may be entered in.
+__device__ __forceinline__ void wg_items(const AsmArgs& a, uint32_t g, uint32_t tid,
+                                         const ItemIn& in, Summ (&wagg)[kGT / 64],
+                                         uint32_t (&wsum)[kGT / 64][kScenarios], Items& it) {
+  const uint32_t lane = tid & 63u, w = tid >> 6;
+  const uint64_t below = (uint64_t{1} << lane) - 1u;
+  wave_items(a, g, tid, in, wagg, it);
+  __syncthreads();
+  items_compose(wagg, w, it);
   // output positions for each entering scenario: per item at most one
   // record and two reports, so the wave's prefix counts are ballots; and the
   // returned bytes (Agg::nbytes / uses)
@@ -600,7 +668,6 @@ __device__ __forceinline__ void wg_items(const AsmArgs& a, uint32_t K, uint32_t 
     }
   }
   __syncthreads();
-  if (tid == 0) asm_stamp(a, 6);
 #pragma unroll
   for (uint32_t sw = 0; sw < kScenarios; ++sw) {
     uint32_t before = 0, all = 0, uses = 0;
@@ -631,8 +698,9 @@ __global__ void __launch_bounds__(kGT) log_asm_reduce(AsmArgs a) {
   __shared__ uint32_t wsum[kGT / 64][kScenarios];
   const uint32_t K = asm_items(a);
   if (blockIdx.x >= asm_groups(a, K)) return;
+  const ItemIn in = load_item(a, K, blockIdx.x * kGT + threadIdx.x);
   Items it;
-  wg_items(a, K, blockIdx.x, threadIdx.x, wagg, wsum, it);
+  wg_items(a, blockIdx.x, threadIdx.x, in, wagg, wsum, it);
   if (threadIdx.x == 0) a.aggs[blockIdx.x] = it.agg;
 }
 
@@ -672,90 +740,189 @@ __global__ void __launch_bounds__(kGT) log_asm_scan(AsmArgs a) {
   }
 }
 
-// ReadRecord, launch 2 of 2: the waves fold the aggregates of the
-// workgroups before this one (64 at a time, window_fold; each wave a
-// contiguous share) into its entering state and output positions, and the
-// items are rescanned; then each item goes
-// through step() once. Workgroup G - 1 writes the report: counts and the
-// records' bytes both come from the composed aggregates (Agg::nbytes), so no
+// The reader entering a run: its state (kIdle, kInFrag, kStopped, kResync)
+// and the open fragment's bytes.
+struct Entry {
+  uint32_t st;
+  uint64_t scratch;
+};
+
+__device__ __forceinline__ Entry entry_after(Entry e, const Summ& y) {
+  if (e.st == kStopped) return e;
+  if (!y.pass) return Entry{y.c, y.c == kInFrag ? y.scratch : 0u};
+  if (e.st == kInFrag) e.scratch += y.len;
+  return e;
+}
+
+__device__ __forceinline__ uint32_t entry_sc(const Entry& e) { return scenario(e.st, e.scratch); }
+
+// ReadRecord, launch 2 of 2. Wave w takes a contiguous share of the windows
+// of earlier workgroups' aggregates (with the windows' prefixes scanned,
+// a.pref: wave 0 takes g's window prefix and the workgroups of g's own window
+// before it) and composes their summaries while the items are scanned; after
+// one barrier every wave knows the state its share is entered in, so it counts
+// that share's records, reports and bytes for that one scenario (not all four)
+// and the items their positions for the workgroup's; after a second barrier
+// each item goes through step() once. Workgroup G - 1 writes the report; no
 // workgroup waits for or counts the others (round 3's completion counter, one
-// device-scope atomic per workgroup on one address, cost ~5 us).
+// device-scope atomic per workgroup on one address, cost ~5 us). Instruction
+// issue is the bound here (one wave per SIMD, every step a latency chain), so
+// the single scenario is the saving: round 4 measured 12.2 us folding and
+// counting all four.
 __global__ void __launch_bounds__(kGT) log_asm_emit(AsmArgs a) {
-  __shared__ Summ wagg[kGT / 64];
-  __shared__ uint32_t wsum[kGT / 64][kScenarios];
-  __shared__ Agg part_s[kGT / 64];
+  constexpr uint32_t kW = kGT / 64;
+  constexpr uint32_t kMaxWin = kAsmFoldMax / 64;
+  __shared__ Summ wagg[kW];      // the waves' items
+  __shared__ Summ share_s[kW];   // the waves' shares of the earlier workgroups
+  __shared__ Summ win_s[kMaxWin];  // each window of them (window 0: a.pref's form)
+  __shared__ uint32_t srec[kW], srep[kW], own_v[kW], own_u[kW];
+  __shared__ unsigned long long sbytes[kW], own_b[kW];
   const uint32_t tid = threadIdx.x;
-  const uint32_t lane = tid & 63u;
+  const uint32_t lane = tid & 63u, w = tid >> 6;
   const uint32_t K = asm_items(a);
   const uint32_t G = asm_groups(a, K);
   const uint32_t g = blockIdx.x;
   if (g >= G) return;  // the whole workgroup
   if (tid == 0) asm_stamp(a, 0);
-  {
-    // the workgroups before g, 64 a window; wave w folds its contiguous
-    // share of the windows, the shares are composed below. With the windows'
-    // prefixes scanned (a.pref): wave 0 takes g's window prefix and folds the
-    // workgroups of g's own window before it.
-    const uint32_t w = tid >> 6, nwin = (g + 63) / 64;
-    Agg part = kAggIdentity;
-    if (a.pref != nullptr && G > kAsmFoldMax) {
-      if (w == 0) {
-        const uint32_t idx = (g & ~63u) + lane;
-        part = agg_compose(a.pref[g >> 6], window_fold(idx < g ? a.aggs[idx] : kAggIdentity, lane));
-      }
-    } else {
-      for (uint32_t wi = w * nwin / (kGT / 64); wi < (w + 1) * nwin / (kGT / 64); ++wi) {
-        const uint32_t idx = wi * 64 + lane;
-        part = agg_compose(part, window_fold(idx < g ? a.aggs[idx] : kAggIdentity, lane));
-      }
-    }
-    if (lane == 0) part_s[w] = part;
-    if (tid == 0) asm_stamp(a, 1);
+  const ItemIn in = load_item(a, K, g * kGT + tid);
+  // 1. this wave's share: its summary, each window's kept for step 3
+  const bool scanned = a.pref != nullptr && G > kAsmFoldMax;
+  uint32_t wi0 = 0, wi1 = 0;
+  if (!scanned) {
+    const uint32_t nwin = (g + 63) / 64;
+    wi0 = w * nwin / kW;
+    wi1 = (w + 1) * nwin / kW;
+  } else if (w == 0) {
+    wi0 = g >> 6;
+    wi1 = wi0 + 1;
   }
+  Summ sh = kIdentity;
+  if (scanned && w == 0) sh = a.pref[g >> 6].s;
+  // the share's first window whole (step 3 counts it from registers; a wave
+  // has one window below 256 workgroups), the others' summaries
+  const Agg A0 = wi0 < wi1 && wi0 * 64 + lane < g ? a.aggs[wi0 * 64 + lane] : kAggIdentity;
+  for (uint32_t wi = wi0; wi < wi1; ++wi) {
+    const uint32_t idx = wi * 64 + lane;
+    const Summ ws = window_summ(wi == wi0 ? A0.s : idx < g ? a.aggs[idx].s : kIdentity, lane);
+    if (lane == 0) win_s[scanned ? 0u : wi] = ws;
+    sh = compose(sh, ws);
+  }
+  if (lane == 0) share_s[w] = sh;
   Items it;
-  wg_items(a, K, g, tid, wagg, wsum, it);  // its barriers also publish part_s
-  if (tid == 0) asm_stamp(a, 3);
-  Agg p = part_s[0];
+  wave_items(a, g, tid, in, wagg, it);
+  if (tid == 0) asm_stamp(a, 1);
+  __syncthreads();
+  if (tid == 0) asm_stamp(a, 2);
+  items_compose(wagg, w, it);
+  // 2. the state each share is entered in (e_w), the workgroup's (e), and the
+  // earlier workgroups' summary (P)
+  Entry e = {a.init_st, 0}, e_w = e;
+  Summ P = kIdentity;
 #pragma unroll
-  for (uint32_t w = 1; w < kGT / 64; ++w) p = agg_compose(p, part_s[w]);
+  for (uint32_t v = 0; v < kW; ++v) {
+    if (v == w) e_w = e;
+    const Summ sv = share_s[v];
+    e = entry_after(e, sv);
+    P = compose(P, sv);
+  }
+  // 3. this wave's share counted from e_w
+  uint32_t crec = 0, crep = 0;
+  uint64_t cby = 0;
+  if (scanned && w == 0) {
+    const Agg& pf = a.pref[g >> 6];
+    const uint32_t sc = entry_sc(e_w);
+    crec = pick(pf.nrec, sc);
+    crep = pick(pf.nrep, sc);
+    cby = pick(pf.nbytes, sc) + (pick(pf.uses, sc) ? e_w.scratch : 0u);
+    e_w = entry_after(e_w, pf.s);
+  }
+  for (uint32_t wi = wi0; wi < wi1 && e_w.st != kStopped; ++wi) {
+    const uint32_t idx = wi * 64 + lane;
+    const Agg A = wi == wi0 ? A0 : idx < g ? a.aggs[idx] : kAggIdentity;
+    const Counts c = window_counts_sc(A, window_lane(A.s, lane), entry_sc(e_w));
+    crec += c.nrec;
+    crep += c.nrep;
+    cby += c.nbytes + (c.uses ? e_w.scratch : 0u);
+    e_w = entry_after(e_w, win_s[scanned ? 0u : wi]);
+  }
+  // the items' positions for the workgroup's entering scenario (per item at
+  // most one record and two reports: ballots), and for the report the
+  // returned bytes
+  const uint64_t below = (uint64_t{1} << lane) - 1u;
+  const uint32_t isc = chunk_scenario(entry_sc(e), it.x);
+  uint32_t cnt[kScenarios];
+  event_counts(it.ev, cnt);
+  const uint32_t c1 = pick(cnt, isc);
+  const uint64_t br = __ballot(c1 & 1u), b0 = __ballot((c1 >> 16) & 1u), b1 = __ballot((c1 >> 17) & 1u);
+  const uint32_t vpos = static_cast<uint32_t>(__popcll(br & below)) |
+                        static_cast<uint32_t>(__popcll(b0 & below) + 2 * __popcll(b1 & below)) << 16;
+  const bool last = g == G - 1;
+  uint64_t ob = 0;
+  uint32_t ou = 0;
+  if (last) {
+    uint32_t eb[kScenarios], eu[kScenarios];
+    event_bytes(it.ev, eb, eu);
+    const uint64_t carried = it.x.pass ? it.x.len : (it.x.c == kInFrag ? it.x.scratch : 0u);
+    const uint32_t u = pick(eu, isc);
+    ob = wave_sum64(pick(eb, isc) + (u ? carried : 0u));
+    ou = __ballot(it.x.pass && u) ? 1u : 0u;
+  }
+  if (lane == 0) {
+    srec[w] = crec;
+    srep[w] = crep;
+    sbytes[w] = cby;
+    own_v[w] = static_cast<uint32_t>(__popcll(br)) |
+               static_cast<uint32_t>(__popcll(b0) + 2 * __popcll(b1)) << 16;
+    own_b[w] = ob;
+    own_u[w] = ou;
+  }
+  __syncthreads();
+  if (tid == 0) asm_stamp(a, 3);
+  uint32_t base_rec = 0, base_rep = 0, before = 0, all = 0, ouses = 0;
+  uint64_t by = 0;
+#pragma unroll
+  for (uint32_t v = 0; v < kW; ++v) {
+    base_rec += srec[v];
+    base_rep += srep[v];
+    by += sbytes[v] + own_b[v];
+    before += v < w ? own_v[v] : 0u;
+    all += own_v[v];
+    ouses |= own_u[v];
+  }
   const Summ& x = it.x;
   const uint32_t ev = it.ev;
-  const uint32_t in_st = p.s.pass ? a.init_st : p.s.c;
-  const uint64_t in_scratch = p.s.pass ? 0 : p.s.scratch;
-  const uint32_t init_sc = scenario(a.init_st, 0);
-  const uint32_t sw = scenario(in_st, in_scratch);
-  const uint32_t pos = pick(it.v, sw);  // 0 once stopped
-  const uint32_t rb = pick(p.nrec, init_sc) + (pos & 0xffffu);
-  const uint32_t pb = pick(p.nrep, init_sc) + (pos >> 16);
-  const uint32_t j = p.s.nrec + x.nrec;  // the item's candidate index
-  Reader r = {in_st, p.s.first, in_scratch, 0, 0};
-  if (in_st == kStopped) {
+  const uint32_t pos = before + vpos;
+  const uint32_t rb = base_rec + (pos & 0xffffu);
+  const uint32_t pb = base_rep + (pos >> 16);
+  const uint32_t j = P.nrec + x.nrec;  // the item's candidate index
+  Reader r = {e.st, P.first, e.scratch, 0, P.first_off};
+  if (e.st == kStopped) {
     // a stop before this workgroup: nothing after it is read
   } else if (!x.pass) {
     r.st = x.c;
-    r.first = p.s.nrec + x.first;
+    r.first = P.nrec + x.first;
     r.scratch = x.scratch;
+    r.first_off = x.first_off;
   } else if (r.st == kInFrag) {
     r.scratch += x.len;
   }
-  const uint32_t kind = ev & 15u, type = (ev >> 8) & 255u;
-  const uint64_t hoff = kind == kEvRec && type == 1 && r.st != kStopped ? a.hdr_off[j] : 0;
-  if (r.st == kInFrag && kind == kEvRec && type == 4) r.first_off = a.hdr_off[r.first];
+  // a FULL record's offset is its own header's, a LAST's its FIRST's (carried
+  // in the summaries): no load waits on the shares or the scan
   Sink out = {true, 0, 0, 0, a.recs + rb, a.rec_cap > rb ? a.rec_cap - rb : 0u, a.reps + pb,
               a.rep_cap > pb ? a.rep_cap - pb : 0u};
-  step<true>(r, ev, j, hoff, out);
-  // the report: the last workgroup's prefix composed with its own aggregate
-  // (counts and returned bytes, from the reader's first state)
-  if (g == G - 1 && tid == 0) {
-    const Agg tot = agg_compose(p, it.agg);
-    const uint32_t r0 = pick(tot.nrec, init_sc), r1 = pick(tot.nrep, init_sc);
+  step<true>(r, ev, j, it.off, out);
+  // the report: the earlier workgroups' counts and this one's, from the
+  // reader's first state
+  if (last && tid == 0) {
+    const Summ ts = compose(P, it.agg.s);
+    const uint32_t r0 = base_rec + (all & 0xffffu), r1 = base_rep + (all >> 16);
     a.out->status = (a.phys->status != LVKV_OK || r0 > a.rec_cap || r1 > a.rep_cap)
                         ? LVKV_LOG_CAPACITY
                         : LVKV_OK;
     a.out->nrecords = r0;
     a.out->nreports = r1;
-    a.out->stopped = (!tot.s.pass && tot.s.c == kStopped) ? tot.s.stop5 : 0u;
-    a.out->bytes = pick(tot.nbytes, init_sc);
+    a.out->stopped = (!ts.pass && ts.c == kStopped) ? ts.stop5 : 0u;
+    a.out->bytes = by + (ouses ? e.scratch : 0u);
   }
   if (tid == 0) asm_stamp(a, 5);
 }
@@ -902,12 +1069,7 @@ __global__ void __launch_bounds__(kGatherT) log_gather_kernel(GatherArgs a) {
     for (uint32_t b = 0; b < g; b += 64) before += wave_sum64(b + lane < g ? a.look[b + lane].sum : 0u);
     if (lane == 0) base_s = before;
   }
-  uint64_t inc = mine;
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint64_t o = __shfl_up(static_cast<unsigned long long>(inc), d, 64);
-    if (lane >= d) inc += o;
-  }
+  const uint64_t inc = wave_scan_dpp<uint64_t>(mine, lane);
   if (lane == 63) wsum[wave] = inc;
   __syncthreads();
   uint64_t pre = 0;
@@ -1064,17 +1226,18 @@ size_t log_asm_scratch_bytes(size_t max_items) {
 }
 
 // `scratch`: log_asm_scratch_bytes(capacity + nblocks) bytes, 16-byte aligned
-// (any contents); `done` and `bytes`: a u32 and a u64 that are 0 (zeroed
-// once; every call leaves them at 0), used by one call at a time; `tag` is
-// unused (the launches exchange through a kernel boundary).
-hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
-                               const lvkv_log_report* phys, uint64_t size, uint32_t capacity,
-                               uint64_t initial_offset, lvkv_log_record* recs, uint32_t rec_cap,
+// (any contents); `events` / `item_off`: the verify's event stream and the
+// items' header offsets (lvkv_log_events.h); `hdr_off`: the candidates'
+// (log_asm_seek's search).
+hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* item_off,
+                               const uint64_t* hdr_off, const lvkv_log_report* phys,
+                               uint64_t size, uint32_t capacity, uint64_t initial_offset,
+                               lvkv_log_record* recs, uint32_t rec_cap,
                                lvkv_log_corruption* reps, uint32_t rep_cap,
-                               lvkv_log_read_report* out, void* scratch, uint32_t* done,
-                               unsigned long long* bytes, uint32_t tag, hipStream_t stream) {
+                               lvkv_log_read_report* out, void* scratch, hipStream_t stream) {
   AsmArgs a;
   a.events = events;
+  a.item_off = item_off;
   a.hdr_off = hdr_off;
   a.phys = phys;
   a.nblocks = static_cast<uint32_t>((size + 32767) / 32768);
@@ -1094,9 +1257,6 @@ hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* hdr_off,
   const uint32_t nwin = (a.groups + 63) / 64;
   a.pref = a.groups > kAsmFoldMax ? a.aggs + a.groups : nullptr;
   a.lohi = reinterpret_cast<uint32_t*>(a.aggs + a.groups + nwin);
-  (void)tag;
-  (void)done;
-  (void)bytes;
   a.init_st = initial_offset ? kResync : kIdle;
   a.seek.offset = initial_offset;
   // SkipToInitialBlock (log_reader.cc:33-54): the block holding the offset,

@@ -97,6 +97,7 @@ struct LogArgs {
   const uint32_t* zpow;
   const uint32_t* lane_cols;
   uint32_t* events;  // nullable: the ReadRecord event stream (lvkv_log_events.h)
+  uint64_t* item_off;  // with events: each item's header offset
   // many blocks: the records before each block (nblocks + 1 entries), scanned
   // by log_scan_kernel for the emit; else nullptr
   unsigned long long* first_of;
@@ -793,12 +794,7 @@ __global__ void __launch_bounds__(kScanThreads) log_scan_kernel(LogArgs a) {
   const uint32_t b0 = min(n, tid * per), b1 = min(n, b0 + per);
   unsigned long long mine = 0;
   for (uint32_t b = b0; b < b1; ++b) mine += static_cast<uint32_t>(a.info[b].x);
-  unsigned long long inc = mine;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const unsigned long long o = __shfl_up(inc, d, 64);
-    if (lane >= static_cast<uint32_t>(d)) inc += o;
-  }
+  const unsigned long long inc = wave_scan_dpp<unsigned long long>(mine, lane);
   if (lane == 63) wtot[wave] = inc;
   __syncthreads();
   unsigned long long run = inc - mine;
@@ -852,14 +848,11 @@ __global__ void __launch_bounds__(64 * kEmitWaves) log_emit_kernel(LogArgs a) {
       if (b >= b0) cnt += uint64_t{c} << 32;  // this workgroup's own blocks, kept apart
     }
   }
-#pragma unroll
-  for (uint32_t dd = 32; dd >= 1; dd >>= 1) {
-    cnt += __shfl_xor(cnt, dd, 64);
-    good += __shfl_xor(good, dd, 64);
-    drop += __shfl_xor(drop, dd, 64);
-    corrupt += __shfl_xor(corrupt, dd, 64);
-    fb = min(fb, static_cast<uint32_t>(__shfl_xor(fb, dd, 64)));
-  }
+  cnt = wave_sum_dpp(cnt);
+  good = wave_sum_dpp(good);
+  drop = wave_sum_dpp(drop);
+  corrupt = wave_sum_dpp(corrupt);
+  fb = wave_min_dpp(fb);
   if (lane == 0) {
     s_cnt[wave] = cnt;
     s_good[wave] = good;
@@ -902,9 +895,7 @@ __global__ void __launch_bounds__(64 * kEmitWaves) log_emit_kernel(LogArgs a) {
   const uint32_t b = b0 + wave;
   if (b >= a.nblocks) return;
   // this wave's place: the counts of the workgroup's blocks before it
-  uint32_t pre = lane < wave ? static_cast<uint32_t>(a.info[b0 + lane].x) : 0u;
-#pragma unroll
-  for (uint32_t dd = 32; dd >= 1; dd >>= 1) pre += __shfl_xor(pre, dd, 64);
+  const uint32_t pre = wave_sum_dpp(lane < wave ? static_cast<uint32_t>(a.info[b0 + lane].x) : 0u);
   const uint64_t base = before + pre;
   const uint32_t c = static_cast<uint32_t>(a.info[b].x), off = a.stg_off[b];
   const uint64_t start = uint64_t{b} * kLogBlock;
@@ -912,12 +903,15 @@ __global__ void __launch_bounds__(64 * kEmitWaves) log_emit_kernel(LogArgs a) {
     const uint64_t gi = base + j;
     if (gi >= a.capacity || off + j >= a.capacity) break;
     const uint4 e = a.stg[off + j];
-    a.hdr_off[gi] = start + (e.y & 0xffffu);
+    const uint64_t ho = start + (e.y & 0xffffu);
+    a.hdr_off[gi] = ho;
     a.actual[gi] = e.x;
     a.rec_status[gi] = static_cast<uint8_t>(e.w);
-    if (a.events != nullptr)
+    if (a.events != nullptr) {
       a.events[gi + b] = e.w == LVKV_REC_OK ? log_event(kEvRec, e.z, e.y >> 16)
                                              : log_event(kEvSkip, 0, 0);
+      a.item_off[gi + b] = ho;
+    }
   }
   if (lane == 0 && a.events != nullptr && base + c <= a.capacity)
     a.events[base + c + b] = log_block_event(a.block_status[b], a.block_drop[b]);
@@ -957,7 +951,8 @@ hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_o
                              uint32_t* actual, uint8_t* rec_status, uint32_t capacity,
                              uint8_t* block_status, uint32_t* block_drop, lvkv_log_report* r,
                              const uint32_t* zpow, const uint32_t* lane_cols, int cus,
-                             void* scratch, uint32_t* events, hipStream_t stream) {
+                             void* scratch, uint32_t* events, uint64_t* item_off,
+                             hipStream_t stream) {
   const uint32_t nblocks = static_cast<uint32_t>((size + kLogBlock - 1) / kLogBlock);
   LogArgs a;
   memset(&a, 0, sizeof(a));
@@ -984,6 +979,7 @@ hipError_t launch_log_blocks(const uint8_t* file, uint64_t size, uint64_t* hdr_o
   a.zpow = zpow;
   a.lane_cols = lane_cols;
   a.events = events;
+  a.item_off = item_off;
 #ifdef LVKV_PROBE_BUILD
   a.stamps = g_log_stamps;
   a.knobs = g_log_knobs;

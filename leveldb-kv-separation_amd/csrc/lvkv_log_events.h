@@ -3,7 +3,10 @@
 // the logical-record kernel (lvkv_log_assemble.hip): item order is block by
 // block, each block's candidate physical records in file order, then the
 // block's own event. Candidate record g of block b is item g + b; block b's
-// event is item (records in blocks 0..b) + b.
+// event is item (records in blocks 0..b) + b. Beside it, one u64 per item:
+// a candidate's header offset in the file (hdr_off of its record), so the
+// logical layer reads an item's offset with its event instead of after
+// counting the candidates before it.
 //
 //   bits 0-3   kind (kEv*)
 //   bits 8-15  kEvRec: the header's type byte

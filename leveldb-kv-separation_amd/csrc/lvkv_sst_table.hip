@@ -292,12 +292,7 @@ __device__ uint32_t place_table(lvkv_sst_report* reports, uint32_t t, uint32_t n
       v = x & 0xffffffffull;
     }
     // inclusive prefix over the 64 lanes
-    uint64_t inc = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint64_t o = __shfl_up(static_cast<unsigned long long>(inc), d, 64);
-      if (lane >= static_cast<uint32_t>(d)) inc += o;
-    }
+    const uint64_t inc = wave_scan_dpp<uint64_t>(v, lane);
     const uint64_t p = run + inc;
     // first table (in order) whose end passes the capacity: the total stops
     // at its start
@@ -306,9 +301,9 @@ __device__ uint32_t place_table(lvkv_sst_report* reports, uint32_t t, uint32_t n
     const uint64_t mask = __ballot(over);
     if (mask != 0 && cut == ~uint64_t{0}) {
       const uint32_t src = static_cast<uint32_t>(__builtin_ctzll(mask));
-      cut = __shfl(static_cast<unsigned long long>(start), src, 64);
+      cut = lane_u64(start, src);
     }
-    run = __shfl(static_cast<unsigned long long>(p), 63, 64);
+    run = lane_u64(p, 63);
   }
   if (t == ntables - 1) {
     *total = static_cast<uint32_t>(min<uint64_t>(run, min<uint64_t>(cut, capacity)));
@@ -1007,12 +1002,7 @@ __device__ __forceinline__ void spec_crc_group(const KernelArgs& a, const uint8_
       L.slot_c = G;
     }
   } else {
-    uint64_t inc = mysz;  // inclusive prefix within the wave
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint64_t o = __shfl_up(static_cast<unsigned long long>(inc), d, 64);
-      if (lane >= static_cast<uint32_t>(d)) inc += o;
-    }
+    const uint64_t inc = wave_scan_dpp<uint64_t>(mysz, lane);  // inclusive prefix within the wave
     if (lane == 63) L.wsum[wave] = inc;
     __syncthreads();
     uint64_t before = 0, T = 0;

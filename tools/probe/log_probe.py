@@ -154,7 +154,8 @@ def main():
         print(f"log_read {nrec} records: {us2:.1f} us/call (verify + ReadRecord)", flush=True)
         if "--asm-stamps" in sys.argv:
             # log_asm_emit phases per workgroup (probe build; s_memrealtime,
-            # 100 MHz): 0 start, 1 prefix folded, 3 items scanned, 5 written
+            # 100 MHz): 0 start, 1 shares and items summed, 2 barrier 1, 3 counts
+            # (barrier 2), 5 written
             P = ctypes.CDLL(str(HERE / "liblvkv_probe.so"))
             P.lvkv_debug_asm_stamps.argtypes = [vp]
             P.lvkv_log_read_device.argtypes = L.lvkv_log_read_device.argtypes
@@ -176,11 +177,10 @@ def main():
             t0s = x[:, 0].min()
             rel = (x - t0s) / 100.0
             print(f"asm emit workgroups {len(x)}: start max {rel[:, 0].max():.2f}; med phases "
-                  f"fold {np.median(rel[:, 1] - rel[:, 0]):.2f} scan {np.median(rel[:, 3] - rel[:, 1]):.2f} "
-                  f"(event loaded +{np.median(rel[:, 2] - rel[:, 1]):.2f}, barrier 1 "
-                  f"+{np.median(rel[:, 4] - rel[:, 2]):.2f}, barrier 2 +{np.median(rel[:, 6] - rel[:, 4]):.2f}, "
-                  f"rest +{np.median(rel[:, 3] - rel[:, 6]):.2f}) "
-                  f"step+write {np.median(rel[:, 5] - rel[:, 3]):.2f}; end max {rel[:, 5].max():.2f}",
+                  f"shares+items {np.median(rel[:, 1] - rel[:, 0]):.2f}, barrier 1 "
+                  f"+{np.median(rel[:, 2] - rel[:, 1]):.2f}, counts+barrier 2 "
+                  f"+{np.median(rel[:, 3] - rel[:, 2]):.2f}, step+write "
+                  f"+{np.median(rel[:, 5] - rel[:, 3]):.2f}; end max {rel[:, 5].max():.2f}",
                   flush=True)
         # + the records' bytes laid end to end (lvkv_log_gather_device)
         payload = torch.empty(len(img), dtype=torch.uint8, device=dev)
