@@ -211,6 +211,33 @@ def test_device_log_read_large_and_capacity(lvkv, gpu):
 
 
 @pytest.mark.gpu
+def test_device_log_read_dense_blocks(lvkv, gpu):
+    """Blocks of hundreds of tiny records (over a thousand items a block, so
+    ReadRecord's 256-item workgroups fall many to a block), fragmented
+    records between them (big_every), damage, initial offsets."""
+    import torch
+    import log_synth
+    rng = np.random.default_rng(3)
+    base = log_synth.build_log(60_000, seed=5, max_len=40, big_every=1999)
+    for trial in range(3):
+        img = bytearray(base)
+        for _ in range(trial * 4):
+            img[int(rng.integers(0, len(img)))] ^= int(rng.integers(1, 256))
+        img = bytes(img)
+        buf = torch.from_numpy(np.frombuffer(img, dtype=np.uint8).copy()).to(gpu)
+        for off in [0, 32768 * 2 + 100, int(rng.integers(1, len(img)))]:
+            rd, records, reports, phys, gathered = lvkv.log_read(buf, initial_offset=off,
+                                                                 gather=True)
+            hdrs = [int(x) for x in phys[1].cpu().numpy()]
+            o_recs, o_reps, stopped = lw.read_all(img, off)
+            assert rd["status"] == 0, (trial, off)
+            assert _device_log_records(img, records, hdrs, gathered) == o_recs, (trial, off)
+            assert reports == o_reps, (trial, off)
+            assert rd["stopped"] == int(stopped), (trial, off)
+            assert rd["bytes"] == sum(r[1] for r in o_recs), (trial, off)
+
+
+@pytest.mark.gpu
 def test_device_log_gather_large_image_default_capacity(lvkv, gpu):
     """A ~650 MB log (a clean 20k-record, 40 MB log padded to whole 32 KiB blocks
     with zeros — zero-type zero-length trailers, skipped silently, as
