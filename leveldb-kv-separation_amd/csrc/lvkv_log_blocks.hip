@@ -102,7 +102,8 @@ struct LogArgs {
   // by log_scan_kernel for the emit; else nullptr
   unsigned long long* first_of;
   uint64_t* stamps;  // probe build only: 8 u64 per (workgroup, slot, block)
-  uint32_t knobs;    // probe build only: bit 0 = workers idle, no CRCs (timing)
+  uint32_t knobs;    // probe build only: bit 0 = workers idle, no CRCs; bits 8-11:
+                     // worker waves that sit out (timing)
 };
 
 // Manager phase stamps (probe build): 0 claimed, 1 in LDS, 2 walked,
@@ -328,62 +329,77 @@ __device__ __forceinline__ uint8_t walk_block(const uint8_t* blk, uint32_t n, bo
                                               uint32_t gen, uint32_t* count, uint32_t* stop,
                                               const LogArgs& la, uint32_t sm, uint32_t sk) {
   const uint32_t lane = lane_id();
-  const uint32_t base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(blk));
-  const uint32_t end = base + n;
+  // (uniform, and seen so: the walk's tests and branches stay scalar)
+  const uint32_t base =
+      __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(blk)));
+  const uint32_t end = base + __builtin_amdgcn_readfirstlane(n);
   uint32_t k = 0, bp = base, len = 0, typ = 0;
   uint32_t nseg = 0;  // long-record segments registered
   uint32_t held = 0;  // position of record k in lane k % 64
   if (n >= kLogHeader) {
-    uint32_t nlen, ntyp;
+    uint32_t nlen, ntyp, vlen, vtyp;
     asm volatile("ds_read_u16 %0, %2 offset:4\n\tds_read_u8 %1, %2 offset:6\n\ts_waitcnt lgkmcnt(0)"
-                 : "=v"(len), "=v"(typ)
+                 : "=&v"(vlen), "=&v"(vtyp)
                  : "v"(bp));
     log_stamp(la, sm, sk, 5);
+    // the header's fields as scalars: the tests and the next address on the
+    // scalar unit, two v_readfirstlane after each LDS trip
+    len = __builtin_amdgcn_readfirstlane(vlen);
+    typ = __builtin_amdgcn_readfirstlane(vtyp);
     for (;;) {
       const uint32_t nbp = bp + kLogHeader + len;
       asm volatile("ds_read_u16 %0, %2 offset:4\n\tds_read_u8 %1, %2 offset:6"
-                   : "=v"(nlen), "=v"(ntyp)
+                   : "=&v"(nlen), "=&v"(ntyp)
                    : "v"(nbp));
       __builtin_amdgcn_sched_barrier(0);  // the reads issue before the tests below
-      // bit 0: a bad length (:221-232) or a zero record (:234-240) ends the
-      // walk; bit 1: the record ends within 7 bytes of the block end; bit 2:
-      // a record longer than kSegBytes
-      const uint32_t f = __builtin_amdgcn_readfirstlane(
-          (nbp > end || (len | typ) == 0 ? 1u : 0u) | (end - nbp < kLogHeader ? 2u : 0u) |
-          (len + 1u > kSegBytes ? 4u : 0u));
-      if (f & 1u) break;
+      // a bad length (:221-232) or a zero record (:234-240) ends the walk
+      // (tests as sign bits of 32-bit differences: one scalar compare and
+      // branch each, not a chain of selects; offsets and lengths < 2^31)
+      const uint32_t left = end - nbp;
+      if (((left | ((len | typ) - 1u)) >> 31) != 0) break;
       held = lane == (k & 63u) ? bp - base : held;
-      if (__builtin_expect(f & 4u, 0)) {
-        // a long record: its segments go to the long queue
-        const uint32_t m = (len + 1u + kSegBytes - 1u) / kSegBytes;
-        if (lane == 0) {
-          const uint32_t e = S.nlong++;
-          S.lj[e] = static_cast<uint16_t>(k);
-          S.lp[e] = static_cast<uint16_t>(bp - base);
-          S.lseg[e] = static_cast<uint8_t>(m);
-          S.lfirst[e] = static_cast<uint8_t>(nseg);
-          S.lacc[e] = 0;
-          S.lrem[e] = m;
+      const uint32_t kk = k + 1u;
+      // the rare cases behind one test: a record longer than kSegBytes, a
+      // batch of 8 positions to publish, a record ending within 7 bytes of
+      // the block end
+      static_assert(kSegBytes == 4096u && kLogHeader == 7u, "the tests below");
+      if (__builtin_expect(((len >> 12) | (((kk & 7u) - 1u) >> 31) | ((left - 7u) >> 31)) != 0, 0)) {
+        if (len + 1u > kSegBytes) {
+          // a long record: its segments go to the long queue
+          const uint32_t m = (len + 1u + kSegBytes - 1u) / kSegBytes;
+          if (lane == 0) {
+            const uint32_t e = S.nlong++;
+            S.lj[e] = static_cast<uint16_t>(k);
+            S.lp[e] = static_cast<uint16_t>(bp - base);
+            S.lseg[e] = static_cast<uint8_t>(m);
+            S.lfirst[e] = static_cast<uint8_t>(nseg);
+            S.lacc[e] = 0;
+            S.lrem[e] = m;
+          }
+          nseg += m;
+          if (lane == 0) lds_store_rel(&S.lavail, (gen << 16) | nseg);
         }
-        nseg += m;
-        if (lane == 0) lds_store_rel(&S.lavail, (gen << 16) | nseg);
-      }
-      ++k;
-      if ((k & 7u) == 0) {
-        // records k-8 .. k-1: their lanes write their positions, then the
-        // first of them publishes the count (LDS keeps one wave's order; the
-        // overflow's sc1 stores are waited for first)
-        const uint32_t g0 = (k - 8u) & 63u;
-        if ((lane & ~7u) == g0) {
-          put_pos(pos, over, k - 8u + (lane & 7u), held);
-          if (lane == g0) lds_store_rel(&S.prog, (gen << kGenShift) | k);
+        if ((kk & 7u) == 0) {
+          // records kk-8 .. kk-1: their lanes write their positions, then the
+          // first of them publishes the count (LDS keeps one wave's order; the
+          // overflow's sc1 stores are waited for first)
+          const uint32_t g0 = (kk - 8u) & 63u;
+          if ((lane & ~7u) == g0) {
+            put_pos(pos, over, kk - 8u + (lane & 7u), held);
+            if (lane == g0) lds_store_rel(&S.prog, (gen << kGenShift) | kk);
+          }
+        }
+        if (left < kLogHeader) {
+          k = kk;
+          bp = nbp;
+          break;
         }
       }
+      k = kk;
       bp = nbp;
-      if (f & 2u) break;
       asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nlen), "+v"(ntyp));
-      len = nlen;
-      typ = ntyp;
+      len = __builtin_amdgcn_readfirstlane(nlen);
+      typ = __builtin_amdgcn_readfirstlane(ntyp);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nlen), "+v"(ntyp));
   }
@@ -583,7 +599,9 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
     LogLane L;
     L.keys = lane_keys(lane);
     L.lane_base = compact_lane_base(lane);
-    for (uint32_t idle = 0;;) {
+    // probe knob bits 8-11: that many worker waves sit out (timing)
+    const uint32_t nidle = (a.knobs >> 8) & 15u;
+    for (uint32_t idle = 0; wave < static_cast<uint32_t>(kVW) - nidle;) {
       if (a.knobs & 1u) {
         if (lds_load_acq(&fin) == kSlots) break;
         __builtin_amdgcn_s_sleep(127);
