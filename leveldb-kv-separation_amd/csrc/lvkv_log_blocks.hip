@@ -434,6 +434,31 @@ __device__ __forceinline__ void record_done(const uint8_t* blk, uint32_t p, uint
   hb[3] = static_cast<uint8_t>(crc >> 24);
 }
 
+// Block b into a slot's LDS buffer by LDS-DMA from its 16-byte aligned
+// start: full 16-byte lines as dwordx4, the last 0-15 bytes by byte loads
+// (a sub-dword LDS-DMA does not land one byte per lane). Issued only: the
+// caller waits (vmcnt) before reading the slot. Returns the block's
+// misalignment (its first byte is at sbuf + shift).
+__device__ __forceinline__ uint32_t dma_block(const LogArgs& a, uint32_t b, uint8_t* sbuf,
+                                              uint32_t lane) {
+  const uint64_t start = uint64_t{b} * kLogBlock;
+  const uint32_t n = static_cast<uint32_t>(min(a.size, start + kLogBlock) - start);
+  const uint8_t* src = a.file + start;
+  const uint32_t shift = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src) & 15u);
+  const uint32_t nbytes = shift + n;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(src - shift), 0, static_cast<int>(nbytes), kBufferDword3);
+  const uint32_t lines = nbytes >> 4;
+  for (uint32_t i = 0; i * 64u < lines; ++i) {
+    const uint32_t line = i * 64u + lane;
+    if (line < lines)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          r, (__attribute__((address_space(3))) void*)(sbuf + 1024u * i), 16, 16u * line, 0, 0, 0);
+  }
+  if (lane < (nbytes & 15u)) sbuf[16u * lines + lane] = (src - shift)[16u * lines + lane];
+  return shift;
+}
+
 // ---- the kernel ------------------------------------------------------------
 
 __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
@@ -459,7 +484,22 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
   }
   if (tid == 0) fin = 0;
   if (tid == 0) log_stamp(a, 0, 15, 0);
-  build_compact_image<kVW>(img, a.zpow, a.lane_cols, tid, wave, lane);  // ends with a barrier
+  // the CRC image (build_compact_image's steps); each slot's first block is
+  // assigned (workgroup g, slot m: block g * kSlots + m; the tickets count
+  // the rest) and its DMA issued before the barrier, once the image's loads
+  // have landed (vmcnt is in order), so no ticket round trip comes first
+  uint32_t first_shift = 0;
+  const uint32_t first_b = blockIdx.x * kSlots + wave;
+  {
+    RowTabStage<64 * kVW> rt;
+    LaneTabGen<kVW> lg;
+    rt.load(a.zpow, tid);
+    lg.load(a.lane_cols, wave, lane);
+    rt.store(img, tid);
+    lg.store(img, wave, lane);
+    if (wave < kSlots && first_b < a.nblocks) first_shift = dma_block(a, first_b, buf[wave], lane);
+    __syncthreads();
+  }
   if (tid == 0) log_stamp(a, 0, 15, 1);
 
   if (wave < kSlots) {
@@ -472,10 +512,11 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
     uint16_t* spos = pos[m];
     uint32_t* sover = a.over + (static_cast<uint64_t>(blockIdx.x) * kSlots + m) * kPosOver;
     uint32_t gen = 0;  // slot generation (gen 0's block is the first)
-    // tickets: the next block's is claimed as soon as this one is in LDS, so
-    // the atomic's round trip overlaps the walk
-    uint32_t tk = 0;
-    if (lane == 0) tk = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // tickets (after the grid's first kSlots blocks a workgroup): the next
+    // block's is claimed as soon as this one is in LDS, so the atomic's round
+    // trip overlaps the walk
+    const uint32_t tk0 = gridDim.x * kSlots;
+    uint32_t tk = first_b;
     for (uint32_t k = 0;; ++k) {
       const uint32_t b = __builtin_amdgcn_readfirstlane(tk);
       if (b >= a.nblocks) break;
@@ -484,28 +525,13 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
       const uint64_t end = min(a.size, start + kLogBlock);
       const uint32_t n = static_cast<uint32_t>(end - start);
       const bool eof = n < kLogBlock;
-      // the block into the slot by LDS-DMA from its 16-byte aligned start:
-      // full 16-byte lines as dwordx4, the last 0-15 bytes by byte loads
-      {
-        const uint8_t* src = a.file + start;
-        const uint32_t shift = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src) & 15u);
-        const uint32_t nbytes = shift + n;
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t*>(src - shift), 0, static_cast<int>(nbytes), kBufferDword3);
-        const uint32_t lines = nbytes >> 4;
-        for (uint32_t i = 0; i * 64u < lines; ++i) {
-          const uint32_t line = i * 64u + lane;
-          if (line < lines)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                r, (__attribute__((address_space(3))) void*)(sbuf + 1024u * i), 16,
-                16u * line, 0, 0, 0);
-        }
-        // (a sub-dword LDS-DMA does not land one byte per lane: plain loads)
-        if (lane < (nbytes & 15u)) sbuf[16u * lines + lane] = (src - shift)[16u * lines + lane];
-        __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0): the DMA has landed
-        if (lane == 0) S.shift = shift;
-      }
-      if (lane == 0) tk = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // the block into the slot (the first one's DMA was issued before the
+      // image barrier)
+      const uint32_t shift = k == 0 ? first_shift : dma_block(a, b, sbuf, lane);
+      __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0): the DMA has landed
+      if (lane == 0) S.shift = shift;
+      if (lane == 0)
+        tk = tk0 + __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       log_stamp(a, m, k, 1);
       const uint8_t* blk = sbuf + S.shift;
       uint32_t c, stop_at;
