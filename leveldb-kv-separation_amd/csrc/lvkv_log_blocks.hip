@@ -585,13 +585,11 @@ __global__ void __launch_bounds__(kVThreads, 1) log_verify_kernel(LogArgs a) {
         a.block_status[b] = status;
         a.block_drop[b] = static_cast<uint32_t>(drop);
         a.stg_off[b] = off;
-        // what the last workgroup reads, as sc1 stores (read back with sc1
-        // loads: no agent-scope fence on either side)
-        __hip_atomic_store(&a.info[b].x,
-                           uint64_t{c} | (uint64_t{bad != 0xffffffffu ? bad : c} << 32),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&a.info[b].y, drop | (uint64_t{status} << 32), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        // what the emit launch reads (after this kernel's end: plain stores;
+        // device-scope ones are acknowledged late, and the next block's DMA
+        // wait, vmcnt being in order, waits for them)
+        a.info[b] = make_ulonglong2(uint64_t{c} | (uint64_t{bad != 0xffffffffu ? bad : c} << 32),
+                                    drop | (uint64_t{status} << 32));
       }
       log_stamp(a, m, k, 4);
       // recycle the slot: reset, then open the next generation (workers
