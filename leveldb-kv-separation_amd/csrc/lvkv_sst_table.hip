@@ -478,8 +478,6 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
       mtail = group_crc_tail(mstart, mend);
     }
   }
-  if (mfit && h.ms < kMetaStage)
-    for (uint32_t i = tid; i < h.ms; i += kT) L.mbuf[i] = tb.img[h.mo + i];
   // a small index, as the aligned dwords holding it (the dword before it
   // only when that is inside the image)
   const uint64_t ia4 = istart & ~uint64_t{3};
@@ -507,6 +505,18 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
   } else if (mfit) {
     part = group_crc_part(lds, mstart, mend, 0u, wave - wi, W - wi,
                           group_log2seg(h.ms + 1, W - wi), keys, lane, lane_base, zpow);
+  }
+  // ReadMeta's filter lookup (table.cc:76-102) on the last wave, beside the
+  // index CRC: speculative, it counts only once the index and the metaindex
+  // prove readable (step 4), and it no longer stands between the verdicts
+  // and the placement. The wave stages the metaindex in LDS itself (its own
+  // stores, then its loads: one wave's LDS accesses are in order).
+  if (wave == W - 1 && mfit) {
+    const bool staged = h.ms < kMetaStage;
+    if (staged)
+      for (uint32_t i = lane; i < h.ms; i += 64) L.mbuf[i] = tb.img[h.mo + i];
+    find_filter(h, staged ? L.mbuf : tb.img + h.mo, h.ms, reinterpret_cast<const uint8_t*>(L.fkey),
+                fk.len, tb, lane);
   }
   if (lane == 0) L.acc[wave] = part;
   __syncthreads();
@@ -546,18 +556,20 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
       else
         h.nr = inr;
     }
-    h.has_filter = 0;
-    h.fo = h.fs = 0;
-    h.filter_status = LVKV_BLOCK_OK;
+    // ReadMeta runs only when Table::Open read the index (table.cc:62-76),
+    // and ReadFilter only on a readable metaindex
+    if (h.index_status != LVKV_BLOCK_OK || h.meta_status != LVKV_BLOCK_OK) {
+      h.has_filter = 0;
+      h.fo = h.fs = 0;
+      h.filter_status = LVKV_BLOCK_OK;
+    }
   }
   __syncthreads();
   // Table::Open succeeded iff the index block was read (Block::Block's
   // restart test only makes the index iterator fail, table.cc:62-75); then
   // ReadMeta runs (:76).
   sst_stamp(stamps, t, 3);
-  const bool index_read = footer_ok && h.index_status == LVKV_BLOCK_OK;
   const bool index_usable = h.status == LVKV_SST_OK;
-  const bool stage_meta = index_read && h.meta_status == LVKV_BLOCK_OK && h.ms < kMetaStage;
   const bool stage_index = !spec && index_usable && h.is <= kIndexStage;
   uint8_t* ibuf = reinterpret_cast<uint8_t*>(lds);  // the CRC image is spent
   if (stage_index) {
@@ -574,10 +586,6 @@ __device__ __forceinline__ void sst_head(uint32_t* lds, const uint8_t* file, con
   }
   __syncthreads();
   sst_stamp(stamps, t, 4);
-  if (wave == 0 && index_read && h.meta_status == LVKV_BLOCK_OK)
-    find_filter(h, stage_meta ? L.mbuf : tb.img + h.mo, h.ms,
-                reinterpret_cast<const uint8_t*>(L.fkey), fk.len, tb, lane);
-  __syncthreads();
   // entries: the data blocks the index lists (none when its restart array is
   // unusable), then the filter block
   if (tid == 0) h.nb = (index_usable ? h.nr : 0u) + h.has_filter;
