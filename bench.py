@@ -60,6 +60,16 @@ GIB = float(1 << 30)
 BLOCK = 4096
 SPLIT_TOTAL = 1_000_000
 METRIC = "device-resident CRC32C GiB/s over 10k×4KiB blocks; % of MI355X HBM peak"
+# each config's own line names its own workload (the headline's is BASELINE.json's)
+METRICS = {
+    "headline": METRIC,
+    "blocks1m": "device-resident CRC32C GiB/s over 1M×4KiB blocks per GPU (config 4); "
+                "% of MI355X HBM peak",
+    "blocks1m_split": "device-resident CRC32C GiB/s over 1M×4KiB blocks split across the GPUs "
+                      "(config 5), aggregate; % of MI355X HBM peak per GPU",
+    "wal32k": "device-resident CRC32C GiB/s over 16384×32KiB WAL blocks, CRC over [6, 32768) "
+              "(config 3); % of MI355X HBM peak",
+}
 
 CONFIGS = {
     # name: (nblocks, block_bytes, stride, crc_offset_in_block, description)
@@ -109,6 +119,15 @@ class Comm:
         if self.world > 1:
             import torch.distributed as dist
             dist.barrier()
+
+    def gather(self, obj):
+        """Every rank's `obj`, in rank order (all_gather_object; [obj] at world 1)."""
+        if self.world == 1:
+            return [obj]
+        import torch.distributed as dist
+        out = [None] * self.world
+        dist.all_gather_object(out, obj)
+        return out
 
     def max(self, x: float) -> float:
         if self.world == 1:
@@ -165,13 +184,18 @@ def split_measure(make_runner, comm: Comm, rank: int, world: int, steps: int, wa
     runner = make_runner(start, count)
     elapsed, _ = timed_region(runner, comm, steps, warmup, warmup_s)
     value = total * block * steps / elapsed / GIB
+    # every rank's slice and how many of its blocks were checked against the
+    # oracle (the whole slice, before the timed region)
+    slices = comm.gather({"rank": rank, "start": start, "blocks": count,
+                          "parity_blocks": getattr(runner, "parity_blocks", None)})
     rec = {"workload": CONFIGS["blocks1m_split"][4], "total_blocks": total,
            "block_bytes": block, "ranks": world, "slice_blocks_rank0": shard.shard_range(total, 0, world)[1],
            "slice_copies": getattr(runner, "nrot", 1),
            "steps": steps, "ms_per_step": round(elapsed / steps * 1e3, 5),
            "value": round(value, 4), "unit": "GiB/s",
            "pct_hbm_peak_per_gpu": round(100.0 * value * GIB / 1e9 / HBM_PEAK_GBS / world, 2),
-           "timing": "common start barrier to the last rank's completion (max over ranks)"}
+           "timing": "common start barrier to the last rank's completion (max over ranks)",
+           "slices": slices}
     return runner, rec
 
 
@@ -212,41 +236,6 @@ class EngineRunner:
 
     def finish(self):
         self.eng.wait()
-
-    def sync(self):
-        self.torch.cuda.synchronize()
-
-
-class HipRunner:
-    """Steps through the HIP launch path (lvkv_crc32c_uniform_device) on two
-    streams (blocks beyond the engine's 4 KiB kernel)."""
-
-    def __init__(self, lvkv, buf, nb, L, stride, crc_off, nrot, window, outs, dev):
-        import torch
-        self.torch = torch
-        self.fn = lvkv.lib.lvkv_crc32c_uniform_device
-        self.nb, self.L, self.stride = nb, L, stride
-        self.bases = [buf.data_ptr() + w * window + crc_off for w in range(nrot)]
-        self.outs = [o.data_ptr() for o in outs]
-        self.nrot = nrot
-        self.main = torch.cuda.current_stream(dev)
-        self.side = torch.cuda.Stream(dev)
-        self.hs = [self.main.cuda_stream, self.side.cuda_stream]
-        self.forked = False
-
-    def step(self, i):
-        if not self.forked:
-            self.side.wait_stream(self.main)
-            self.forked = True
-        rc = self.fn(self.bases[i % self.nrot], self.stride, self.L, 0,
-                     self.outs[i % len(self.outs)], self.nb, 0, self.hs[i % 2])
-        if rc != 0:
-            raise SystemExit(f"bench: lvkv_crc32c_uniform_device failed ({rc})")
-
-    def finish(self):
-        if self.forked:
-            self.main.wait_stream(self.side)
-            self.forked = False
 
     def sync(self):
         self.torch.cuda.synchronize()
@@ -410,6 +399,8 @@ def main():
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the rocprofv3 FETCH_SIZE pass behind roofline.traffic")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--no-ceiling", action="store_true",
+                    help="skip the read-only ceiling kernels behind roofline.ceiling")
     ap.add_argument("--isolated", type=int, default=0,
                     help="only run N ordered (one-at-a-time) launches and exit: the "
                          "command a rocprofv3 kernel trace of the roofline kernel wraps")
@@ -464,23 +455,17 @@ def main():
     nb, L, stride, crc_off, desc = CONFIGS[args.config]
     # every config runs on the AQL engine: the burst kernel for the 4 KiB
     # blocks, the general walk (lvkv_ek_ragged) for config 3's 32 KiB blocks
-    use_engine = True
     burst = L <= 16 * 256 and stride % 4 == 0 and (crc_off + L) % 4 == 0
     buf, nrot, window = make_buffers(torch, dev, rank, nb, stride, args.rotate_bytes)
     outs = [torch.empty(nb, dtype=torch.int32, device=dev) for _ in range(4)]
-    eng = lvkv.Engine(local) if use_engine else None
-    if use_engine:
-        runner = EngineRunner(lvkv, eng, buf, nb, L, stride, crc_off, nrot, window, outs)
-    else:
-        runner = HipRunner(lvkv, buf, nb, L, stride, crc_off, nrot, window, outs, dev)
+    eng = lvkv.Engine(local)
+    runner = EngineRunner(lvkv, eng, buf, nb, L, stride, crc_off, nrot, window, outs)
     runner.step(0)
     runner.finish()
     runner.sync()
-    parity_check(buf, outs[0], nb, L, stride, crc_off, rank, args.config)
+    checked = parity_check(buf, outs[0], nb, L, stride, crc_off, rank, args.config)
 
     if args.isolated:
-        if not use_engine:
-            raise SystemExit("bench: --isolated times the engine kernel")
         runner.flags = 2
         for k in range(args.isolated):
             runner.step(1 + k)
@@ -492,45 +477,50 @@ def main():
     value = world * nb * L * args.steps / elapsed / GIB
     algo_bytes = nb * (L + 4)
 
+    # every rank prices its own launches (its own GPU's packet-processor times)
     roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": None, "traffic": None, "algo_bytes_per_launch": algo_bytes}
-    if use_engine:
-        # one launch alone (ordered: the engine drains, then the whole-chip kernel)
-        iso = profile_launches(runner, eng, 64, True, nxt)
-        # a batch beyond one dispatch's capacity is several dispatches: its
-        # duration is first start to last end of its group
-        per = max(1, len(iso) // 64)
-        d = [iso[i + per - 1][1] - iso[i][0] for i in range(0, per * 64, per)]
-        kern_us = statistics.mean(d)
-        achieved = algo_bytes / (kern_us * 1e-6) / 1e9
-        # K overlapped launches: device span (first start -> last end) / K
-        runner.step(nxt + 64)
-        eng.wait()
-        pipe = profile_launches(runner, eng, args.steps, False, nxt + 65)
-        span = (max(b for _, b in pipe) - min(a for a, _ in pipe)) / args.steps
-        w, c, gr = eng.shape()
-        roof.update({
-            "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
-            "kernel": ("lvkv_ek_uniform_pair (ordered launch, 2 workgroups x 8 waves per CU)"
-                       if burst else
-                       "lvkv_ek_ragged (ordered launch, 2 workgroups x 8 waves x 2 chains per CU)"),
-            "kernel_us_avg": round(kern_us, 3), "kernel_us_median": round(statistics.median(d), 3),
-            "kernel_us_min": round(min(d), 3), "launches": len(d), "dispatches_per_launch": per,
-            "timing": "HSA packet-processor start/end per dispatch (engine profiling)",
-            "pipelined": {"kernel": (f"lvkv_ek_uniform ({w} waves x {c} chains, {gr} workgroups, "
-                                     f"{eng.queues()} queues)" if burst else
-                                     f"lvkv_ek_ragged ({eng.queues()} queues)"),
-                          "launches": args.steps, "dispatches": len(pipe),
-                          "period_us": round(span, 3),
-                          "achieved": round(algo_bytes / (span * 1e-6) / 1e9, 1),
-                          "frac": round(algo_bytes / (span * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-                          "dispatch_us_avg": round(statistics.mean(b - a for a, b in pipe), 3)}})
-    else:
-        roof.update({"kernel": "HIP launch path (two streams)", "achieved":
-                     round(algo_bytes / (ms_per_step * 1e-3) / 1e9, 1)})
-        roof["frac"] = round(roof["achieved"] / HBM_PEAK_GBS, 4)
-        roof["timing"] = "host wall of the timed region / K (no per-launch device timing)"
+    # one launch alone (ordered: the engine drains, then the whole-chip kernel)
+    iso = profile_launches(runner, eng, 64, True, nxt)
+    # a batch beyond one dispatch's capacity is several dispatches: its
+    # duration is first start to last end of its group
+    per = max(1, len(iso) // 64)
+    d = [iso[i + per - 1][1] - iso[i][0] for i in range(0, per * 64, per)]
+    kern_us = statistics.mean(d)
+    achieved = algo_bytes / (kern_us * 1e-6) / 1e9
+    # K overlapped launches: device span (first start -> last end) / K
+    runner.step(nxt + 64)
+    eng.wait()
+    pipe = profile_launches(runner, eng, args.steps, False, nxt + 65)
+    nxt += 65 + args.steps
+    span = (max(b for _, b in pipe) - min(a for a, _ in pipe)) / args.steps
+    w, c, gr = eng.shape()
+    roof.update({
+        "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": None,
+        "kernel": ("lvkv_ek_uniform_pair (ordered launch, 2 workgroups x 8 waves per CU)"
+                   if burst else
+                   "lvkv_ek_ragged (ordered launch, 2 workgroups x 8 waves x 2 chains per CU)"),
+        "kernel_us_avg": round(kern_us, 3), "kernel_us_median": round(statistics.median(d), 3),
+        "kernel_us_min": round(min(d), 3), "launches": len(d), "dispatches_per_launch": per,
+        "timing": "HSA packet-processor start/end per dispatch (engine profiling)",
+        "pipelined": {"kernel": (f"lvkv_ek_uniform ({w} waves x {c} chains, {gr} workgroups, "
+                                 f"{eng.queues()} queues)" if burst else
+                                 f"lvkv_ek_ragged ({eng.queues()} queues)"),
+                      "launches": args.steps, "dispatches": len(pipe),
+                      "period_us": round(span, 3),
+                      "achieved": round(algo_bytes / (span * 1e-6) / 1e9, 1),
+                      "frac": round(algo_bytes / (span * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                      "dispatch_us_avg": round(statistics.mean(b - a for a, b in pipe), 3)}})
+    if burst and not args.no_ceiling:
+        roof["ceiling"] = measure_ceiling(torch, eng, runner, comm, args.steps, args.warmup,
+                                          warm_s, nxt, algo_bytes, roof)
+
+    rank_rec = {"rank": rank, "device": local, "nblocks": nb, "parity_blocks": checked,
+                "kernel_us_avg": roof["kernel_us_avg"], "frac": roof["frac"],
+                "pipelined_period_us": roof["pipelined"]["period_us"],
+                "pipelined_frac": roof["pipelined"]["frac"],
+                "ceiling_frac": (roof.get("ceiling") or {}).get("frac")}
 
     split = None
     if args.config == "headline" and not args.no_split:
@@ -542,26 +532,109 @@ def main():
         del split_runner
         torch.cuda.empty_cache()
 
-    if use_engine and rank == 0 and world == 1 and args.config == "headline" and not args.no_pmc:
+    ranks = comm.gather(rank_rec)
+    if rank == 0 and args.config == "headline" and not args.no_pmc:
+        # rank 0's GPU (device 0 of the node); the other ranks are done with theirs
         t = live_pmc_traffic()
         if t is not None:
             roof["traffic"] = t["bytes"]
-            roof["traffic_source"] = t["source"]
+            roof["traffic_source"] = t["source"] + (f"; rank 0 of {world}" if world > 1 else "")
 
     if rank == 0:
         line = _line_base(args, world, value, ms_per_step / 1e3, {
             "workload": desc, "nblocks_per_gpu": nb, "block_bytes": L, "stride": stride,
             "rotation_buffers": nrot, "rotation_bytes": nrot * window,
-            "path": ("AQL engine, batches overlapped" + ("" if burst else ", general walk"))
-                    if use_engine else "HIP launch, 2 streams",
-            "parallelism": f"{world} independent block batches (no collective)"})
+            "path": "AQL engine, batches overlapped" + ("" if burst else ", general walk"),
+            "parallelism": f"{world} independent block batches (no collective)",
+            "parity_blocks": sum(r["parity_blocks"] for r in ranks)})
         line["pct_hbm_peak"] = round(100.0 * value * GIB / 1e9 / HBM_PEAK_GBS / world, 2)
         line["roofline"] = roof
+        if world > 1:
+            line["roofline"]["per_rank"] = ranks
         line["split"] = split
-        line["cpu_baseline"] = (cpu_baseline(args.cpu_seconds)
-                                if world == 1 and not args.no_cpu_baseline else None)
+        line["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline(
+            args.cpu_seconds if world == 1 else min(args.cpu_seconds, 4.0))
+        if line["cpu_baseline"] is not None and world > 1:
+            line["cpu_baseline"]["note"] = (f"rank 0's host after every rank's GPU work "
+                                            f"({world} ranks on this node)")
         print(json.dumps(line), flush=True)
     _end(world)
+
+
+CEILING_CO = REPO / "tools" / "probe" / "ceiling_kernels.co"
+
+
+def measure_ceiling(torch, eng, runner, comm, steps, warmup, warm_s, first, algo_bytes, roof):
+    """What the chip gives a kernel that only reads, measured the way the
+    headline is ('a measured copy-kernel ceiling'): the
+    engine dispatches read-only kernels (tools/probe/ceiling_kernels.hip) in
+    place of the CRC kernel over the same rotating windows, K overlapped
+    launches on the same queues, priced with the same algorithmic bytes.
+      burst_bare  the production overlapped kernel's own loads, no tables/walk
+      stream      a plain 16 B/lane streaming read of each window
+      ordered     the ordered kernel's loads, one launch alone
+      warm_mall   the production kernel over 4 windows (164 MB: resident in
+                  the 256 MiB Infinity Cache), to show what a MALL-served
+                  rate looks like next to the cold rotation
+      copy_d2d    torch's device copy of 512 MiB (read + write bytes)."""
+    if not CEILING_CO.exists():
+        return None
+    co = CEILING_CO.read_bytes()
+    i = first
+    out = {"unit": "GB/s", "peak": HBM_PEAK_GBS,
+           "source": "AQL engine dispatching tools/probe/ceiling_kernels.co (lvkv_engine_load_probe)"}
+
+    def pipelined(tag):
+        nonlocal i
+        el, i = timed_region(runner, comm, steps, warmup, warm_s, first=i)
+        spans = profile_launches(runner, eng, steps, False, i)
+        i += steps
+        period = (max(b for _, b in spans) - min(a for a, _ in spans)) / steps
+        return {"kernel": tag, "launches": steps, "period_us": round(period, 3),
+                "achieved": round(algo_bytes / (period * 1e-6) / 1e9, 1),
+                "timed_region_GBs": round(algo_bytes * steps / el / 1e9, 1)}
+
+    try:
+        eng.load_probe(co, "ck_burst_bare", 8, 5, 1, overlapped=True)
+        out["burst_bare"] = pipelined("ck_burst_bare (8 waves x 5 chains, 1 per CU, 3 queues)")
+        eng.load_probe(co, "ck_stream", 8, 5, 1, overlapped=True)
+        out["stream"] = pipelined("ck_stream (16 B/lane, 8 loads in flight, 1 per CU, 3 queues)")
+        eng.load_probe(co, "ck_pair_bare", 8, 3, 2, overlapped=False)
+        iso = profile_launches(runner, eng, 64, True, i)
+        i += 64
+        per = max(1, len(iso) // 64)
+        d = [iso[k + per - 1][1] - iso[k][0] for k in range(0, per * 64, per)]
+        out["ordered"] = {"kernel": "ck_pair_bare (8 x 3, 2 per CU), one launch alone",
+                          "kernel_us_avg": round(statistics.mean(d), 3),
+                          "achieved": round(algo_bytes / (statistics.mean(d) * 1e-6) / 1e9, 1)}
+    finally:
+        eng.load_probe(None)
+    nrot = runner.nrot
+    runner.nrot = min(4, nrot)
+    try:
+        out["warm_mall"] = pipelined(f"production lvkv_ek_uniform over {runner.nrot} windows "
+                                     f"({runner.nrot * runner.nb * runner.stride / 1e6:.0f} MB)")
+    finally:
+        runner.nrot = nrot
+    n = 1 << 29
+    src = torch.empty(n, dtype=torch.uint8, device=runner.outs_t[0].device)
+    dst = torch.empty_like(src)
+    best = float("inf")
+    for _ in range(6):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        dst.copy_(src)
+        e1.record()
+        e1.synchronize()
+        best = min(best, e0.elapsed_time(e1) * 1e-3)
+    out["copy_d2d"] = {"bytes": 2 * n, "achieved": round(2 * n / best / 1e9, 1),
+                       "timing": "torch copy_ of 512 MiB, best of 6, HIP events"}
+    del src, dst
+    best_bare = max(out["burst_bare"]["achieved"], out["stream"]["achieved"])
+    out["achieved"] = best_bare
+    out["frac"] = round(best_bare / HBM_PEAK_GBS, 4)
+    out["production_over_ceiling"] = round(roof["pipelined"]["achieved"] / best_bare, 4)
+    return out
 
 
 SPLIT_ROTATE_BYTES = 1 << 30  # a rank's slice copies span at least this much
@@ -583,8 +656,7 @@ def _split_runner(torch, lvkv, eng, dev, rank, start, count):
     r.step(0)
     r.finish()
     r.sync()
-    if count:
-        parity_check(buf, outs[0], count, BLOCK, BLOCK, 0, rank, "split")
+    r.parity_blocks = parity_check(buf, outs[0], count, BLOCK, BLOCK, 0, rank, "split") if count else 0
     r.buf = buf
     return r
 
@@ -608,17 +680,30 @@ def _launch_ranks(n: int) -> int:
 class CpuPlumbingRunner:
     """Test-only stand-in for the engine (--plumbing-cpu): the library's
     per-call CPU CRC32C (lvkv_crc32c_value, the drop-in symbol) over this
-    rank's slice, so a CPU-only run exercises the rank launch, the slicing and
-    the timed region end to end. Never a measured line."""
+    rank's slice, so a CPU-only run exercises the rank launch, the slicing,
+    the parity count, the per-rank records and the timed region end to end.
+    Never a measured line."""
 
     def __init__(self, lvkv, start, count):
         self.value = lvkv.Value
-        data = np.frombuffer(np.random.default_rng(start).bytes(max(count, 1) * BLOCK), np.uint8)
-        self.blocks = [data[i * BLOCK:(i + 1) * BLOCK].tobytes() for i in range(count)]
+        self.data = np.frombuffer(np.random.default_rng(start).bytes(max(count, 1) * BLOCK),
+                                  np.uint8)
+        self.blocks = [self.data[i * BLOCK:(i + 1) * BLOCK].tobytes() for i in range(count)]
         self.count = count
         self.crc = None
+        self.step(0)
+        self.parity_blocks = self.parity()
 
-    def step(self, i):
+    def parity(self):
+        """This rank's CRCs against the oracle (checker), as parity_check does."""
+        sys.path.insert(0, str(REPO / "oracle"))
+        import oracle
+        want = oracle.uniform(self.data, self.count, BLOCK, threads=1)
+        if [int(x) for x in want] != self.crc:
+            raise SystemExit("bench: plumbing parity FAILED")
+        return self.count
+
+    def step(self, i, final=False):
         self.crc = [self.value(b) for b in self.blocks]
 
     def finish(self):
@@ -635,26 +720,25 @@ def _plumbing_cpu(args, lvkv, world, rank, warm_s):
     comm = Comm(world, None)
     runner, rec = split_measure(lambda s, c: CpuPlumbingRunner(lvkv, s, c), comm, rank, world,
                                 args.steps, args.warmup, warm_s, total=args.split_total)
-    counts = [runner.count]
-    if world > 1:
-        import torch.distributed as dist
-        gathered = [None] * world
-        dist.all_gather_object(gathered, runner.count)
-        counts = gathered
+    ranks = comm.gather({"rank": rank, "device": None, "nblocks": runner.count,
+                         "parity_blocks": runner.parity_blocks})
     if rank == 0:
         line = _line_base(args, world, rec["value"], rec["ms_per_step"] / 1e3,
                           {"workload": "plumbing test (CPU per-call CRC, not a measurement)",
                            "total_blocks": args.split_total, "block_bytes": BLOCK,
-                           "parallelism": f"{world} contiguous slices (no collective)"})
+                           "parallelism": f"{world} contiguous slices (no collective)",
+                           "parity_blocks": sum(r["parity_blocks"] for r in ranks)})
         line["split"] = rec
-        line["rank_counts"] = counts
+        line["rank_counts"] = [r["nblocks"] for r in ranks]
+        line["roofline"] = {"per_rank": ranks}
+        line["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline(args.cpu_seconds)
         line["data"] = "plumbing-cpu: NOT a device measurement"
         print(json.dumps(line), flush=True)
     _end(world)
 
 
 def _line_base(args, world, value, sec_per_step, config):
-    return {"metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
+    return {"metric": METRICS[args.config], "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(sec_per_step * 1e3, 5), "higher_is_better": True,
             "scaling": "weak" if args.config != "blocks1m_split" else "strong",

@@ -131,6 +131,9 @@ def _load() -> ctypes.CDLL:
     L.lvkv_engine_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_double), sz]
     L.lvkv_engine_profile_read.restype = ctypes.c_long
+    L.lvkv_engine_load_probe.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_char_p, u32, u32,
+                                         u32, i32]
+    L.lvkv_engine_load_probe.restype = i32
     L.lvkv_debug_engine_stall.argtypes = [vp, i32, ctypes.c_double]
     L.lvkv_debug_engine_stall.restype = i32
     L.lvkv_strerror.argtypes = [i32]
@@ -789,6 +792,19 @@ class Engine:
         k = int(_lib.lvkv_engine_profile_read(self.handle, t0, t1, n))
         _check("lvkv_engine_profile_read", k if k < 0 else 0)
         return list(zip(t0[:k], t1[:k]))
+
+    def load_probe(self, code_object: Optional[bytes], kernel: str = "", waves: int = 8,
+                   chains: int = 5, per_cu: int = 1, overlapped: bool = True) -> None:
+        """Measurement only (lvkv_engine_load_probe): overlapped (or ordered)
+        uniform submits dispatch `kernel` from a separate gfx950 code object
+        instead of the engine's own; None restores them."""
+        if code_object is None:
+            rc = _lib.lvkv_engine_load_probe(self.handle, None, 0, None, 0, 0, 0, 0)
+        else:
+            rc = _lib.lvkv_engine_load_probe(self.handle, code_object, len(code_object),
+                                             (kernel + ".kd").encode(), waves, chains, per_cu,
+                                             int(overlapped))
+        _check("lvkv_engine_load_probe", rc)
 
     def close(self) -> None:
         if self.handle:

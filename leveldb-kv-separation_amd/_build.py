@@ -26,6 +26,10 @@ ORACLE_DIR = REPO / "oracle"
 ORACLE_LIB = ORACLE_DIR / "liboracle_crc32c.so"
 REF_LIB = ORACLE_DIR / "_ref" / "libref_crc32c.so"
 REFERENCE = Path("/root/reference")
+# HBM read-ceiling kernels (bench.py roofline.ceiling; measurement only, not in
+# the library): an unbundled code object the engine loads as a probe.
+CEILING_SRC = REPO / "tools" / "probe" / "ceiling_kernels.hip"
+CEILING_CO = REPO / "tools" / "probe" / "ceiling_kernels.co"
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("LVKV_OFFLOAD_ARCH", "gfx950")
@@ -102,6 +106,18 @@ def build_lib(verbose: bool = False, force: bool = False, probe: bool = False) -
     return lib
 
 
+def build_ceiling(verbose: bool = False, force: bool = False) -> Path:
+    deps = [CEILING_SRC, Path(__file__)] + [CSRC / h for h in HEADERS]
+    if not force and _newer(CEILING_CO, deps):
+        return CEILING_CO
+    tmp = CEILING_CO.with_suffix(".co.tmp")
+    _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "--cuda-device-only",
+          "--no-gpu-bundle-output", "-I", INCLUDE, "-I", CSRC, "-c", CEILING_SRC, "-o", tmp],
+         verbose)
+    os.replace(tmp, CEILING_CO)
+    return CEILING_CO
+
+
 def build_oracle(verbose: bool = False) -> Path:
     """Build the C restatement (always) and the reference-backed checker
     oracle/_ref (only where /root/reference exists, i.e. this container)."""
@@ -114,6 +130,7 @@ def build_oracle(verbose: bool = False) -> Path:
 def build_all(verbose: bool = False, force: bool = False) -> None:
     build_lib(verbose=verbose, force=force)
     build_lib(verbose=verbose, force=force, probe=True)
+    build_ceiling(verbose=verbose, force=force)
     build_oracle(verbose=verbose)
 
 

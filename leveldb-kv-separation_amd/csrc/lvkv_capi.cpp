@@ -380,7 +380,7 @@ hipError_t log_scratch_acquire(DeviceCtx& c, hipStream_t stream, size_t bytes, v
   hipError_t e = hipStreamIsCapturing(stream, &cs);
   if (e != hipSuccess) return e;
   if (cs != hipStreamCaptureStatusNone) return hipErrorStreamCaptureUnsupported;
-  std::lock_guard<std::mutex> lk(c.scratch_mu);
+  std::unique_lock<std::mutex> lk(c.scratch_mu);
   constexpr size_t kPoolMax = 4;
   size_t same = SIZE_MAX, any = SIZE_MAX, idle_small = SIZE_MAX, busy_small = SIZE_MAX;
   for (size_t i = 0; i < c.log_pool.size(); ++i) {
@@ -424,21 +424,37 @@ hipError_t log_scratch_acquire(DeviceCtx& c, hipStream_t stream, size_t bytes, v
     c.log_pool.push_back(n);
     idle_small = c.log_pool.size() - 1;
   }
-  auto& b = c.log_pool[idle_small];
-  if (b.p != nullptr) {
-    if ((e = hipEventSynchronize(b.ev)) != hipSuccess) return e;
-    if ((e = hipFree(b.p)) != hipSuccess) return e;
-  }
-  b.p = nullptr;
-  b.bytes = 0;
+  // Take the slot out of the pool, then wait for its last call and
+  // reallocate without the lock: other streams' acquires and releases on
+  // this device go on meanwhile (the slot is addressed by index, since the
+  // pool may grow).
+  const size_t k = idle_small;
+  void* old = c.log_pool[k].p;
+  const hipEvent_t ev = c.log_pool[k].ev;
+  c.log_pool[k].lent = true;
+  c.log_pool[k].p = nullptr;
+  c.log_pool[k].bytes = 0;
+  lk.unlock();
   const size_t cap = std::max<size_t>(bytes, size_t{1} << 16);
-  if ((e = hipMalloc(&b.p, cap)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(b.p, 0, 32, stream)) != hipSuccess) return e;
+  void* p = nullptr;
+  if (old != nullptr) {
+    e = hipEventSynchronize(ev);
+    if (e == hipSuccess) e = hipFree(old);
+  }
+  if (e == hipSuccess) e = hipMalloc(&p, cap);
+  if (e == hipSuccess) e = hipMemsetAsync(p, 0, 32, stream);
+  lk.lock();
+  auto& b = c.log_pool[k];
+  if (e != hipSuccess) {
+    if (p != nullptr) (void)hipFree(p);
+    b.lent = false;  // empty: the next acquire allocates it afresh
+    return e;
+  }
+  b.p = p;
   b.bytes = cap;
-  b.lent = true;
   b.stream = stream;
-  *out = b.p;
-  *slot = idle_small;
+  *out = p;
+  *slot = k;
   return hipSuccess;
 }
 

@@ -286,6 +286,8 @@ __device__ uint32_t place_table(lvkv_sst_report* reports, uint32_t t, uint32_t n
     uint64_t v = 0;
     if (j < upto) {
       uint64_t x;
+      // tag and count travel in one 64-bit atomic word: nothing else is read
+      // on the strength of it, so no acquire is needed
       do {
         x = __hip_atomic_load(&reports[j].link_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } while (static_cast<uint32_t>(x >> 32) != gen);
@@ -879,14 +881,16 @@ __global__ void __launch_bounds__(64 * kFW, 2)
   if (tid == 0) lds[RagLds<kFW>::kFlag] = 0;
   build_compact_image<kFW>(lds, zpow, lane_cols, tid, wave, lane);  // ends with a barrier
   if (blockIdx.x == ntables) sst_stamp(stamps, 0, 10);
-  // Wait for every head. No acquire fence afterwards (one per workgroup
-  // would invalidate the XCD's L2 hundreds of times): everything the heads
-  // wrote is read with agent-scope atomic loads (desc_u64/_u32, the
-  // kModeSstTable store), which see the released values.
+  // Wait for every head, then one agent-scope acquire (pairing with the
+  // heads' release of done_). Everything the heads wrote is also read with
+  // agent-scope atomic loads (desc_u64/_u32, the kModeSstTable store).
   if (wave == 0) {
     for (uint32_t j = lane; j < ntables; j += 64)
       while (__hip_atomic_load(&reports[j].done_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen)
         __builtin_amdgcn_s_sleep(8);
+    // pairs with the heads' release of done_ (one acquire once every wait
+    // has ended, not one per spin)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
   const bool probe = blockIdx.x == ntables;  // the first CRC workgroup's stamps (table 0's row)
@@ -1155,6 +1159,9 @@ __device__ __forceinline__ void spec_crc_group(const KernelArgs& a, const uint8_
       if (tid == 0) {
         while (__hip_atomic_load(&r->done_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen)
           __builtin_amdgcn_s_sleep(8);
+        // pairs with the head's release of done_: the report's fields below
+        // are read after it
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         L.first = __hip_atomic_load(&r->first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         L.nblocks = __hip_atomic_load(&r->nblocks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         L.ndata = __hip_atomic_load(&r->ndata, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1189,6 +1196,10 @@ __device__ __forceinline__ void spec_crc_group(const KernelArgs& a, const uint8_
       atomicMin(&r->first_bad, L.minbad);
     }
     if (p0 == i0) sst_stamp(st, t, 12);
+    // The staged tail shares its LDS with the window and the CRCs, which
+    // this pass overwrote: later passes read their restart offsets from the
+    // index in memory.
+    tail_ok = false;
   }
 }
 

@@ -237,6 +237,76 @@ def test_device_log_read_dense_blocks(lvkv, gpu):
             assert rd["bytes"] == sum(r[1] for r in o_recs), (trial, off)
 
 
+def _windowed_log(target_items: int, seed: int, window: int = 64 * 256):
+    """Tiny records, plus a 100 KB record (FIRST, MIDDLEs, LAST over four
+    blocks) whose fragments straddle every multiple of `window` ReadRecord
+    items (one item per physical record and one per block, in file order)."""
+    import log_synth
+    rng = np.random.default_rng(seed)
+    w = log_synth.LogWriter()
+    emitted = [0]
+    emit = w.emit
+
+    def counted(rtype, payload):
+        emitted[0] += 1
+        emit(rtype, payload)
+    w.emit = counted
+    nxt = window - 3
+    while emitted[0] + len(w.buf) // 32768 < target_items:
+        if emitted[0] + len(w.buf) // 32768 >= nxt:
+            w.add_record(rng.integers(0, 256, 100_000, dtype=np.uint8).tobytes())
+            nxt += window
+        else:
+            w.add_record(rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8).tobytes())
+    return bytes(w.buf)
+
+
+@pytest.mark.gpu
+def test_device_log_read_scanned_windows(lvkv, gpu):
+    """Over 1,024 ReadRecord workgroups (> 262k items) the emit launch takes
+    its window's prefix from log_asm_scan instead of folding every earlier
+    aggregate: fragmented records across every 64-workgroup
+    window boundary, damage (a flipped byte, a retyped header, a kEof-type
+    header late in the log), and initial offsets inside and between those
+    records, each against the oracle's log::Reader."""
+    import torch
+    import log_synth
+    rng = np.random.default_rng(17)
+    base = _windowed_log(300_000, seed=19)
+    hdrs0 = lw.block_verdicts(base).hdrs
+    assert len(hdrs0) + len(base) // 32768 > 262_144
+    big = [off for off, n, _ in lw.read_records(base)[0] if n == 100_000]  # their FIRSTs
+    assert len(big) >= 17
+    for trial in range(3):
+        img = bytearray(base)
+        if trial >= 1:
+            for _ in range(6):
+                img[int(rng.integers(0, len(img)))] ^= int(rng.integers(1, 256))
+            h = big[5] + 7 + 32768  # inside a MIDDLE
+            img[h] ^= 0x11
+            for h in rng.choice(hdrs0, 8, replace=False):
+                img[int(h) + 6] = int(rng.integers(0, 8))
+                log_synth.fix_header_crc(img, int(h))
+        if trial == 2:
+            h = int(hdrs0[len(hdrs0) - 5000])
+            img[h + 6] = 5
+            log_synth.fix_header_crc(img, h)
+        img = bytes(img)
+        buf = torch.from_numpy(np.frombuffer(img, dtype=np.uint8).copy()).to(gpu)
+        offs = [0, big[3] + 1, big[9] + 40_000, (big[12] // 32768) * 32768 + 32768,
+                int(rng.integers(1, len(img)))]
+        for off in offs:
+            rd, records, reports, phys, gathered = lvkv.log_read(buf, initial_offset=off,
+                                                                 gather=True)
+            hdrs = [int(x) for x in phys[1].cpu().numpy()]
+            o_recs, o_reps, stopped = lw.read_all(img, off)
+            assert rd["status"] == 0, (trial, off)
+            assert _device_log_records(img, records, hdrs, gathered) == o_recs, (trial, off)
+            assert reports == o_reps, (trial, off)
+            assert rd["stopped"] == int(stopped), (trial, off)
+            assert rd["bytes"] == sum(r[1] for r in o_recs), (trial, off)
+
+
 @pytest.mark.gpu
 def test_device_log_gather_large_image_default_capacity(lvkv, gpu):
     """A ~650 MB log (a clean 20k-record, 40 MB log padded to whole 32 KiB blocks

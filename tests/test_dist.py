@@ -149,11 +149,25 @@ def test_bench_gpus2_launches_two_ranks():
     both: n_gpus, the split's ranks and each rank's slice."""
     rc, line, err = _bench(["--gpus", "2", "--plumbing-cpu", "--config", "blocks1m_split",
                             "--split-total", "65", "--steps", "3", "--warmup", "1",
-                            "--warmup-ms", "0"])
+                            "--warmup-ms", "0", "--cpu-seconds", "0.3"])
     assert rc == 0, err[-2000:]
     assert line["n_gpus"] == 2
     assert line["split"]["ranks"] == 2 and line["split"]["total_blocks"] == 65
     assert line["rank_counts"] == [33, 32]
+    # the N > 1 line (VERDICT r4): the config's own metric, every rank's slice
+    # and parity count, per-rank records, and rank 0's CPU baseline
+    import sys
+    sys.path.insert(0, str(REPO))
+    import bench
+    assert line["metric"] == bench.METRICS["blocks1m_split"] != bench.METRIC
+    assert line["split"]["slices"] == [
+        {"rank": 0, "start": 0, "blocks": 33, "parity_blocks": 33},
+        {"rank": 1, "start": 33, "blocks": 32, "parity_blocks": 32}]
+    assert [r["rank"] for r in line["roofline"]["per_rank"]] == [0, 1]
+    assert line["config"]["parity_blocks"] == 65
+    cb = line["cpu_baseline"]
+    assert cb["kind"] in ("reference", "port") and cb["cores"] == 1 and cb["value"] > 0
+    assert cb["multi_thread"]["cores"] >= 1
 
 
 def test_bench_refuses_world_mismatch():

@@ -225,6 +225,35 @@ def test_engine_1m_blocks_overlapped_and_ordered(lvkv, oracle, eng, gpu):
         assert c >= b - 1e-3, "dispatches of one ordered batch overlapped"
 
 
+def test_engine_config3_wal_blocks_at_surveyed_size(lvkv, oracle, eng, gpu):
+    """Config 3 at its surveyed size: 16,384 log blocks of
+    32 KiB (512 MiB, beyond the 256 MiB Infinity Cache), each CRC over bytes
+    [6, 32768) -- type + 32761-byte payload, what log::Reader checks
+    (db/log_reader.cc:243-247; kBlockSize / kHeaderSize, db/log_format.h:27,30)
+    -- built as `bench.py --config wal32k` builds them (make_buffers, base + 6,
+    stride 32768) and submitted through lvkv_engine_crc32c_uniform, overlapped
+    and then LVKV_FLAG_ORDERED; every CRC against the oracle."""
+    import torch
+
+    import bench
+    nb, L, stride, crc_off, _ = bench.CONFIGS["wal32k"]
+    assert (nb, L, stride, crc_off) == (16_384, 32762, 32768, 6)
+    buf, nrot, window = bench.make_buffers(torch, gpu, 0, nb, stride, 0)
+    assert nrot == 1 and window == 512 << 20
+    torch.cuda.synchronize()
+    host = buf.cpu().numpy()
+    want = oracle.uniform(host[crc_off:], nb, L, stride, threads=_oracle_threads())
+    del host
+    over = eng.crc32c_uniform(buf[crc_off:], nb, L, stride, fresh=False)
+    eng.wait()
+    assert np.array_equal(over.cpu().numpy().view(np.uint32), want)
+    ordered = eng.crc32c_uniform(buf[crc_off:], nb, L, stride, fresh=False, ordered=True,
+                                 mask=True)
+    eng.wait()
+    want_masked = np.array([oracle.mask(int(c)) for c in want], dtype=np.uint32)
+    assert np.array_equal(ordered.cpu().numpy().view(np.uint32), want_masked)
+
+
 def test_engine_config5_slice_as_bench_builds_it(lvkv, oracle, eng, gpu):
     """Config 5: rank 3 of 8's slice of the 1M-block batch (125,000 blocks
     at a non-zero start), built by bench.py's own _split_runner (which checks

@@ -374,3 +374,37 @@ def test_device_multi_table_verify(lvkv, gpu, sst_form):
     k = stats.index(st.SST_CAPACITY)
     assert all(s_ in (st.SST_CAPACITY, st.SST_BAD_MAGIC) for s_ in stats[k:])
     assert res[2][0]["nbad"] == 1 and res[3][0]["status"] == st.SST_BAD_MAGIC
+
+
+@pytest.mark.gpu
+def test_device_table_shares_over_one_pass(lvkv, gpu, sst_form):
+    # 150k tiny blocks: the speculative form's CRC workgroups (2 x CUs - 1 for
+    # one table) each own ~290 index entries, more than one pass of 256, and
+    # the shares at the index's end took their restart offsets from the
+    # staged tail on the first pass (later passes must not read it
+    # back after the window overwrote it). One table, then three in one call,
+    # each with a damaged block in the last entries.
+    import torch
+    img = bytearray(sst_synth.build_sst(150_000, 16, seed=5, ragged=False))
+    r0 = st.verify_table(bytes(img))
+    for e in (149_999, 149_800, 149_300):
+        o, n = r0.handles[e]
+        img[o + 3] ^= 0x40
+    img = bytes(img)
+    rep, _ = _assert_matches_oracle(lvkv, img, gpu)
+    assert rep["ndata"] == 150_000 and rep["nbad"] == 3 and rep["first_bad"] == 149_300
+    imgs = [img, sst_synth.build_sst(120_000, 24, seed=6, ragged=False), img]
+    offs, pos = [], 0
+    for im in imgs:
+        offs.append(pos)
+        pos += len(im) + 5
+    buf = bytearray(pos)
+    for o_, im in zip(offs, imgs):
+        buf[o_: o_ + len(im)] = im
+    dbuf = torch.from_numpy(np.frombuffer(bytes(buf), dtype=np.uint8).copy()).to(gpu)
+    res = lvkv.sst_verify_tables(dbuf, offs, [len(im) for im in imgs], capacity=430_000)
+    torch.cuda.synchronize()
+    for o_, im, (rep, off, size, actual, status) in zip(offs, imgs, res):
+        got = (rep, off.cpu().numpy(), size.cpu().numpy().view(np.uint32),
+               actual.cpu().numpy().view(np.uint32), status.cpu().numpy())
+        _assert_matches_oracle(lvkv, im, gpu, got=got, base=o_)

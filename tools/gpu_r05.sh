@@ -1,14 +1,20 @@
 #!/bin/bash
-# Round-4 evidence on one GPU: every GPU test, smoke, the driver's bench
-# command and the default bench, kernel traces (isolated headline launches,
-# the SST forms, the engine's general shapes, the WAL read path), the edges
-# probe. Every GPU step has its own time limit; the first failure ends it.
-#   bash tools/gpu_r04_prof.sh [tests|bench|prof|shapes]...
+# Round-5 evidence on one GPU. Every GPU step has its own time limit; the
+# first failure ends the script.
+#   bash tools/gpu_r05.sh [tests|bench|prof|logpmc|shapes|sst|edges]...
+#   tests   every -m gpu test, then smoke()
+#   bench   the driver's command (K = 20) and the default (K = 200) lines
+#   prof    rocprofv3 kernel trace of isolated headline launches and of the
+#           WAL read path
+#   logpmc  PMC passes over the WAL verify (one counter group per run)
+#   shapes  the engine's general shapes (tools/probe/engine_shapes.py)
+#   sst     kernel traces of the SST forms
+#   edges   the K = 20 region's edges (tools/probe/edges.py)
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-/root/repo} && mkdir -p gpurun_out && export TMPDIR=/tmp
-steps=${*:-tests bench prof shapes}
+steps=${*:-tests bench}
 want() { [[ " $steps " == *" $1 "* ]]; }
-O=gpurun_out/r04
+O=gpurun_out/r05
 mkdir -p $O
 stats() {  # kernel stats of a rocprofv3 csv output dir, short names
   python3 -c "
@@ -20,7 +26,7 @@ for f in glob.glob(sys.argv[1] + '/**/*kernel_stats.csv', recursive=True):
 " $1
 }
 if want tests; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 \
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread > $O/pytest_gpu.log 2>&1 \
     || { echo "gpu tests failed"; tail -40 $O/pytest_gpu.log; exit 1; }
   tail -2 $O/pytest_gpu.log
   timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 \
@@ -34,6 +40,8 @@ if want bench; then
   timeout -k 10 400 python bench.py > $O/bench_default.json 2> $O/bench_default.err \
     || { echo "bench failed"; tail -20 $O/bench_default.err; exit 1; }
   cat $O/bench_default.json
+fi
+if want edges; then
   timeout -k 10 200 python tools/probe/edges.py > $O/edges.log 2>&1 || { tail -20 $O/edges.log; exit 1; }
   cp gpurun_out/edges.json $O/edges.json
   grep -v amdgpu.ids $O/edges.log | tail -12
@@ -43,19 +51,33 @@ if want prof; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 bench.py --isolated 200 --no-cpu-baseline --no-split --no-pmc > $D.log 2>&1 \
     || { echo "iso prof failed"; tail -20 $D.log; exit 1; }
   stats $D
+  D=$O/logread_prof; rm -rf $D
+  timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 tools/probe/log_probe.py 60000 --read > $D.log 2>&1 \
+    || { echo "log prof failed"; tail -20 $D.log; exit 1; }
+  grep "us/call" $D.log; stats $D
+fi
+if want logpmc; then
+  i=0
+  for grp in "FETCH_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+             "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_ACTIVE_INST_VALU" \
+             "SQ_INSTS_VMEM SQ_ACTIVE_INST_VMEM SQ_INSTS_SALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE"; do
+    i=$((i+1)); D=$O/logpmc/p$i; rm -rf $D
+    timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d $D -o run -- python3 tools/probe/log_probe.py 60000 > $D.log 2>&1 \
+      || { echo "log pmc pass $i failed"; tail -5 $D.log; exit 1; }
+  done
+  python3 tools/pmc_table.py $O/logpmc > $O/logpmc.txt 2>&1 || true
+  cat $O/logpmc.txt | head -40
+fi
+if want shapes; then
+  timeout -k 10 400 python tools/probe/engine_shapes.py > $O/engine_shapes.log 2>&1 || { echo shapes failed; tail -20 $O/engine_shapes.log; exit 1; }
+  cp gpurun_out/engine_shapes.json $O/engine_shapes.json 2>/dev/null
+  grep -v amdgpu.ids $O/engine_shapes.log | tail -40
+fi
+if want sst; then
   for A in "512 --form=3" "512 --form=3 --tables=32" "512 --form=2 --tables=32" "16384 --form=0"; do
     N=$(echo "$A" | tr -d ' =-' ); D=$O/sst_$N; rm -rf $D
     timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 tools/probe/sst_probe.py $A > $D.log 2>&1 \
       || { echo "sst prof failed"; tail -20 $D.log; exit 1; }
     grep "us/call" $D.log; stats $D
   done
-  D=$O/logread_prof; rm -rf $D
-  timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 tools/probe/log_probe.py 60000 --read > $D.log 2>&1 \
-    || { echo "log prof failed"; tail -20 $D.log; exit 1; }
-  grep "us/call" $D.log; stats $D
-fi
-if want shapes; then
-  timeout -k 10 400 python tools/probe/engine_shapes.py > $O/engine_shapes.log 2>&1 || { echo shapes failed; tail -20 $O/engine_shapes.log; exit 1; }
-  cp gpurun_out/engine_shapes.json $O/engine_shapes.json 2>/dev/null
-  grep -v amdgpu.ids $O/engine_shapes.log | tail -40
 fi

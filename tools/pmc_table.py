@@ -1,4 +1,5 @@
-"""Per-kernel mean of every PMC counter found under a gpu_pmc_probe.sh output dir."""
+"""Per-kernel mean of every PMC counter found under an output dir of PMC passes
+(p1/, p2/, ...: tools/pmc.sh, tools/gpu_r05.sh logpmc)."""
 import collections, csv, glob, sys
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(sys.argv[1] + '/p*/run_counter_collection.csv')):
@@ -6,7 +7,7 @@ for f in sorted(glob.glob(sys.argv[1] + '/p*/run_counter_collection.csv')):
         k = r['Kernel_Name']
         if 'lvkv::' not in k:
             continue
-        k = k.split('lvkv::')[1].split('(')[0]
+        k = k.replace('(anonymous namespace)::', '').split('lvkv::')[1].split('(')[0]
         agg[k][r['Counter_Name']].append(float(r['Counter_Value']))
 for k in sorted(agg):
     d = {c: sum(v) / len(v) for c, v in agg[k].items()}
