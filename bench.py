@@ -399,6 +399,9 @@ def main():
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the rocprofv3 FETCH_SIZE pass behind roofline.traffic")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--ceiling-trace", type=int, default=0,
+                    help="only run K launches of the production and read-ceiling kernels "
+                         "(the command a rocprofv3 kernel trace of the ceiling wraps)")
     ap.add_argument("--no-ceiling", action="store_true",
                     help="skip the read-only ceiling kernels behind roofline.ceiling")
     ap.add_argument("--isolated", type=int, default=0,
@@ -470,6 +473,9 @@ def main():
         for k in range(args.isolated):
             runner.step(1 + k)
         eng.wait()
+        return
+    if args.ceiling_trace:
+        _ceiling_trace(torch, lvkv, eng, runner, dev, rank, args.ceiling_trace)
         return
 
     elapsed, nxt = timed_region(runner, comm, args.steps, args.warmup, warm_s, first=1)
@@ -562,6 +568,36 @@ def main():
 
 
 CEILING_CO = REPO / "tools" / "probe" / "ceiling_kernels.co"
+
+
+def _ceiling_trace(torch, lvkv, eng, runner, dev, rank, k):
+    """The command a rocprofv3 kernel trace of the read ceiling wraps
+    (--ceiling-trace K): the production kernel, then ck_burst_bare and
+    ck_stream, K overlapped launches each over the headline rotation (after
+    a warm-up of 2K), then ck_burst_bare over the 4 GB config-5 buffer (1M
+    blocks a step, K // 10 + 1 steps). Each dispatch's start/end is in the
+    trace; tools/trace_period.py reads the period per kernel."""
+    co = CEILING_CO.read_bytes()
+    i = 1
+    for kern in (None, "ck_burst_bare", "ck_stream"):
+        if kern is not None:
+            eng.load_probe(co, kern, 8, 5, 1, overlapped=True)
+        for _ in range(2 * k):
+            runner.step(i)
+            i += 1
+        eng.wait()
+        for n in range(k):
+            runner.step(i, final=n >= k - 3)
+            i += 1
+        eng.wait()
+    del runner
+    torch.cuda.empty_cache()
+    r = _split_runner(torch, lvkv, eng, dev, rank, 0, SPLIT_TOTAL)
+    eng.load_probe(co, "ck_burst_bare", 8, 5, 1, overlapped=True)
+    for n in range(k // 10 + 1):
+        r.step(n)
+    eng.wait()
+    eng.load_probe(None)
 
 
 def measure_ceiling(torch, eng, runner, comm, steps, warmup, warm_s, first, algo_bytes, roof):

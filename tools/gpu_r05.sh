@@ -9,6 +9,7 @@
 #   logpmc  PMC passes over the WAL verify (one counter group per run)
 #   shapes  the engine's general shapes (tools/probe/engine_shapes.py)
 #   sst     kernel traces of the SST forms
+#   ceiling kernel trace of the production and read-ceiling kernels, overlapped
 #   edges   the K = 20 region's edges (tools/probe/edges.py)
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-/root/repo} && mkdir -p gpurun_out && export TMPDIR=/tmp
@@ -41,8 +42,15 @@ if want bench; then
     || { echo "bench failed"; tail -20 $O/bench_default.err; exit 1; }
   cat $O/bench_default.json
 fi
+if want ceiling; then
+  D=$O/ceiling_prof; rm -rf $D
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 bench.py --ceiling-trace 200 --no-cpu-baseline --no-split --no-pmc > $D.log 2>&1 \
+    || { echo "ceiling prof failed"; tail -20 $D.log; exit 1; }
+  stats $D
+  python3 tools/trace_period.py $D > $O/ceiling_periods.json && cat $O/ceiling_periods.json | head -80
+fi
 if want edges; then
-  timeout -k 10 200 python tools/probe/edges.py > $O/edges.log 2>&1 || { tail -20 $O/edges.log; exit 1; }
+  timeout -k 10 300 python tools/probe/edges.py --scopes=1,0,2 --scopes=0,0,2 --scopes=2,2,2 > $O/edges.log 2>&1 || { tail -20 $O/edges.log; exit 1; }
   cp gpurun_out/edges.json $O/edges.json
   grep -v amdgpu.ids $O/edges.log | tail -12
 fi
