@@ -76,6 +76,18 @@ if want logpmc; then
   python3 tools/pmc_table.py $O/logpmc > $O/logpmc.txt 2>&1 || true
   cat $O/logpmc.txt | head -40
 fi
+if want smallpmc; then
+  i=0
+  for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+             "SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
+             "FETCH_SIZE GRBM_GUI_ACTIVE"; do
+    i=$((i+1)); D=$O/smallpmc/p$i; rm -rf $D
+    timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d $D -o run -- python3 tools/probe/engine_shapes.py --cases rand2000_62k --specs 3,2 --reps 4 > $D.log 2>&1 \
+      || { echo "small pmc pass $i failed"; tail -5 $D.log; exit 1; }
+  done
+  python3 tools/pmc_table.py $O/smallpmc > $O/smallpmc.txt 2>&1 || true
+  cat $O/smallpmc.txt | head -40
+fi
 if want shapes; then
   timeout -k 10 400 python tools/probe/engine_shapes.py > $O/engine_shapes.log 2>&1 || { echo shapes failed; tail -20 $O/engine_shapes.log; exit 1; }
   cp gpurun_out/engine_shapes.json $O/engine_shapes.json 2>/dev/null

@@ -5,9 +5,13 @@ agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(sys.argv[1] + '/p*/run_counter_collection.csv')):
     for r in csv.DictReader(open(f)):
         k = r['Kernel_Name']
-        if 'lvkv::' not in k:
+        k = k.replace('(anonymous namespace)::', '')
+        if 'lvkv::' in k:
+            k = k.split('lvkv::')[1].split('(')[0]
+        elif k.startswith(('lvkv_', 'ck_', 'pk_')):
+            k = k.split('(')[0]
+        else:
             continue
-        k = k.replace('(anonymous namespace)::', '').split('lvkv::')[1].split('(')[0]
         agg[k][r['Counter_Name']].append(float(r['Counter_Value']))
 for k in sorted(agg):
     d = {c: sum(v) / len(v) for c, v in agg[k].items()}
