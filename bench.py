@@ -590,6 +590,7 @@ def _ceiling_trace(torch, lvkv, eng, runner, dev, rank, k):
             runner.step(i, final=n >= k - 3)
             i += 1
         eng.wait()
+    eng.load_probe(None)  # the split runner checks its first step against the oracle
     del runner
     torch.cuda.empty_cache()
     r = _split_runner(torch, lvkv, eng, dev, rank, 0, SPLIT_TOTAL)
