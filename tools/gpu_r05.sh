@@ -51,6 +51,14 @@ if want ceiling; then
 fi
 if want edges; then
   timeout -k 10 300 python tools/probe/edges.py --scopes=1,0,2 --scopes=0,0,2 --scopes=2,2,2 > $O/edges.log 2>&1 || { tail -20 $O/edges.log; exit 1; }
+fi
+if want edgesdev; then  # AQL rings in device memory (ROCr HSA_ALLOCATE_QUEUE_DEV_MEM)
+  HSA_ALLOCATE_QUEUE_DEV_MEM=1 timeout -k 10 300 python tools/probe/edges.py --scopes=1,0,2 > $O/edgesdev.log 2>&1 || { tail -20 $O/edgesdev.log; exit 1; }
+  grep -v amdgpu.ids $O/edgesdev.log | tail -12
+  HSA_ALLOCATE_QUEUE_DEV_MEM=1 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-pmc --no-cpu-baseline > $O/bench_k20_devq.json 2> $O/bench_k20_devq.err || { tail -20 $O/bench_k20_devq.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/bench_k20_devq.json')); print('devq k20', d['pct_hbm_peak'], d['roofline']['kernel_us_avg'], d['roofline']['pipelined']['period_us'])"
+fi
+if want edges; then
   cp gpurun_out/edges.json $O/edges.json
   grep -v amdgpu.ids $O/edges.log | tail -12
 fi
@@ -65,7 +73,7 @@ if want prof; then
   grep "us/call" $D.log; stats $D
 fi
 if want logpmc; then
-  i=0
+  i=0; mkdir -p $O/logpmc
   for grp in "FETCH_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
              "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_ACTIVE_INST_VALU" \
              "SQ_INSTS_VMEM SQ_ACTIVE_INST_VMEM SQ_INSTS_SALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE"; do
@@ -77,7 +85,7 @@ if want logpmc; then
   cat $O/logpmc.txt | head -40
 fi
 if want smallpmc; then
-  i=0
+  i=0; mkdir -p $O/smallpmc
   for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
              "SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
              "FETCH_SIZE GRBM_GUI_ACTIVE"; do
