@@ -85,13 +85,13 @@ __device__ __forceinline__ uint32_t lane_end_shift_c(const uint32_t* lds, uint32
 // 16-byte slots q -> row b = q >> 3, table t = (q >> 1) & 3, copies 4h..4h+3
 // with h = q & 1. Loaded in load(), written in store() (the caller issues
 // other loads in between).
-template <int kThreads>
+template <int kThreads, int J = 8>
 struct RowTabStage {
   static constexpr int kIters = 2048 / kThreads;
   uint32_t v[kIters];
 
   __device__ __forceinline__ void load(const uint32_t* zpow, uint32_t tid) {
-    const uint32_t* z256 = zpow + 8u * 1024u;
+    const uint32_t* z256 = zpow + static_cast<uint32_t>(J) * 1024u;  // Z_{2^J}
 #pragma unroll
     for (int it = 0; it < kIters; ++it) {
       const uint32_t q = tid + static_cast<uint32_t>(kThreads * it);
@@ -153,6 +153,23 @@ __device__ __forceinline__ void build_compact_image(uint32_t* lds, const uint32_
   LaneTabGen<W> lg;
   rt.load(zpow, tid);
   lg.load(lane_cols, wave, lane);
+  rt.store(lds, tid);
+  lg.store(lds, wave, lane);
+  __syncthreads();
+}
+
+// The grouped walk's image (crc32c_group_body.h): the same layout with rows
+// of 64 bytes (16 lanes x 4 B per record) -- row tables Z_64 (zpow set 6),
+// lane s's nibble tables Z_{64-4(s%16)} generated from grp_cols (the
+// lane_cols layout). Ends with a barrier.
+template <int W>
+__device__ __forceinline__ void build_group_image(uint32_t* lds, const uint32_t* zpow,
+                                                  const uint32_t* grp_cols, uint32_t tid,
+                                                  uint32_t wave, uint32_t lane) {
+  RowTabStage<64 * W, 6> rt;
+  LaneTabGen<W> lg;
+  rt.load(zpow, tid);
+  lg.load(grp_cols, wave, lane);
   rt.store(lds, tid);
   lg.store(lds, wave, lane);
   __syncthreads();

@@ -156,12 +156,13 @@ void init_ctx(DeviceCtx& c, int dev) {
     return;
   }
   static_assert(kZPowOffset == kRowTabDwords + kLaneTabDwords + kLaneColDwords, "layout");
-  std::vector<uint32_t> tab(kZPowOffset + kZPowDwords + kZMulDwords);
+  std::vector<uint32_t> tab(kTableDwords);
   build_row_table(tab.data());
   build_lane_table(tab.data() + kRowTabDwords);
   build_lane_columns(tab.data() + kRowTabDwords + kLaneTabDwords);
   build_zpow_tables(tab.data() + kZPowOffset);
   build_zmul_columns(tab.data() + kZPowOffset + kZPowDwords);
+  build_group_lane_columns(tab.data() + kGrpColOffset);
   void* p = nullptr;
   e = hipMalloc(&p, tab.size() * sizeof(uint32_t));
   if (e != hipSuccess) {

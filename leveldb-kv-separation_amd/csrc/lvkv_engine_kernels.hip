@@ -11,6 +11,7 @@
 #include <stdint.h>
 
 #include "crc32c_burst.h"
+#include "crc32c_group_body.h"
 #include "crc32c_ragged_body.h"
 #include "lvkv_kernel_args.h"
 
@@ -86,4 +87,29 @@ extern "C" __global__ void __launch_bounds__(512, 2)
   __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::RagLds<8>::kDwords];
   lvkv::ragged_run<8, 6, 8>(a.k, a.zpow, a.lane_cols, lds, blockIdx.x, a.ngroups, a.k.nblocks,
                             false);
+}
+
+// Short records (WAL records, small values; LVKV_FLAG_SMALL_BLOCKS, uniform
+// blocks of <= 8 rows): four records per wave at once, one per 16-lane row
+// (crc32c_group_body.h), 8 waves x 4 chains x 16 rows of 64 bytes, two
+// workgroups per CU; records over 2 KiB, under 4 bytes or far apart go to the
+// 64-lane walk at the end of the segment. Variants (A/B timing through
+// lvkv_debug_engine_ragged_spec): 4 chains x 8 rows, 2 chains x 16 rows.
+extern "C" __global__ void __launch_bounds__(512, 2)
+    lvkv_ek_group(lvkv::EngineRaggedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::GrpLds<8>::kDwords];
+  lvkv::group_run<8, 4, 16>(a.k, a.zpow, a.lane_cols, a.grp_cols, lds, blockIdx.x, a.ngroups,
+                            a.k.nblocks);
+}
+extern "C" __global__ void __launch_bounds__(512, 2)
+    lvkv_ek_group_r8(lvkv::EngineRaggedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::GrpLds<8>::kDwords];
+  lvkv::group_run<8, 4, 8>(a.k, a.zpow, a.lane_cols, a.grp_cols, lds, blockIdx.x, a.ngroups,
+                           a.k.nblocks);
+}
+extern "C" __global__ void __launch_bounds__(512, 2)
+    lvkv_ek_group_c2(lvkv::EngineRaggedArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::GrpLds<8>::kDwords];
+  lvkv::group_run<8, 2, 16>(a.k, a.zpow, a.lane_cols, a.grp_cols, lds, blockIdx.x, a.ngroups,
+                            a.k.nblocks);
 }

@@ -159,13 +159,14 @@ def test_engine_general_many_in_flight(oracle, eng, gpu):
         assert np.array_equal(got[k], want[k % 8]), k
 
 
-@pytest.mark.parametrize("spec", [2, 3, 4, 5])
+@pytest.mark.parametrize("spec", [2, 3, 4, 5, 6, 7, 8])
 def test_engine_every_general_kernel(lvkv, oracle, eng, gpu, spec):
     """Each of the engine's general-layout kernels forced in turn
     (lvkv_debug_engine_ragged_spec): persistent and one-round burst walks of
-    both shapes, on blocks of every start alignment and
-    lengths 0..12,000 (some over the lane walk's 4 KiB and over 64 KiB), with
-    per-block inits; compute, masked compute, SST verify and WAL verify."""
+    both shapes and the grouped walks (6-8: four records a wave), on blocks
+    of every start alignment and lengths 0..12,000 (some over the lane walk's
+    4 KiB and over 64 KiB), with per-block inits; compute, masked compute,
+    SST verify, and a synthetic WAL's verify and header refill."""
     import ctypes
 
     import torch
@@ -204,5 +205,33 @@ def test_engine_every_general_kernel(lvkv, oracle, eng, gpu, spec):
                                  _dev(torch, ss.view(np.int32), gpu))
         eng.wait()
         assert sorted(np.nonzero(st.cpu().numpy())[0].tolist()) == sorted(bad.tolist())
+        # WAL records (log_reader.cc:243-247, log_writer.cc:94-96): every
+        # fragment kind, records of 0..2999 bytes and 100 KB ones, a few
+        # payload bytes flipped; verify, then refill the wiped header CRCs
+        import log_synth
+        import log_walk as lw
+        img = np.frombuffer(log_synth.build_log(3000, seed=spec, max_len=3000, big_every=211),
+                            np.uint8).copy()
+        hdrs = np.array(lw.block_verdicts(bytes(img)).hdrs, np.int64)
+        lens = np.array([1 + int(img[h + 4]) + 256 * int(img[h + 5]) for h in hdrs], np.uint32)
+        want = oracle.batch(img, (hdrs + 6).astype(np.uint64), lens, threads=8)
+        flip = rng.choice(len(hdrs), 25, replace=False)
+        badimg = img.copy()
+        for i in flip:
+            badimg[int(hdrs[i]) + 6 + int(lens[i]) // 2] ^= 0x08
+        dh = _dev(torch, hdrs, gpu)
+        act, st = eng.log_verify(_dev(torch, img, gpu), dh)
+        act2, st2 = eng.log_verify(_dev(torch, badimg, gpu), dh)
+        eng.wait()
+        assert np.array_equal(_u32(act), want)
+        assert not st.any().item()
+        assert sorted(np.nonzero(st2.cpu().numpy())[0].tolist()) == sorted(flip.tolist())
+        wiped = img.copy()
+        for h in hdrs:
+            wiped[int(h): int(h) + 4] = 0
+        wb = _dev(torch, wiped, gpu)
+        eng.log_fill_headers(wb, dh)
+        eng.wait()
+        assert np.array_equal(wb.cpu().numpy(), img)
     finally:
         lvkv.lib.lvkv_debug_engine_ragged_spec(eng.handle, -1)

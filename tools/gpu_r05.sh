@@ -96,6 +96,13 @@ if want smallpmc; then
   python3 tools/pmc_table.py $O/smallpmc > $O/smallpmc.txt 2>&1 || true
   cat $O/smallpmc.txt | head -40
 fi
+if want group; then  # the grouped small-record walk: parity, then timing by spec
+  timeout -k 10 400 python -u -m pytest tests/test_engine_general.py -x -v --timeout 150 --timeout-method thread -k "every_general or golden" > $O/group_tests.log 2>&1 \
+    || { echo "group tests failed"; tail -60 $O/group_tests.log; exit 1; }
+  tail -3 $O/group_tests.log
+  timeout -k 10 300 python tools/probe/engine_shapes.py --cases rand2000_62k,sst4106_16k --specs 3,6,7,8 --reps 20 > $O/group_shapes.log 2>&1 || { echo shapes failed; tail -20 $O/group_shapes.log; exit 1; }
+  grep -v amdgpu.ids $O/group_shapes.log | tail -12
+fi
 if want shapes; then
   timeout -k 10 400 python tools/probe/engine_shapes.py > $O/engine_shapes.log 2>&1 || { echo shapes failed; tail -20 $O/engine_shapes.log; exit 1; }
   cp gpurun_out/engine_shapes.json $O/engine_shapes.json 2>/dev/null
