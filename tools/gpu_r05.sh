@@ -90,7 +90,7 @@ if want smallpmc; then
              "SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
              "FETCH_SIZE GRBM_GUI_ACTIVE"; do
     i=$((i+1)); D=$O/smallpmc/p$i; rm -rf $D
-    timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d $D -o run -- python3 tools/probe/engine_shapes.py --cases rand2000_62k --specs 3,2 --reps 4 > $D.log 2>&1 \
+    timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d $D -o run -- python3 tools/probe/engine_shapes.py --cases rand2000_62k --specs ${SMALL_SPECS:-3,2} --reps 4 > $D.log 2>&1 \
       || { echo "small pmc pass $i failed"; tail -5 $D.log; exit 1; }
   done
   python3 tools/pmc_table.py $O/smallpmc > $O/smallpmc.txt 2>&1 || true
