@@ -32,6 +32,8 @@ CASES = {
     "sst4271_16k": (16384, 4271, 4272, 0, False),     # SST-sized, ends unaligned
     "sst4106_16k": (16384, 4106, 4106, 3, False),     # 4105 B + type byte, any alignment
     "rand2000_62k": (62000, 2000, 0, 7, False),       # WAL-record-sized, packed (LVKV_FLAG_SMALL_BLOCKS)
+    "eq1000_62k": (62000, -1000, 0, 7, False),        # packed, every record 1000 B
+    "eq200_300k": (300000, -200, 0, 7, False),        # packed, every record 200 B
     "wal32k_16k": (16384, 32762, 32768, 6, True),     # config 3 (512 MiB)
     "wal32k_2k": (2048, 32762, 32768, 6, True),
     "u4096_65k": (65536, 4096, 4096, 0, False),
@@ -60,7 +62,8 @@ def main():
             offs = (np.arange(n, dtype=np.uint64) * stride + first).astype(np.uint64)
             size = int(offs[-1]) + length + 8
         else:
-            lens = rng.integers(0, length, n).astype(np.uint32)
+            lens = (np.full(n, -length, np.uint32) if length < 0 else
+                    rng.integers(0, length, n).astype(np.uint32))
             offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
             size = int(offs[-1]) + int(lens[-1]) + 8
         host = rng.integers(0, 256, size, dtype=np.uint8)
@@ -77,7 +80,7 @@ def main():
             else:
                 # (the small-record case passes the caller's hint)
                 eng.crc32c_batch(buf, d_off, d_len, ordered=ordered, fresh=False, out=out,
-                                 small=name.startswith("rand"))
+                                 small=name.startswith(("rand", "eq")))
         want = (oracle.uniform(host[first:], n, length, stride, threads=16) if uniform else
                 oracle.batch(host, offs, lens, threads=16))
         algo = int(lens.sum()) + 4 * n
