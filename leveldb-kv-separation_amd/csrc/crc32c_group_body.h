@@ -18,18 +18,15 @@
 //
 // Descriptors are loaded by one lane per record, lane 16 g + c for chain c
 // of the wave's round (vector loads, the dependent header / trailer loads a
-// round later), and reach the group's lanes by DPP row_newbcast:c. Each
-// chain's rows come from one buffer resource spanning its four records
-// ([min start, max end), so a row past a record's end reads other bytes of
-// the batch or zeros, never memory outside it; the state is frozen there);
-// row 0's lanes before a record read through an offset past the window
-// (zeros, no access).
-//
-// Records of more than kGrpSplit covered bytes, of fewer than 4, and the
-// records of a chain whose span exceeds a buffer window go to a list in LDS
-// and are walked after the segment by the 64-lane walk (ragged_run over the
-// list, the LDS image rebuilt as Z_256), which also takes blocks over
-// long_split to the whole workgroup.
+// round ahead), sorted by length so a chain's four records are alike, and
+// reach the group's lanes by DPP row_newbcast:c. A chunk's rows come through
+// one buffer resource per chain whose window is the chain's records cut to
+// the chunk's rows, so a row past a record's end reads other bytes of the
+// batch or zeros, never memory outside it (the state is frozen there); row
+// 0's lanes before a record read through an offset past the window (zeros,
+// no access). Records of any length are walked this way; records under 4
+// bytes bit by bit in their desc lanes; chains whose records lie more than a
+// buffer window apart walk one group per pass.
 //
 // Reference: util/crc32c.cc:276-377 (Extend), util/crc32c.h:20-38;
 // db/log_reader.cc:243-247 and table/format.cc:92-99 (the verify modes),
@@ -50,20 +47,10 @@ namespace lvkv {
 namespace {
 
 constexpr uint32_t kGrpRowBytes = 64;     // one group row: 16 lanes x 4 B
-constexpr uint32_t kGrpSplit = 2048;      // covered bytes walked in groups at most
 constexpr uint32_t kGrpBad = 0x80000000u; // a buffer offset past every window
 constexpr uint32_t kGrpSpanMax = 0x7fff0000u;  // a chain's window, bytes
-constexpr uint32_t kGrpDefCap = 1024;     // records per segment (the list's capacity)
 
-enum : uint32_t { kGrpNone = 0, kGrpRows = 1, kGrpDefer = 2 };
-
-// LDS of a W-wave grouped workgroup: RagLds<W> (the image and the 64-lane
-// walk's words), then the deferred list and its count.
-template <int W>
-struct GrpLds {
-  static constexpr uint32_t kDefCount = RagLds<W>::kDwords, kDefList = kDefCount + 1,
-                            kDwords = kDefList + kGrpDefCap;
-};
+enum : uint32_t { kGrpNone = 0, kGrpRows = 1, kGrpTiny = 2 };
 
 template <int C>
 __device__ __forceinline__ uint32_t row_bcast(uint32_t v) {  // row_newbcast:C
@@ -167,7 +154,7 @@ __device__ __forceinline__ uint32_t grp_le32(const GrpHdr& h, uint32_t sh, int w
 }
 
 __device__ __forceinline__ GrpRec grp_record(const KernelArgs& a, const GrpRaw& r, const GrpHdr& h,
-                                             bool live, uint32_t idx, uint32_t split) {
+                                             bool live, uint32_t idx) {
   GrpRec g;
   uint64_t ptr = reinterpret_cast<uint64_t>(a.base) +
                  ((static_cast<uint64_t>(r.off_hi) << 32) | r.off_lo);
@@ -192,7 +179,7 @@ __device__ __forceinline__ GrpRec grp_record(const KernelArgs& a, const GrpRaw& 
   g.s0 = init ^ 0xffffffffu;
   g.expected = expected;
   g.idx = idx;
-  g.kind = !live ? kGrpNone : (len < 4u || len > split) ? kGrpDefer : kGrpRows;
+  g.kind = !live ? kGrpNone : len < 4u ? kGrpTiny : kGrpRows;
   return g;
 }
 
@@ -213,27 +200,6 @@ __device__ __forceinline__ void grp_store(const KernelArgs& a, const GrpRec& g, 
     if (a.out_status != nullptr) a.out_status[b] = crc != g.expected ? 1 : 0;
   }
 }
-
-// The deferred records as a walk source for ragged_run (the list in LDS).
-struct GrpListSrc {
-  const uint32_t* list;
-  __device__ __forceinline__ uint32_t at(uint32_t i) const {
-    return __builtin_amdgcn_readfirstlane(list[i]);
-  }
-  __device__ __forceinline__ bool trailer(const KernelArgs& a) const {
-    return ArgsSrc().trailer(a);
-  }
-  __device__ __forceinline__ RagBlock block(const KernelArgs& a, uint32_t i, bool live) const {
-    return ArgsSrc().block(a, live ? at(i) : 0u, live);
-  }
-  __device__ __forceinline__ void store(const KernelArgs& a, uint32_t i, const RagBlock& g,
-                                        uint32_t crc) const {
-    rag_store(a, at(i), g, crc);
-  }
-  __device__ __forceinline__ uint32_t covered(const KernelArgs& a, uint32_t i) const {
-    return ArgsSrc().covered(a, list[i]);
-  }
-};
 
 // The wave-round's records sorted by covered length before they are dealt
 // to the chains: chain c takes ranks 4c .. 4c + 3, so the four records of a
@@ -271,16 +237,20 @@ __device__ __forceinline__ GrpRec grp_sort(const GrpRec& rec, uint32_t lane, boo
 
 // One chain of one wave-round as its lanes see it: their group's record.
 struct GrpChain {
-  uint32_t rows;   // the group's rows (0: nothing to walk)
-  uint32_t s0l;    // front padding words
-  uint32_t delta;  // front padding bytes of the first word
-  uint32_t e;      // end misalignment (grid word = alignbyte(next dword, own, e))
+  uint32_t rows;   // the group's rows (0: not walked in this pass)
+  uint32_t fix;    // s0l | delta << 8 | e << 12 (front padding words and
+                   // bytes, end misalignment)
   uint32_t s0;     // init ^ ~0
-  uint32_t voff0;  // row 0's buffer offset (kGrpBad: zeros, no access)
-  uint32_t voff1;  // row 1's
-  __amdgpu_buffer_rsrc_t rs;
-  uint32_t rmax, rmin;  // over the chain's groups (wave-uniform)
-  bool aligned;         // every group's e == 0 (wave-uniform)
+  uint32_t gb;     // low half of row 0, lane 0's dword address
+  uint32_t voff0;  // chunk 0, row 0's offset from the window base (kGrpBad: zeros)
+  // wave-uniform: rows over the chain's walked groups, the records' window,
+  // the lowest row-0 address
+  uint32_t rmax, rmin;
+  uint64_t wlo, whi, gbmin, gbmax;
+  bool aligned;
+  __device__ __forceinline__ uint32_t s0l() const { return fix & 15u; }
+  __device__ __forceinline__ uint32_t delta() const { return (fix >> 8) & 3u; }
+  __device__ __forceinline__ uint32_t e() const { return fix >> 12; }
 };
 
 template <int NCH, int R>
@@ -288,83 +258,90 @@ struct GrpRound {
   GrpChain ch[NCH];
   uint32_t w[NCH][R + 1];
 
-  // Chain c from the desc lanes (row_newbcast:c) over the window [wlo, whi)
-  // of its walked records. `rec` is this lane's own record (desc lanes).
-  __device__ __forceinline__ void adopt(int c, const GrpRec& rec, uint32_t t, uint64_t wlo,
-                                        uint64_t whi) {
+  // Chain c from the desc lanes (row_newbcast:c), the groups in `mask`
+  // only. `rec` is this lane's own record (desc lanes).
+  __device__ __forceinline__ void adopt(int c, const GrpRec& rec, uint32_t t, uint32_t lane,
+                                        uint32_t mask) {
     GrpChain& x = ch[c];
-    const bool rk = rec.kind == kGrpRows;
+    const bool in = rec.kind == kGrpRows && ((mask >> (lane >> 4)) & 1u);
     const uint32_t q = (rec.len + 3u) >> 2;
-    const uint32_t rows = rk ? (q + 15u) >> 4 : 0u;
+    const uint32_t rows = in ? (q + 15u) >> 4 : 0u;
     const uint64_t end = rec.ptr() + rec.len;
     const uint64_t gb = (end & ~uint64_t{3}) - 64ull * rows;  // row 0, lane 0's dword
-    const uint32_t pk = rows | (((16u * rows - q) & 15u) << 8) | (((4u * q - rec.len) & 3u) << 12) |
-                        (static_cast<uint32_t>(end & 3u) << 14);
+    const uint32_t fix = ((16u * rows - q) & 15u) | (((4u * q - rec.len) & 3u) << 8) |
+                         (static_cast<uint32_t>(end & 3u) << 12);
+    const uint64_t lo = in ? (rec.ptr() & ~uint64_t{3}) : ~uint64_t{0};
+    const uint64_t hi = in ? ((end + 3u) & ~uint64_t{3}) : 0u;
+    const uint64_t gl = in ? gb : ~uint64_t{0};
+    const uint64_t gh = in ? gb : 0u;
     uint32_t rmax = 0, rmin = 0xffffffffu, emask = 0;
+    uint64_t wlo = ~uint64_t{0}, whi = 0, gbmin = ~uint64_t{0}, gbmax = 0;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const uint32_t p = lane_u32(pk, 16u * g + c);
-      rmax = max(rmax, p & 255u);
-      rmin = min(rmin, p & 255u);
-      emask |= p >> 14;
+      const uint32_t src = 16u * g + c;
+      const uint32_t r = lane_u32(rows, src);
+      rmax = max(rmax, r);
+      rmin = min(rmin, r);
+      emask |= r != 0 ? lane_u32(fix, src) >> 12 : 0u;
+      wlo = min(wlo, lane_u64(lo, src));
+      whi = max(whi, lane_u64(hi, src));
+      gbmin = min(gbmin, lane_u64(gl, src));
+      gbmax = max(gbmax, lane_u64(gh, src));
     }
     x.rmax = rmax;
     x.rmin = rmin;
     x.aligned = emask == 0;
-    const uint32_t gpk = row_bcast_c(pk, c);
-    const uint64_t ggb = (static_cast<uint64_t>(row_bcast_c(static_cast<uint32_t>(gb >> 32), c)) << 32) |
-                         row_bcast_c(static_cast<uint32_t>(gb), c);
+    x.wlo = wlo;
+    x.whi = whi;
+    x.gbmin = gbmin;
+    x.gbmax = gbmax;
+    x.rows = row_bcast_c(rows, c);
+    x.fix = row_bcast_c(fix, c);
     x.s0 = row_bcast_c(rec.s0, c);
-    x.rows = gpk & 255u;
-    x.s0l = (gpk >> 8) & 15u;
-    x.delta = (gpk >> 12) & 3u;
-    x.e = gpk >> 14;
-    const bool any = rmax != 0;
-    const uint64_t base = any ? wlo : 0u;
-    const uint32_t span = any ? static_cast<uint32_t>(whi - wlo) : 0u;
-    x.rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), 0,
-                                             static_cast<int>(span), kBufferDword3);
-    // row 0: lane t's dword at gb + 4t holds record bytes from the first
-    // aligned dword of the record on, lane s0l + (e + delta >= 4) (the lanes
-    // before it are front padding: zeros, no access)
-    const uint64_t a0 = ggb + 4u * t;
-    const uint32_t t0 = x.s0l + ((x.e + x.delta) >= 4u ? 1u : 0u);
-    x.voff0 = (x.rows != 0 && t >= t0) ? static_cast<uint32_t>(a0 - base) : kGrpBad;
-    x.voff1 = x.rows != 0 ? static_cast<uint32_t>(a0 + 64u - base) : kGrpBad;
+    x.gb = row_bcast_c(static_cast<uint32_t>(gb), c);
+    // chunk 0, row 0: lane t's dword holds record bytes from the record's
+    // first aligned dword on, lane s0l + (e + delta >= 4); the lanes before
+    // it are front padding (zeros, no access)
+    const uint32_t t0 = x.s0l() + ((x.e() + x.delta()) >= 4u ? 1u : 0u);
+    x.voff0 = (x.rows != 0 && t >= t0) ? x.gb + 4u * t - static_cast<uint32_t>(wlo) : kGrpBad;
   }
 
   // The R + 1 row loads of chunk k of every chain (row R: the next row's
-  // dwords, for the realignment), unconditional: a kGrpBad offset or a row
-  // past the window reads zeros without a memory access.
-  __device__ __forceinline__ void issue(uint32_t k) {
+  // dwords, for the realignment) through a window of the chunk's own rows
+  // ([wlo, whi) of the records, cut to the rows of this chunk, so a window
+  // is never wider than the records' spread plus a chunk): unconditional; a
+  // kGrpBad offset or a row past the window reads zeros without an access.
+  __device__ __forceinline__ void issue(uint32_t k, uint32_t t) {
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const GrpChain& x = ch[c];
-      uint32_t o0, o1;
-      if (k == 0) {
-        o0 = x.voff0;
-        o1 = x.voff1;
-      } else {
-        o0 = x.voff1 + kGrpRowBytes * (R * k - 1u);
-        o1 = o0 + kGrpRowBytes;
-      }
-      int32_t v0 = static_cast<int32_t>(o0), v1 = static_cast<int32_t>(o1);
+      const uint64_t kr = 64ull * R * k;
+      const uint64_t b = k == 0 ? x.wlo : x.gbmin + kr;
+      const uint64_t e = min(x.whi, x.gbmax + kr + 64ull * (R + 1));
+      const bool any = x.rmax != 0 && e > b;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          reinterpret_cast<void*>(any ? b : 0u), 0, static_cast<int>(any ? e - b : 0u),
+          kBufferDword3);
+      const uint32_t lane_off = x.rows != 0 ? x.gb + static_cast<uint32_t>(kr) + 4u * t -
+                                                  static_cast<uint32_t>(b)
+                                            : kGrpBad;
+      int32_t v0 = static_cast<int32_t>(k == 0 ? x.voff0 : lane_off);
+      int32_t v1 = static_cast<int32_t>(lane_off + (x.rows != 0 ? 64u : 0u));
       asm volatile("" : "+v"(v0));
       asm volatile("" : "+v"(v1));
-      w[c][0] = __builtin_amdgcn_raw_buffer_load_b32(x.rs, v0, 0, kRagCachePolicy);
+      w[c][0] = __builtin_amdgcn_raw_buffer_load_b32(rs, v0, 0, kRagCachePolicy);
 #pragma unroll
       for (int j = 1; j <= R; ++j)
         w[c][j] = __builtin_amdgcn_raw_buffer_load_b32(
-            x.rs, v1 + static_cast<int32_t>(kGrpRowBytes) * (j - 1), 0, kRagCachePolicy);
+            rs, v1 + static_cast<int32_t>(kGrpRowBytes) * (j - 1), 0, kRagCachePolicy);
     }
   }
 
-  // Grid words from the aligned dwords: lane t's word is
+  // Grid words from the aligned dwords, rows [0, nrow): lane t's word is
   // alignbyte(lane t + 1's dword, its own, e); lane 15 takes lane 0 of the
   // next row.
-  // Rows [0, nrow) only (the rows the chunk walks).
   __device__ __forceinline__ void realign(int c, uint32_t t, uint32_t nrow) {
-    const uint32_t e = ch[c].e;
+    const uint32_t e = ch[c].e();
     uint32_t r0 = row_rol1(w[c][0]);
 #pragma unroll
     for (int j = 0; j < R; ++j) {
@@ -382,27 +359,44 @@ struct GrpRound {
   // s0l + 1, or lane 0 of row 1 when s0l = 15).
   __device__ __forceinline__ uint32_t first_row(int c, uint32_t t) {
     const GrpChain& x = ch[c];
-    const uint32_t sh = 8u * x.delta;
-    const uint32_t spill = x.delta ? (x.s0 >> (32u - sh)) : 0u;
+    const uint32_t s0l = x.s0l(), sh = 8u * x.delta();
+    const uint32_t spill = sh ? (x.s0 >> (32u - sh)) : 0u;
     uint32_t v = w[c][0];
-    v = t < x.s0l ? 0u : v;
-    v = t == x.s0l ? ((v & (0xffffffffu << sh)) ^ (x.s0 << sh)) : v;
-    v = t == x.s0l + 1u ? v ^ spill : v;
-    w[c][1] = (x.s0l == 15u && t == 0) ? w[c][1] ^ spill : w[c][1];
+    v = t < s0l ? 0u : v;
+    v = t == s0l ? ((v & (0xffffffffu << sh)) ^ (x.s0 << sh)) : v;
+    v = t == s0l + 1u ? v ^ spill : v;
+    w[c][1] = (s0l == 15u && t == 0) ? w[c][1] ^ spill : w[c][1];
     return x.rows != 0 ? v : 0u;
   }
 };
 
+// CRC32C of a record of fewer than 4 bytes from `init ^ ~0` = s0, bit by bit
+// (desc lanes).
+__device__ __forceinline__ uint32_t grp_tiny(const GrpRec& g) {
+  uint32_t reg = g.s0;
+  if (g.len != 0) {
+    const uint64_t a4 = g.ptr() & ~uint64_t{3};
+    const uint32_t sh = static_cast<uint32_t>(g.ptr() & 3u) * 8u;
+    const uint32_t d0 = gload32(a4);
+    const uint32_t d1 = (g.ptr() & 3u) + g.len > 4u ? gload32(a4 + 4u) : 0u;
+    const uint32_t bytes = static_cast<uint32_t>(((static_cast<uint64_t>(d1) << 32) | d0) >> sh);
+    for (uint32_t i = 0; i < g.len; ++i) {
+      reg ^= (bytes >> (8u * i)) & 0xffu;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) reg = (reg >> 1) ^ (kCastagnoliReflected & (0u - (reg & 1u)));
+    }
+  }
+  return reg ^ 0xffffffffu;
+}
+
 // Workgroup `grp` of G walks its run of [0, total) in groups of four records
-// a chain. lds: GrpLds<W>::kDwords. Every thread calls it.
+// a chain. lds: the compact image (kCompactLdsBytes). Every thread calls it.
 template <int W, int NCH, int R>
 __device__ __forceinline__ void group_run(const KernelArgs& a, const uint32_t* zpow,
-                                          const uint32_t* lane_cols, const uint32_t* grp_cols,
-                                          uint32_t* lds, uint32_t grp, uint32_t G,
-                                          uint32_t total) {
+                                          const uint32_t* grp_cols, uint32_t* lds, uint32_t grp,
+                                          uint32_t G, uint32_t total) {
   static_assert(NCH >= 1 && NCH <= 4 && R >= 2 && (R + 1) * kGrpRowBytes < 4096, "shape");
   constexpr uint32_t kPerWave = 4u * NCH;  // records per wave-round
-  constexpr uint32_t kDefCount = GrpLds<W>::kDefCount, kDefList = GrpLds<W>::kDefList;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = lane_id();
   const uint32_t t = lane & 15u;
@@ -411,73 +405,68 @@ __device__ __forceinline__ void group_run(const KernelArgs& a, const uint32_t* z
   const uint32_t n = per + (grp < extra ? 1u : 0u);
   const uint32_t start = grp * per + min(grp, extra);
   if (n == 0) return;  // the whole workgroup
-  const uint32_t split = min(a.long_split ? a.long_split : kGrpSplit, kGrpSplit);
   const bool desc_lane = t < static_cast<uint32_t>(NCH);
   // desc lane 16 g + c holds record 4c + g of the wave's round
   const uint32_t my = 4u * t + (lane >> 4);
+  build_group_image<W>(lds, zpow, grp_cols, tid, wave, lane);  // (ends with a barrier)
   const LaneKeys keys = lane_keys(lane);
   const uint32_t lane_base = compact_lane_base(lane);
 
-  for (uint32_t seg = 0; seg < n; seg += kGrpDefCap) {
-    const uint32_t sn = min(kGrpDefCap, n - seg);  // this segment's records
-    const uint32_t first = start + seg;
-    build_group_image<W>(lds + 0, zpow, grp_cols, tid, wave, lane);  // (ends with a barrier)
-    if (tid == 0) lds[kDefCount] = 0;
-    __syncthreads();
-    // wave w takes rounds w, w + W, ... of kPerWave records
-    const uint32_t nrounds = (sn + kPerWave - 1) / kPerWave;
-    uint32_t r = wave;
-    auto live_of = [&](uint32_t rr) { return desc_lane && rr < nrounds && rr * kPerWave + my < sn; };
-    // the descriptor pipeline: stage 2 of this round, stage 1 of the next
-    bool live0 = live_of(r);
-    GrpRaw raw0 = grp_stage1(a, first + r * kPerWave + my, live0);
-    GrpHdr hdr0 = grp_stage2(a, raw0, live0);
-    bool live1 = live_of(r + W);
-    GrpRaw raw1 = grp_stage1(a, first + (r + W) * kPerWave + my, live1);
-    for (; r < nrounds; r += W) {
-      GrpRec rec = grp_record(a, raw0, hdr0, live0, first + r * kPerWave + my, split);
-      // the next round's stage 2, the one after's stage 1 (in flight during
-      // this round's rows)
-      const GrpHdr hdr1 = grp_stage2(a, raw1, live1);
-      const bool live2 = live_of(r + 2 * W);
-      const GrpRaw raw2 = grp_stage1(a, first + (r + 2 * W) * kPerWave + my, live2);
+  // wave w takes rounds w, w + W, ... of kPerWave records
+  const uint32_t nrounds = (n + kPerWave - 1) / kPerWave;
+  uint32_t r = wave;
+  auto live_of = [&](uint32_t rr) { return desc_lane && rr < nrounds && rr * kPerWave + my < n; };
+  // the descriptor pipeline: stage 2 of this round, stage 1 of the next
+  bool live0 = live_of(r);
+  GrpRaw raw0 = grp_stage1(a, start + r * kPerWave + my, live0);
+  GrpHdr hdr0 = grp_stage2(a, raw0, live0);
+  bool live1 = live_of(r + W);
+  GrpRaw raw1 = grp_stage1(a, start + (r + W) * kPerWave + my, live1);
+  for (; r < nrounds; r += W) {
+    GrpRec rec = grp_record(a, raw0, hdr0, live0, start + r * kPerWave + my);
+    // the next round's stage 2, the one after's stage 1 (in flight during
+    // this round's rows)
+    const GrpHdr hdr1 = grp_stage2(a, raw1, live1);
+    const bool live2 = live_of(r + 2 * W);
+    const GrpRaw raw2 = grp_stage1(a, start + (r + 2 * W) * kPerWave + my, live2);
+    rec = grp_sort<NCH>(rec, lane, desc_lane);
 
-      rec = grp_sort<NCH>(rec, lane, desc_lane);
-      // each chain's window: a chain that would pass kGrpSpanMax goes to the
-      // list whole (records far apart in one batch: rare)
-      uint64_t wlo[NCH], whi[NCH];
-      {
-        const bool rk = rec.kind == kGrpRows;
-        const uint64_t lo = rk ? (rec.ptr() & ~uint64_t{3}) : ~uint64_t{0};
-        const uint64_t hi = rk ? ((rec.ptr() + rec.len + 3u) & ~uint64_t{3}) : 0u;
-        uint32_t far = 0;
+    // chains whose records lie more than a buffer window apart walk one
+    // group per pass (four passes; scattered batches only)
+    uint32_t far = 0;
+    {
+      const bool rk = rec.kind == kGrpRows;
+      const uint64_t lo = rk ? (rec.ptr() & ~uint64_t{3}) : ~uint64_t{0};
+      const uint64_t hi = rk ? ((rec.ptr() + rec.len + 3u) & ~uint64_t{3}) : 0u;
 #pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-          wlo[c] = ~uint64_t{0};
-          whi[c] = 0;
+      for (int c = 0; c < NCH; ++c) {
+        uint64_t wlo = ~uint64_t{0}, whi = 0, wmax = 0;
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            wlo[c] = min(wlo[c], lane_u64(lo, 16u * g + c));
-            whi[c] = max(whi[c], lane_u64(hi, 16u * g + c));
-          }
-          if (whi[c] > wlo[c] && whi[c] - wlo[c] > kGrpSpanMax) far |= 1u << c;
+        for (int g = 0; g < 4; ++g) {
+          const uint64_t l = lane_u64(lo, 16u * g + c);
+          wlo = min(wlo, l);
+          wmax = l != ~uint64_t{0} ? max(wmax, l) : wmax;
+          whi = max(whi, lane_u64(hi, 16u * g + c));
         }
-        if (far != 0 && rk && ((far >> t) & 1u)) rec.kind = kGrpDefer;
+        // the starts' spread (the chunk windows span it)
+        if (whi > wlo && wmax - wlo > kGrpSpanMax) far |= 1u << c;
       }
-      if (rec.kind == kGrpDefer) lds[kDefList + atomicAdd(&lds[kDefCount], 1u)] = rec.idx;
-
+    }
+    const uint32_t npass = far != 0 ? 4u : 1u;
+    for (uint32_t p = 0; p < npass; ++p) {
       GrpRound<NCH, R> rd;
       uint32_t nchunks = 0;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
-        rd.adopt(c, rec, t, wlo[c], whi[c]);
+        const uint32_t m = ((far >> c) & 1u) ? (1u << p) : (p == 0 ? 15u : 0u);
+        rd.adopt(c, rec, t, lane, m);
         nchunks = max(nchunks, (rd.ch[c].rmax + R - 1) / R);
       }
       uint32_t st[NCH];
       uint32_t crc[NCH];
 #pragma unroll
       for (int c = 0; c < NCH; ++c) crc[c] = 0;
-      if (nchunks != 0) rd.issue(0);
+      if (nchunks != 0) rd.issue(0, t);
       for (uint32_t k = 0; k < nchunks; ++k) {
         // rows j0 .. R - 1 (row kR + j of the records): first every chain up
         // to its shortest group, interleaved, without the freeze; then each
@@ -531,30 +520,32 @@ __device__ __forceinline__ void group_run(const KernelArgs& a, const uint32_t* z
           if (rd.ch[c].rmax != 0 && rd.ch[c].rmax <= (k + 1) * R)
             crc[c] = row_xor16(lane_end_shift_c(lds, st[c], lane_base)) ^ 0xffffffffu;
         }
-        if (k + 1 < nchunks) rd.issue(k + 1);
+        if (k + 1 < nchunks) rd.issue(k + 1, t);
       }
-      // desc lane 16 g + c stores its record (chain c's group g)
+      // desc lane 16 g + c stores its record (chain c's group g) in the pass
+      // that walked it
       if (rec.kind == kGrpRows) {
         uint32_t mine = 0;
+        bool walked = false;
 #pragma unroll
-        for (int c = 0; c < NCH; ++c) mine = t == static_cast<uint32_t>(c) ? crc[c] : mine;
-        grp_store(a, rec, mine);
+        for (int c = 0; c < NCH; ++c) {
+          if (t == static_cast<uint32_t>(c)) {
+            mine = crc[c];
+            walked = ((far >> c) & 1u) ? (lane >> 4) == p : p == 0;
+          }
+        }
+        if (walked) grp_store(a, rec, mine);
       }
-      raw0 = raw1;
-      hdr0 = hdr1;
-      live0 = live1;
-      raw1 = raw2;
-      live1 = live2;
     }
-    // the deferred records (short, long, or far apart): the 64-lane walk over
-    // the list, the LDS image rebuilt as Z_256 by ragged_run
-    __syncthreads();
-    const uint32_t cnt = __builtin_amdgcn_readfirstlane(lds[kDefCount]);
-    if (cnt != 0) {
-      ragged_run<W, 2, 24, GrpListSrc>(a, zpow, lane_cols, lds, 0, 1, cnt, false,
-                                       GrpListSrc{lds + kDefList});
-      __syncthreads();
+    // records of fewer than 4 bytes: bit by bit in their desc lanes
+    if (__builtin_amdgcn_ballot_w64(rec.kind == kGrpTiny) != 0) {
+      if (rec.kind == kGrpTiny) grp_store(a, rec, grp_tiny(rec));
     }
+    raw0 = raw1;
+    hdr0 = hdr1;
+    live0 = live1;
+    raw1 = raw2;
+    live1 = live2;
   }
 }
 

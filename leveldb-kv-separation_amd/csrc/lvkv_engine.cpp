@@ -101,9 +101,9 @@ constexpr KernelSpec kSpecs[] = {
     {"lvkv_ek_ragged_burst.kd", nullptr, 8, 4, 1, kArgsRagged},
     {"lvkv_ek_ragged_burst_small.kd", nullptr, 8, 6, 1, kArgsRagged},
     // grouped walks: `chains` counts records per wave-round (4 per chain)
-    {"lvkv_ek_group.kd", nullptr, 8, 16, 2, kArgsRagged},
-    {"lvkv_ek_group_r8.kd", nullptr, 8, 16, 2, kArgsRagged},
-    {"lvkv_ek_group_c2.kd", nullptr, 8, 8, 2, kArgsRagged},
+    {"lvkv_ek_group.kd", nullptr, 8, 8, 2, kArgsRagged},
+    {"lvkv_ek_group_r16.kd", nullptr, 8, 8, 2, kArgsRagged},
+    {"lvkv_ek_group_r12.kd", nullptr, 8, 8, 2, kArgsRagged},
 };
 constexpr int kNumSpecs = static_cast<int>(sizeof(kSpecs) / sizeof(kSpecs[0]));
 constexpr int kNumUniformSpecs = 2;  // lvkv_engine_set_variant's choices

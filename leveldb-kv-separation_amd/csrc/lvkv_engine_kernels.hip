@@ -89,27 +89,15 @@ extern "C" __global__ void __launch_bounds__(512, 2)
                             false);
 }
 
-// Short records (WAL records, small values; LVKV_FLAG_SMALL_BLOCKS, uniform
-// blocks of <= 8 rows): four records per wave at once, one per 16-lane row
-// (crc32c_group_body.h), 8 waves x 4 chains x 16 rows of 64 bytes, two
-// workgroups per CU; records over 2 KiB, under 4 bytes or far apart go to the
-// 64-lane walk at the end of the segment. Variants (A/B timing through
-// lvkv_debug_engine_ragged_spec): 4 chains x 8 rows, 2 chains x 16 rows.
-extern "C" __global__ void __launch_bounds__(512, 2)
-    lvkv_ek_group(lvkv::EngineRaggedArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::GrpLds<8>::kDwords];
-  lvkv::group_run<8, 4, 16>(a.k, a.zpow, a.lane_cols, a.grp_cols, lds, blockIdx.x, a.ngroups,
-                            a.k.nblocks);
-}
-extern "C" __global__ void __launch_bounds__(512, 2)
-    lvkv_ek_group_r8(lvkv::EngineRaggedArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::GrpLds<8>::kDwords];
-  lvkv::group_run<8, 4, 8>(a.k, a.zpow, a.lane_cols, a.grp_cols, lds, blockIdx.x, a.ngroups,
-                           a.k.nblocks);
-}
-extern "C" __global__ void __launch_bounds__(512, 2)
-    lvkv_ek_group_c2(lvkv::EngineRaggedArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::GrpLds<8>::kDwords];
-  lvkv::group_run<8, 2, 16>(a.k, a.zpow, a.lane_cols, a.grp_cols, lds, blockIdx.x, a.ngroups,
-                            a.k.nblocks);
-}
+// Short records (WAL records, small values): four records per wave at once,
+// one per 16-lane row (crc32c_group_body.h), 8 waves x 2 chains x 8 rows of
+// 64 bytes, two workgroups per CU. Variants (A/B timing through
+// lvkv_debug_engine_ragged_spec): 2 chains x 16 rows, 2 chains x 12 rows.
+#define LVKV_GROUP_KERNEL(NAME, NCH, R)                                                         \
+  extern "C" __global__ void __launch_bounds__(512, 2) NAME(lvkv::EngineRaggedArgs a) {        \
+    __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::kCompactLdsBytes / 4];         \
+    lvkv::group_run<8, NCH, R>(a.k, a.zpow, a.grp_cols, lds, blockIdx.x, a.ngroups, a.k.nblocks); \
+  }
+LVKV_GROUP_KERNEL(lvkv_ek_group, 2, 8)
+LVKV_GROUP_KERNEL(lvkv_ek_group_r16, 2, 16)
+LVKV_GROUP_KERNEL(lvkv_ek_group_r12, 2, 12)
