@@ -158,23 +158,6 @@ __device__ __forceinline__ void build_compact_image(uint32_t* lds, const uint32_
   __syncthreads();
 }
 
-// The grouped walk's image (crc32c_group_body.h): the same layout with rows
-// of 64 bytes (16 lanes x 4 B per record) -- row tables Z_64 (zpow set 6),
-// lane s's nibble tables Z_{64-4(s%16)} generated from grp_cols (the
-// lane_cols layout). Ends with a barrier.
-template <int W>
-__device__ __forceinline__ void build_group_image(uint32_t* lds, const uint32_t* zpow,
-                                                  const uint32_t* grp_cols, uint32_t tid,
-                                                  uint32_t wave, uint32_t lane) {
-  RowTabStage<64 * W, 6> rt;
-  LaneTabGen<W> lg;
-  rt.load(zpow, tid);
-  lg.load(grp_cols, wave, lane);
-  rt.store(lds, tid);
-  lg.store(lds, wave, lane);
-  __syncthreads();
-}
-
 // ---- long blocks: one workgroup per block -------------------------------
 
 __device__ __forceinline__ uint32_t zshift_g(const uint32_t* zpow, uint32_t v, uint64_t n) {

@@ -162,7 +162,6 @@ void init_ctx(DeviceCtx& c, int dev) {
   build_lane_columns(tab.data() + kRowTabDwords + kLaneTabDwords);
   build_zpow_tables(tab.data() + kZPowOffset);
   build_zmul_columns(tab.data() + kZPowOffset + kZPowDwords);
-  build_group_lane_columns(tab.data() + kGrpColOffset);
   void* p = nullptr;
   e = hipMalloc(&p, tab.size() * sizeof(uint32_t));
   if (e != hipSuccess) {

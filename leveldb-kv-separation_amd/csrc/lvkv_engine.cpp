@@ -100,17 +100,12 @@ constexpr KernelSpec kSpecs[] = {
     {"lvkv_ek_ragged_small.kd", nullptr, 8, 4, 2, kArgsRagged},
     {"lvkv_ek_ragged_burst.kd", nullptr, 8, 4, 1, kArgsRagged},
     {"lvkv_ek_ragged_burst_small.kd", nullptr, 8, 6, 1, kArgsRagged},
-    // grouped walks: `chains` counts records per wave-round (4 per chain)
-    {"lvkv_ek_group.kd", nullptr, 8, 8, 2, kArgsRagged},
-    {"lvkv_ek_group_r16.kd", nullptr, 8, 8, 2, kArgsRagged},
-    {"lvkv_ek_group_r12.kd", nullptr, 8, 8, 2, kArgsRagged},
 };
 constexpr int kNumSpecs = static_cast<int>(sizeof(kSpecs) / sizeof(kSpecs[0]));
 constexpr int kNumUniformSpecs = 2;  // lvkv_engine_set_variant's choices
 // general-layout kernels: persistent runs (two workgroups per CU, rounds of
 // 16 / 32 blocks), and one round per dispatch (one workgroup per CU)
-constexpr int kRaggedSpec = 2, kRaggedSmallSpec = 3, kBurstSpec = 4, kBurstSmallSpec = 5,
-              kGroupSpec = 6;
+constexpr int kRaggedSpec = 2, kRaggedSmallSpec = 3, kBurstSpec = 4, kBurstSmallSpec = 5;
 constexpr uint32_t kBurstRows = 17, kBurstSmallRows = 8;  // chunk rows of the SST / small shapes
 static_assert(sizeof(EngineRaggedArgs) <= 256 && sizeof(UniformArgs) <= 256, "kernarg slot");
 
@@ -748,7 +743,6 @@ int submit_general(Engine& eng, KernelArgs a, size_t nblocks, uint32_t flags) {
     if (a.out_status != nullptr) r.k.out_status = a.out_status + done;
     r.zpow = e->d_tables + kZPowOffset;
     r.lane_cols = e->d_tables + kRowTabDwords + kLaneTabDwords;
-    r.grp_cols = e->d_tables + kGrpColOffset;
     r.ngroups = static_cast<uint32_t>(std::min(max_groups, (n + per_round - 1) / per_round));
     const int rc = dispatch(*e, k, &r, sizeof(r), r.ngroups, /*acquire=*/true,
                             /*barrier=*/ordered, (flags & LVKV_FLAG_SYSTEM_ACQUIRE) != 0, queue,

@@ -11,7 +11,6 @@
 #include <stdint.h>
 
 #include "crc32c_burst.h"
-#include "crc32c_group_body.h"
 #include "crc32c_ragged_body.h"
 #include "lvkv_kernel_args.h"
 
@@ -88,16 +87,3 @@ extern "C" __global__ void __launch_bounds__(512, 2)
   lvkv::ragged_run<8, 6, 8>(a.k, a.zpow, a.lane_cols, lds, blockIdx.x, a.ngroups, a.k.nblocks,
                             false);
 }
-
-// Short records (WAL records, small values): four records per wave at once,
-// one per 16-lane row (crc32c_group_body.h), 8 waves x 2 chains x 8 rows of
-// 64 bytes, two workgroups per CU. Variants (A/B timing through
-// lvkv_debug_engine_ragged_spec): 2 chains x 16 rows, 2 chains x 12 rows.
-#define LVKV_GROUP_KERNEL(NAME, NCH, R)                                                         \
-  extern "C" __global__ void __launch_bounds__(512, 2) NAME(lvkv::EngineRaggedArgs a) {        \
-    __shared__ __attribute__((aligned(16))) uint32_t lds[lvkv::kCompactLdsBytes / 4];         \
-    lvkv::group_run<8, NCH, R>(a.k, a.zpow, a.grp_cols, lds, blockIdx.x, a.ngroups, a.k.nblocks); \
-  }
-LVKV_GROUP_KERNEL(lvkv_ek_group, 2, 8)
-LVKV_GROUP_KERNEL(lvkv_ek_group_r16, 2, 16)
-LVKV_GROUP_KERNEL(lvkv_ek_group_r12, 2, 12)

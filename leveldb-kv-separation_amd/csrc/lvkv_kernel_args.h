@@ -43,11 +43,7 @@ constexpr uint32_t kZPowOffset = 1024 + 8 * 16 * 64 + 8 * 64 * 4;  // in d_table
 // [1, kZMulMaxC] (lvkv_tables.h), right after zpow in d_tables.
 constexpr uint32_t kZMulLog0 = 8, kZMulLogs = 16, kZMulMaxC = 16;
 constexpr uint32_t kZMulDwords = kZMulLogs * kZMulMaxC * 32;
-// Columns of Z_{64-4(s%16)} per lane s (the lane_cols layout), for the
-// grouped small-record walk's 64-byte rows (crc32c_group_body.h), after zmul.
-constexpr uint32_t kGrpColOffset = kZPowOffset + kZPowDwords + kZMulDwords;
-constexpr uint32_t kGrpColDwords = kLaneColDwords;
-constexpr uint32_t kTableDwords = kGrpColOffset + kGrpColDwords;
+constexpr uint32_t kTableDwords = kZPowOffset + kZPowDwords + kZMulDwords;
 constexpr uint32_t kLdsRowRegionBytes = 64 * 1024;
 constexpr uint32_t kLdsLaneTabBase = 128 * 1024;
 constexpr uint32_t kLdsBytes = 160 * 1024;
@@ -154,7 +150,6 @@ struct EngineRaggedArgs {
   KernelArgs k;
   const uint32_t* zpow;
   const uint32_t* lane_cols;
-  const uint32_t* grp_cols;  // the grouped walk's lane columns (kGrpColOffset)
   uint32_t ngroups;
   uint32_t pad_;
 };

@@ -77,14 +77,6 @@ void build_lane_columns(uint32_t* lane_cols) {
   }
 }
 
-void build_group_lane_columns(uint32_t* grp_cols) {
-  for (uint32_t s = 0; s < 64; ++s) {
-    const Gf2Op z = gf2_zero_advance(64 - 4 * (s & 15u));
-    for (uint32_t k = 0; k < 8; ++k)
-      for (uint32_t j = 0; j < 4; ++j) grp_cols[(k * 64 + s) * 4 + j] = z.col[4 * k + j];
-  }
-}
-
 void build_zpow_tables(uint32_t* zpow) {
   for (uint32_t j = 0; j < kZPowCount; ++j) {
     const Gf2Op z = gf2_zero_advance(uint64_t{1} << j);

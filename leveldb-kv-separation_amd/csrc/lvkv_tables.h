@@ -30,9 +30,6 @@ void build_lane_table(uint32_t* lane_tab);
 //   lane_cols[(k*64 + s)*4 + j]     = Z_{256-4s}(1 << (4k + j)) (2048 dwords):
 //   the columns lane s needs to generate its lane-table entries of nibble k
 void build_lane_columns(uint32_t* lane_cols);
-//   grp_cols[(k*64 + s)*4 + j]      = Z_{64-4(s%16)}(1 << (4k + j)): the same
-//   for the grouped walk's 16-lane rows of 64 bytes
-void build_group_lane_columns(uint32_t* grp_cols);
 //   zpow[j*1024 + t*256 + b]        = Z_{2^j}(b << 8t), j < kZPowCount:
 //   Z_n(v) for any n = the product over the set bits j of n
 void build_zpow_tables(uint32_t* zpow);
