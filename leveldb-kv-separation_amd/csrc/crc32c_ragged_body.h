@@ -337,22 +337,18 @@ struct RagRound {
     }
   }
 
-  // Grid words of chain c from its aligned dwords (end misalignment e != 0),
-  // rows [0, nrow) (the rows this chunk walks; a constant R unrolls without
-  // tests).
-  __device__ __forceinline__ void realign(int c, uint32_t lane, uint32_t nrow = R) {
+  // Grid words of chain c from its aligned dwords (end misalignment e != 0).
+  __device__ __forceinline__ void realign(int c, uint32_t lane) {
     const uint32_t e = g[c].e();
     uint32_t r0 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(w[c][0]), 0x134,
                                                                  0xF, 0xF, false));
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-      if (static_cast<uint32_t>(j) < nrow) {
-        const uint32_t r1 = static_cast<uint32_t>(
-            __builtin_amdgcn_mov_dpp(static_cast<int>(w[c][j + 1]), 0x134, 0xF, 0xF, false));
-        const uint32_t hi = lane == 63u ? r1 : r0;  // wave_rol:1 = lane s + 1's dword
-        w[c][j] = __builtin_amdgcn_alignbyte(hi, w[c][j], e);
-        r0 = r1;
-      }
+      const uint32_t r1 = static_cast<uint32_t>(
+          __builtin_amdgcn_mov_dpp(static_cast<int>(w[c][j + 1]), 0x134, 0xF, 0xF, false));
+      const uint32_t hi = lane == 63u ? r1 : r0;  // wave_rol:1 = lane s + 1's dword
+      w[c][j] = __builtin_amdgcn_alignbyte(hi, w[c][j], e);
+      r0 = r1;
     }
   }
 };
@@ -475,18 +471,9 @@ __device__ __forceinline__ void ragged_run(const KernelArgs& a, const uint32_t* 
     //    flight. Row 0: start every chain (fix-ups) or continue it. Idle
     //    chains walk zeros and store nothing.
     if (k == 0) RagRound<NCH, R>::fetch(gn, a, src, start, n, r0 + W * NCH, wave, W);
-    // the rows of each chain this chunk walks: only they are realigned
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      if (rd.g[c].e() != 0) {
-        const uint32_t rows = rd.g[c].kind == kRagRows ? rd.g[c].rows() : 0u;
-        const uint32_t nr = rows > k * R ? rows - k * R : 0u;
-        if (nr >= static_cast<uint32_t>(R))
-          rd.realign(c, lane);
-        else
-          rd.realign(c, lane, nr);
-      }
-    }
+    for (int c = 0; c < NCH; ++c)
+      if (rd.g[c].e() != 0) rd.realign(c, lane);
     if (k == 0) {
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
