@@ -41,6 +41,9 @@ struct lvkv_engine;
  * one workgroup per CU per dispatch (overlapped default); 1 = 8 x 3, two
  * workgroups per CU (ordered default). */
 int lvkv_engine_set_variant(struct lvkv_engine* engine, int variant, int ordered_variant);
+/* Kernel of LVKV_FLAG_FINAL uniform dispatches (the last before a wait):
+ * -1 = as the overlapped ones (default), 0 or 1 as above. */
+int lvkv_engine_set_final_variant(struct lvkv_engine* engine, int variant);
 /* Ordered (overlapped = 0) or overlapped dispatches run `kernel` (a
  * UniformArgs kernel of the given shape, symbol name with ".kd") from a
  * separate gfx950 code object in memory (tools/probe/build.sh) instead of the

@@ -224,6 +224,7 @@ struct Engine {
   int fence_acq = HSA_FENCE_SCOPE_NONE, fence_rel = HSA_FENCE_SCOPE_SYSTEM;
   int variant = 0;          // kernel of overlapped dispatches
   int ordered_variant = 1;  // kernel of ordered dispatches (the whole chip)
+  int final_variant = -1;   // of LVKV_FLAG_FINAL dispatches (-1: as overlapped)
   uint8_t* kernarg = nullptr;     // (kSlots + kCacheSlots) x kSlotBytes
   bool kernarg_vram = false;      // BAR-written VRAM (else system memory)
   struct CachedArgs {             // host copy of a cached kernarg slot
@@ -804,7 +805,9 @@ int lvkv_engine_crc32c_uniform(lvkv_engine* eng, const void* d_base, uint64_t st
   // gets the kernel shaped for the whole chip.
   if (ordered && e->nq > 1 && e->fenced != e->next && fence(*e) != LVKV_OK) return LVKV_ERR_HIP;
   const int queue = ordered ? static_cast<int>(e->next % static_cast<uint64_t>(e->nq)) : -1;
-  const int v = ordered ? e->ordered_variant : e->variant;
+  const int v = ordered ? e->ordered_variant
+                : ((flags & LVKV_FLAG_FINAL) && e->final_variant >= 0) ? e->final_variant
+                                                                      : e->variant;
   const EngineKernel& k = (e->probe_on && ordered != e->probe_overlapped) ? e->probe
                           : e->stamps                ? e->kern_stamps[v]
                                                      : e->kern[v];
@@ -995,6 +998,14 @@ int lvkv_engine_set_variant(lvkv_engine* eng, int variant, int ordered_variant) 
   if (e->fenced != e->next && fence(*e) != LVKV_OK) return LVKV_ERR_HIP;
   e->variant = variant;
   e->ordered_variant = ordered_variant;
+  return LVKV_OK;
+}
+
+int lvkv_engine_set_final_variant(lvkv_engine* eng, int variant) {
+  if (eng == nullptr || variant < -1 || variant >= kNumUniformSpecs) return LVKV_ERR_INVALID;
+  Engine* e = reinterpret_cast<Engine*>(eng);
+  std::lock_guard<std::mutex> lk(e->mu);
+  e->final_variant = variant;
   return LVKV_OK;
 }
 

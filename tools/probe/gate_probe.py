@@ -28,6 +28,7 @@ lvkv = g.load_package()
 hsa = ctypes.CDLL("libhsa-runtime64.so.1")
 hsa.hsa_system_get_info.argtypes = [ctypes.c_int, ctypes.c_void_p]
 lvkv.lib.lvkv_debug_engine_stall.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double]
+lvkv.lib.lvkv_engine_set_final_variant.argtypes = [ctypes.c_void_p, ctypes.c_int]
 
 
 def now_us():
@@ -55,32 +56,39 @@ def main():
         assert rc == 0
 
     K = 20
-    res = {"plain": [], "gated": []}
-    for rep in range(30):
-        gated = rep % 2 == 1
+    modes = ["plain", "gated", "final_pair", "gated_final_pair"]
+    res = {m: [] for m in modes}
+    for rep in range(60):
+        mode = modes[rep % 4]
+        gated = mode.startswith("gated")
+        assert lvkv.lib.lvkv_engine_set_final_variant(h, 1 if "final_pair" in mode else -1) == 0
         for _ in range(40):
             step()
         eng.wait()
         torch.cuda.synchronize()
-        eng.profile(True)
-        if gated:
-            assert stall(h, 1, 60.0) == 0
-            time.sleep(0.0002)  # the packet processors reach the barriers
-        torch.cuda.synchronize()
-        t0 = now_us()
-        step()
-        if gated:
-            stall(h, 0, 60.0)
-        for k in range(1, K):
-            step(final=k >= K - 3)
-        eng.wait()
-        torch.cuda.synchronize()
-        t1 = now_us()
-        sp = eng.profile_read()
-        eng.profile(False)
-        res["gated" if gated else "plain"].append(
-            {"t0_to_first_start": sp[0][0] - t0, "host_us": t1 - t0,
-             "span": max(b for _, b in sp) - sp[0][0]})
+        for prof in (False, True):
+            if prof:
+                eng.profile(True)
+            if gated:
+                assert stall(h, 1, 60.0) == 0
+                time.sleep(0.0002)  # the packet processors reach the barriers
+            torch.cuda.synchronize()
+            t0 = now_us()
+            step()
+            if gated:
+                stall(h, 0, 60.0)
+            for k in range(1, K):
+                step(final=k >= K - 3)
+            eng.wait()
+            torch.cuda.synchronize()
+            t1 = now_us()
+            if prof:
+                sp = eng.profile_read()
+                eng.profile(False)
+                res[mode][-1].update({"t0_to_first_start": sp[0][0] - t0, "span": max(b for _, b in sp) - sp[0][0],
+                                      "last_dur": sp[-1][1] - sp[-1][0]})
+            else:
+                res[mode].append({"host_us": t1 - t0})
     agg = {k: {f: round(statistics.median(r[f] for r in v), 3) for f in v[0]} for k, v in res.items()}
     print(json.dumps(agg), flush=True)
     (REPO / "gpurun_out").mkdir(exist_ok=True)
