@@ -11,6 +11,8 @@
 #   sst     kernel traces of the SST forms
 #   ceiling kernel trace of the production and read-ceiling kernels, overlapped
 #   edges   the K = 20 region's edges (tools/probe/edges.py)
+#   e2e     host-memory rates (tools/e2e_bench.py)
+#   gate    parked queues / pair kernel for the last batches (tools/probe/gate_probe.py)
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-/root/repo} && mkdir -p gpurun_out && export TMPDIR=/tmp
 steps=${*:-tests bench}
@@ -102,6 +104,14 @@ if want group; then  # the grouped small-record walk: parity, then timing by spe
   tail -3 $O/group_tests.log
   timeout -k 10 300 python tools/probe/engine_shapes.py --cases rand2000_62k,sst4106_16k --specs 3,6,7,8 --reps 20 > $O/group_shapes.log 2>&1 || { echo shapes failed; tail -20 $O/group_shapes.log; exit 1; }
   grep -v amdgpu.ids $O/group_shapes.log | tail -12
+fi
+if want e2e; then  # the host-memory rates of DESIGN §8
+  timeout -k 10 300 python tools/e2e_bench.py > $O/e2e.json 2> $O/e2e.err || { tail -20 $O/e2e.err; exit 1; }
+  cat $O/e2e.json
+fi
+if want gate; then
+  timeout -k 10 200 python tools/probe/gate_probe.py > $O/gate.log 2>&1 || { tail -20 $O/gate.log; exit 1; }
+  grep -v amdgpu.ids $O/gate.log | tail -3
 fi
 if want shapes; then
   timeout -k 10 400 python tools/probe/engine_shapes.py > $O/engine_shapes.log 2>&1 || { echo shapes failed; tail -20 $O/engine_shapes.log; exit 1; }
