@@ -1,0 +1,95 @@
+/*
+ * lvkv_snappy.h — C-ABI of the device Snappy block codec (SURVEY.md §8(f)
+ * row 4): the codec on either side of the block CRC when tables are written
+ * or read with kSnappyCompression.
+ *
+ * Library: leveldb-kv-separation_amd/liblvkv_crc32c.so (the same library as
+ * lvkv_crc32c.h; return codes LVKV_OK / LVKV_ERR_* from there). Blocks are
+ * described by plain device arrays; one call handles a batch of independent
+ * blocks on `stream` (a hipStream_t, NULL = the default stream) and returns
+ * once the work is enqueued.
+ *
+ * Format and bytes: Google Snappy's raw format as libsnappy 1.1.8 writes and
+ * reads it (the snappy the image carries; the as-built reference has
+ * HAVE_SNAPPY=0, port/port_stdcxx.h:90-133). The compressor emits exactly
+ * the bytes of snappy::RawCompress 1.1.8; the decompressor accepts exactly
+ * the streams snappy::RawUncompress accepts and produces the same bytes.
+ * The device keeps a block in LDS: blocks up to LVKV_SNAPPY_MAX_BLOCK bytes
+ * uncompressed (LevelDB's blocks are ~block_size, 4 KiB by default); a block
+ * beyond what the call was sized for is reported per block
+ * (LVKV_SNAPPY_TOO_LARGE) and is the caller's to handle on the host.
+ */
+#ifndef LVKV_SNAPPY_H_
+#define LVKV_SNAPPY_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* per-block status */
+#define LVKV_SNAPPY_OK 0
+#define LVKV_SNAPPY_BAD_LENGTH 1   /* Snappy_GetUncompressedLength failed: "corrupted snappy
+                                      compressed block length" (table/format.cc:122-124) */
+#define LVKV_SNAPPY_BAD_CONTENTS 2 /* Snappy_Uncompress failed: "corrupted snappy compressed
+                                      block contents" (table/format.cc:127-131) */
+#define LVKV_SNAPPY_CAPACITY 3     /* the block's uncompressed length exceeds d_dst_cap[i]
+                                      (out_len says how much it needs) */
+#define LVKV_SNAPPY_TOO_LARGE 4    /* beyond the call's max_len / max_ulen (or, for a
+                                      stream, longer than 2 max_ulen + 8 bytes: valid only
+                                      with padded elements no encoder writes) */
+
+#define LVKV_SNAPPY_MAX_BLOCK 49152u /* largest max_ulen of the decompressor */
+
+/* snappy::MaxCompressedLength: 32 + n + n / 6. */
+size_t lvkv_snappy_max_compressed_length(size_t n);
+
+/*
+ * Compress block i = d_src[d_src_off[i], + d_src_len[i]) into
+ * d_dst[d_dst_off[i], ...) (room for lvkv_snappy_max_compressed_length of
+ * its length), d_dst_len[i] = bytes written, d_status[i] = LVKV_SNAPPY_OK or
+ * LVKV_SNAPPY_TOO_LARGE (a block longer than max_len; fragments of 64 KiB
+ * are compressed alone, so any max_len >= 65536 takes every block).
+ * Replaces port::Snappy_Compress (port/port_stdcxx.h:90-106) in
+ * TableBuilder::WriteBlock (table/table_builder.cc:158-168); the 12.5% rule
+ * that keeps a block raw stays with the caller (it needs both lengths).
+ */
+int lvkv_snappy_compress_device(const void* d_src, const uint64_t* d_src_off,
+                                const uint32_t* d_src_len, void* d_dst,
+                                const uint64_t* d_dst_off, uint32_t* d_dst_len,
+                                uint8_t* d_status, size_t nblocks, uint32_t max_len,
+                                void* stream);
+
+/*
+ * Uncompressed lengths: d_ulen[i] = the varint32 preamble of stream i,
+ * d_status[i] = LVKV_SNAPPY_OK or LVKV_SNAPPY_BAD_LENGTH. Replaces
+ * port::Snappy_GetUncompressedLength (port/port_stdcxx.h:108-119), the
+ * first half of ReadBlock's snappy case (table/format.cc:120-125).
+ */
+int lvkv_snappy_uncompressed_length_device(const void* d_src, const uint64_t* d_src_off,
+                                           const uint32_t* d_src_len, uint32_t* d_ulen,
+                                           uint8_t* d_status, size_t nblocks, void* stream);
+
+/*
+ * Uncompress stream i = d_src[d_src_off[i], + d_src_len[i]) into
+ * d_dst[d_dst_off[i], + d_dst_cap[i]): d_out_len[i] = its uncompressed
+ * length (when the preamble decodes), d_status[i] = one of the statuses
+ * above; on LVKV_SNAPPY_BAD_CONTENTS the destination holds garbage, as
+ * after a failed RawUncompress. max_ulen (<= LVKV_SNAPPY_MAX_BLOCK) bounds
+ * the uncompressed length the call handles and sizes its LDS. Replaces
+ * port::Snappy_Uncompress (port/port_stdcxx.h:121-133) in ReadBlock
+ * (table/format.cc:126-135).
+ */
+int lvkv_snappy_uncompress_device(const void* d_src, const uint64_t* d_src_off,
+                                  const uint32_t* d_src_len, void* d_dst,
+                                  const uint64_t* d_dst_off, const uint32_t* d_dst_cap,
+                                  uint32_t* d_out_len, uint8_t* d_status, size_t nblocks,
+                                  uint32_t max_ulen, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LVKV_SNAPPY_H_ */

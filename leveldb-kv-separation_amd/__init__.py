@@ -136,6 +136,14 @@ def _load() -> ctypes.CDLL:
     L.lvkv_engine_load_probe.restype = i32
     L.lvkv_debug_engine_stall.argtypes = [vp, i32, ctypes.c_double]
     L.lvkv_debug_engine_stall.restype = i32
+    L.lvkv_snappy_max_compressed_length.argtypes = [sz]
+    L.lvkv_snappy_max_compressed_length.restype = sz
+    L.lvkv_snappy_compress_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, sz, u32, vp]
+    L.lvkv_snappy_compress_device.restype = i32
+    L.lvkv_snappy_uncompressed_length_device.argtypes = [vp, vp, vp, vp, vp, sz, vp]
+    L.lvkv_snappy_uncompressed_length_device.restype = i32
+    L.lvkv_snappy_uncompress_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, sz, u32, vp]
+    L.lvkv_snappy_uncompress_device.restype = i32
     L.lvkv_strerror.argtypes = [i32]
     L.lvkv_strerror.restype = ctypes.c_char_p
     L.lvkv_last_hip_error.argtypes = []
@@ -460,6 +468,120 @@ def log_fill_headers(file_buf, hdr_offsets, *, stream=None):
             _stream_handle(stream, file_buf.device))
     _check("lvkv_log_fill_headers_device", rc)
     return crc
+
+
+# --------------------------------------------------------------------------
+# Snappy block codec (include/lvkv_snappy.h; port/port_stdcxx.h:90-133)
+
+SNAPPY_OK, SNAPPY_BAD_LENGTH, SNAPPY_BAD_CONTENTS, SNAPPY_CAPACITY, SNAPPY_TOO_LARGE = range(5)
+SNAPPY_MAX_BLOCK = 49152
+
+
+def snappy_max_compressed_length(n: int) -> int:
+    """snappy::MaxCompressedLength (32 + n + n/6)."""
+    return int(_lib.lvkv_snappy_max_compressed_length(n))
+
+
+def _packed_offsets(torch, sizes, device):
+    """Exclusive prefix sum of sizes (int64, on device)."""
+    off = torch.zeros(sizes.numel(), dtype=torch.int64, device=device)
+    if sizes.numel() > 1:
+        off[1:] = torch.cumsum(sizes[:-1].to(torch.int64), 0)
+    return off
+
+
+def snappy_compress(src, offsets, lengths, *, max_len: Optional[int] = None, dst=None,
+                    dst_offsets=None, stream=None):
+    """Batched port::Snappy_Compress (port/port_stdcxx.h:90-106) of block
+    i = src[offsets[i] : offsets[i] + lengths[i]]: snappy 1.1.8's bytes.
+
+    Without dst, every block gets MaxCompressedLength bytes, packed. Returns
+    (dst uint8, dst_offsets int64, compressed lengths int32, status uint8:
+    SNAPPY_OK or SNAPPY_TOO_LARGE for a block longer than max_len)."""
+    torch = _torch()
+    n = offsets.numel()
+    dev = src.device
+    if lengths.numel() != n:
+        raise ValueError("offsets and lengths differ in length")
+    if max_len is None:
+        max_len = int(lengths.max().item()) if n else 0
+    if dst is None:
+        lens = lengths.to(torch.int64)
+        room = 32 + lens + lens // 6
+        dst_offsets = _packed_offsets(torch, room, dev)
+        dst = torch.empty(int(room.sum().item()) if n else 0, dtype=torch.uint8, device=dev)
+    elif dst_offsets is None:
+        raise ValueError("dst needs dst_offsets")
+    out_len = torch.empty(n, dtype=torch.int32, device=dev)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    if n:
+        with torch.cuda.device(dev):
+            rc = _lib.lvkv_snappy_compress_device(
+                _dev_ptr(src, "src", (torch.uint8, torch.int8)),
+                _dev_ptr(offsets, "offsets", (torch.int64,)),
+                _dev_ptr(lengths, "lengths", (torch.int32,)),
+                _dev_ptr(dst, "dst", (torch.uint8, torch.int8)),
+                _dev_ptr(dst_offsets, "dst_offsets", (torch.int64,), n),
+                _dev_ptr(out_len, "out_len"), _dev_ptr(status, "status"), n,
+                max(0, min(int(max_len), 0xFFFFFFFF)), _stream_handle(stream, dev))
+        _check("lvkv_snappy_compress_device", rc)
+    return dst, dst_offsets, out_len, status
+
+
+def snappy_uncompressed_length(src, offsets, lengths, *, stream=None):
+    """Batched port::Snappy_GetUncompressedLength (port/port_stdcxx.h:108-119).
+    Returns (lengths int32 as u32 bit patterns, status uint8: SNAPPY_OK /
+    SNAPPY_BAD_LENGTH)."""
+    torch = _torch()
+    n = offsets.numel()
+    dev = src.device
+    ulen = torch.zeros(n, dtype=torch.int32, device=dev)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    if n:
+        with torch.cuda.device(dev):
+            rc = _lib.lvkv_snappy_uncompressed_length_device(
+                _dev_ptr(src, "src", (torch.uint8, torch.int8)),
+                _dev_ptr(offsets, "offsets", (torch.int64,)),
+                _dev_ptr(lengths, "lengths", (torch.int32,), n),
+                _dev_ptr(ulen, "ulen"), _dev_ptr(status, "status"), n,
+                _stream_handle(stream, dev))
+        _check("lvkv_snappy_uncompressed_length_device", rc)
+    return ulen, status
+
+
+def snappy_uncompress(src, offsets, lengths, *, max_ulen: int, dst=None, dst_offsets=None,
+                      dst_caps=None, stream=None):
+    """Batched port::Snappy_Uncompress (port/port_stdcxx.h:121-133) as
+    ReadBlock runs it (table/format.cc:120-135). Without dst, every stream
+    gets max_ulen bytes. Returns (dst uint8, dst_offsets int64, uncompressed
+    lengths int32, status uint8: SNAPPY_OK / BAD_LENGTH / BAD_CONTENTS /
+    CAPACITY / TOO_LARGE)."""
+    torch = _torch()
+    n = offsets.numel()
+    dev = src.device
+    if not 0 <= max_ulen <= SNAPPY_MAX_BLOCK:
+        raise ValueError(f"max_ulen must be in [0, {SNAPPY_MAX_BLOCK}]")
+    if dst is None:
+        dst_caps = torch.full((n,), max_ulen, dtype=torch.int32, device=dev)
+        dst_offsets = torch.arange(n, dtype=torch.int64, device=dev) * max_ulen
+        dst = torch.empty(max(1, n * max_ulen), dtype=torch.uint8, device=dev)
+    elif dst_offsets is None or dst_caps is None:
+        raise ValueError("dst needs dst_offsets and dst_caps")
+    out_len = torch.zeros(n, dtype=torch.int32, device=dev)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    if n:
+        with torch.cuda.device(dev):
+            rc = _lib.lvkv_snappy_uncompress_device(
+                _dev_ptr(src, "src", (torch.uint8, torch.int8)),
+                _dev_ptr(offsets, "offsets", (torch.int64,)),
+                _dev_ptr(lengths, "lengths", (torch.int32,), n),
+                _dev_ptr(dst, "dst", (torch.uint8, torch.int8)),
+                _dev_ptr(dst_offsets, "dst_offsets", (torch.int64,), n),
+                _dev_ptr(dst_caps, "dst_caps", (torch.int32,), n),
+                _dev_ptr(out_len, "out_len"), _dev_ptr(status, "status"), n, max_ulen,
+                _stream_handle(stream, dev))
+        _check("lvkv_snappy_uncompress_device", rc)
+    return dst, dst_offsets, out_len, status
 
 
 class LogReport(ctypes.Structure):

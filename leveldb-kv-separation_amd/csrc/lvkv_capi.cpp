@@ -18,6 +18,7 @@
 
 #include "lvkv_crc32c.h"
 #include "lvkv_kernel_args.h"
+#include "lvkv_snappy.h"
 #include "lvkv_tables.h"
 
 namespace lvkv {
@@ -74,6 +75,14 @@ hipError_t launch_log_assemble(const uint32_t* events, const uint64_t* item_off,
 size_t log_asm_scratch_bytes(size_t max_items);
 hipError_t launch_crc32c_long(const KernelArgs& args, const uint32_t* zpow,
                               const uint32_t* lane_cols, int num_groups, hipStream_t stream);
+hipError_t launch_snappy_compress(const uint8_t* src, const uint64_t* src_off,
+                                  const uint32_t* src_len, uint8_t* dst, const uint64_t* dst_off,
+                                  uint32_t* dst_len, uint8_t* status, uint32_t nblocks,
+                                  uint32_t max_len, hipStream_t stream);
+hipError_t launch_snappy_uncompress(const uint8_t* src, const uint64_t* src_off,
+                                    const uint32_t* src_len, uint8_t* dst, const uint64_t* dst_off,
+                                    const uint32_t* dst_cap, uint32_t* out_len, uint8_t* status,
+                                    uint32_t nblocks, uint32_t max_ulen, hipStream_t stream);
 int compact_capacity(int cfg);
 int compact_occupancy(int cfg);
 // 8 waves x 3 chains, two workgroups per CU, generated lane tables
@@ -833,6 +842,59 @@ int lvkv_log_verify_device(const void* d_file, const uint64_t* d_hdr_offsets,
   a.out_status = d_status;
   a.mode = kModeLogVerify;
   return run_batch(a, nrecords, static_cast<hipStream_t>(stream));
+}
+
+size_t lvkv_snappy_max_compressed_length(size_t n) { return 32 + n + n / 6; }
+
+int lvkv_snappy_compress_device(const void* d_src, const uint64_t* d_src_off,
+                                const uint32_t* d_src_len, void* d_dst,
+                                const uint64_t* d_dst_off, uint32_t* d_dst_len,
+                                uint8_t* d_status, size_t nblocks, uint32_t max_len,
+                                void* stream) {
+  if (nblocks == 0) return LVKV_OK;
+  if (!d_src || !d_src_off || !d_src_len || !d_dst || !d_dst_off || !d_dst_len || !d_status ||
+      nblocks > kMaxBlocksPerLaunch)
+    return LVKV_ERR_INVALID;
+  int rc = LVKV_OK;
+  if (current_ctx(&rc) == nullptr) return rc;
+  const hipError_t e = launch_snappy_compress(
+      static_cast<const uint8_t*>(d_src), d_src_off, d_src_len, static_cast<uint8_t*>(d_dst),
+      d_dst_off, d_dst_len, d_status, static_cast<uint32_t>(nblocks), max_len,
+      static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? LVKV_OK : hip_fail(e);
+}
+
+int lvkv_snappy_uncompressed_length_device(const void* d_src, const uint64_t* d_src_off,
+                                           const uint32_t* d_src_len, uint32_t* d_ulen,
+                                           uint8_t* d_status, size_t nblocks, void* stream) {
+  if (nblocks == 0) return LVKV_OK;
+  if (!d_src || !d_src_off || !d_src_len || !d_ulen || !d_status ||
+      nblocks > kMaxBlocksPerLaunch)
+    return LVKV_ERR_INVALID;
+  int rc = LVKV_OK;
+  if (current_ctx(&rc) == nullptr) return rc;
+  const hipError_t e = launch_snappy_uncompress(
+      static_cast<const uint8_t*>(d_src), d_src_off, d_src_len, nullptr, nullptr, nullptr,
+      d_ulen, d_status, static_cast<uint32_t>(nblocks), 0, static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? LVKV_OK : hip_fail(e);
+}
+
+int lvkv_snappy_uncompress_device(const void* d_src, const uint64_t* d_src_off,
+                                  const uint32_t* d_src_len, void* d_dst,
+                                  const uint64_t* d_dst_off, const uint32_t* d_dst_cap,
+                                  uint32_t* d_out_len, uint8_t* d_status, size_t nblocks,
+                                  uint32_t max_ulen, void* stream) {
+  if (nblocks == 0) return LVKV_OK;
+  if (!d_src || !d_src_off || !d_src_len || !d_dst || !d_dst_off || !d_dst_cap || !d_out_len ||
+      !d_status || nblocks > kMaxBlocksPerLaunch || max_ulen > LVKV_SNAPPY_MAX_BLOCK)
+    return LVKV_ERR_INVALID;
+  int rc = LVKV_OK;
+  if (current_ctx(&rc) == nullptr) return rc;
+  const hipError_t e = launch_snappy_uncompress(
+      static_cast<const uint8_t*>(d_src), d_src_off, d_src_len, static_cast<uint8_t*>(d_dst),
+      d_dst_off, d_dst_cap, d_out_len, d_status, static_cast<uint32_t>(nblocks), max_ulen,
+      static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? LVKV_OK : hip_fail(e);
 }
 
 int lvkv_crc32c_batch_host(const void* h_base, const uint64_t* offsets,

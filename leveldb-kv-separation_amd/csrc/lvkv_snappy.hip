@@ -1,0 +1,427 @@
+// Snappy block codec on the device: the codec
+// LevelDB calls around the block CRC when a table is written or read with
+// kSnappyCompression -- port::Snappy_Compress / Snappy_GetUncompressedLength /
+// Snappy_Uncompress (port/port_stdcxx.h:90-133) behind TableBuilder::
+// WriteBlock (table/table_builder.cc:151-168) and ReadBlock
+// (table/format.cc:120-136). The as-built reference has HAVE_SNAPPY=0; the
+// codec is google/snappy, restated from the published algorithm of the
+// version in this image (snappy 1.1.8, /opt/conda/lib): the compressor emits
+// the same bytes as snappy::RawCompress 1.1.8, the decompressor accepts and
+// rejects exactly what snappy::RawUncompress does (oracle/snappy_oracle.py,
+// tests/test_snappy.py).
+//
+// One wave per block (a 64-thread workgroup), its bytes staged in LDS
+// (dynamic, sized from the caller's largest block): the codec is a serial
+// chain per block (each element's place depends on the one before), so the
+// wave runs it with wave-uniform control flow, and its 64 lanes copy
+// literals, extend matches 64 bytes at a time (a ballot finds the first
+// difference) and write the result out. Blocks are independent: the grid is
+// one workgroup per block.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lvkv_snappy.h"
+
+namespace lvkv {
+namespace {
+
+constexpr uint32_t kFrag = 1u << 16;       // kBlockSize: fragments compressed alone
+constexpr uint32_t kMaxTable = 1u << 14;   // kMaxHashTableSize
+constexpr uint32_t kMul = 0x1e35a7bdu;
+
+__device__ __forceinline__ uint32_t table_size(uint32_t n) {
+  uint32_t t = 256;
+  while (t < kMaxTable && t < n) t <<= 1;
+  return t;
+}
+
+// Little-endian dword at byte p of an LDS buffer (4-byte aligned base, padded
+// by 8 bytes): two aligned reads.
+__device__ __forceinline__ uint32_t ld32(const uint8_t* b, uint32_t p) {
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(b + (p & ~3u));
+  return __builtin_amdgcn_alignbyte(d[1], d[0], p & 3u);
+}
+__device__ __forceinline__ uint64_t ld64(const uint8_t* b, uint32_t p) {
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(b + (p & ~3u));
+  const uint32_t s = p & 3u;
+  const uint32_t lo = __builtin_amdgcn_alignbyte(d[1], d[0], s);
+  const uint32_t hi = __builtin_amdgcn_alignbyte(d[2], d[1], s);
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// Block b's bytes [0, n) from global memory into LDS (dword loads; the
+// last 0-3 bytes one by one), zero padding after them.
+__device__ __forceinline__ void stage(uint8_t* dst, const uint8_t* src, uint32_t n, uint32_t pad,
+                                      uint32_t lane) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(src);
+  if ((a & 3u) == 0) {
+    const uint32_t nd = n >> 2;
+    for (uint32_t i = lane; i < nd; i += 64)
+      reinterpret_cast<uint32_t*>(dst)[i] = reinterpret_cast<const uint32_t*>(src)[i];
+    for (uint32_t i = 4 * nd + lane; i < n; i += 64) dst[i] = src[i];
+  } else {
+    for (uint32_t i = lane; i < n; i += 64) dst[i] = src[i];
+  }
+  for (uint32_t i = n + lane; i < n + pad; i += 64) dst[i] = 0;
+}
+
+// ---- compression (snappy::RawCompress 1.1.8) ------------------------------
+
+struct Out {
+  uint8_t* p;  // the block's output
+  uint32_t n;  // bytes written
+};
+
+// A literal: tag (+ 1-4 length bytes) by lane 0, the bytes by every lane.
+__device__ __forceinline__ void emit_literal(Out& o, const uint8_t* in, uint32_t from,
+                                             uint32_t len, uint32_t lane) {
+  const uint32_t n = len - 1;
+  uint32_t h;
+  if (n < 60) {
+    if (lane == 0) o.p[o.n] = static_cast<uint8_t>(n << 2);
+    h = 1;
+  } else {
+    const uint32_t count = ((31u - __builtin_clz(n)) >> 3) + 1u;
+    if (lane == 0) {
+      o.p[o.n] = static_cast<uint8_t>((59u + count) << 2);
+      for (uint32_t k = 0; k < count; ++k) o.p[o.n + 1 + k] = static_cast<uint8_t>(n >> (8 * k));
+    }
+    h = 1 + count;
+  }
+  for (uint32_t k = lane; k < len; k += 64) o.p[o.n + h + k] = in[from + k];
+  o.n += h + len;
+}
+
+__device__ __forceinline__ void emit_copy_at_most_64(Out& o, uint32_t off, uint32_t len, bool lt12,
+                                                     uint32_t lane) {
+  if (lt12 && off < 2048) {
+    if (lane == 0) {
+      o.p[o.n] = static_cast<uint8_t>(1u + ((len - 4u) << 2) + ((off >> 3) & 0xe0u));
+      o.p[o.n + 1] = static_cast<uint8_t>(off);
+    }
+    o.n += 2;
+  } else {
+    const uint32_t u = 2u + ((len - 1u) << 2) + (off << 8);
+    if (lane == 0) {
+      o.p[o.n] = static_cast<uint8_t>(u);
+      o.p[o.n + 1] = static_cast<uint8_t>(u >> 8);
+      o.p[o.n + 2] = static_cast<uint8_t>(u >> 16);
+    }
+    o.n += 3;
+  }
+}
+
+__device__ __forceinline__ void emit_copy(Out& o, uint32_t off, uint32_t len, uint32_t lane) {
+  if (len < 12) {
+    emit_copy_at_most_64(o, off, len, true, lane);
+    return;
+  }
+  while (len >= 68) {
+    emit_copy_at_most_64(o, off, 64, false, lane);
+    len -= 64;
+  }
+  if (len > 64) {
+    emit_copy_at_most_64(o, off, 60, false, lane);
+    len -= 60;
+  }
+  emit_copy_at_most_64(o, off, len, len < 12, lane);
+}
+
+// Bytes matching from a + 4 and b + 4 (b > a), b + 4 + result <= n: the
+// wave compares 64 bytes a step and the ballot of differences stops it.
+__device__ __forceinline__ uint32_t match_length(const uint8_t* in, uint32_t a, uint32_t b,
+                                                 uint32_t n, uint32_t lane) {
+  uint32_t m = 4;
+  for (;;) {
+    const uint32_t pb = b + m + lane;
+    const bool diff = pb >= n || in[a + m + lane] != in[pb];
+    const uint64_t bal = __ballot(diff);
+    if (bal != 0) return m + static_cast<uint32_t>(__builtin_ctzll(bal));
+    m += 64;
+  }
+}
+
+__device__ __forceinline__ uint32_t hash32(uint32_t v, uint32_t shift) {
+  return (v * kMul) >> shift;
+}
+
+// CompressFragment of frag = in[0, n) (n <= kFrag) with table (u16 x tsize in
+// LDS, zeroed here). Control flow is wave-uniform.
+__device__ void compress_fragment(const uint8_t* in, uint32_t n, uint16_t* table, Out& o,
+                                  uint32_t lane) {
+  const uint32_t tsize = table_size(n);
+  const uint32_t shift = 32u - (31u - __builtin_clz(tsize));
+  for (uint32_t i = lane; i < tsize; i += 64) table[i] = 0;
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the zeroes land first
+  uint32_t ip = 0, next_emit = 0;
+  if (n >= 15) {
+    const uint32_t ip_limit = n - 15;
+    ip = 1;
+    uint32_t next_hash = hash32(ld32(in, ip), shift);
+    for (;;) {
+      uint32_t skip = 32, next_ip = ip, cand = 0;
+      bool remainder = false;
+      for (;;) {
+        ip = next_ip;
+        const uint32_t h = next_hash;
+        const uint32_t step = skip >> 5;
+        skip += step;
+        next_ip = ip + step;
+        if (next_ip > ip_limit) {
+          remainder = true;
+          break;
+        }
+        next_hash = hash32(ld32(in, next_ip), shift);
+        cand = table[h];
+        table[h] = static_cast<uint16_t>(ip);
+        if (ld32(in, ip) == ld32(in, cand)) break;
+      }
+      if (remainder) break;
+      emit_literal(o, in, next_emit, ip - next_emit, lane);
+      uint64_t eight = 0;
+      for (;;) {
+        const uint32_t base = ip;
+        const uint32_t m = match_length(in, cand, ip, n, lane);
+        ip += m;
+        emit_copy(o, base - cand, m, lane);
+        next_emit = ip;
+        if (ip >= ip_limit) {
+          remainder = true;
+          break;
+        }
+        eight = ld64(in, ip - 1);
+        const uint32_t prev_hash = hash32(static_cast<uint32_t>(eight), shift);
+        table[prev_hash] = static_cast<uint16_t>(ip - 1);
+        const uint32_t cur = static_cast<uint32_t>(eight >> 8);
+        const uint32_t cur_hash = hash32(cur, shift);
+        cand = table[cur_hash];
+        const uint32_t cand_bytes = ld32(in, cand);
+        table[cur_hash] = static_cast<uint16_t>(ip);
+        if (cur != cand_bytes) break;
+      }
+      if (remainder) break;
+      next_hash = hash32(static_cast<uint32_t>(eight >> 16), shift);
+      ++ip;
+    }
+  }
+  if (next_emit < n) emit_literal(o, in, next_emit, n - next_emit, lane);
+}
+
+struct CompressArgs {
+  const uint8_t* src;
+  const uint64_t* src_off;
+  const uint32_t* src_len;
+  uint8_t* dst;
+  const uint64_t* dst_off;
+  uint32_t* dst_len;
+  uint8_t* status;
+  uint32_t nblocks;
+  uint32_t frag_cap;  // the largest fragment the LDS holds (<= kFrag)
+};
+
+__global__ void __launch_bounds__(64) snappy_compress_kernel(CompressArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t b = blockIdx.x;
+  if (b >= a.nblocks) return;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t len = a.src_len[b];
+  const uint8_t* src = a.src + a.src_off[b];
+  const uint32_t in_bytes = (a.frag_cap + 16u + 15u) & ~15u;
+  uint8_t* in = smem;
+  uint16_t* table = reinterpret_cast<uint16_t*>(smem + in_bytes);
+  if (min(len, kFrag) > a.frag_cap) {  // the caller's max_len was too small
+    if (lane == 0) {
+      a.dst_len[b] = 0;
+      a.status[b] = LVKV_SNAPPY_TOO_LARGE;
+    }
+    return;
+  }
+  Out o{a.dst + a.dst_off[b], 0};
+  // varint32 of the uncompressed length
+  uint32_t v = len;
+  while (v >= 128) {
+    if (lane == 0) o.p[o.n] = static_cast<uint8_t>(v | 128u);
+    ++o.n;
+    v >>= 7;
+  }
+  if (lane == 0) o.p[o.n] = static_cast<uint8_t>(v);
+  ++o.n;
+  for (uint32_t s = 0; s < len; s += kFrag) {
+    const uint32_t fn = min(kFrag, len - s);
+    stage(in, src + s, fn, 16, lane);
+    __builtin_amdgcn_s_waitcnt(0);
+    compress_fragment(in, fn, table, o, lane);
+    __builtin_amdgcn_s_waitcnt(0);
+  }
+  if (lane == 0) {
+    a.dst_len[b] = o.n;
+    a.status[b] = LVKV_SNAPPY_OK;
+  }
+}
+
+// ---- decompression (snappy::GetUncompressedLength / RawUncompress) --------
+
+struct UncompressArgs {
+  const uint8_t* src;
+  const uint64_t* src_off;
+  const uint32_t* src_len;
+  uint8_t* dst;
+  const uint64_t* dst_off;
+  const uint32_t* dst_cap;  // nullptr: lengths only
+  uint32_t* out_len;
+  uint8_t* status;
+  uint32_t nblocks;
+  uint32_t out_cap;  // the largest output the LDS holds
+};
+
+// The varint32 preamble at in[0, n): its value and size, or size 0 (bad).
+__device__ __forceinline__ uint32_t preamble(const uint8_t* in, uint32_t n, uint32_t* value) {
+  uint32_t v = 0;
+  for (uint32_t i = 0; i < 5 && i < n; ++i) {
+    const uint32_t c = in[i];
+    if (i == 4 && c >= 16) return 0;  // past 32 bits (or a continuation)
+    v |= (c & 127u) << (7 * i);
+    if (c < 128) {
+      *value = v;
+      return i + 1;
+    }
+  }
+  return 0;
+}
+
+__global__ void __launch_bounds__(64) snappy_uncompress_kernel(UncompressArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t b = blockIdx.x;
+  if (b >= a.nblocks) return;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t n = a.src_len[b];
+  const uint8_t* src = a.src + a.src_off[b];
+  // a valid stream of at most out_cap bytes is at most 2 out_cap + 5 bytes
+  // (a one-byte literal costs two); a longer one cannot be valid
+  const uint32_t in_cap = 2u * a.out_cap + 8u;
+  const uint32_t in_bytes = (in_cap + 16u + 15u) & ~15u;
+  uint8_t* in = smem;
+  uint8_t* out = smem + in_bytes;
+  // the preamble from global memory (at most 5 bytes)
+  uint32_t ulen = 0;
+  const uint32_t pl = preamble(src, n, &ulen);
+  auto finish = [&](uint32_t st, uint32_t ol) {
+    if (lane == 0) {
+      a.status[b] = static_cast<uint8_t>(st);
+      a.out_len[b] = ol;
+    }
+  };
+  if (pl == 0) return finish(LVKV_SNAPPY_BAD_LENGTH, 0);  // format.cc:122-124
+  if (a.dst_cap == nullptr) return finish(LVKV_SNAPPY_OK, ulen);
+  if (ulen > a.dst_cap[b]) return finish(LVKV_SNAPPY_CAPACITY, ulen);
+  if (ulen > a.out_cap) return finish(LVKV_SNAPPY_TOO_LARGE, ulen);
+  // a stream longer than the staging area is valid only with padded
+  // (non-canonical) elements -- no snappy encoder writes one; the caller
+  // decodes it on the host
+  if (n > in_cap) return finish(LVKV_SNAPPY_TOO_LARGE, ulen);
+  stage(in, src, n, 16, lane);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  uint32_t ip = pl, op = 0;
+  bool ok = true;
+  while (ip < n) {
+    const uint64_t t8 = ld64(in, ip);
+    const uint32_t tag = static_cast<uint32_t>(t8) & 255u;
+    ++ip;
+    if ((tag & 3u) == 0) {
+      uint64_t len64 = (tag >> 2) + 1u;
+      if (len64 > 60) {
+        const uint32_t k = static_cast<uint32_t>(len64) - 60u;
+        if (ip + k > n) {
+          ok = false;
+          break;
+        }
+        // (64-bit: a 4-byte length of 0xffffffff is 2^32, not 0)
+        len64 = ((t8 >> 8) & ((uint64_t{1} << (8 * k)) - 1u)) + 1u;
+        ip += k;
+      }
+      if (len64 > n - ip || len64 > ulen - op) {
+        ok = false;
+        break;
+      }
+      const uint32_t len = static_cast<uint32_t>(len64);
+      for (uint32_t k = lane; k < len; k += 64) out[op + k] = in[ip + k];
+      ip += len;
+      op += len;
+      continue;
+    }
+    uint32_t len, off;
+    if ((tag & 3u) == 1) {
+      if (ip + 1 > n) {
+        ok = false;
+        break;
+      }
+      len = ((tag >> 2) & 7u) + 4u;
+      off = ((tag >> 5) << 8) | static_cast<uint32_t>((t8 >> 8) & 255u);
+      ip += 1;
+    } else if ((tag & 3u) == 2) {
+      if (ip + 2 > n) {
+        ok = false;
+        break;
+      }
+      len = (tag >> 2) + 1u;
+      off = static_cast<uint32_t>((t8 >> 8) & 0xffffu);
+      ip += 2;
+    } else {
+      if (ip + 4 > n) {
+        ok = false;
+        break;
+      }
+      len = (tag >> 2) + 1u;
+      off = static_cast<uint32_t>((t8 >> 8) & 0xffffffffu);
+      ip += 4;
+    }
+    if (off == 0 || off > op || len > ulen - op) {
+      ok = false;
+      break;
+    }
+    // len <= 64: one lane a byte; an overlapping copy repeats its last
+    // `off` bytes (byte k = out[op - off + k % off])
+    if (lane < len) {
+      const uint32_t k = off >= len ? lane : lane % off;
+      out[op + lane] = out[op - off + k];
+    }
+    op += len;
+  }
+  if (!ok || op != ulen) return finish(LVKV_SNAPPY_BAD_CONTENTS, ulen);
+  __syncthreads();
+  uint8_t* dst = a.dst + a.dst_off[b];
+  for (uint32_t k = lane; k < ulen; k += 64) dst[k] = out[k];
+  finish(LVKV_SNAPPY_OK, ulen);
+}
+
+}  // namespace
+
+hipError_t launch_snappy_compress(const uint8_t* src, const uint64_t* src_off,
+                                  const uint32_t* src_len, uint8_t* dst, const uint64_t* dst_off,
+                                  uint32_t* dst_len, uint8_t* status, uint32_t nblocks,
+                                  uint32_t max_len, hipStream_t stream) {
+  CompressArgs a{src, src_off, src_len, dst, dst_off, dst_len, status, nblocks, 0};
+  a.frag_cap = max(16u, min(max_len, kFrag));
+  const uint32_t in_bytes = (a.frag_cap + 16u + 15u) & ~15u;
+  uint32_t t = 256;
+  while (t < kMaxTable && t < a.frag_cap) t <<= 1;
+  const size_t lds = in_bytes + 2u * t;
+  hipLaunchKernelGGL(snappy_compress_kernel, dim3(nblocks), dim3(64), lds, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_snappy_uncompress(const uint8_t* src, const uint64_t* src_off,
+                                    const uint32_t* src_len, uint8_t* dst, const uint64_t* dst_off,
+                                    const uint32_t* dst_cap, uint32_t* out_len, uint8_t* status,
+                                    uint32_t nblocks, uint32_t max_ulen, hipStream_t stream) {
+  UncompressArgs a{src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks, 0};
+  a.out_cap = dst_cap == nullptr ? 0u : max(16u, max_ulen);
+  const size_t lds = dst_cap == nullptr ? 16u
+                                        : ((2u * a.out_cap + 8u + 16u + 15u) & ~15u) +
+                                              ((a.out_cap + 15u) & ~15u);
+  hipLaunchKernelGGL(snappy_uncompress_kernel, dim3(nblocks), dim3(64), lds, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace lvkv
