@@ -38,8 +38,8 @@ extern "C" {
 #define LVKV_SNAPPY_CAPACITY 3     /* the block's uncompressed length exceeds d_dst_cap[i]
                                       (out_len says how much it needs) */
 #define LVKV_SNAPPY_TOO_LARGE 4    /* beyond the call's max_len / max_ulen (or, for a
-                                      stream, longer than 2 max_ulen + 8 bytes: valid only
-                                      with padded elements no encoder writes) */
+                                      stream, longer than MaxCompressedLength(max_ulen):
+                                      valid only with padded elements no encoder writes) */
 
 #define LVKV_SNAPPY_MAX_BLOCK 49152u /* largest max_ulen of the decompressor */
 

@@ -29,6 +29,25 @@ constexpr uint32_t kFrag = 1u << 16;       // kBlockSize: fragments compressed a
 constexpr uint32_t kMaxTable = 1u << 14;   // kMaxHashTableSize
 constexpr uint32_t kMul = 0x1e35a7bdu;
 
+// Offsets of the literal search's probes after a reset (skip = 32, step =
+// skip >> 5, skip += step), clamped at 0xffff: any later probe lies past
+// every ip_limit. 267 offsets reach past 64 KiB; the table holds 5 windows.
+constexpr uint32_t kProbes = 5 * 64 + 1;
+struct ProbeOffsets {
+  uint16_t v[kProbes + 7];
+  constexpr ProbeOffsets() : v() {
+    uint32_t off = 0, skip = 32;
+    for (uint32_t i = 0; i < kProbes + 7; ++i) {
+      v[i] = static_cast<uint16_t>(off < 0xffffu ? off : 0xffffu);
+      if (off < 0xffffu) {
+        off += skip >> 5;
+        skip += skip >> 5;
+      }
+    }
+  }
+};
+__constant__ ProbeOffsets kProbe;
+
 __device__ __forceinline__ uint32_t table_size(uint32_t n) {
   uint32_t t = 256;
   while (t < kMaxTable && t < n) t <<= 1;
@@ -49,20 +68,21 @@ __device__ __forceinline__ uint64_t ld64(const uint8_t* b, uint32_t p) {
   return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
-// Block b's bytes [0, n) from global memory into LDS (dword loads; the
-// last 0-3 bytes one by one), zero padding after them.
+// Block b's bytes [0, n) from global memory into LDS (4-aligned), zero
+// padding after them. Aligned dword loads at any source alignment: LDS
+// dword i = alignbyte of source dwords i and i+1 (the second only where it
+// holds bytes of the block, so nothing past the block's last dword is read).
 __device__ __forceinline__ void stage(uint8_t* dst, const uint8_t* src, uint32_t n, uint32_t pad,
                                       uint32_t lane) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(src);
-  if ((a & 3u) == 0) {
-    const uint32_t nd = n >> 2;
-    for (uint32_t i = lane; i < nd; i += 64)
-      reinterpret_cast<uint32_t*>(dst)[i] = reinterpret_cast<const uint32_t*>(src)[i];
-    for (uint32_t i = 4 * nd + lane; i < n; i += 64) dst[i] = src[i];
-  } else {
-    for (uint32_t i = lane; i < n; i += 64) dst[i] = src[i];
+  const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src)) & 3u;
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(src - mis);
+  const uint32_t nd = (n + 3u) >> 2;
+  for (uint32_t i = lane; i < nd; i += 64) {
+    const uint32_t lo = s[i];
+    const uint32_t hi = (mis != 0 && 4u * (i + 1u) < mis + n) ? s[i + 1] : 0u;
+    reinterpret_cast<uint32_t*>(dst)[i] = __builtin_amdgcn_alignbyte(hi, lo, mis);
   }
-  for (uint32_t i = n + lane; i < n + pad; i += 64) dst[i] = 0;
+  for (uint32_t i = n + lane; i < n + pad; i += 64) dst[i] = 0;  // (pad >= 3)
 }
 
 // ---- compression (snappy::RawCompress 1.1.8) ------------------------------
@@ -145,10 +165,79 @@ __device__ __forceinline__ uint32_t hash32(uint32_t v, uint32_t shift) {
   return (v * kMul) >> shift;
 }
 
+// The literal search of CompressFragment (the loop that hashes ip, swaps it
+// into the table and compares 4 bytes with the old entry, stepping by
+// skip >> 5 with skip += step), 64 probes a step, one a lane. The probe
+// positions after a reset do not depend on the data: probe k sits at
+// base + probe[k] (kProbe), and is made only if probe k+1 is <= ip_limit.
+// Probe k's candidate is the table entry as probes 0..k-1 left it: the
+// entry before the step, or the last earlier lane with the same hash. The
+// lanes write their positions, read them back, and a lane that lost a write
+// marks a collision group, resolved with ballots (rare: 64 hashes into
+// >= 256 entries). The first lane whose 4 bytes match ends the search; the
+// writes of the lanes after it are undone, so the table ends exactly as the
+// sequential loop leaves it. Returns false at emit_remainder.
+__device__ __forceinline__ bool search_probes(const uint8_t* in, uint16_t* table,
+                                              const uint16_t* probe, uint32_t base,
+                                              uint32_t ip_limit, uint32_t shift, uint32_t lane,
+                                              uint32_t* out_ip, uint32_t* out_cand) {
+  const uint64_t lt = (uint64_t{1} << lane) - 1u;  // lanes below this one
+  for (uint32_t n0 = 0;; n0 += 64) {
+    const uint32_t p = base + probe[n0 + lane];
+    const bool valid = base + probe[n0 + lane + 1] <= ip_limit;
+    const uint64_t vmask = __ballot(valid);
+    const uint32_t v = ld32(in, valid ? p : 0u);
+    const uint32_t h = hash32(v, shift);
+    uint32_t c0 = 0;
+    if (valid) c0 = table[h];
+    if (valid) table[h] = static_cast<uint16_t>(p);
+    // (a compiler barrier: the read-back must see which lane's write
+    // landed, not be forwarded from this lane's own store)
+    asm volatile("" ::: "memory");
+    const uint32_t r = valid ? table[h] : p;
+    uint64_t losers = __ballot(valid && r != p);
+    const uint64_t groups = losers;
+    uint32_t cand = c0;
+    while (losers) {
+      const uint32_t hv = __builtin_amdgcn_readlane(h, __builtin_ctzll(losers));
+      const uint64_t g = __ballot(valid && h == hv);
+      losers &= ~g;
+      const uint64_t prev = g & lt;
+      const bool mine = ((g >> lane) & 1u) && prev != 0;
+      const uint32_t pp = __shfl(p, mine ? 63 - __builtin_clzll(prev) : lane);
+      if (mine) cand = pp;
+    }
+    const uint32_t vc = ld32(in, valid ? cand : 0u);
+    const uint64_t mm = __ballot(valid && vc == v);
+    const uint32_t km = mm ? __builtin_ctzll(mm) : 64u;
+    const uint32_t ki = ~vmask ? __builtin_ctzll(~vmask) : 64u;
+    if (ki < km) return false;  // the search runs past ip_limit first
+    // K = the last probe made
+    const uint64_t upto = km < 64 ? (uint64_t{2} << km) - 1u : ~uint64_t{0};
+    if (valid && !((upto >> lane) & 1u)) table[h] = static_cast<uint16_t>(c0);
+    uint64_t gl = groups;
+    while (gl) {
+      const uint32_t hv = __builtin_amdgcn_readlane(h, __builtin_ctzll(gl));
+      const uint64_t g = __ballot(valid && h == hv);
+      gl &= ~g;
+      const uint64_t made = g & upto;
+      if (made) {
+        const uint32_t pl = __builtin_amdgcn_readlane(p, 63 - __builtin_clzll(made));
+        if (lane == 0) table[hv] = static_cast<uint16_t>(pl);
+      }
+    }
+    if (km < 64) {
+      *out_ip = __builtin_amdgcn_readlane(p, km);
+      *out_cand = __builtin_amdgcn_readlane(cand, km);
+      return true;
+    }
+  }
+}
+
 // CompressFragment of frag = in[0, n) (n <= kFrag) with table (u16 x tsize in
 // LDS, zeroed here). Control flow is wave-uniform.
-__device__ void compress_fragment(const uint8_t* in, uint32_t n, uint16_t* table, Out& o,
-                                  uint32_t lane) {
+__device__ void compress_fragment(const uint8_t* in, uint32_t n, uint16_t* table,
+                                  const uint16_t* probe, Out& o, uint32_t lane) {
   const uint32_t tsize = table_size(n);
   const uint32_t shift = 32u - (31u - __builtin_clz(tsize));
   for (uint32_t i = lane; i < tsize; i += 64) table[i] = 0;
@@ -157,26 +246,10 @@ __device__ void compress_fragment(const uint8_t* in, uint32_t n, uint16_t* table
   if (n >= 15) {
     const uint32_t ip_limit = n - 15;
     ip = 1;
-    uint32_t next_hash = hash32(ld32(in, ip), shift);
     for (;;) {
-      uint32_t skip = 32, next_ip = ip, cand = 0;
+      uint32_t cand = 0;
       bool remainder = false;
-      for (;;) {
-        ip = next_ip;
-        const uint32_t h = next_hash;
-        const uint32_t step = skip >> 5;
-        skip += step;
-        next_ip = ip + step;
-        if (next_ip > ip_limit) {
-          remainder = true;
-          break;
-        }
-        next_hash = hash32(ld32(in, next_ip), shift);
-        cand = table[h];
-        table[h] = static_cast<uint16_t>(ip);
-        if (ld32(in, ip) == ld32(in, cand)) break;
-      }
-      if (remainder) break;
+      if (!search_probes(in, table, probe, ip, ip_limit, shift, lane, &ip, &cand)) break;
       emit_literal(o, in, next_emit, ip - next_emit, lane);
       uint64_t eight = 0;
       for (;;) {
@@ -200,7 +273,6 @@ __device__ void compress_fragment(const uint8_t* in, uint32_t n, uint16_t* table
         if (cur != cand_bytes) break;
       }
       if (remainder) break;
-      next_hash = hash32(static_cast<uint32_t>(eight >> 16), shift);
       ++ip;
     }
   }
@@ -228,7 +300,8 @@ __global__ void __launch_bounds__(64) snappy_compress_kernel(CompressArgs a) {
   const uint8_t* src = a.src + a.src_off[b];
   const uint32_t in_bytes = (a.frag_cap + 16u + 15u) & ~15u;
   uint8_t* in = smem;
-  uint16_t* table = reinterpret_cast<uint16_t*>(smem + in_bytes);
+  uint16_t* probe = reinterpret_cast<uint16_t*>(smem + in_bytes);
+  uint16_t* table = probe + ((kProbes + 7) & ~7u);
   if (min(len, kFrag) > a.frag_cap) {  // the caller's max_len was too small
     if (lane == 0) {
       a.dst_len[b] = 0;
@@ -246,11 +319,12 @@ __global__ void __launch_bounds__(64) snappy_compress_kernel(CompressArgs a) {
   }
   if (lane == 0) o.p[o.n] = static_cast<uint8_t>(v);
   ++o.n;
+  for (uint32_t i = lane; i < kProbes; i += 64) probe[i] = kProbe.v[i];
   for (uint32_t s = 0; s < len; s += kFrag) {
     const uint32_t fn = min(kFrag, len - s);
     stage(in, src + s, fn, 16, lane);
     __builtin_amdgcn_s_waitcnt(0);
-    compress_fragment(in, fn, table, o, lane);
+    compress_fragment(in, fn, table, probe, o, lane);
     __builtin_amdgcn_s_waitcnt(0);
   }
   if (lane == 0) {
@@ -274,6 +348,11 @@ struct UncompressArgs {
   uint32_t out_cap;  // the largest output the LDS holds
 };
 
+// snappy::MaxCompressedLength: the longest stream the decompressor stages.
+__host__ __device__ constexpr uint32_t snappy_in_cap(uint32_t out_cap) {
+  return 32u + out_cap + out_cap / 6u;
+}
+
 // The varint32 preamble at in[0, n): its value and size, or size 0 (bad).
 __device__ __forceinline__ uint32_t preamble(const uint8_t* in, uint32_t n, uint32_t* value) {
   uint32_t v = 0;
@@ -296,32 +375,33 @@ __global__ void __launch_bounds__(64) snappy_uncompress_kernel(UncompressArgs a)
   const uint32_t lane = threadIdx.x;
   const uint32_t n = a.src_len[b];
   const uint8_t* src = a.src + a.src_off[b];
-  // a valid stream of at most out_cap bytes is at most 2 out_cap + 5 bytes
-  // (a one-byte literal costs two); a longer one cannot be valid
-  const uint32_t in_cap = 2u * a.out_cap + 8u;
+  // the staging area holds MaxCompressedLength(out_cap) bytes: every stream
+  // a snappy encoder writes for out_cap bytes
+  const uint32_t in_cap = snappy_in_cap(a.out_cap);
   const uint32_t in_bytes = (in_cap + 16u + 15u) & ~15u;
   uint8_t* in = smem;
   uint8_t* out = smem + in_bytes;
-  // the preamble from global memory (at most 5 bytes)
-  uint32_t ulen = 0;
-  const uint32_t pl = preamble(src, n, &ulen);
   auto finish = [&](uint32_t st, uint32_t ol) {
     if (lane == 0) {
       a.status[b] = static_cast<uint8_t>(st);
       a.out_len[b] = ol;
     }
   };
+  uint32_t ulen = 0, pl;
+  const bool staged = a.dst_cap != nullptr && n <= in_cap;
+  if (staged) {  // the preamble from LDS, after one round trip for the lot
+    stage(in, src, n, 16, lane);
+    pl = preamble(in, n, &ulen);
+  } else {  // (at most 5 bytes from global memory)
+    pl = preamble(src, n, &ulen);
+  }
   if (pl == 0) return finish(LVKV_SNAPPY_BAD_LENGTH, 0);  // format.cc:122-124
   if (a.dst_cap == nullptr) return finish(LVKV_SNAPPY_OK, ulen);
   if (ulen > a.dst_cap[b]) return finish(LVKV_SNAPPY_CAPACITY, ulen);
   if (ulen > a.out_cap) return finish(LVKV_SNAPPY_TOO_LARGE, ulen);
-  // a stream longer than the staging area is valid only with padded
-  // (non-canonical) elements -- no snappy encoder writes one; the caller
-  // decodes it on the host
-  if (n > in_cap) return finish(LVKV_SNAPPY_TOO_LARGE, ulen);
-  stage(in, src, n, 16, lane);
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
+  // a longer stream is valid only with padded (non-canonical) elements --
+  // no snappy encoder writes one; the caller decodes it on the host
+  if (!staged) return finish(LVKV_SNAPPY_TOO_LARGE, ulen);
   uint32_t ip = pl, op = 0;
   bool ok = true;
   while (ip < n) {
@@ -389,9 +469,15 @@ __global__ void __launch_bounds__(64) snappy_uncompress_kernel(UncompressArgs a)
     op += len;
   }
   if (!ok || op != ulen) return finish(LVKV_SNAPPY_BAD_CONTENTS, ulen);
-  __syncthreads();
   uint8_t* dst = a.dst + a.dst_off[b];
-  for (uint32_t k = lane; k < ulen; k += 64) dst[k] = out[k];
+  uint32_t k0 = 0;
+  if ((reinterpret_cast<uintptr_t>(dst) & 3u) == 0) {
+    const uint32_t nd = ulen >> 2;
+    for (uint32_t i = lane; i < nd; i += 64)
+      reinterpret_cast<uint32_t*>(dst)[i] = reinterpret_cast<const uint32_t*>(out)[i];
+    k0 = 4u * nd;
+  }
+  for (uint32_t k = k0 + lane; k < ulen; k += 64) dst[k] = out[k];
   finish(LVKV_SNAPPY_OK, ulen);
 }
 
@@ -406,7 +492,7 @@ hipError_t launch_snappy_compress(const uint8_t* src, const uint64_t* src_off,
   const uint32_t in_bytes = (a.frag_cap + 16u + 15u) & ~15u;
   uint32_t t = 256;
   while (t < kMaxTable && t < a.frag_cap) t <<= 1;
-  const size_t lds = in_bytes + 2u * t;
+  const size_t lds = in_bytes + 2u * ((kProbes + 7) & ~7u) + 2u * t;
   hipLaunchKernelGGL(snappy_compress_kernel, dim3(nblocks), dim3(64), lds, stream, a);
   return hipGetLastError();
 }
@@ -418,7 +504,7 @@ hipError_t launch_snappy_uncompress(const uint8_t* src, const uint64_t* src_off,
   UncompressArgs a{src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks, 0};
   a.out_cap = dst_cap == nullptr ? 0u : max(16u, max_ulen);
   const size_t lds = dst_cap == nullptr ? 16u
-                                        : ((2u * a.out_cap + 8u + 16u + 15u) & ~15u) +
+                                        : ((snappy_in_cap(a.out_cap) + 16u + 15u) & ~15u) +
                                               ((a.out_cap + 15u) & ~15u);
   hipLaunchKernelGGL(snappy_uncompress_kernel, dim3(nblocks), dim3(64), lds, stream, a);
   return hipGetLastError();

@@ -173,7 +173,7 @@ def _expected_device_verdict(lvkv, d, v, cap):
     ulen = so.uncompressed_length(d)
     if ulen > cap:
         return lvkv.SNAPPY_CAPACITY
-    if len(d) > 2 * cap + 8:
+    if len(d) > so.max_compressed_length(cap):
         return lvkv.SNAPPY_TOO_LARGE
     return v["status"]
 

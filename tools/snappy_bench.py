@@ -1,0 +1,151 @@
+"""Device Snappy codec throughput on db_bench's workload (GPU box).
+
+    python tools/snappy_bench.py [--blocks 65536] [--steps 20]
+
+db_bench's snappycomp / snappyuncomp (benchmarks/db_bench.cc:384-433)
+compress one 4096-byte block of RandomGenerator data (compression ratio 0.5)
+over and over, one thread, and report MB/s of uncompressed bytes. Here a
+batch of `--blocks` such blocks (the generator's consecutive 4 KiB slices,
+db_bench.cc:195-202) sits in HBM; one step compresses (or uncompresses) the
+whole batch in one launch, timed with HIP events on the launch stream. The
+CPU lines run libsnappy 1.1.8 (the library the reference would link) the
+db_bench way on one thread, and on 16 threads over distinct blocks.
+Prints one JSON line; writes gpurun_out/snappy_bench.json.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO))
+sys.path.insert(0, str(REPO / "oracle"))
+from tools.db_bench_data import block_batch  # noqa: E402
+
+
+def cpu_lines(blocks: np.ndarray, seconds: float = 2.0):
+    import snappy_oracle as so  # libsnappy 1.1.8 handle (test infrastructure)
+    lib = so.system_snappy()
+    if lib is None:
+        return None
+    import ctypes
+    blk = blocks[:4096].tobytes()
+    comp = so.lib_compress(lib, blk)
+    out = ctypes.create_string_buffer(lib.snappy_max_compressed_length(4096))
+    unc = ctypes.create_string_buffer(4096)
+
+    def loop_comp(b, secs):
+        n, t0 = 0, time.perf_counter()
+        ol = ctypes.c_size_t()
+        o = ctypes.create_string_buffer(lib.snappy_max_compressed_length(4096))
+        while time.perf_counter() - t0 < secs:
+            for _ in range(64):
+                ol.value = len(o)
+                lib.snappy_compress(b, 4096, o, ctypes.byref(ol))
+            n += 64
+        return n * 4096 / (time.perf_counter() - t0)
+
+    def loop_unc(c, secs):
+        n, t0 = 0, time.perf_counter()
+        ol = ctypes.c_size_t()
+        o = ctypes.create_string_buffer(4096)
+        while time.perf_counter() - t0 < secs:
+            for _ in range(64):
+                ol.value = 4096
+                lib.snappy_uncompress(c, len(c), o, ctypes.byref(ol))
+            n += 64
+        return n * 4096 / (time.perf_counter() - t0)
+
+    del out, unc
+    res = {"comp_1t_MBps": loop_comp(blk, seconds) / 1e6, "uncomp_1t_MBps": loop_unc(comp, seconds) / 1e6,
+           "output_pct": round(100.0 * len(comp) / 4096, 1)}
+    # 16 threads (ctypes drops the GIL), distinct blocks
+    bl = [blocks[i * 4096:(i + 1) * 4096].tobytes() for i in range(16)]
+    cl = [so.lib_compress(lib, b) for b in bl]
+    with ThreadPoolExecutor(16) as ex:
+        res["comp_16t_MBps"] = sum(ex.map(lambda b: loop_comp(b, seconds), bl)) / 1e6
+        res["uncomp_16t_MBps"] = sum(ex.map(lambda c: loop_unc(c, seconds), cl)) / 1e6
+    return {k: round(v, 1) for k, v in res.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--blocks", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+    import torch
+    import __graft_entry__ as g
+    lvkv = g.load_package()
+    dev = torch.device("cuda:0")
+    nb, L = args.blocks, 4096
+    host = block_batch(nb, L)
+    src = torch.from_numpy(host).to(dev)
+    off = torch.arange(nb, dtype=torch.int64, device=dev) * L
+    ln = torch.full((nb,), L, dtype=torch.int32, device=dev)
+    dst, doff, dlen, st = lvkv.snappy_compress(src, off, ln, max_len=L)
+    torch.cuda.synchronize()
+    assert int(st.max()) == 0
+    # parity on a sample: the device streams decode to the inputs and match
+    # libsnappy / the oracle (tests/test_snappy.py covers the rest)
+    import snappy_oracle as so
+    lib = so.system_snappy()
+    d_host = dst.cpu().numpy()
+    for i in range(0, nb, max(1, nb // 64)):
+        s = d_host[int(doff[i]):int(doff[i]) + int(dlen[i])].tobytes()
+        want = so.lib_compress(lib, host[i * L:(i + 1) * L].tobytes()) if lib else \
+            so.compress(host[i * L:(i + 1) * L].tobytes())
+        assert s == want, i
+    comp_bytes = int(dlen.to(torch.int64).sum())
+    stream = torch.cuda.current_stream(dev)
+
+    def timed(fn):
+        for _ in range(args.warmup):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.steps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e-3 / args.steps
+
+    out_len, out_st = torch.empty_like(dlen), torch.empty_like(st)
+    t_comp = timed(lambda: lvkv.lib.lvkv_snappy_compress_device(
+        src.data_ptr(), off.data_ptr(), ln.data_ptr(), dst.data_ptr(), doff.data_ptr(),
+        out_len.data_ptr(), out_st.data_ptr(), nb, L, stream.cuda_stream))
+    cap = torch.full((nb,), L, dtype=torch.int32, device=dev)
+    udst = torch.empty(nb * L, dtype=torch.uint8, device=dev)
+    ulen, ust = torch.empty_like(dlen), torch.empty_like(st)
+    t_unc = timed(lambda: lvkv.lib.lvkv_snappy_uncompress_device(
+        dst.data_ptr(), doff.data_ptr(), dlen.data_ptr(), udst.data_ptr(), off.data_ptr(),
+        cap.data_ptr(), ulen.data_ptr(), ust.data_ptr(), nb, L, stream.cuda_stream))
+    torch.cuda.synchronize()
+    assert int(ust.max()) == 0 and torch.equal(udst, src)
+    assert torch.equal(out_len, dlen)
+    raw = nb * L
+    res = {
+        "workload": f"db_bench snappycomp/snappyuncomp blocks: {nb} x {L} B (RandomGenerator, ratio 0.5)",
+        "blocks": nb, "block_bytes": L, "output_pct": round(100.0 * comp_bytes / raw, 2),
+        "compress": {"us_per_launch": round(t_comp * 1e6, 1), "GBps_uncompressed": round(raw / t_comp / 1e9, 2),
+                     "hbm_GBps": round((raw + comp_bytes) / t_comp / 1e9, 2)},
+        "uncompress": {"us_per_launch": round(t_unc * 1e6, 1), "GBps_uncompressed": round(raw / t_unc / 1e9, 2),
+                       "hbm_GBps": round((raw + comp_bytes) / t_unc / 1e9, 2)},
+    }
+    if not args.no_cpu:
+        res["cpu_libsnappy_1_1_8"] = cpu_lines(host)
+    print(json.dumps(res), flush=True)
+    (REPO / "gpurun_out").mkdir(exist_ok=True)
+    (REPO / "gpurun_out" / "snappy_bench.json").write_text(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
