@@ -88,6 +88,56 @@ int lvkv_snappy_uncompress_device(const void* d_src, const uint64_t* d_src_off,
                                   uint32_t* d_out_len, uint8_t* d_status, size_t nblocks,
                                   uint32_t max_ulen, void* stream);
 
+/* ---- the block writer and reader around the codec ----------------------- */
+
+/* Scratch for lvkv_sst_write_blocks_device with compression 1. */
+size_t lvkv_sst_write_scratch_bytes(size_t nblocks, uint32_t max_len);
+
+/*
+ * TableBuilder::WriteBlock + WriteRawBlock over a batch of finished blocks
+ * (table/table_builder.cc:141-209): block i = d_raw[d_raw_off[i], +
+ * d_raw_len[i]) (each at most max_len bytes), written in order from file
+ * offset `file_offset` of d_file (the image of the file; d_file[0] is file
+ * offset 0): with compression 1 (kSnappyCompression) the snappy form when it
+ * is smaller than raw - raw/8, else raw with type 0; the type byte; the
+ * masked CRC32C of contents + type (the batch CRC kernel). d_handle_off /
+ * d_handle_size = the BlockHandles, d_type = the kept type, d_end[0] = the
+ * file offset after the last trailer (Rep::offset). compression 0 writes
+ * every block raw (no scratch needed). d_file must hold the whole output:
+ * at most sum(raw + 5) bytes from file_offset.
+ */
+int lvkv_sst_write_blocks_device(const void* d_raw, const uint64_t* d_raw_off,
+                                 const uint32_t* d_raw_len, size_t nblocks, int compression,
+                                 uint32_t max_len, void* d_scratch, void* d_file,
+                                 uint64_t file_offset, uint64_t* d_handle_off,
+                                 uint32_t* d_handle_size, uint8_t* d_type, uint64_t* d_end,
+                                 void* stream);
+
+/* ReadBlock verdicts */
+#define LVKV_READ_OK 0
+#define LVKV_READ_CHECKSUM 1        /* "block checksum mismatch" (table/format.cc:95-98) */
+#define LVKV_READ_BAD_TYPE 2        /* "bad block type" (:156-158) */
+#define LVKV_READ_SNAPPY_LENGTH 3   /* "corrupted snappy compressed block length" (:122-124) */
+#define LVKV_READ_SNAPPY_CONTENTS 4 /* "corrupted snappy compressed block contents" (:127-131) */
+#define LVKV_READ_ZSTD 5            /* type kZstdCompression: no device codec, the caller's */
+#define LVKV_READ_CAPACITY 6        /* contents longer than d_out_cap[i] (d_out_len says) */
+#define LVKV_READ_TOO_LARGE 7       /* beyond max_ulen (see LVKV_SNAPPY_TOO_LARGE) */
+
+/*
+ * ReadBlock over a batch of block handles of one file image
+ * (table/format.cc:69-162): the CRC of contents + type checked against the
+ * trailer (verify != 0, ReadOptions::verify_checksums), then by type:
+ * kNoCompression copies the contents, kSnappyCompression decodes them, into
+ * d_out[d_out_off[i], + d_out_cap[i]); d_out_len[i] = the block's length,
+ * d_status[i] = LVKV_READ_*. Handles must lie inside the file (as for
+ * lvkv_sst_verify_device; Table::Open's index decode checks that).
+ */
+int lvkv_sst_read_blocks_device(const void* d_file, const uint64_t* d_handle_off,
+                                const uint32_t* d_handle_size, size_t nblocks, int verify,
+                                void* d_out, const uint64_t* d_out_off, const uint32_t* d_out_cap,
+                                uint32_t* d_out_len, uint8_t* d_status, uint32_t max_ulen,
+                                void* stream);
+
 #ifdef __cplusplus
 }
 #endif

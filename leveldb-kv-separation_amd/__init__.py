@@ -144,6 +144,13 @@ def _load() -> ctypes.CDLL:
     L.lvkv_snappy_uncompressed_length_device.restype = i32
     L.lvkv_snappy_uncompress_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, sz, u32, vp]
     L.lvkv_snappy_uncompress_device.restype = i32
+    L.lvkv_sst_write_scratch_bytes.argtypes = [sz, u32]
+    L.lvkv_sst_write_scratch_bytes.restype = sz
+    L.lvkv_sst_write_blocks_device.argtypes = [vp, vp, vp, sz, i32, u32, vp, vp, u64, vp, vp, vp,
+                                               vp, vp]
+    L.lvkv_sst_write_blocks_device.restype = i32
+    L.lvkv_sst_read_blocks_device.argtypes = [vp, vp, vp, sz, i32, vp, vp, vp, vp, vp, u32, vp]
+    L.lvkv_sst_read_blocks_device.restype = i32
     L.lvkv_strerror.argtypes = [i32]
     L.lvkv_strerror.restype = ctypes.c_char_p
     L.lvkv_last_hip_error.argtypes = []
@@ -582,6 +589,81 @@ def snappy_uncompress(src, offsets, lengths, *, max_ulen: int, dst=None, dst_off
                 _stream_handle(stream, dev))
         _check("lvkv_snappy_uncompress_device", rc)
     return dst, dst_offsets, out_len, status
+
+
+READ_OK, READ_CHECKSUM, READ_BAD_TYPE, READ_SNAPPY_LENGTH, READ_SNAPPY_CONTENTS, READ_ZSTD, \
+    READ_CAPACITY, READ_TOO_LARGE = range(8)
+
+
+def sst_write_blocks(raw, offsets, lengths, *, compression: int = 1, max_len: Optional[int] = None,
+                     file=None, file_offset: int = 0, stream=None):
+    """Batched TableBuilder::WriteBlock + WriteRawBlock (table/table_builder.cc:
+    141-209): blocks raw[offsets[i] : offsets[i] + lengths[i]] written in order
+    from file_offset of the file image `file` (allocated when None: file_offset
+    + sum(lengths + 5) bytes). Returns (file, handle offsets int64, handle
+    sizes int32, types uint8, end offset int64 tensor of one)."""
+    torch = _torch()
+    n = offsets.numel()
+    dev = raw.device
+    if max_len is None:
+        max_len = int(lengths.max().item()) if n else 0
+    if file is None:
+        total = file_offset + (int(lengths.to(torch.int64).sum().item()) if n else 0) + 5 * n
+        file = torch.zeros(max(1, total), dtype=torch.uint8, device=dev)
+    hoff = torch.empty(n, dtype=torch.int64, device=dev)
+    hsize = torch.empty(n, dtype=torch.int32, device=dev)
+    typ = torch.empty(n, dtype=torch.uint8, device=dev)
+    end = torch.empty(1, dtype=torch.int64, device=dev)
+    scratch = None
+    if compression == 1 and n:
+        scratch = torch.empty(int(_lib.lvkv_sst_write_scratch_bytes(n, max_len)),
+                              dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        rc = _lib.lvkv_sst_write_blocks_device(
+            _dev_ptr(raw, "raw", (torch.uint8, torch.int8)) if n else None,
+            _dev_ptr(offsets, "offsets", (torch.int64,)) if n else None,
+            _dev_ptr(lengths, "lengths", (torch.int32,), n) if n else None, n, compression,
+            max_len, _dev_ptr(scratch, "scratch") if scratch is not None else None,
+            _dev_ptr(file, "file", (torch.uint8, torch.int8)), file_offset,
+            _dev_ptr(hoff, "hoff") if n else None, _dev_ptr(hsize, "hsize") if n else None,
+            _dev_ptr(typ, "type") if n else None, _dev_ptr(end, "end"),
+            _stream_handle(stream, dev))
+    _check("lvkv_sst_write_blocks_device", rc)
+    return file, hoff, hsize, typ, end
+
+
+def sst_read_blocks(file, handle_off, handle_size, *, max_ulen: int, verify: bool = True,
+                    out=None, out_offsets=None, out_caps=None, stream=None):
+    """Batched ReadBlock (table/format.cc:69-162): checksum, then contents by
+    type (raw copied, snappy decoded). Without out, each block gets max_ulen
+    bytes. Returns (out uint8, out_offsets int64, lengths int32, status uint8
+    READ_*)."""
+    torch = _torch()
+    n = handle_off.numel()
+    dev = file.device
+    if not 0 <= max_ulen <= SNAPPY_MAX_BLOCK:
+        raise ValueError(f"max_ulen must be in [0, {SNAPPY_MAX_BLOCK}]")
+    if out is None:
+        out_caps = torch.full((n,), max_ulen, dtype=torch.int32, device=dev)
+        out_offsets = torch.arange(n, dtype=torch.int64, device=dev) * max_ulen
+        out = torch.empty(max(1, n * max_ulen), dtype=torch.uint8, device=dev)
+    elif out_offsets is None or out_caps is None:
+        raise ValueError("out needs out_offsets and out_caps")
+    out_len = torch.zeros(n, dtype=torch.int32, device=dev)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    if n:
+        with torch.cuda.device(dev):
+            rc = _lib.lvkv_sst_read_blocks_device(
+                _dev_ptr(file, "file", (torch.uint8, torch.int8)),
+                _dev_ptr(handle_off, "handle_off", (torch.int64,)),
+                _dev_ptr(handle_size, "handle_size", (torch.int32,), n), n, 1 if verify else 0,
+                _dev_ptr(out, "out", (torch.uint8, torch.int8)),
+                _dev_ptr(out_offsets, "out_offsets", (torch.int64,), n),
+                _dev_ptr(out_caps, "out_caps", (torch.int32,), n),
+                _dev_ptr(out_len, "out_len"), _dev_ptr(status, "status"), max_ulen,
+                _stream_handle(stream, dev))
+        _check("lvkv_sst_read_blocks_device", rc)
+    return out, out_offsets, out_len, status
 
 
 class LogReport(ctypes.Structure):

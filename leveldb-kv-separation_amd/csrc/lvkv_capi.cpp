@@ -83,6 +83,16 @@ hipError_t launch_snappy_uncompress(const uint8_t* src, const uint64_t* src_off,
                                     const uint32_t* src_len, uint8_t* dst, const uint64_t* dst_off,
                                     const uint32_t* dst_cap, uint32_t* out_len, uint8_t* status,
                                     uint32_t nblocks, uint32_t max_ulen, hipStream_t stream);
+uint64_t snappy_write_stride(uint32_t max_len);
+hipError_t launch_sst_write_blocks(const uint8_t* raw, const uint64_t* raw_off,
+                                   const uint32_t* raw_len, uint32_t nblocks, int compression,
+                                   uint32_t max_len, uint8_t* scratch, uint8_t* file,
+                                   uint64_t file_offset, uint64_t* hoff, uint32_t* hsize,
+                                   uint8_t* type, uint64_t* end, hipStream_t stream);
+hipError_t launch_sst_read_blocks(const uint8_t* file, const uint64_t* hoff, const uint32_t* hsize,
+                                  uint32_t nblocks, uint8_t* out, const uint64_t* out_off,
+                                  const uint32_t* out_cap, uint32_t* out_len, uint8_t* status,
+                                  const uint8_t* vstatus, uint32_t max_ulen, hipStream_t stream);
 int compact_capacity(int cfg);
 int compact_occupancy(int cfg);
 // 8 waves x 3 chains, two workgroups per CU, generated lane tables
@@ -893,6 +903,63 @@ int lvkv_snappy_uncompress_device(const void* d_src, const uint64_t* d_src_off,
   const hipError_t e = launch_snappy_uncompress(
       static_cast<const uint8_t*>(d_src), d_src_off, d_src_len, static_cast<uint8_t*>(d_dst),
       d_dst_off, d_dst_cap, d_out_len, d_status, static_cast<uint32_t>(nblocks), max_ulen,
+      static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? LVKV_OK : hip_fail(e);
+}
+
+size_t lvkv_sst_write_scratch_bytes(size_t nblocks, uint32_t max_len) {
+  return nblocks * (snappy_write_stride(max_len) + 5);
+}
+
+int lvkv_sst_write_blocks_device(const void* d_raw, const uint64_t* d_raw_off,
+                                 const uint32_t* d_raw_len, size_t nblocks, int compression,
+                                 uint32_t max_len, void* d_scratch, void* d_file,
+                                 uint64_t file_offset, uint64_t* d_handle_off,
+                                 uint32_t* d_handle_size, uint8_t* d_type, uint64_t* d_end,
+                                 void* stream) {
+  if (!d_end || (compression != 0 && compression != 1)) return LVKV_ERR_INVALID;
+  if (nblocks == 0) {
+    const hipError_t e = hipMemcpyAsync(d_end, &file_offset, 8, hipMemcpyHostToDevice,
+                                        static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? LVKV_OK : hip_fail(e);
+  }
+  if (!d_raw || !d_raw_off || !d_raw_len || !d_file || !d_handle_off || !d_handle_size ||
+      !d_type || (compression == 1 && !d_scratch) || nblocks > kMaxBlocksPerLaunch)
+    return LVKV_ERR_INVALID;
+  int rc = LVKV_OK;
+  if (current_ctx(&rc) == nullptr) return rc;
+  const hipStream_t hs = static_cast<hipStream_t>(stream);
+  hipError_t e = launch_sst_write_blocks(
+      static_cast<const uint8_t*>(d_raw), d_raw_off, d_raw_len, static_cast<uint32_t>(nblocks),
+      compression, max_len, static_cast<uint8_t*>(d_scratch), static_cast<uint8_t*>(d_file),
+      file_offset, d_handle_off, d_handle_size, d_type, d_end, hs);
+  if (e != hipSuccess) return hip_fail(e);
+  // the trailers: Mask(CRC32C(contents + type)) by the batch CRC kernel
+  return lvkv_sst_fill_trailers_device(d_file, d_handle_off, d_handle_size, nullptr, nblocks,
+                                       stream);
+}
+
+int lvkv_sst_read_blocks_device(const void* d_file, const uint64_t* d_handle_off,
+                                const uint32_t* d_handle_size, size_t nblocks, int verify,
+                                void* d_out, const uint64_t* d_out_off, const uint32_t* d_out_cap,
+                                uint32_t* d_out_len, uint8_t* d_status, uint32_t max_ulen,
+                                void* stream) {
+  if (nblocks == 0) return LVKV_OK;
+  if (!d_file || !d_handle_off || !d_handle_size || !d_out || !d_out_off || !d_out_cap ||
+      !d_out_len || !d_status || nblocks > kMaxBlocksPerLaunch ||
+      max_ulen > LVKV_SNAPPY_MAX_BLOCK)
+    return LVKV_ERR_INVALID;
+  int rc = LVKV_OK;
+  if (current_ctx(&rc) == nullptr) return rc;
+  if (verify) {  // the verdicts land in d_status (the CRCs in d_out_len) first
+    rc = lvkv_sst_verify_device(d_file, d_handle_off, d_handle_size, d_out_len, d_status,
+                                nblocks, stream);
+    if (rc != LVKV_OK) return rc;
+  }
+  const hipError_t e = launch_sst_read_blocks(
+      static_cast<const uint8_t*>(d_file), d_handle_off, d_handle_size,
+      static_cast<uint32_t>(nblocks), static_cast<uint8_t*>(d_out), d_out_off, d_out_cap,
+      d_out_len, d_status, verify ? d_status : nullptr, max_ulen,
       static_cast<hipStream_t>(stream));
   return e == hipSuccess ? LVKV_OK : hip_fail(e);
 }

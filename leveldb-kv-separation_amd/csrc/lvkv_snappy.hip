@@ -181,7 +181,6 @@ __device__ __forceinline__ bool search_probes(const uint8_t* in, uint16_t* table
                                               const uint16_t* probe, uint32_t base,
                                               uint32_t ip_limit, uint32_t shift, uint32_t lane,
                                               uint32_t* out_ip, uint32_t* out_cand) {
-  const uint64_t lt = (uint64_t{1} << lane) - 1u;  // lanes below this one
   for (uint32_t n0 = 0;; n0 += 64) {
     const uint32_t p = base + probe[n0 + lane];
     const bool valid = base + probe[n0 + lane + 1] <= ip_limit;
@@ -200,12 +199,18 @@ __device__ __forceinline__ bool search_probes(const uint8_t* in, uint16_t* table
     uint32_t cand = c0;
     while (losers) {
       const uint32_t hv = __builtin_amdgcn_readlane(h, __builtin_ctzll(losers));
-      const uint64_t g = __ballot(valid && h == hv);
+      uint64_t g = __ballot(valid && h == hv);
       losers &= ~g;
-      const uint64_t prev = g & lt;
-      const bool mine = ((g >> lane) & 1u) && prev != 0;
-      const uint32_t pp = __shfl(p, mine ? 63 - __builtin_clzll(prev) : lane);
-      if (mine) cand = pp;
+      // each later member's candidate is the member before it
+      uint32_t prev = __builtin_ctzll(g);
+      g &= g - 1u;
+      while (g) {
+        const uint32_t m = __builtin_ctzll(g);
+        g &= g - 1u;
+        const uint32_t pv = __builtin_amdgcn_readlane(p, prev);
+        cand = lane == m ? pv : cand;
+        prev = m;
+      }
     }
     const uint32_t vc = ld32(in, valid ? cand : 0u);
     const uint64_t mm = __ballot(valid && vc == v);
@@ -288,7 +293,8 @@ struct CompressArgs {
   uint32_t* dst_len;
   uint8_t* status;
   uint32_t nblocks;
-  uint32_t frag_cap;  // the largest fragment the LDS holds (<= kFrag)
+  uint32_t frag_cap;    // the largest fragment the LDS holds (<= kFrag)
+  uint64_t dst_stride;  // dst_off == nullptr: block b's output at b * dst_stride
 };
 
 __global__ void __launch_bounds__(64) snappy_compress_kernel(CompressArgs a) {
@@ -309,7 +315,7 @@ __global__ void __launch_bounds__(64) snappy_compress_kernel(CompressArgs a) {
     }
     return;
   }
-  Out o{a.dst + a.dst_off[b], 0};
+  Out o{a.dst + (a.dst_off ? a.dst_off[b] : b * a.dst_stride), 0};
   // varint32 of the uncompressed length
   uint32_t v = len;
   while (v >= 128) {
@@ -346,6 +352,11 @@ struct UncompressArgs {
   uint8_t* status;
   uint32_t nblocks;
   uint32_t out_cap;  // the largest output the LDS holds
+  // ReadBlock mode (lvkv_sst_read_blocks_device): src_off/src_len are block
+  // handles, the type byte follows the contents, statuses are LVKV_READ_*;
+  // vstatus = the checksum verdicts (nullptr: verify_checksums off)
+  uint32_t block_mode;
+  const uint8_t* vstatus;
 };
 
 // snappy::MaxCompressedLength: the longest stream the decompressor stages.
@@ -381,12 +392,31 @@ __global__ void __launch_bounds__(64) snappy_uncompress_kernel(UncompressArgs a)
   const uint32_t in_bytes = (in_cap + 16u + 15u) & ~15u;
   uint8_t* in = smem;
   uint8_t* out = smem + in_bytes;
-  auto finish = [&](uint32_t st, uint32_t ol) {
+  auto finish_read = [&](uint32_t st, uint32_t ol) {
     if (lane == 0) {
       a.status[b] = static_cast<uint8_t>(st);
       a.out_len[b] = ol;
     }
   };
+  // codec status -> ReadBlock status in block mode
+  auto finish = [&](uint32_t st, uint32_t ol) {
+    constexpr uint8_t kRead[5] = {LVKV_READ_OK, LVKV_READ_SNAPPY_LENGTH, LVKV_READ_SNAPPY_CONTENTS,
+                                  LVKV_READ_CAPACITY, LVKV_READ_TOO_LARGE};
+    finish_read(a.block_mode ? kRead[st] : st, ol);
+  };
+  if (a.block_mode) {  // ReadBlock (table/format.cc:90-159): checksum, then the type
+    const uint32_t type = src[n];
+    if (a.vstatus != nullptr && a.vstatus[b] != 0)
+      return finish_read(LVKV_READ_CHECKSUM, 0);  // :95-98
+    if (type == 2) return finish_read(LVKV_READ_ZSTD, 0);
+    if (type > 2) return finish_read(LVKV_READ_BAD_TYPE, 0);  // :156-158
+    if (type == 0) {  // kNoCompression: the contents as they are (:103-119)
+      if (n > a.dst_cap[b]) return finish_read(LVKV_READ_CAPACITY, n);
+      uint8_t* dst = a.dst + a.dst_off[b];
+      for (uint32_t k = lane; k < n; k += 64) dst[k] = src[k];
+      return finish_read(LVKV_READ_OK, n);
+    }
+  }
   uint32_t ulen = 0, pl;
   const bool staged = a.dst_cap != nullptr && n <= in_cap;
   if (staged) {  // the preamble from LDS, after one round trip for the lot
@@ -481,7 +511,135 @@ __global__ void __launch_bounds__(64) snappy_uncompress_kernel(UncompressArgs a)
   finish(LVKV_SNAPPY_OK, ulen);
 }
 
+// ---- TableBuilder::WriteBlock over a batch (table/table_builder.cc:141-209) --
+
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, uint32_t d) {
+  const uint32_t lo = __shfl_up(static_cast<uint32_t>(v), d);
+  const uint32_t hi = __shfl_up(static_cast<uint32_t>(v >> 32), d);
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// Which form each block keeps and where it lands: the compressed form when
+// it is smaller than raw - raw/8 (table_builder.cc:160-168), else raw with
+// type kNoCompression; handles are an exclusive scan of size + 5 (the
+// trailer, :206) from file_offset. One workgroup, 4 blocks a thread a pass.
+__global__ void __launch_bounds__(1024) sst_layout_kernel(const uint32_t* raw_len,
+                                                          const uint32_t* clen, const uint8_t* cst,
+                                                          uint32_t n, uint64_t file_offset,
+                                                          uint64_t* hoff, uint32_t* hsize,
+                                                          uint8_t* type, uint64_t* end) {
+  __shared__ uint64_t wsum[17];
+  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+  uint64_t carry = file_offset;
+  for (uint32_t base = 0; base < n; base += 4096) {
+    uint32_t sz[4];
+    uint8_t ty[4];
+    uint64_t local = 0;
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint32_t i = base + 4 * t + j;
+      sz[j] = 0;
+      ty[j] = 0;
+      if (i < n) {
+        const uint32_t L = raw_len[i];
+        const bool c = clen != nullptr && cst[i] == LVKV_SNAPPY_OK && clen[i] < L - L / 8u;
+        sz[j] = c ? clen[i] : L;
+        ty[j] = c ? 1 : 0;
+        local += sz[j] + 5u;
+      }
+    }
+    uint64_t incl = local;
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint64_t y = shfl_up64(incl, d);
+      if (lane >= d) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    if (w == 0) {
+      const uint64_t v = lane < 16 ? wsum[lane] : 0;
+      uint64_t s = v;
+      for (uint32_t d = 1; d < 16; d <<= 1) {
+        const uint64_t y = shfl_up64(s, d);
+        if (lane >= d) s += y;
+      }
+      if (lane < 16) wsum[lane] = s - v;  // exclusive
+      if (lane == 15) wsum[16] = s;       // the pass's total
+    }
+    __syncthreads();
+    uint64_t at = carry + wsum[w] + incl - local;
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint32_t i = base + 4 * t + j;
+      if (i < n) {
+        hoff[i] = at;
+        hsize[i] = sz[j];
+        type[i] = ty[j];
+        at += sz[j] + 5u;
+      }
+    }
+    carry += wsum[16];
+    __syncthreads();
+  }
+  if (t == 0) *end = carry;
+}
+
+// WriteRawBlock's bytes but the CRC (table_builder.cc:195-204): the kept
+// contents at the handle, the type byte after them. The masked CRC is the
+// batch CRC kernel's (lvkv_sst_fill_trailers_device) over the same handles.
+__global__ void __launch_bounds__(256) sst_place_kernel(const uint8_t* raw, const uint64_t* raw_off,
+                                                        const uint8_t* comp, uint64_t comp_stride,
+                                                        const uint64_t* hoff, const uint32_t* hsize,
+                                                        const uint8_t* type, uint8_t* file) {
+  const uint32_t b = blockIdx.x, t = threadIdx.x;
+  const uint32_t ty = type[b];
+  const uint8_t* src = ty ? comp + b * comp_stride : raw + raw_off[b];
+  uint8_t* dst = file + hoff[b];
+  const uint32_t n = hsize[b];
+  for (uint32_t k = t; k < n; k += 256) dst[k] = src[k];
+  if (t == 0) dst[n] = static_cast<uint8_t>(ty);
+}
+
 }  // namespace
+
+uint64_t snappy_write_stride(uint32_t max_len) {
+  return (snappy_in_cap(max_len) + 15u) & ~uint64_t{15};
+}
+
+hipError_t launch_sst_write_blocks(const uint8_t* raw, const uint64_t* raw_off,
+                                   const uint32_t* raw_len, uint32_t nblocks, int compression,
+                                   uint32_t max_len, uint8_t* scratch, uint8_t* file,
+                                   uint64_t file_offset, uint64_t* hoff, uint32_t* hsize,
+                                   uint8_t* type, uint64_t* end, hipStream_t stream) {
+  const uint64_t stride = snappy_write_stride(max_len);
+  uint32_t* clen = nullptr;
+  uint8_t* cst = nullptr;
+  if (compression == 1) {
+    clen = reinterpret_cast<uint32_t*>(scratch + stride * nblocks);
+    cst = reinterpret_cast<uint8_t*>(clen + nblocks);
+    CompressArgs a{raw, raw_off, raw_len, scratch, nullptr, clen, cst, nblocks, 0, stride};
+    a.frag_cap = max(16u, min(max_len, kFrag));
+    const uint32_t in_bytes = (a.frag_cap + 16u + 15u) & ~15u;
+    uint32_t t = 256;
+    while (t < kMaxTable && t < a.frag_cap) t <<= 1;
+    const size_t lds = in_bytes + 2u * ((kProbes + 7) & ~7u) + 2u * t;
+    hipLaunchKernelGGL(snappy_compress_kernel, dim3(nblocks), dim3(64), lds, stream, a);
+  }
+  hipLaunchKernelGGL(sst_layout_kernel, dim3(1), dim3(1024), 0, stream, raw_len, clen, cst,
+                     nblocks, file_offset, hoff, hsize, type, end);
+  hipLaunchKernelGGL(sst_place_kernel, dim3(nblocks), dim3(256), 0, stream, raw, raw_off,
+                     scratch, stride, hoff, hsize, type, file);
+  return hipGetLastError();
+}
+
+hipError_t launch_sst_read_blocks(const uint8_t* file, const uint64_t* hoff, const uint32_t* hsize,
+                                  uint32_t nblocks, uint8_t* out, const uint64_t* out_off,
+                                  const uint32_t* out_cap, uint32_t* out_len, uint8_t* status,
+                                  const uint8_t* vstatus, uint32_t max_ulen, hipStream_t stream) {
+  UncompressArgs a{file, hoff, hsize, out, out_off, out_cap, out_len, status, nblocks, 0, 1,
+                   vstatus};
+  a.out_cap = max(16u, max_ulen);
+  const size_t lds = ((snappy_in_cap(a.out_cap) + 16u + 15u) & ~15u) + ((a.out_cap + 15u) & ~15u);
+  hipLaunchKernelGGL(snappy_uncompress_kernel, dim3(nblocks), dim3(64), lds, stream, a);
+  return hipGetLastError();
+}
 
 hipError_t launch_snappy_compress(const uint8_t* src, const uint64_t* src_off,
                                   const uint32_t* src_len, uint8_t* dst, const uint64_t* dst_off,

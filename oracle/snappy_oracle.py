@@ -249,6 +249,66 @@ def uncompress(src: bytes) -> Tuple[int, bytes]:
     return OK, bytes(out)
 
 
+# ---- the block writer / reader around the codec -------------------------
+
+def _crc():
+    """The CRC32C restatement (oracle/oracle.py, pinned to util/crc32c.cc)."""
+    import importlib.util
+    from pathlib import Path
+    spec = importlib.util.spec_from_file_location("lvkv_crc_oracle", Path(__file__).with_name("oracle.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def write_blocks(raws, compression: int, file_offset: int = 0):
+    """TableBuilder::WriteBlock + WriteRawBlock (table/table_builder.cc:141-209)
+    for each raw block in order: (file bytes from file_offset, handles
+    [(offset, size)], types)."""
+    crc = _crc()
+    out = bytearray()
+    handles, types = [], []
+    for raw in raws:
+        raw = bytes(raw)
+        contents, typ = raw, 0
+        if compression == 1:
+            c = compress(raw)
+            if len(c) < len(raw) - len(raw) // 8:  # :160-168
+                contents, typ = c, 1
+        handles.append((file_offset + len(out), len(contents)))
+        types.append(typ)
+        out += contents
+        out.append(typ)
+        v = crc.extend(crc.value(contents), bytes([typ]))
+        out += crc.mask(v).to_bytes(4, "little")
+    return bytes(out), handles, types
+
+
+READ_OK, READ_CHECKSUM, READ_BAD_TYPE, READ_SNAPPY_LENGTH, READ_SNAPPY_CONTENTS, READ_ZSTD = range(6)
+
+
+def read_block(img: bytes, off: int, size: int, verify: bool = True):
+    """ReadBlock (table/format.cc:69-162) of handle (off, size) in a file
+    image: (READ_*, contents)."""
+    crc = _crc()
+    data = img[off: off + size + 5]
+    if verify:
+        stored = crc.unmask(int.from_bytes(data[size + 1: size + 5], "little"))
+        if crc.value(data[: size + 1]) != stored:
+            return READ_CHECKSUM, b""
+    t = data[size]
+    if t == 0:
+        return READ_OK, data[:size]
+    if t == 1:
+        if uncompressed_length(data[:size]) is None:
+            return READ_SNAPPY_LENGTH, b""
+        st, out = uncompress(data[:size])
+        return (READ_OK, out) if st == OK else (READ_SNAPPY_CONTENTS, b"")
+    if t == 2:
+        return READ_ZSTD, b""
+    return READ_BAD_TYPE, b""
+
+
 # ---- the system library itself (the pin), where the image has it --------
 
 _LIB_PATHS = ("/opt/conda/lib/libsnappy.so.1.1.8", "/opt/conda/lib/libsnappy.so.1")

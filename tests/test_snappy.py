@@ -249,3 +249,104 @@ def test_device_codec_empty_batch(lvkv, gpu):
     assert dl.numel() == 0 and st.numel() == 0
     _, _, dl, st = lvkv.snappy_uncompress(z8, e64, e32, max_ulen=4096)
     assert dl.numel() == 0 and st.numel() == 0
+
+
+# ---- WriteBlock / ReadBlock around the codec -------------------------------
+
+def _block_set(n=300, seed=3):
+    from tools.db_bench_data import block_batch
+    rng = np.random.default_rng(seed)
+    bench = block_batch(64).tobytes()
+    out = []
+    for k in range(n):
+        L = int(rng.integers(0, 6000))
+        kind = k % 3
+        if kind == 0:
+            s = int(rng.integers(0, len(bench) - L))
+            out.append(bench[s:s + L])
+        elif kind == 1:
+            out.append(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+        else:  # barely compressible: around the 12.5% rule
+            a = rng.integers(0, 256, L, dtype=np.uint8)
+            a[: L // 7] = 7
+            out.append(a.tobytes())
+    return out
+
+
+def test_oracle_write_then_read_blocks():
+    raws = _block_set(60)
+    img, handles, types = so.write_blocks(raws, 1, file_offset=0)
+    assert 1 in types and 0 in types
+    for raw, (off, size), t in zip(raws, handles, types):
+        assert so.read_block(img, off, size) == (so.READ_OK, raw)
+        assert img[off + size] == t
+    off, size = handles[0]
+    bad = bytearray(img)
+    bad[off] ^= 1
+    assert so.read_block(bytes(bad), off, size)[0] == so.READ_CHECKSUM
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("compression,file_offset", [(1, 0), (1, 1234567), (0, 17)])
+def test_device_write_blocks_matches_oracle(lvkv, gpu, compression, file_offset):
+    import torch
+    raws = _block_set()
+    src, off, ln = _pack(torch, gpu, raws, skew=1)
+    file, hoff, hsize, typ, end = lvkv.sst_write_blocks(src, off, ln, compression=compression,
+                                                        file_offset=file_offset)
+    torch.cuda.synchronize()
+    img, handles, types = so.write_blocks(raws, compression, file_offset)
+    assert hoff.cpu().tolist() == [h[0] for h in handles]
+    assert hsize.cpu().tolist() == [h[1] for h in handles]
+    assert typ.cpu().tolist() == types
+    assert int(end.item()) == file_offset + len(img)
+    got = file.cpu().numpy()[file_offset:file_offset + len(img)].tobytes()
+    assert got == img
+
+
+@pytest.mark.gpu
+def test_device_read_blocks_roundtrip_and_verdicts(lvkv, gpu):
+    import torch
+    raws = _block_set(200, seed=9)
+    img, handles, types = so.write_blocks(raws, 1)
+    buf = bytearray(img)
+    rng = np.random.default_rng(4)
+    hurt = {}
+    for i in rng.choice(len(raws), 40, replace=False).tolist():
+        off, size = handles[i]
+        kind = len(hurt) % 4
+        if kind == 0 and size:  # contents flipped: checksum mismatch
+            buf[off + int(rng.integers(0, size))] ^= 0x10
+        elif kind == 1:  # type 2 (zstd) or 9 (bad), CRC refilled to match
+            buf[off + size] = 2 if i % 2 else 9
+        elif kind == 2 and size:  # snappy bytes damaged, CRC refilled
+            buf[off + int(rng.integers(0, min(size, 8)))] ^= 0x80
+        else:  # trailer damaged
+            buf[off + size + 2] ^= 1
+        hurt[i] = kind
+    crc = so._crc()
+    for i, kind in hurt.items():
+        if kind in (1, 2):
+            off, size = handles[i]
+            v = crc.mask(crc.value(bytes(buf[off:off + size + 1])))
+            buf[off + size + 1: off + size + 5] = v.to_bytes(4, "little")
+    img2 = bytes(buf)
+    file = torch.from_numpy(np.frombuffer(img2, dtype=np.uint8).copy()).to(gpu)
+    ho = torch.tensor([h[0] for h in handles], dtype=torch.int64, device=gpu)
+    hs = torch.tensor([h[1] for h in handles], dtype=torch.int32, device=gpu)
+    for verify in (True, False):
+        out, ooff, olen, st = lvkv.sst_read_blocks(file, ho, hs, max_ulen=8192, verify=verify)
+        torch.cuda.synchronize()
+        st, olen = st.cpu().tolist(), olen.cpu().tolist()
+        got = _unpack(out, ooff, torch.tensor(olen))
+        for i, (off, size) in enumerate(handles):
+            want_st, want = so.read_block(img2, off, size, verify)
+            ul = so.uncompressed_length(img2[off:off + size])
+            if want_st in (so.READ_OK, so.READ_SNAPPY_CONTENTS) and img2[off + size] == 1 \
+                    and ul is not None and ul > 8192:
+                want_st = lvkv.READ_CAPACITY  # a damaged preamble asks for more than the cap
+            assert st[i] == want_st, (i, hurt.get(i), st[i], want_st)
+            if want_st == so.READ_OK:
+                assert got[i] == want
+                if i not in hurt:
+                    assert want == raws[i]
