@@ -9,7 +9,8 @@ batch of `--blocks` such blocks (the generator's consecutive 4 KiB slices,
 db_bench.cc:195-202) sits in HBM; one step compresses (or uncompresses) the
 whole batch in one launch, timed with HIP events on the launch stream. The
 CPU lines run libsnappy 1.1.8 (the library the reference would link) the
-db_bench way on one thread, and on 16 threads over distinct blocks.
+db_bench way on one thread, and in 16 processes over distinct blocks (run
+before the GPU is initialised: the pool forks).
 Prints one JSON line; writes gpurun_out/snappy_bench.json.
 """
 from __future__ import annotations
@@ -18,7 +19,6 @@ import argparse
 import json
 import sys
 import time
-from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
 import numpy as np
@@ -29,7 +29,7 @@ sys.path.insert(0, str(REPO / "oracle"))
 from tools.db_bench_data import block_batch  # noqa: E402
 
 
-def cpu_lines(blocks: np.ndarray, seconds: float = 2.0):
+def cpu_lines(blocks: np.ndarray, seconds: float = 2.0, procs: int = 16):
     import snappy_oracle as so  # libsnappy 1.1.8 handle (test infrastructure)
     lib = so.system_snappy()
     if lib is None:
@@ -65,13 +65,34 @@ def cpu_lines(blocks: np.ndarray, seconds: float = 2.0):
     del out, unc
     res = {"comp_1t_MBps": loop_comp(blk, seconds) / 1e6, "uncomp_1t_MBps": loop_unc(comp, seconds) / 1e6,
            "output_pct": round(100.0 * len(comp) / 4096, 1)}
-    # 16 threads (ctypes drops the GIL), distinct blocks
-    bl = [blocks[i * 4096:(i + 1) * 4096].tobytes() for i in range(16)]
-    cl = [so.lib_compress(lib, b) for b in bl]
-    with ThreadPoolExecutor(16) as ex:
-        res["comp_16t_MBps"] = sum(ex.map(lambda b: loop_comp(b, seconds), bl)) / 1e6
-        res["uncomp_16t_MBps"] = sum(ex.map(lambda c: loop_unc(c, seconds), cl)) / 1e6
+    if procs > 1:  # one process a core (no GIL between them), distinct blocks
+        import multiprocessing as mp
+        with mp.get_context("fork").Pool(procs) as pool:
+            r = pool.map(_cpu_worker, [(blocks[i * 4096:(i + 1) * 4096].tobytes(), seconds)
+                                       for i in range(procs)])
+        res[f"comp_{procs}p_MBps"] = sum(a for a, _ in r) / 1e6
+        res[f"uncomp_{procs}p_MBps"] = sum(b for _, b in r) / 1e6
     return {k: round(v, 1) for k, v in res.items()}
+
+
+def _cpu_worker(arg):
+    blk, seconds = arg
+    import ctypes
+    import snappy_oracle as so
+    lib = so.system_snappy()
+    comp = so.lib_compress(lib, blk)
+    o = ctypes.create_string_buffer(lib.snappy_max_compressed_length(4096))
+    ol = ctypes.c_size_t()
+    rates = []
+    for fn, src, cap in ((lib.snappy_compress, blk, len(o)), (lib.snappy_uncompress, comp, 4096)):
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            for _ in range(256):
+                ol.value = cap
+                fn(src, len(src), o, ctypes.byref(ol))
+            n += 256
+        rates.append(n * 4096 / (time.perf_counter() - t0))
+    return tuple(rates)
 
 
 def main():
@@ -81,6 +102,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
+    cpu = None if args.no_cpu else cpu_lines(block_batch(64))
     import torch
     import __graft_entry__ as g
     lvkv = g.load_package()
@@ -140,8 +162,8 @@ def main():
         "uncompress": {"us_per_launch": round(t_unc * 1e6, 1), "GBps_uncompressed": round(raw / t_unc / 1e9, 2),
                        "hbm_GBps": round((raw + comp_bytes) / t_unc / 1e9, 2)},
     }
-    if not args.no_cpu:
-        res["cpu_libsnappy_1_1_8"] = cpu_lines(host)
+    if cpu is not None:
+        res["cpu_libsnappy_1_1_8"] = cpu
     print(json.dumps(res), flush=True)
     (REPO / "gpurun_out").mkdir(exist_ok=True)
     (REPO / "gpurun_out" / "snappy_bench.json").write_text(json.dumps(res, indent=1))
