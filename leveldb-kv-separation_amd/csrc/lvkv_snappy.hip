@@ -171,69 +171,65 @@ __device__ __forceinline__ uint32_t hash32(uint32_t v, uint32_t shift) {
 // positions after a reset do not depend on the data: probe k sits at
 // base + probe[k] (kProbe), and is made only if probe k+1 is <= ip_limit.
 // Probe k's candidate is the table entry as probes 0..k-1 left it: the
-// entry before the step, or the last earlier lane with the same hash. The
-// lanes write their positions, read them back, and a lane that lost a write
-// marks a collision group, resolved with ballots (rare: 64 hashes into
-// >= 256 entries). The first lane whose 4 bytes match ends the search; the
-// writes of the lanes after it are undone, so the table ends exactly as the
-// sequential loop leaves it. Returns false at emit_remainder.
+// entry before the step (c0), or the latest earlier lane with the same hash,
+// whose 4 bytes are that lane's own v. A 256-slot LDS scratch keeps the
+// lowest lane per (hash & 255) (an atomic min): a lane that is lowest in its
+// slot is the first of its hash, so its c0 test is exact, and the first
+// such match bounds the answer. Only the lanes below it with a lower lane in
+// their slot (~4 of 64 on db_bench's data) are resolved one by one. The
+// table is written once, after: each hash's last probe at or before the
+// match. Returns false at emit_remainder.
 __device__ __forceinline__ bool search_probes(const uint8_t* in, uint16_t* table,
-                                              const uint16_t* probe, uint32_t base,
-                                              uint32_t ip_limit, uint32_t shift, uint32_t lane,
+                                              const uint16_t* probe, uint32_t* slots,
+                                              uint32_t base, uint32_t ip_limit, uint32_t shift,
+                                              uint32_t lane, uint32_t w0, uint32_t w1,
                                               uint32_t* out_ip, uint32_t* out_cand) {
   for (uint32_t n0 = 0;; n0 += 64) {
-    const uint32_t p = base + probe[n0 + lane];
-    const bool valid = base + probe[n0 + lane + 1] <= ip_limit;
+    // (the first step's offsets come in registers: most searches end there)
+    const uint32_t p = base + (n0 == 0 ? w0 : probe[n0 + lane]);
+    const bool valid = base + (n0 == 0 ? w1 : probe[n0 + lane + 1]) <= ip_limit;
     const uint64_t vmask = __ballot(valid);
     const uint32_t v = ld32(in, valid ? p : 0u);
     const uint32_t h = hash32(v, shift);
-    uint32_t c0 = 0;
-    if (valid) c0 = table[h];
-    if (valid) table[h] = static_cast<uint16_t>(p);
-    // (a compiler barrier: the read-back must see which lane's write
-    // landed, not be forwarded from this lane's own store)
-    asm volatile("" ::: "memory");
-    const uint32_t r = valid ? table[h] : p;
-    uint64_t losers = __ballot(valid && r != p);
-    const uint64_t groups = losers;
-    uint32_t cand = c0;
-    while (losers) {
-      const uint32_t hv = __builtin_amdgcn_readlane(h, __builtin_ctzll(losers));
-      uint64_t g = __ballot(valid && h == hv);
-      losers &= ~g;
-      // each later member's candidate is the member before it
-      uint32_t prev = __builtin_ctzll(g);
-      g &= g - 1u;
-      while (g) {
-        const uint32_t m = __builtin_ctzll(g);
-        g &= g - 1u;
-        const uint32_t pv = __builtin_amdgcn_readlane(p, prev);
-        cand = lane == m ? pv : cand;
-        prev = m;
-      }
-    }
-    const uint32_t vc = ld32(in, valid ? cand : 0u);
-    const uint64_t mm = __ballot(valid && vc == v);
-    const uint32_t km = mm ? __builtin_ctzll(mm) : 64u;
+    const uint32_t c0 = valid ? table[h] : 0u;
+    uint32_t* slot = slots + (h & 255u);
+    *slot = 0xffffffffu;
+    if (valid) atomicMin(slot, lane);
+    const uint32_t first = *slot;
+    const uint32_t vc = ld32(in, valid ? c0 : 0u);
+    const uint64_t m0 = __ballot(valid && vc == v);
+    const uint64_t dupe = __ballot(valid && first < lane);
     const uint32_t ki = ~vmask ? __builtin_ctzll(~vmask) : 64u;
-    if (ki < km) return false;  // the search runs past ip_limit first
-    // K = the last probe made
-    const uint64_t upto = km < 64 ? (uint64_t{2} << km) - 1u : ~uint64_t{0};
-    if (valid && !((upto >> lane) & 1u)) table[h] = static_cast<uint16_t>(c0);
-    uint64_t gl = groups;
-    while (gl) {
-      const uint32_t hv = __builtin_amdgcn_readlane(h, __builtin_ctzll(gl));
-      const uint64_t g = __ballot(valid && h == hv);
-      gl &= ~g;
-      const uint64_t made = g & upto;
-      if (made) {
-        const uint32_t pl = __builtin_amdgcn_readlane(p, 63 - __builtin_clzll(made));
-        if (lane == 0) table[hv] = static_cast<uint16_t>(pl);
+    const uint64_t sure = m0 & ~dupe;
+    uint32_t km = sure ? __builtin_ctzll(sure) : 64u;
+    uint32_t kcand = km < 64 ? __builtin_amdgcn_readlane(c0, km) : 0u;
+    uint32_t nxt = 64;  // the next lane of this lane's hash, once resolved
+    for (uint64_t dl = dupe; dl;) {
+      const uint32_t d = __builtin_ctzll(dl);
+      if (d >= km) break;
+      dl &= dl - 1u;
+      const uint32_t hd = __builtin_amdgcn_readlane(h, d);
+      const uint64_t g = __ballot(valid && h == hd) & ((uint64_t{1} << d) - 1u);
+      if (g == 0) {  // a slot shared by another hash: d is its hash's first
+        if ((m0 >> d) & 1u) {
+          km = d;
+          kcand = __builtin_amdgcn_readlane(c0, d);
+        }
+        continue;
+      }
+      const uint32_t prev = 63u - __builtin_clzll(g);
+      nxt = lane == prev ? d : nxt;
+      if (__builtin_amdgcn_readlane(v, prev) == __builtin_amdgcn_readlane(v, d)) {
+        km = d;
+        kcand = __builtin_amdgcn_readlane(p, prev);
       }
     }
+    if (ki < km) return false;  // the search runs past ip_limit first
+    const uint32_t K = km < 64 ? km : 63u;  // the last probe made
+    if (valid && lane <= K && nxt > K) table[h] = static_cast<uint16_t>(p);
     if (km < 64) {
       *out_ip = __builtin_amdgcn_readlane(p, km);
-      *out_cand = __builtin_amdgcn_readlane(cand, km);
+      *out_cand = kcand;
       return true;
     }
   }
@@ -242,7 +238,8 @@ __device__ __forceinline__ bool search_probes(const uint8_t* in, uint16_t* table
 // CompressFragment of frag = in[0, n) (n <= kFrag) with table (u16 x tsize in
 // LDS, zeroed here). Control flow is wave-uniform.
 __device__ void compress_fragment(const uint8_t* in, uint32_t n, uint16_t* table,
-                                  const uint16_t* probe, Out& o, uint32_t lane) {
+                                  const uint16_t* probe, uint32_t* slots, Out& o,
+                                  uint32_t lane) {
   const uint32_t tsize = table_size(n);
   const uint32_t shift = 32u - (31u - __builtin_clz(tsize));
   for (uint32_t i = lane; i < tsize; i += 64) table[i] = 0;
@@ -254,7 +251,9 @@ __device__ void compress_fragment(const uint8_t* in, uint32_t n, uint16_t* table
     for (;;) {
       uint32_t cand = 0;
       bool remainder = false;
-      if (!search_probes(in, table, probe, ip, ip_limit, shift, lane, &ip, &cand)) break;
+      if (!search_probes(in, table, probe, slots, ip, ip_limit, shift, lane, kProbe.v[lane],
+                         kProbe.v[lane + 1], &ip, &cand))
+        break;
       emit_literal(o, in, next_emit, ip - next_emit, lane);
       uint64_t eight = 0;
       for (;;) {
@@ -306,7 +305,8 @@ __global__ void __launch_bounds__(64) snappy_compress_kernel(CompressArgs a) {
   const uint8_t* src = a.src + a.src_off[b];
   const uint32_t in_bytes = (a.frag_cap + 16u + 15u) & ~15u;
   uint8_t* in = smem;
-  uint16_t* probe = reinterpret_cast<uint16_t*>(smem + in_bytes);
+  uint32_t* slots = reinterpret_cast<uint32_t*>(smem + in_bytes);  // 256
+  uint16_t* probe = reinterpret_cast<uint16_t*>(slots + 256);
   uint16_t* table = probe + ((kProbes + 7) & ~7u);
   if (min(len, kFrag) > a.frag_cap) {  // the caller's max_len was too small
     if (lane == 0) {
@@ -330,7 +330,7 @@ __global__ void __launch_bounds__(64) snappy_compress_kernel(CompressArgs a) {
     const uint32_t fn = min(kFrag, len - s);
     stage(in, src + s, fn, 16, lane);
     __builtin_amdgcn_s_waitcnt(0);
-    compress_fragment(in, fn, table, probe, o, lane);
+    compress_fragment(in, fn, table, probe, slots, o, lane);
     __builtin_amdgcn_s_waitcnt(0);
   }
   if (lane == 0) {
@@ -619,7 +619,7 @@ hipError_t launch_sst_write_blocks(const uint8_t* raw, const uint64_t* raw_off,
     const uint32_t in_bytes = (a.frag_cap + 16u + 15u) & ~15u;
     uint32_t t = 256;
     while (t < kMaxTable && t < a.frag_cap) t <<= 1;
-    const size_t lds = in_bytes + 2u * ((kProbes + 7) & ~7u) + 2u * t;
+    const size_t lds = in_bytes + 1024u + 2u * ((kProbes + 7) & ~7u) + 2u * t;
     hipLaunchKernelGGL(snappy_compress_kernel, dim3(nblocks), dim3(64), lds, stream, a);
   }
   hipLaunchKernelGGL(sst_layout_kernel, dim3(1), dim3(1024), 0, stream, raw_len, clen, cst,
@@ -650,7 +650,7 @@ hipError_t launch_snappy_compress(const uint8_t* src, const uint64_t* src_off,
   const uint32_t in_bytes = (a.frag_cap + 16u + 15u) & ~15u;
   uint32_t t = 256;
   while (t < kMaxTable && t < a.frag_cap) t <<= 1;
-  const size_t lds = in_bytes + 2u * ((kProbes + 7) & ~7u) + 2u * t;
+  const size_t lds = in_bytes + 1024u + 2u * ((kProbes + 7) & ~7u) + 2u * t;
   hipLaunchKernelGGL(snappy_compress_kernel, dim3(nblocks), dim3(64), lds, stream, a);
   return hipGetLastError();
 }
