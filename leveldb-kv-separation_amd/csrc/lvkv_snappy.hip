@@ -180,14 +180,14 @@ __device__ __forceinline__ uint32_t hash32(uint32_t v, uint32_t shift) {
 // table is written once, after: each hash's last probe at or before the
 // match. Returns false at emit_remainder.
 __device__ __forceinline__ bool search_probes(const uint8_t* in, uint16_t* table,
-                                              const uint16_t* probe, uint32_t* slots,
+                                              uint32_t* slots,
                                               uint32_t base, uint32_t ip_limit, uint32_t shift,
                                               uint32_t lane, uint32_t w0, uint32_t w1,
                                               uint32_t* out_ip, uint32_t* out_cand) {
   for (uint32_t n0 = 0;; n0 += 64) {
     // (the first step's offsets come in registers: most searches end there)
-    const uint32_t p = base + (n0 == 0 ? w0 : probe[n0 + lane]);
-    const bool valid = base + (n0 == 0 ? w1 : probe[n0 + lane + 1]) <= ip_limit;
+    const uint32_t p = base + (n0 == 0 ? w0 : kProbe.v[n0 + lane]);
+    const bool valid = base + (n0 == 0 ? w1 : kProbe.v[n0 + lane + 1]) <= ip_limit;
     const uint64_t vmask = __ballot(valid);
     const uint32_t v = ld32(in, valid ? p : 0u);
     const uint32_t h = hash32(v, shift);
@@ -238,8 +238,7 @@ __device__ __forceinline__ bool search_probes(const uint8_t* in, uint16_t* table
 // CompressFragment of frag = in[0, n) (n <= kFrag) with table (u16 x tsize in
 // LDS, zeroed here). Control flow is wave-uniform.
 __device__ void compress_fragment(const uint8_t* in, uint32_t n, uint16_t* table,
-                                  const uint16_t* probe, uint32_t* slots, Out& o,
-                                  uint32_t lane) {
+                                  uint32_t* slots, Out& o, uint32_t lane) {
   const uint32_t tsize = table_size(n);
   const uint32_t shift = 32u - (31u - __builtin_clz(tsize));
   for (uint32_t i = lane; i < tsize; i += 64) table[i] = 0;
@@ -251,7 +250,7 @@ __device__ void compress_fragment(const uint8_t* in, uint32_t n, uint16_t* table
     for (;;) {
       uint32_t cand = 0;
       bool remainder = false;
-      if (!search_probes(in, table, probe, slots, ip, ip_limit, shift, lane, kProbe.v[lane],
+      if (!search_probes(in, table, slots, ip, ip_limit, shift, lane, kProbe.v[lane],
                          kProbe.v[lane + 1], &ip, &cand))
         break;
       emit_literal(o, in, next_emit, ip - next_emit, lane);
@@ -306,8 +305,7 @@ __global__ void __launch_bounds__(64) snappy_compress_kernel(CompressArgs a) {
   const uint32_t in_bytes = (a.frag_cap + 16u + 15u) & ~15u;
   uint8_t* in = smem;
   uint32_t* slots = reinterpret_cast<uint32_t*>(smem + in_bytes);  // 256
-  uint16_t* probe = reinterpret_cast<uint16_t*>(slots + 256);
-  uint16_t* table = probe + ((kProbes + 7) & ~7u);
+  uint16_t* table = reinterpret_cast<uint16_t*>(slots + 256);
   if (min(len, kFrag) > a.frag_cap) {  // the caller's max_len was too small
     if (lane == 0) {
       a.dst_len[b] = 0;
@@ -325,12 +323,11 @@ __global__ void __launch_bounds__(64) snappy_compress_kernel(CompressArgs a) {
   }
   if (lane == 0) o.p[o.n] = static_cast<uint8_t>(v);
   ++o.n;
-  for (uint32_t i = lane; i < kProbes; i += 64) probe[i] = kProbe.v[i];
   for (uint32_t s = 0; s < len; s += kFrag) {
     const uint32_t fn = min(kFrag, len - s);
     stage(in, src + s, fn, 16, lane);
     __builtin_amdgcn_s_waitcnt(0);
-    compress_fragment(in, fn, table, probe, slots, o, lane);
+    compress_fragment(in, fn, table, slots, o, lane);
     __builtin_amdgcn_s_waitcnt(0);
   }
   if (lane == 0) {
@@ -619,7 +616,7 @@ hipError_t launch_sst_write_blocks(const uint8_t* raw, const uint64_t* raw_off,
     const uint32_t in_bytes = (a.frag_cap + 16u + 15u) & ~15u;
     uint32_t t = 256;
     while (t < kMaxTable && t < a.frag_cap) t <<= 1;
-    const size_t lds = in_bytes + 1024u + 2u * ((kProbes + 7) & ~7u) + 2u * t;
+    const size_t lds = in_bytes + 1024u + 2u * t;
     hipLaunchKernelGGL(snappy_compress_kernel, dim3(nblocks), dim3(64), lds, stream, a);
   }
   hipLaunchKernelGGL(sst_layout_kernel, dim3(1), dim3(1024), 0, stream, raw_len, clen, cst,
@@ -650,7 +647,7 @@ hipError_t launch_snappy_compress(const uint8_t* src, const uint64_t* src_off,
   const uint32_t in_bytes = (a.frag_cap + 16u + 15u) & ~15u;
   uint32_t t = 256;
   while (t < kMaxTable && t < a.frag_cap) t <<= 1;
-  const size_t lds = in_bytes + 1024u + 2u * ((kProbes + 7) & ~7u) + 2u * t;
+  const size_t lds = in_bytes + 1024u + 2u * t;
   hipLaunchKernelGGL(snappy_compress_kernel, dim3(nblocks), dim3(64), lds, stream, a);
   return hipGetLastError();
 }
