@@ -350,3 +350,46 @@ def test_device_read_blocks_roundtrip_and_verdicts(lvkv, gpu):
                 assert got[i] == want
                 if i not in hurt:
                     assert want == raws[i]
+
+
+@pytest.mark.gpu
+def test_device_uncompress_fuzz_against_oracle(lvkv, gpu):
+    """Random byte strings and lightly-mutated valid streams, 6,000 of them:
+    the device's verdict and bytes equal the oracle's (the oracle is pinned
+    to libsnappy's verdicts above)."""
+    import torch
+    rng = np.random.default_rng(23)
+    from tools.db_bench_data import block_batch
+    base = [so.compress(block_batch(1, 4096, r).tobytes()) for r in (0.2, 0.5, 0.9)]
+    streams = []
+    for k in range(6000):
+        kind = k % 3
+        if kind == 0:  # random bytes behind a plausible preamble
+            n = int(rng.integers(1, 300))
+            body = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            streams.append(so._varint32(int(rng.integers(0, 600))) + body)
+        else:  # a valid stream with 1-3 bytes changed or a cut
+            s = bytearray(base[k % 3])
+            for _ in range(int(rng.integers(1, 4))):
+                s[int(rng.integers(0, len(s)))] = int(rng.integers(0, 256))
+            if kind == 2:
+                s = s[: int(rng.integers(1, len(s) + 1))]
+            streams.append(bytes(s))
+    src, off, ln = _pack(torch, gpu, streams, skew=2)
+    cap = 4096
+    dst, doff, dlen, st = lvkv.snappy_uncompress(src, off, ln, max_ulen=cap)
+    torch.cuda.synchronize()
+    st, dl = st.cpu().tolist(), dlen.cpu().tolist()
+    got = _unpack(dst, doff, torch.tensor(dl))
+    for i, s in enumerate(streams):
+        ost, out = so.uncompress(s)
+        ul = so.uncompressed_length(s)
+        if ost != so.BAD_LENGTH and ul is not None and ul > cap:
+            want = lvkv.SNAPPY_CAPACITY
+        elif ost != so.BAD_LENGTH and len(s) > so.max_compressed_length(cap):
+            want = lvkv.SNAPPY_TOO_LARGE
+        else:
+            want = ost
+        assert st[i] == want, (i, s[:12].hex(), st[i], want)
+        if want == so.OK:
+            assert got[i] == out
