@@ -31,6 +31,14 @@ int lvkv_debug_set_general_kernel(int cfg);
 int lvkv_debug_set_log_kernel(int cfg);
 int lvkv_debug_set_sst_form(int form);
 
+/* lvkv_zstd_uncompress_device with the failure site of each stream
+ * (d_detail[i]: 0 none, else the decoder's check that failed; tests). */
+int lvkv_debug_zstd_uncompress_device(const void* d_src, const uint64_t* d_src_off,
+                                      const uint32_t* d_src_len, void* d_dst,
+                                      const uint64_t* d_dst_off, const uint32_t* d_dst_cap,
+                                      uint32_t* d_out_len, uint8_t* d_status, uint32_t* d_detail,
+                                      size_t nblocks, uint32_t max_ulen, void* stream);
+
 /* The kernel-variant, timestamp and read-bandwidth probes live in the probe
  * build of the library (tools/probe/liblvkv_probe.so, tools/probe/lvkv_probe.h),
  * not in liblvkv_crc32c.so. */

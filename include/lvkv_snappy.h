@@ -88,6 +88,35 @@ int lvkv_snappy_uncompress_device(const void* d_src, const uint64_t* d_src_off,
                                   uint32_t* d_out_len, uint8_t* d_status, size_t nblocks,
                                   uint32_t max_ulen, void* stream);
 
+/* ---- Zstd frames (the read side of kZstdCompression) --------------------- */
+
+/*
+ * port::Zstd_GetUncompressedLength (port/port_stdcxx.h:163-177) over a batch:
+ * d_ulen[i] = ZSTD_getFrameContentSize of stream i, d_status[i] =
+ * LVKV_SNAPPY_OK, LVKV_SNAPPY_BAD_LENGTH (the size is 0: an empty frame or a
+ * skippable one) or LVKV_SNAPPY_TOO_LARGE (unknown, malformed, or past
+ * 32 bits; d_ulen = 0xffffffff).
+ */
+int lvkv_zstd_uncompressed_length_device(const void* d_src, const uint64_t* d_src_off,
+                                         const uint32_t* d_src_len, uint32_t* d_ulen,
+                                         uint8_t* d_status, size_t nblocks, void* stream);
+
+/*
+ * port::Zstd_Uncompress (port/port_stdcxx.h:179-199) over a batch: stream i
+ * decoded as ZSTD_decompressDCtx does (libzstd 1.4.9; frames one after
+ * another, skippable frames skipped, checksums verified) into exactly its
+ * content size at d_dst[d_dst_off[i], + d_dst_cap[i]). Statuses as
+ * lvkv_snappy_uncompress_device: OK, BAD_LENGTH (content size 0), BAD_CONTENTS
+ * (any ZSTD_isError), CAPACITY (content size past d_dst_cap[i], or unknown),
+ * TOO_LARGE (past max_ulen, or a stream longer than ZSTD_compressBound of
+ * it). max_ulen <= LVKV_SNAPPY_MAX_BLOCK. No compressor: zstd's bytes come
+ * from its match finder and entropy heuristics (the host library's).
+ */
+int lvkv_zstd_uncompress_device(const void* d_src, const uint64_t* d_src_off,
+                                const uint32_t* d_src_len, void* d_dst, const uint64_t* d_dst_off,
+                                const uint32_t* d_dst_cap, uint32_t* d_out_len, uint8_t* d_status,
+                                size_t nblocks, uint32_t max_ulen, void* stream);
+
 /* ---- the block writer and reader around the codec ----------------------- */
 
 /* Scratch for lvkv_sst_write_blocks_device with compression 1. */
@@ -119,18 +148,20 @@ int lvkv_sst_write_blocks_device(const void* d_raw, const uint64_t* d_raw_off,
 #define LVKV_READ_BAD_TYPE 2        /* "bad block type" (:156-158) */
 #define LVKV_READ_SNAPPY_LENGTH 3   /* "corrupted snappy compressed block length" (:122-124) */
 #define LVKV_READ_SNAPPY_CONTENTS 4 /* "corrupted snappy compressed block contents" (:127-131) */
-#define LVKV_READ_ZSTD 5            /* type kZstdCompression: no device codec, the caller's */
+#define LVKV_READ_ZSTD_LENGTH 5     /* "corrupted zstd compressed block length" (:140-143) */
 #define LVKV_READ_CAPACITY 6        /* contents longer than d_out_cap[i] (d_out_len says) */
 #define LVKV_READ_TOO_LARGE 7       /* beyond max_ulen (see LVKV_SNAPPY_TOO_LARGE) */
+#define LVKV_READ_ZSTD_CONTENTS 8   /* "corrupted zstd compressed block contents" (:145-149) */
 
 /*
  * ReadBlock over a batch of block handles of one file image
  * (table/format.cc:69-162): the CRC of contents + type checked against the
  * trailer (verify != 0, ReadOptions::verify_checksums), then by type:
- * kNoCompression copies the contents, kSnappyCompression decodes them, into
- * d_out[d_out_off[i], + d_out_cap[i]); d_out_len[i] = the block's length,
- * d_status[i] = LVKV_READ_*. Handles must lie inside the file (as for
- * lvkv_sst_verify_device; Table::Open's index decode checks that).
+ * kNoCompression copies the contents, kSnappyCompression and
+ * kZstdCompression decode them, into d_out[d_out_off[i], + d_out_cap[i]);
+ * d_out_len[i] = the block's length, d_status[i] = LVKV_READ_*. Handles
+ * must lie inside the file (as for lvkv_sst_verify_device; Table::Open's
+ * index decode checks that).
  */
 int lvkv_sst_read_blocks_device(const void* d_file, const uint64_t* d_handle_off,
                                 const uint32_t* d_handle_size, size_t nblocks, int verify,

@@ -144,6 +144,13 @@ def _load() -> ctypes.CDLL:
     L.lvkv_snappy_uncompressed_length_device.restype = i32
     L.lvkv_snappy_uncompress_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, sz, u32, vp]
     L.lvkv_snappy_uncompress_device.restype = i32
+    L.lvkv_zstd_uncompressed_length_device.argtypes = [vp, vp, vp, vp, vp, sz, vp]
+    L.lvkv_zstd_uncompressed_length_device.restype = i32
+    L.lvkv_zstd_uncompress_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, sz, u32, vp]
+    L.lvkv_zstd_uncompress_device.restype = i32
+    L.lvkv_debug_zstd_uncompress_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, u32,
+                                                    vp]
+    L.lvkv_debug_zstd_uncompress_device.restype = i32
     L.lvkv_sst_write_scratch_bytes.argtypes = [sz, u32]
     L.lvkv_sst_write_scratch_bytes.restype = sz
     L.lvkv_sst_write_blocks_device.argtypes = [vp, vp, vp, sz, i32, u32, vp, vp, u64, vp, vp, vp,
@@ -591,8 +598,69 @@ def snappy_uncompress(src, offsets, lengths, *, max_ulen: int, dst=None, dst_off
     return dst, dst_offsets, out_len, status
 
 
-READ_OK, READ_CHECKSUM, READ_BAD_TYPE, READ_SNAPPY_LENGTH, READ_SNAPPY_CONTENTS, READ_ZSTD, \
-    READ_CAPACITY, READ_TOO_LARGE = range(8)
+READ_OK, READ_CHECKSUM, READ_BAD_TYPE, READ_SNAPPY_LENGTH, READ_SNAPPY_CONTENTS, \
+    READ_ZSTD_LENGTH, READ_CAPACITY, READ_TOO_LARGE, READ_ZSTD_CONTENTS = range(9)
+
+
+def zstd_uncompressed_length(src, offsets, lengths, *, stream=None):
+    """Batched port::Zstd_GetUncompressedLength (port/port_stdcxx.h:163-177):
+    (lengths int32 as u32, status uint8: SNAPPY_OK / SNAPPY_BAD_LENGTH (0) /
+    SNAPPY_TOO_LARGE (unknown, malformed, > 32 bits))."""
+    torch = _torch()
+    n = offsets.numel()
+    dev = src.device
+    ulen = torch.zeros(n, dtype=torch.int32, device=dev)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    if n:
+        with torch.cuda.device(dev):
+            rc = _lib.lvkv_zstd_uncompressed_length_device(
+                _dev_ptr(src, "src", (torch.uint8, torch.int8)),
+                _dev_ptr(offsets, "offsets", (torch.int64,)),
+                _dev_ptr(lengths, "lengths", (torch.int32,), n),
+                _dev_ptr(ulen, "ulen"), _dev_ptr(status, "status"), n,
+                _stream_handle(stream, dev))
+        _check("lvkv_zstd_uncompressed_length_device", rc)
+    return ulen, status
+
+
+def zstd_uncompress(src, offsets, lengths, *, max_ulen: int, dst=None, dst_offsets=None,
+                    dst_caps=None, detail: bool = False, stream=None):
+    """Batched port::Zstd_Uncompress (port/port_stdcxx.h:179-199) as ReadBlock
+    runs it (table/format.cc:138-155). Statuses as snappy_uncompress. With
+    detail=True also returns the failure site per stream (a debug hook)."""
+    torch = _torch()
+    n = offsets.numel()
+    dev = src.device
+    if not 0 <= max_ulen <= SNAPPY_MAX_BLOCK:
+        raise ValueError(f"max_ulen must be in [0, {SNAPPY_MAX_BLOCK}]")
+    if dst is None:
+        dst_caps = torch.full((n,), max_ulen, dtype=torch.int32, device=dev)
+        dst_offsets = torch.arange(n, dtype=torch.int64, device=dev) * max_ulen
+        dst = torch.empty(max(1, n * max_ulen), dtype=torch.uint8, device=dev)
+    elif dst_offsets is None or dst_caps is None:
+        raise ValueError("dst needs dst_offsets and dst_caps")
+    out_len = torch.zeros(n, dtype=torch.int32, device=dev)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    why = torch.zeros(max(1, n), dtype=torch.int32, device=dev)
+    if n:
+        args = [_dev_ptr(src, "src", (torch.uint8, torch.int8)),
+                _dev_ptr(offsets, "offsets", (torch.int64,)),
+                _dev_ptr(lengths, "lengths", (torch.int32,), n),
+                _dev_ptr(dst, "dst", (torch.uint8, torch.int8)),
+                _dev_ptr(dst_offsets, "dst_offsets", (torch.int64,), n),
+                _dev_ptr(dst_caps, "dst_caps", (torch.int32,), n),
+                _dev_ptr(out_len, "out_len"), _dev_ptr(status, "status")]
+        with torch.cuda.device(dev):
+            if detail:
+                rc = _lib.lvkv_debug_zstd_uncompress_device(*args, _dev_ptr(why, "detail"), n,
+                                                            max_ulen, _stream_handle(stream, dev))
+            else:
+                rc = _lib.lvkv_zstd_uncompress_device(*args, n, max_ulen,
+                                                      _stream_handle(stream, dev))
+        _check("lvkv_zstd_uncompress_device", rc)
+    if detail:
+        return dst, dst_offsets, out_len, status, why
+    return dst, dst_offsets, out_len, status
 
 
 def sst_write_blocks(raw, offsets, lengths, *, compression: int = 1, max_len: Optional[int] = None,

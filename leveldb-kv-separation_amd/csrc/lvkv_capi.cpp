@@ -93,6 +93,11 @@ hipError_t launch_sst_read_blocks(const uint8_t* file, const uint64_t* hoff, con
                                   uint32_t nblocks, uint8_t* out, const uint64_t* out_off,
                                   const uint32_t* out_cap, uint32_t* out_len, uint8_t* status,
                                   const uint8_t* vstatus, uint32_t max_ulen, hipStream_t stream);
+hipError_t launch_zstd_uncompress(const uint8_t* src, const uint64_t* src_off,
+                                  const uint32_t* src_len, uint8_t* dst, const uint64_t* dst_off,
+                                  const uint32_t* dst_cap, uint32_t* out_len, uint8_t* status,
+                                  uint32_t* detail, uint32_t nblocks, uint32_t max_ulen,
+                                  uint32_t block_mode, const uint8_t* vstatus, hipStream_t stream);
 int compact_capacity(int cfg);
 int compact_occupancy(int cfg);
 // 8 waves x 3 chains, two workgroups per CU, generated lane tables
@@ -956,12 +961,69 @@ int lvkv_sst_read_blocks_device(const void* d_file, const uint64_t* d_handle_off
                                 nblocks, stream);
     if (rc != LVKV_OK) return rc;
   }
-  const hipError_t e = launch_sst_read_blocks(
+  const hipStream_t hs = static_cast<hipStream_t>(stream);
+  // raw and snappy blocks (zstd ones are left for the next launch)
+  hipError_t e = launch_sst_read_blocks(
       static_cast<const uint8_t*>(d_file), d_handle_off, d_handle_size,
       static_cast<uint32_t>(nblocks), static_cast<uint8_t*>(d_out), d_out_off, d_out_cap,
-      d_out_len, d_status, verify ? d_status : nullptr, max_ulen,
+      d_out_len, d_status, verify ? d_status : nullptr, max_ulen, hs);
+  if (e != hipSuccess) return hip_fail(e);
+  // kZstdCompression blocks whose checksum held (table/format.cc:138-155)
+  e = launch_zstd_uncompress(static_cast<const uint8_t*>(d_file), d_handle_off, d_handle_size,
+                             static_cast<uint8_t*>(d_out), d_out_off, d_out_cap, d_out_len,
+                             d_status, nullptr, static_cast<uint32_t>(nblocks), max_ulen, 1,
+                             verify ? d_status : nullptr, hs);
+  return e == hipSuccess ? LVKV_OK : hip_fail(e);
+}
+
+int lvkv_zstd_uncompressed_length_device(const void* d_src, const uint64_t* d_src_off,
+                                         const uint32_t* d_src_len, uint32_t* d_ulen,
+                                         uint8_t* d_status, size_t nblocks, void* stream) {
+  if (nblocks == 0) return LVKV_OK;
+  if (!d_src || !d_src_off || !d_src_len || !d_ulen || !d_status ||
+      nblocks > kMaxBlocksPerLaunch)
+    return LVKV_ERR_INVALID;
+  int rc = LVKV_OK;
+  if (current_ctx(&rc) == nullptr) return rc;
+  const hipError_t e = launch_zstd_uncompress(
+      static_cast<const uint8_t*>(d_src), d_src_off, d_src_len, nullptr, nullptr, nullptr,
+      d_ulen, d_status, nullptr, static_cast<uint32_t>(nblocks), 0, 0, nullptr,
       static_cast<hipStream_t>(stream));
   return e == hipSuccess ? LVKV_OK : hip_fail(e);
+}
+
+static int zstd_uncompress(const void* d_src, const uint64_t* d_src_off, const uint32_t* d_src_len,
+                    void* d_dst, const uint64_t* d_dst_off, const uint32_t* d_dst_cap,
+                    uint32_t* d_out_len, uint8_t* d_status, uint32_t* d_detail, size_t nblocks,
+                    uint32_t max_ulen, void* stream) {
+  if (nblocks == 0) return LVKV_OK;
+  if (!d_src || !d_src_off || !d_src_len || !d_dst || !d_dst_off || !d_dst_cap || !d_out_len ||
+      !d_status || nblocks > kMaxBlocksPerLaunch || max_ulen > LVKV_SNAPPY_MAX_BLOCK)
+    return LVKV_ERR_INVALID;
+  int rc = LVKV_OK;
+  if (current_ctx(&rc) == nullptr) return rc;
+  const hipError_t e = launch_zstd_uncompress(
+      static_cast<const uint8_t*>(d_src), d_src_off, d_src_len, static_cast<uint8_t*>(d_dst),
+      d_dst_off, d_dst_cap, d_out_len, d_status, d_detail, static_cast<uint32_t>(nblocks),
+      max_ulen, 0, nullptr, static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? LVKV_OK : hip_fail(e);
+}
+
+int lvkv_zstd_uncompress_device(const void* d_src, const uint64_t* d_src_off,
+                                const uint32_t* d_src_len, void* d_dst, const uint64_t* d_dst_off,
+                                const uint32_t* d_dst_cap, uint32_t* d_out_len, uint8_t* d_status,
+                                size_t nblocks, uint32_t max_ulen, void* stream) {
+  return zstd_uncompress(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len,
+                         d_status, nullptr, nblocks, max_ulen, stream);
+}
+
+int lvkv_debug_zstd_uncompress_device(const void* d_src, const uint64_t* d_src_off,
+                                      const uint32_t* d_src_len, void* d_dst,
+                                      const uint64_t* d_dst_off, const uint32_t* d_dst_cap,
+                                      uint32_t* d_out_len, uint8_t* d_status, uint32_t* d_detail,
+                                      size_t nblocks, uint32_t max_ulen, void* stream) {
+  return zstd_uncompress(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len,
+                         d_status, d_detail, nblocks, max_ulen, stream);
 }
 
 int lvkv_crc32c_batch_host(const void* h_base, const uint64_t* offsets,

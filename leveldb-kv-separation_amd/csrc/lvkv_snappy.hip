@@ -405,7 +405,7 @@ __global__ void __launch_bounds__(64) snappy_uncompress_kernel(UncompressArgs a)
     const uint32_t type = src[n];
     if (a.vstatus != nullptr && a.vstatus[b] != 0)
       return finish_read(LVKV_READ_CHECKSUM, 0);  // :95-98
-    if (type == 2) return finish_read(LVKV_READ_ZSTD, 0);
+    if (type == 2) return;  // kZstdCompression: the zstd kernel's, launched next
     if (type > 2) return finish_read(LVKV_READ_BAD_TYPE, 0);  // :156-158
     if (type == 0) {  // kNoCompression: the contents as they are (:103-119)
       if (n > a.dst_cap[b]) return finish_read(LVKV_READ_CAPACITY, n);

@@ -1,0 +1,998 @@
+// Zstd frame decoder on the device (the read side of
+// kZstdCompression): what port::Zstd_GetUncompressedLength / Zstd_Uncompress
+// (port/port_stdcxx.h:163-199) do in ReadBlock (table/format.cc:138-155).
+// The frames are RFC 8878's, decoded the way libzstd 1.4.9 decodes them
+// (oracle/zstd_oracle.py is the restatement it is tested against, and that
+// is pinned to the library). The compressor stays the library's: its bytes
+// depend on zstd's match finder and entropy heuristics, which this project
+// does not restate.
+//
+// One wave per frame (64-thread workgroups), the frame staged in LDS. The
+// frame is a chain (headers, a Huffman tree, FSE tables, backward
+// bitstreams, sequences whose matches read earlier output), so control flow
+// is wave-uniform; the lanes copy literals and matches, fill decode tables,
+// and decode the four Huffman streams of a block side by side (lanes 0-3,
+// each with its own bit reader).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lvkv_snappy.h"
+
+namespace lvkv {
+namespace {
+
+constexpr uint32_t kMagic = 0xFD2FB528u;
+constexpr uint32_t kBlockMax = 128u * 1024u;
+
+// failure sites (the debug detail array; 0 = none)
+enum : uint32_t {
+  kFOk = 0, kFHeader, kFDict, kFBlockHdr, kFBlockType, kFBlockSize, kFCap, kFLitHdr,
+  kFLitSize, kFHufHdr, kFHufWeights, kFHufTable, kFHufStream, kFJump, kFSeqHdr, kFNcount,
+  kFFseSpread, kFRle, kFRepeat, kFSeqBits, kFLitOverrun, kFOffset, kFContentSize, kFChecksum,
+  kFTrailing, kFSkippable, kFEmpty
+};
+
+__device__ __forceinline__ uint32_t ld32(const uint8_t* b, uint32_t p) {
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(b + (p & ~3u));
+  return __builtin_amdgcn_alignbyte(d[1], d[0], p & 3u);
+}
+__device__ __forceinline__ uint64_t ld64(const uint8_t* b, uint32_t p) {
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(b + (p & ~3u));
+  const uint32_t s = p & 3u;
+  const uint32_t lo = __builtin_amdgcn_alignbyte(d[1], d[0], s);
+  const uint32_t hi = __builtin_amdgcn_alignbyte(d[2], d[1], s);
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// Global -> LDS (4-aligned), as the Snappy kernels stage (aligned dword loads
+// at any source alignment, nothing read past the block's last dword).
+__device__ __forceinline__ void stage(uint8_t* dst, const uint8_t* src, uint32_t n, uint32_t pad,
+                                      uint32_t lane) {
+  const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src)) & 3u;
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(src - mis);
+  const uint32_t nd = (n + 3u) >> 2;
+  for (uint32_t i = lane; i < nd; i += 64) {
+    const uint32_t lo = s[i];
+    const uint32_t hi = (mis != 0 && 4u * (i + 1u) < mis + n) ? s[i + 1] : 0u;
+    reinterpret_cast<uint32_t*>(dst)[i] = __builtin_amdgcn_alignbyte(hi, lo, mis);
+  }
+  for (uint32_t i = n + lane; i < n + pad; i += 64) dst[i] = 0;
+}
+
+// ---- backward bitstreams (RFC 8878 §4.1.1.1) ------------------------------
+// Bits [0, pos) of the stream, read from the top down; bits below 0 read as
+// zeros. A 64-bit window of the staged bytes is cached in registers.
+struct BitR {
+  const uint8_t* in;  // staged frame (4-aligned)
+  uint32_t start;     // the stream's first byte in `in`
+  int32_t pos;        // bits left
+  int32_t cb;         // window's first byte (relative), or -1
+  uint64_t win;
+};
+
+__device__ __forceinline__ bool br_init(BitR& r, const uint8_t* in, uint32_t lo, uint32_t hi) {
+  r.in = in;
+  r.start = lo;
+  r.cb = -1;
+  r.win = 0;
+  if (hi <= lo) return false;
+  const uint32_t last = in[hi - 1];
+  if (last == 0) return false;
+  r.pos = static_cast<int32_t>(8u * (hi - lo - 1u) + (31u - __builtin_clz(last)));
+  return true;
+}
+
+// bits [p, p + n) (n <= 32), zeros below 0
+__device__ __forceinline__ uint32_t br_bits(BitR& r, int32_t p, uint32_t n) {
+  const int32_t top = p + static_cast<int32_t>(n);
+  if (n == 0 || top <= 0) return 0;
+  const int32_t lo = p < 0 ? 0 : p;
+  if (r.cb < 0 || lo < 8 * r.cb || top > 8 * r.cb + 64) {
+    int32_t cb = ((top + 7) >> 3) - 8;
+    if (cb < 0) cb = 0;
+    r.cb = cb;
+    r.win = ld64(r.in, r.start + static_cast<uint32_t>(cb));
+  }
+  uint64_t v = r.win >> (lo - 8 * r.cb);
+  v &= (uint64_t{1} << (top - lo)) - 1u;
+  return static_cast<uint32_t>(v << (lo - p));
+}
+
+__device__ __forceinline__ uint32_t br_read(BitR& r, uint32_t n) {
+  r.pos -= static_cast<int32_t>(n);
+  return br_bits(r, r.pos, n);
+}
+
+// ---- FSE tables (RFC 8878 §4.1; FSE_readNCount / FSE_buildDTable) --------
+// Decode entries: symbol | nbBits << 8 | baseline << 16.
+
+// The table description at in[p, end): false when malformed. Scalar code.
+__device__ bool read_ncount(const uint8_t* in, uint32_t p, uint32_t end, uint32_t max_sym,
+                            uint32_t max_log, int16_t* counts, uint32_t* nsym, uint32_t* log_out,
+                            uint32_t* used) {
+  if (end <= p) return false;
+  const uint32_t len = end - p;
+  // 32 bits at byte offset i of the description, zeros past its end
+  auto rd32 = [&](uint32_t i) -> uint32_t {
+    if (i + 4 <= len) return ld32(in, p + i);
+    uint32_t v = 0;
+    for (uint32_t k = 0; k < 4; ++k)
+      if (i + k < len) v |= static_cast<uint32_t>(in[p + i + k]) << (8 * k);
+    return v;
+  };
+  uint32_t ip = 0;
+  uint32_t bits = rd32(0);
+  const uint32_t log = (bits & 0xFu) + 5u;
+  if (log > max_log) return false;
+  bits >>= 4;
+  int32_t bit_count = 4;
+  int32_t nb = static_cast<int32_t>(log) + 1;
+  int32_t remaining = (1 << log) + 1;
+  int32_t threshold = 1 << log;
+  bool prev0 = false;
+  uint32_t s = 0;
+  while (remaining > 1 && s <= max_sym) {
+    if (prev0) {
+      uint32_t n0 = s;
+      while ((bits & 0xFFFFu) == 0xFFFFu) {
+        n0 += 24;
+        ip += 2;
+        bits = rd32(ip) >> bit_count;
+      }
+      while ((bits & 3u) == 3u) {
+        n0 += 3;
+        bits >>= 2;
+        bit_count += 2;
+      }
+      n0 += bits & 3u;
+      bit_count += 2;
+      if (n0 > max_sym) return false;
+      while (s < n0) counts[s++] = 0;
+      ip += static_cast<uint32_t>(bit_count >> 3);
+      bit_count &= 7;
+      bits = rd32(ip) >> bit_count;
+    }
+    const int32_t mx = (2 * threshold - 1) - remaining;
+    int32_t count;
+    if (static_cast<int32_t>(bits & static_cast<uint32_t>(threshold - 1)) < mx) {
+      count = static_cast<int32_t>(bits & static_cast<uint32_t>(threshold - 1));
+      bit_count += nb - 1;
+    } else {
+      count = static_cast<int32_t>(bits & static_cast<uint32_t>(2 * threshold - 1));
+      if (count >= threshold) count -= mx;
+      bit_count += nb;
+    }
+    count -= 1;
+    remaining -= count < 0 ? -count : count;
+    counts[s++] = static_cast<int16_t>(count);
+    prev0 = count == 0;
+    while (remaining < threshold) {
+      nb -= 1;
+      threshold >>= 1;
+    }
+    ip += static_cast<uint32_t>(bit_count >> 3);
+    bit_count &= 7;
+    bits = rd32(ip) >> bit_count;
+  }
+  if (remaining != 1 || bit_count > 32) return false;
+  const uint32_t u = ip + static_cast<uint32_t>((bit_count + 7) >> 3);
+  if (u > len) return false;
+  *nsym = s;
+  *log_out = log;
+  *used = u;
+  return true;
+}
+
+// Spread and decode entries for counts[0, nsym) at accuracy `log` into
+// table (1 << log entries). `scratch` holds the per-symbol next state.
+// Scalar: a table has at most 512 entries.
+__device__ bool build_fse(const int16_t* counts, uint32_t nsym, uint32_t log, uint32_t* table,
+                          uint16_t* nxt, uint32_t lane) {
+  const uint32_t size = 1u << log;
+  int32_t high = static_cast<int32_t>(size) - 1;
+  // symbols with count -1 at the top; everyone's next state starts at its count
+  for (uint32_t s = 0; s < nsym; ++s) {
+    const int32_t c = counts[s];
+    if (c == -1) {
+      if (lane == 0) table[high] = s;
+      --high;
+      if (lane == 0) nxt[s] = 1;
+    } else if (lane == 0) {
+      nxt[s] = static_cast<uint16_t>(c);
+    }
+  }
+  const uint32_t step = (size >> 1) + (size >> 3) + 3u;
+  const uint32_t mask = size - 1u;
+  uint32_t pos = 0;
+  for (uint32_t s = 0; s < nsym; ++s) {
+    const int32_t c = counts[s];
+    for (int32_t i = 0; i < c; ++i) {
+      if (lane == 0) table[pos] = s;
+      pos = (pos + step) & mask;
+      while (static_cast<int32_t>(pos) > high) pos = (pos + step) & mask;
+    }
+  }
+  if (pos != 0) return false;
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  // decode entries in table order: symbol s's k-th entry gets state nxt[s]++
+  for (uint32_t u = 0; u < size; ++u) {
+    const uint32_t s = table[u] & 255u;
+    const uint32_t ns = nxt[s];
+    if (lane == 0) nxt[s] = static_cast<uint16_t>(ns + 1u);
+    const uint32_t nbits = log - (31u - __builtin_clz(ns));
+    const uint32_t base = (ns << nbits) - size;
+    if (lane == 0) table[u] = s | (nbits << 8) | (base << 16);
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  return true;
+}
+
+// The predefined distributions (RFC 8878 §3.1.1.3.2.2)
+__constant__ int16_t kLLDefault[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
+                                       2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
+__constant__ int16_t kMLDefault[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                       1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                       1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+__constant__ int16_t kOFDefault[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
+                                       1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+__constant__ uint32_t kLLBase[36] = {0,    1,    2,    3,     4,     5,     6,    7,    8,
+                                     9,    10,   11,   12,    13,    14,    15,   16,   18,
+                                     20,   22,   24,   28,    32,    40,    48,   64,   128,
+                                     256,  512,  1024, 2048,  4096,  8192,  16384, 32768, 65536};
+__constant__ uint8_t kLLBits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,  0,  0,  1,  1,
+                                    1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+__constant__ uint32_t kMLBase[53] = {3,  4,  5,  6,  7,  8,  9,  10,  11,  12,   13,   14,   15,  16,
+                                     17, 18, 19, 20, 21, 22, 23, 24,  25,  26,   27,   28,   29,  30,
+                                     31, 32, 33, 34, 35, 37, 39, 41,  43,  47,   51,   59,   67,  83,
+                                     99, 131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771, 65539};
+__constant__ uint8_t kMLBits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,  0,  0,  0,
+                                    0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1,  1,  1,  1,
+                                    2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+
+// ---- LDS layout -----------------------------------------------------------
+
+struct Lds {
+  uint8_t* in;      // the staged frame (+16 zero bytes)
+  uint8_t* out;     // the frame's output
+  uint8_t* lits;    // a block's literals
+  uint16_t* huf;    // Huffman decode table: symbol | nbBits << 8 (<= 2048)
+  uint32_t* ll;     // FSE tables: 512 / 256 / 512 entries, and 64 for weights
+  uint32_t* of;
+  uint32_t* ml;
+  uint32_t* wt;
+  uint8_t* w;       // Huffman weights (256 + 1)
+  int16_t* cnt;     // normalized counts scratch (256: the weights' FSE may name 256)
+  uint16_t* nxt;    // FSE next-state scratch (256)
+};
+
+constexpr uint32_t kHufEntries = 2048, kFseLL = 512, kFseOF = 256, kFseML = 512, kFseW = 64;
+
+__host__ __device__ constexpr uint32_t zstd_in_cap(uint32_t out_cap) {
+  // ZSTD_compressBound(out_cap) (1.4.9): every frame the library writes
+  return out_cap + (out_cap >> 8) + (out_cap < (128u << 10) ? ((128u << 10) - out_cap) >> 11 : 0u);
+}
+__host__ __device__ constexpr uint32_t round16(uint32_t x) { return (x + 15u) & ~15u; }
+__host__ __device__ constexpr uint32_t zstd_lds_bytes(uint32_t out_cap) {
+  return round16(zstd_in_cap(out_cap) + 16u + 4u) + round16(out_cap) + round16(out_cap + 32u) +
+         2u * kHufEntries + 4u * (kFseLL + kFseOF + kFseML + kFseW) + 272u + 512u + 512u;
+}
+
+__device__ Lds lds_layout(uint8_t* smem, uint32_t out_cap) {
+  Lds L;
+  uint32_t o = 0;
+  L.in = smem;
+  o += round16(zstd_in_cap(out_cap) + 16u + 4u);
+  L.out = smem + o;
+  o += round16(out_cap);
+  L.lits = smem + o;
+  o += round16(out_cap + 32u);
+  L.huf = reinterpret_cast<uint16_t*>(smem + o);
+  o += 2u * kHufEntries;
+  L.ll = reinterpret_cast<uint32_t*>(smem + o);
+  o += 4u * kFseLL;
+  L.of = reinterpret_cast<uint32_t*>(smem + o);
+  o += 4u * kFseOF;
+  L.ml = reinterpret_cast<uint32_t*>(smem + o);
+  o += 4u * kFseML;
+  L.wt = reinterpret_cast<uint32_t*>(smem + o);
+  o += 4u * kFseW;
+  L.w = smem + o;
+  o += 272u;
+  L.cnt = reinterpret_cast<int16_t*>(smem + o);
+  o += 512u;
+  L.nxt = reinterpret_cast<uint16_t*>(smem + o);
+  return L;
+}
+
+// ---- Huffman (RFC 8878 §4.2; HUF_readStats / HUF_readDTableX1) -----------
+
+// The tree description at in[p, end): weights into L.w (with the implied
+// last), *nw = symbols, *maxbits, *used. Scalar.
+__device__ bool huf_weights(const Lds& L, uint32_t p, uint32_t end, uint32_t* nw,
+                            uint32_t* maxbits, uint32_t* used, uint32_t lane, uint32_t* fail) {
+  if (p >= end) return *fail = kFHufHdr, false;
+  const uint32_t hb = L.in[p];
+  uint32_t n = 0;
+  if (hb >= 128) {  // direct 4-bit weights
+    n = hb - 127u;
+    const uint32_t nbytes = (n + 1u) >> 1;
+    if (p + 1u + nbytes > end) return *fail = kFHufHdr, false;
+    for (uint32_t i = lane; i < n; i += 64) {
+      const uint32_t b = L.in[p + 1u + (i >> 1)];
+      L.w[i] = static_cast<uint8_t>((i & 1u) ? (b & 15u) : (b >> 4));
+    }
+    *used = 1u + nbytes;
+  } else {  // FSE-compressed weights, two interleaved states
+    if (hb == 0 || p + 1u + hb > end) return *fail = kFHufHdr, false;
+    uint32_t nsym, log, nc;
+    if (!read_ncount(L.in, p + 1u, p + 1u + hb, 255u, 6u, L.cnt, &nsym, &log, &nc))
+      return *fail = kFNcount, false;
+    if (!build_fse(L.cnt, nsym, log, L.wt, L.nxt, lane)) return *fail = kFFseSpread, false;
+    BitR r;
+    if (!br_init(r, L.in, p + 1u + nc, p + 1u + hb)) return *fail = kFHufWeights, false;
+    uint32_t s1 = br_read(r, log), s2 = br_read(r, log);
+    for (;;) {
+      if (n > 253u) return *fail = kFHufWeights, false;
+      uint32_t e = L.wt[s1];
+      if (lane == 0) L.w[n] = static_cast<uint8_t>(e & 255u);
+      ++n;
+      s1 = (e >> 16) + br_read(r, (e >> 8) & 255u);
+      if (r.pos < 0) {
+        if (lane == 0) L.w[n] = static_cast<uint8_t>(L.wt[s2] & 255u);
+        ++n;
+        break;
+      }
+      if (n > 253u) return *fail = kFHufWeights, false;
+      e = L.wt[s2];
+      if (lane == 0) L.w[n] = static_cast<uint8_t>(e & 255u);
+      ++n;
+      s2 = (e >> 16) + br_read(r, (e >> 8) & 255u);
+      if (r.pos < 0) {
+        if (lane == 0) L.w[n] = static_cast<uint8_t>(L.wt[s1] & 255u);
+        ++n;
+        break;
+      }
+    }
+    *used = 1u + hb;
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  // total weight, the implied last weight, and rank 1's count
+  uint32_t total = 0, bad = 0;
+  for (uint32_t i = lane; i < n; i += 64) {
+    const uint32_t x = L.w[i];
+    bad |= x > 11u;
+    total += (1u << x) >> 1;
+  }
+  for (uint32_t d = 32; d >= 1; d >>= 1) {
+    total += __shfl_xor(total, d);
+    bad |= __shfl_xor(bad, d);
+  }
+  if (bad || total == 0) return *fail = kFHufWeights, false;
+  const uint32_t mb = 32u - __builtin_clz(total);  // highbit(total) + 1
+  if (mb > 11u) return *fail = kFHufWeights, false;
+  const uint32_t rest = (1u << mb) - total;
+  if (rest & (rest - 1u)) return *fail = kFHufWeights, false;
+  const uint32_t last = 32u - __builtin_clz(rest);
+  if (lane == 0) L.w[n] = static_cast<uint8_t>(last);
+  ++n;
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  uint32_t r1 = 0;
+  for (uint32_t i = lane; i < n; i += 64) r1 += L.w[i] == 1u ? 1u : 0u;
+  for (uint32_t d = 32; d >= 1; d >>= 1) r1 += __shfl_xor(r1, d);
+  if (r1 < 2u || (r1 & 1u)) return *fail = kFHufWeights, false;
+  *nw = n;
+  *maxbits = mb;
+  return true;
+}
+
+// Decode table: symbols by weight, then by symbol value, each over
+// 2^(w-1) entries of 2^maxbits.
+__device__ void huf_table(const Lds& L, uint32_t nw, uint32_t mb, uint32_t lane) {
+  uint32_t pos = 0;
+  for (uint32_t wgt = 1; wgt <= mb; ++wgt) {
+    const uint32_t span = 1u << (wgt - 1u);
+    const uint32_t e = (mb + 1u - wgt) << 8;
+    for (uint32_t g = 0; g < nw; g += 64) {
+      const uint32_t s = g + lane;
+      uint64_t m = __ballot(s < nw && L.w[s] == wgt);
+      while (m) {
+        const uint32_t sym = g + static_cast<uint32_t>(__builtin_ctzll(m));
+        m &= m - 1u;
+        for (uint32_t k = lane; k < span; k += 64)
+          L.huf[pos + k] = static_cast<uint16_t>(sym | e);
+        pos += span;
+      }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+}
+
+// Huffman stream in[lo, hi) -> n symbols at dst; true when consumed exactly.
+// Per lane (the four streams run on lanes 0-3).
+__device__ __forceinline__ bool huf_stream(const Lds& L, uint32_t lo, uint32_t hi, uint32_t n,
+                                           uint32_t mb, uint8_t* dst) {
+  BitR r;
+  if (!br_init(r, L.in, lo, hi)) return false;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t e = L.huf[br_bits(r, r.pos - static_cast<int32_t>(mb), mb)];
+    r.pos -= static_cast<int32_t>(e >> 8);
+    dst[i] = static_cast<uint8_t>(e & 255u);
+  }
+  return r.pos == 0;
+}
+
+// ---- a frame --------------------------------------------------------------
+
+struct Frame {
+  uint32_t hsize;   // header bytes
+  uint64_t csize;   // content size (~0 unknown)
+  uint32_t single, checksum, dict;
+  bool ok;
+};
+
+// RFC 8878 §3.1.1.1 at g[0, n) (any memory); ok = false when malformed.
+template <typename Rd>
+__device__ Frame frame_header(Rd rd, uint32_t n) {
+  Frame f{};
+  f.ok = false;
+  f.csize = ~uint64_t{0};
+  if (n < 5) return f;
+  const uint32_t magic = rd(0) | rd(1) << 8 | rd(2) << 16 | rd(3) << 24;
+  if (magic != kMagic) return f;
+  const uint32_t fhd = rd(4);
+  if (fhd & 8u) return f;
+  const uint32_t fcs_flag = fhd >> 6;
+  f.single = (fhd >> 5) & 1u;
+  f.checksum = (fhd >> 2) & 1u;
+  const uint32_t did = (fhd & 3u) == 3u ? 4u : (fhd & 3u);
+  uint32_t p = 5;
+  if (!f.single) {
+    if (p >= n) return f;
+    if (10u + (rd(p) >> 3) > 31u) return f;
+    ++p;
+  }
+  const uint32_t fcs_size = fcs_flag == 0 ? f.single : (1u << fcs_flag);
+  if (p + did + fcs_size > n) return f;
+  uint32_t d = 0;
+  for (uint32_t k = 0; k < did; ++k) d |= rd(p + k) << (8 * k);
+  f.dict = d;
+  p += did;
+  if (fcs_size) {
+    uint64_t v = 0;
+    for (uint32_t k = 0; k < fcs_size; ++k) v |= static_cast<uint64_t>(rd(p + k)) << (8 * k);
+    if (fcs_size == 2) v += 256;
+    f.csize = v;
+  }
+  p += fcs_size;
+  f.hsize = p;
+  f.ok = true;
+  return f;
+}
+
+struct ZArgs {
+  const uint8_t* src;
+  const uint64_t* src_off;
+  const uint32_t* src_len;
+  uint8_t* dst;
+  const uint64_t* dst_off;
+  const uint32_t* dst_cap;  // nullptr: lengths only
+  uint32_t* out_len;
+  uint8_t* status;
+  uint32_t* detail;  // debug: the failure site per block (nullptr: none)
+  uint32_t nblocks;
+  uint32_t out_cap;
+  uint32_t block_mode;  // ReadBlock mode: handles, type byte 2 only, LVKV_READ_*
+  const uint8_t* vstatus;
+};
+
+// One compressed block's literals into L.lits; *nlit, *used. Uniform.
+__device__ bool literals(const Lds& L, uint32_t p, uint32_t end, uint32_t cap, bool* have_tree,
+                         uint32_t* mb_tree, uint32_t* nlit, uint32_t* used, uint32_t lane,
+                         uint32_t* fail) {
+  if (end - p < 3u) return *fail = kFLitHdr, false;  // MIN_CBLOCK_SIZE
+  const uint32_t b0 = L.in[p];
+  const uint32_t type = b0 & 3u, sf = (b0 >> 2) & 3u;
+  if (type <= 1u) {  // raw / RLE
+    uint32_t n, hs;
+    if (sf == 0 || sf == 2) {
+      n = b0 >> 3;
+      hs = 1;
+    } else if (sf == 1) {
+      n = (b0 >> 4) + (static_cast<uint32_t>(L.in[p + 1]) << 4);
+      hs = 2;
+    } else {
+      n = (b0 >> 4) + (static_cast<uint32_t>(L.in[p + 1]) << 4) +
+          (static_cast<uint32_t>(L.in[p + 2]) << 12);
+      hs = 3;
+    }
+    if (n > kBlockMax) return *fail = kFLitSize, false;
+    if (n > cap) return *fail = kFCap, false;
+    if (type == 0) {
+      if (p + hs + n > end) return *fail = kFLitSize, false;
+      for (uint32_t k = lane; k < n; k += 64) L.lits[k] = L.in[p + hs + k];
+      *used = hs + n;
+    } else {
+      if (p + hs + 1u > end) return *fail = kFLitSize, false;
+      const uint8_t v = L.in[p + hs];
+      for (uint32_t k = lane; k < n; k += 64) L.lits[k] = v;
+      *used = hs + 1u;
+    }
+    *nlit = n;
+    return true;
+  }
+  const uint32_t hs = sf == 0 ? 3u : sf == 1 ? 3u : sf == 2 ? 4u : 5u;
+  if (p + hs > end) return *fail = kFLitHdr, false;
+  uint64_t hv = 0;
+  for (uint32_t k = 0; k < hs; ++k) hv |= static_cast<uint64_t>(L.in[p + k]) << (8 * k);
+  const uint32_t bits = sf <= 1u ? 10u : sf == 2 ? 14u : 18u;
+  const uint32_t n = static_cast<uint32_t>(hv >> 4) & ((1u << bits) - 1u);
+  const uint32_t csize = static_cast<uint32_t>(hv >> (4 + bits)) & ((1u << bits) - 1u);
+  if (n > kBlockMax) return *fail = kFLitSize, false;
+  if (p + hs + csize > end) return *fail = kFLitSize, false;
+  if (n > cap) return *fail = kFCap, false;
+  uint32_t q = p + hs;
+  const uint32_t qend = p + hs + csize;
+  if (type == 2) {
+    uint32_t nw, mb, u;
+    if (!huf_weights(L, q, qend, &nw, &mb, &u, lane, fail)) return false;
+    huf_table(L, nw, mb, lane);
+    *have_tree = true;
+    *mb_tree = mb;
+    q += u;
+  } else if (!*have_tree) {
+    return *fail = kFHufHdr, false;
+  }
+  const uint32_t mb = *mb_tree;
+  bool good;
+  if (sf == 0) {
+    good = lane == 0 ? huf_stream(L, q, qend, n, mb, L.lits) : true;
+  } else {
+    if (qend - q < 10u) return *fail = kFJump, false;
+    const uint32_t s1 = L.in[q] | static_cast<uint32_t>(L.in[q + 1]) << 8;
+    const uint32_t s2 = L.in[q + 2] | static_cast<uint32_t>(L.in[q + 3]) << 8;
+    const uint32_t s3 = L.in[q + 4] | static_cast<uint32_t>(L.in[q + 5]) << 8;
+    const uint32_t a = q + 6u, b = a + s1, c = b + s2, d = c + s3;
+    if (d > qend) return *fail = kFJump, false;
+    const uint32_t seg = (n + 3u) >> 2;
+    if (3u * seg > n) return *fail = kFJump, false;
+    good = true;
+    if (lane < 4) {
+      const uint32_t lo = lane == 0 ? a : lane == 1 ? b : lane == 2 ? c : d;
+      const uint32_t hi = lane == 0 ? b : lane == 1 ? c : lane == 2 ? d : qend;
+      const uint32_t cnt = lane == 3 ? n - 3u * seg : seg;
+      good = huf_stream(L, lo, hi, cnt, mb, L.lits + lane * seg);
+    }
+  }
+  if (__ballot(!good)) return *fail = kFHufStream, false;
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  *nlit = n;
+  *used = hs + csize;
+  return true;
+}
+
+// A sequence table by mode into `table`; *log, *used. Uniform.
+__device__ bool seq_table(const Lds& L, uint32_t p, uint32_t end, uint32_t mode,
+                          const int16_t* dflt, uint32_t dn, uint32_t dlog, uint32_t max_sym,
+                          uint32_t max_log, uint32_t* table, bool* have, uint32_t* log,
+                          uint32_t* used, uint32_t lane, uint32_t* fail) {
+  *used = 0;
+  if (mode == 0) {
+    for (uint32_t s = lane; s < dn; s += 64) L.cnt[s] = dflt[s];
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    if (!build_fse(L.cnt, dn, dlog, table, L.nxt, lane)) return *fail = kFFseSpread, false;
+    *log = dlog;
+  } else if (mode == 1) {
+    if (p >= end) return *fail = kFRle, false;
+    const uint32_t s = L.in[p];
+    if (s > max_sym) return *fail = kFRle, false;
+    if (lane == 0) table[0] = s;
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    *log = 0;
+    *used = 1;
+  } else if (mode == 2) {
+    uint32_t nsym, lg, u;
+    if (!read_ncount(L.in, p, end, max_sym, max_log, L.cnt, &nsym, &lg, &u))
+      return *fail = kFNcount, false;
+    if (!build_fse(L.cnt, nsym, lg, table, L.nxt, lane)) return *fail = kFFseSpread, false;
+    *log = lg;
+    *used = u;
+  } else if (!*have) {
+    return *fail = kFRepeat, false;
+  }
+  *have = true;
+  return true;
+}
+
+struct SeqState {
+  bool have_ll, have_of, have_ml, have_tree;
+  uint32_t ll_log, of_log, ml_log, mb_tree;
+  uint32_t rep0, rep1, rep2;
+};
+
+// Copies n bytes from LDS `from` to out[op, ...): lanes 64 at a time. An
+// overlapping match (off < n) repeats its first `off` bytes.
+__device__ __forceinline__ void lds_copy(uint8_t* dst, const uint8_t* from, uint32_t n,
+                                         uint32_t off, uint32_t lane) {
+  if (off != 0 && off < n) {
+    for (uint32_t k = lane; k < n; k += 64) dst[k] = from[k % off];
+  } else {
+    for (uint32_t k = lane; k < n; k += 64) dst[k] = from[k];
+  }
+}
+
+// A compressed block at in[p, end): output appended at out[*op, ...).
+__device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
+                           uint32_t frame_start, uint32_t cap, SeqState& S, uint32_t lane,
+                           uint32_t* fail) {
+  uint32_t nlit, used;
+  if (!literals(L, p, end, cap - *op, &S.have_tree, &S.mb_tree, &nlit, &used, lane, fail))
+    return false;
+  uint32_t q = p + used;
+  if (q >= end) return *fail = kFSeqHdr, false;
+  const uint32_t b0 = L.in[q];
+  uint32_t nseq;
+  if (b0 == 0) {
+    nseq = 0;
+    q += 1;
+  } else if (b0 < 128) {
+    nseq = b0;
+    q += 1;
+  } else if (b0 < 255) {
+    if (q + 2 > end) return *fail = kFSeqHdr, false;
+    nseq = ((b0 - 128u) << 8) + L.in[q + 1];
+    q += 2;
+  } else {
+    if (q + 3 > end) return *fail = kFSeqHdr, false;
+    nseq = L.in[q + 1] + (static_cast<uint32_t>(L.in[q + 2]) << 8) + 0x7F00u;
+    q += 3;
+  }
+  if (nseq == 0) {
+    if (q != end) return *fail = kFSeqHdr, false;
+    if (nlit > cap - *op) return *fail = kFCap, false;
+    lds_copy(L.out + *op, L.lits, nlit, 0, lane);
+    *op += nlit;
+    return true;
+  }
+  if (q >= end) return *fail = kFSeqHdr, false;
+  const uint32_t modes = L.in[q];
+  ++q;
+  uint32_t u;
+  if (!seq_table(L, q, end, modes >> 6, kLLDefault, 36, 6, 35, 9, L.ll, &S.have_ll, &S.ll_log,
+                 &u, lane, fail))
+    return false;
+  q += u;
+  if (!seq_table(L, q, end, (modes >> 4) & 3u, kOFDefault, 29, 5, 31, 8, L.of, &S.have_of,
+                 &S.of_log, &u, lane, fail))
+    return false;
+  q += u;
+  if (!seq_table(L, q, end, (modes >> 2) & 3u, kMLDefault, 53, 6, 52, 9, L.ml, &S.have_ml,
+                 &S.ml_log, &u, lane, fail))
+    return false;
+  q += u;
+  BitR r;
+  if (!br_init(r, L.in, q, end)) return *fail = kFSeqBits, false;
+  uint32_t sl = br_read(r, S.ll_log), so = br_read(r, S.of_log), sm = br_read(r, S.ml_log);
+  uint32_t lp = 0;
+  for (uint32_t i = 0; i < nseq; ++i) {
+    const uint32_t el = L.ll[sl], eo = L.of[so], em = L.ml[sm];
+    const uint32_t llc = el & 255u, ofc = eo & 255u, mlc = em & 255u;
+    const uint32_t ofv = (1u << ofc) + br_read(r, ofc);
+    const uint32_t ml = kMLBase[mlc] + br_read(r, kMLBits[mlc]);
+    const uint32_t ll = kLLBase[llc] + br_read(r, kLLBits[llc]);
+    uint32_t off;
+    if (ofv > 3u) {
+      off = ofv - 3u;
+      S.rep2 = S.rep1;
+      S.rep1 = S.rep0;
+      S.rep0 = off;
+    } else {
+      const uint32_t idx = ofv - 1u + (ll == 0 ? 1u : 0u);
+      if (idx == 0) {
+        off = S.rep0;
+      } else if (idx == 1) {
+        off = S.rep1;
+        S.rep1 = S.rep0;
+        S.rep0 = off;
+      } else if (idx == 2) {
+        off = S.rep2;
+        S.rep2 = S.rep1;
+        S.rep1 = S.rep0;
+        S.rep0 = off;
+      } else {
+        off = S.rep0 - 1u;
+        S.rep2 = S.rep1;
+        S.rep1 = S.rep0;
+        S.rep0 = off;
+      }
+      if (off == 0) off = S.rep0 = 1;  // (1.4.9 forces a zero repeat offset to 1)
+    }
+    // the states, LL then ML then OF (also after the last sequence)
+    sl = (el >> 16) + br_read(r, (el >> 8) & 255u);
+    sm = (em >> 16) + br_read(r, (em >> 8) & 255u);
+    so = (eo >> 16) + br_read(r, (eo >> 8) & 255u);
+    if (ll > nlit - lp) return *fail = kFLitOverrun, false;
+    if (ll + ml > cap - *op) return *fail = kFCap, false;
+    lds_copy(L.out + *op, L.lits + lp, ll, 0, lane);
+    lp += ll;
+    *op += ll;
+    if (off > *op - frame_start) return *fail = kFOffset, false;
+    lds_copy(L.out + *op, L.out + (*op - off), ml, off, lane);
+    *op += ml;
+  }
+  if (r.pos > 0) return *fail = kFSeqBits, false;
+  const uint32_t rest = nlit - lp;
+  if (rest > cap - *op) return *fail = kFCap, false;
+  lds_copy(L.out + *op, L.lits + lp, rest, 0, lane);
+  *op += rest;
+  return true;
+}
+
+// XXH64 of out[0, n) (seed 0): the frame checksum. Scalar, from LDS.
+__device__ uint64_t rotl64(uint64_t x, uint32_t r) { return (x << r) | (x >> (64 - r)); }
+__device__ __forceinline__ uint64_t xxh_merge(uint64_t h, uint64_t v, uint64_t P1, uint64_t P2,
+                                              uint64_t P4) {
+  h ^= rotl64(v * P2, 31) * P1;
+  return h * P1 + P4;
+}
+// (base 4-aligned; the bytes are base[o, o + n))
+__device__ uint64_t xxh64(const uint8_t* base, uint32_t o, uint32_t n) {
+  const uint64_t P1 = 11400714785074694791ull, P2 = 14029467366897019727ull,
+                 P3 = 1609587929392839161ull, P4 = 9650029242287828579ull,
+                 P5 = 2870177450012600261ull;
+  uint32_t i = 0;
+  uint64_t h;
+  if (n >= 32) {
+    uint64_t v1 = P1 + P2, v2 = P2, v3 = 0, v4 = 0 - P1;
+    for (; i + 32 <= n; i += 32) {
+      v1 = rotl64(v1 + ld64(base, o + i) * P2, 31) * P1;
+      v2 = rotl64(v2 + ld64(base, o + i + 8) * P2, 31) * P1;
+      v3 = rotl64(v3 + ld64(base, o + i + 16) * P2, 31) * P1;
+      v4 = rotl64(v4 + ld64(base, o + i + 24) * P2, 31) * P1;
+    }
+    h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+    h = xxh_merge(h, v1, P1, P2, P4);
+    h = xxh_merge(h, v2, P1, P2, P4);
+    h = xxh_merge(h, v3, P1, P2, P4);
+    h = xxh_merge(h, v4, P1, P2, P4);
+  } else {
+    h = P5;
+  }
+  h += n;
+  for (; i + 8 <= n; i += 8) {
+    h ^= rotl64(ld64(base, o + i) * P2, 31) * P1;
+    h = rotl64(h, 27) * P1 + P4;
+  }
+  if (i + 4 <= n) {
+    h ^= static_cast<uint64_t>(ld32(base, o + i)) * P1;
+    h = rotl64(h, 23) * P2 + P3;
+    i += 4;
+  }
+  for (; i < n; ++i) {
+    h ^= base[o + i] * P5;
+    h = rotl64(h, 11) * P1;
+  }
+  h ^= h >> 33;
+  h *= P2;
+  h ^= h >> 29;
+  h *= P3;
+  h ^= h >> 32;
+  return h;
+}
+
+__global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t b = blockIdx.x;
+  if (b >= a.nblocks) return;
+  const uint32_t lane = threadIdx.x;
+  uint32_t n = a.src_len[b];
+  const uint8_t* src = a.src + a.src_off[b];
+  auto finish = [&](uint32_t st, uint32_t ol, uint32_t why) {
+    if (lane == 0) {
+      a.status[b] = static_cast<uint8_t>(st);
+      a.out_len[b] = ol;
+      if (a.detail) a.detail[b] = why;
+    }
+  };
+  // status codes: codec (LVKV_SNAPPY_*, shared) or ReadBlock's
+  const uint32_t kOK = a.block_mode ? LVKV_READ_OK : LVKV_SNAPPY_OK;
+  const uint32_t kLen = a.block_mode ? LVKV_READ_ZSTD_LENGTH : LVKV_SNAPPY_BAD_LENGTH;
+  const uint32_t kBad = a.block_mode ? LVKV_READ_ZSTD_CONTENTS : LVKV_SNAPPY_BAD_CONTENTS;
+  const uint32_t kCap = a.block_mode ? LVKV_READ_CAPACITY : LVKV_SNAPPY_CAPACITY;
+  const uint32_t kBig = a.block_mode ? LVKV_READ_TOO_LARGE : LVKV_SNAPPY_TOO_LARGE;
+  if (a.block_mode) {  // only type-2 blocks whose checksum held (the rest are done)
+    if (src[n] != 2) return;
+    if (a.vstatus != nullptr && a.vstatus[b] != 0) return;
+  }
+  // port::Zstd_GetUncompressedLength: ZSTD_getFrameContentSize, false on 0
+  // (a skippable frame reads as 0; a malformed header as ERROR, passed on)
+  uint64_t csize;
+  {
+    auto rd = [&](uint32_t i) -> uint32_t { return src[i]; };
+    const uint32_t m = n >= 4 ? (src[0] | src[1] << 8 | src[2] << 16 | src[3] << 24) : 0u;
+    if (n >= 4 && (m & 0xFFFFFFF0u) == 0x184D2A50u) {
+      csize = n >= 8 ? 0 : ~uint64_t{1};
+    } else {
+      const Frame f = frame_header(rd, n);
+      csize = f.ok ? f.csize : ~uint64_t{1};
+    }
+  }
+  if (csize == 0) return finish(kLen, 0, kFOk);
+  if (a.dst_cap == nullptr)  // (unknown, malformed and > 4 GiB sizes: TOO_LARGE)
+    return csize > 0xFFFFFFFFull ? finish(kBig, 0xFFFFFFFFu, kFOk)
+                                 : finish(kOK, static_cast<uint32_t>(csize), kFOk);
+  const uint32_t cap = a.dst_cap[b];
+  if (csize > cap) return finish(kCap, csize > 0xFFFFFFFFull ? 0xFFFFFFFFu : csize, kFOk);
+  if (csize > a.out_cap || n > zstd_in_cap(a.out_cap)) return finish(kBig, csize, kFOk);
+  const Lds L = lds_layout(smem, a.out_cap);
+  stage(L.in, src, n, 16, lane);
+  __builtin_amdgcn_s_waitcnt(0);
+  // ZSTD_decompressDCtx(dst, csize, src, n): frames one after another
+  const uint32_t ocap = static_cast<uint32_t>(csize);
+  uint32_t p = 0, op = 0, fail = kFOk;
+  bool ok = true;
+  while (ok && p < n) {
+    const uint32_t rem = n - p;
+    if (rem < 5) {  // (ZSTD_startingInputLength: input left over)
+      ok = false;
+      fail = kFTrailing;
+      break;
+    }
+    const uint32_t m = ld32(L.in, p);
+    if ((m & 0xFFFFFFF0u) == 0x184D2A50u) {  // skippable frame
+      if (rem < 8) {
+        ok = false;
+        fail = kFSkippable;
+        break;
+      }
+      const uint32_t sz = ld32(L.in, p + 4);
+      if (sz > rem - 8) {
+        ok = false;
+        fail = kFSkippable;
+        break;
+      }
+      p += 8 + sz;
+      continue;
+    }
+    if (rem < 9) {
+      ok = false;
+      fail = kFHeader;
+      break;
+    }
+    auto rd = [&](uint32_t i) -> uint32_t { return L.in[p + i]; };
+    const Frame f = frame_header(rd, rem);
+    if (!f.ok) {
+      ok = false;
+      fail = kFHeader;
+      break;
+    }
+    if (f.dict != 0) {
+      ok = false;
+      fail = kFDict;
+      break;
+    }
+    uint32_t q = p + f.hsize;
+    const uint32_t start = op;
+    SeqState S{};
+    S.rep0 = 1;
+    S.rep1 = 4;
+    S.rep2 = 8;
+    for (;;) {
+      if (q + 3 > n) {
+        ok = false;
+        fail = kFBlockHdr;
+        break;
+      }
+      const uint32_t bh = L.in[q] | static_cast<uint32_t>(L.in[q + 1]) << 8 |
+                          static_cast<uint32_t>(L.in[q + 2]) << 16;
+      q += 3;
+      const uint32_t last = bh & 1u, btype = (bh >> 1) & 3u, bsize = bh >> 3;
+      if (btype == 3) {
+        ok = false;
+        fail = kFBlockType;
+        break;
+      }
+      if (btype == 1) {
+        if (q + 1 > n) {
+          ok = false;
+          fail = kFBlockSize;
+          break;
+        }
+        if (bsize > ocap - op) {
+          ok = false;
+          fail = kFCap;
+          break;
+        }
+        const uint8_t v = L.in[q];
+        for (uint32_t k = lane; k < bsize; k += 64) L.out[op + k] = v;
+        op += bsize;
+        q += 1;
+      } else {
+        if (btype == 2 && bsize >= kBlockMax) {
+          ok = false;
+          fail = kFBlockSize;
+          break;
+        }
+        if (bsize > n - q) {
+          ok = false;
+          fail = kFBlockSize;
+          break;
+        }
+        if (btype == 0) {
+          if (bsize > ocap - op) {
+            ok = false;
+            fail = kFCap;
+            break;
+          }
+          for (uint32_t k = lane; k < bsize; k += 64) L.out[op + k] = L.in[q + k];
+          op += bsize;
+        } else {
+          if (bsize < 3) {
+            ok = false;
+            fail = kFLitHdr;
+            break;
+          }
+          if (!comp_block(L, q, q + bsize, &op, start, ocap, S, lane, &fail)) {
+            ok = false;
+            break;
+          }
+        }
+        q += bsize;
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      if (last) break;
+    }
+    if (!ok) break;
+    if (f.csize != ~uint64_t{0} && op - start != f.csize) {
+      ok = false;
+      fail = kFContentSize;
+      break;
+    }
+    if (f.checksum) {
+      if (q + 4 > n) {
+        ok = false;
+        fail = kFChecksum;
+        break;
+      }
+      const uint32_t want = ld32(L.in, q);
+      if (static_cast<uint32_t>(xxh64(L.out, start, op - start)) != want) {
+        ok = false;
+        fail = kFChecksum;
+        break;
+      }
+      q += 4;
+    }
+    p = q;
+  }
+  if (!ok) return finish(kBad, ocap, fail);
+  if (op != ocap) return finish(kBad, ocap, kFContentSize);  // (short output)
+  uint8_t* dst = a.dst + a.dst_off[b];
+  uint32_t k0 = 0;
+  if ((reinterpret_cast<uintptr_t>(dst) & 3u) == 0) {
+    const uint32_t nd = op >> 2;
+    for (uint32_t i = lane; i < nd; i += 64)
+      reinterpret_cast<uint32_t*>(dst)[i] = reinterpret_cast<const uint32_t*>(L.out)[i];
+    k0 = 4u * nd;
+  }
+  for (uint32_t k = k0 + lane; k < op; k += 64) dst[k] = L.out[k];
+  finish(kOK, op, kFOk);
+}
+
+}  // namespace
+
+uint32_t zstd_lds(uint32_t max_ulen) { return zstd_lds_bytes(max(16u, max_ulen)); }
+
+hipError_t launch_zstd_uncompress(const uint8_t* src, const uint64_t* src_off,
+                                  const uint32_t* src_len, uint8_t* dst, const uint64_t* dst_off,
+                                  const uint32_t* dst_cap, uint32_t* out_len, uint8_t* status,
+                                  uint32_t* detail, uint32_t nblocks, uint32_t max_ulen,
+                                  uint32_t block_mode, const uint8_t* vstatus,
+                                  hipStream_t stream) {
+  ZArgs a{src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, detail, nblocks,
+          0, block_mode, vstatus};
+  a.out_cap = dst_cap == nullptr ? 0u : max(16u, max_ulen);
+  const size_t lds = dst_cap == nullptr ? 16u : zstd_lds_bytes(a.out_cap);
+  hipLaunchKernelGGL(zstd_uncompress_kernel, dim3(nblocks), dim3(64), lds, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace lvkv
