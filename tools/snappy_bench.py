@@ -75,6 +75,39 @@ def cpu_lines(blocks: np.ndarray, seconds: float = 2.0, procs: int = 16):
     return {k: round(v, 1) for k, v in res.items()}
 
 
+def zstd_cpu_lines(frames, seconds: float = 2.0, procs: int = 16):
+    """libzstd 1.4.9 decompressing the same frames: one core, and `procs`
+    processes (port::Zstd_Uncompress: ZSTD_decompress into the content size)."""
+    import zstd_oracle as zo
+    if zo.system_zstd() is None:
+        return None
+    import multiprocessing as mp
+    one = _zstd_worker((frames[:256], seconds))
+    res = {"uncomp_1t_MBps": one / 1e6}
+    if procs > 1:
+        with mp.get_context("fork").Pool(procs) as pool:
+            r = pool.map(_zstd_worker, [(frames[i * 64:(i + 1) * 64], seconds)
+                                        for i in range(procs)])
+        res[f"uncomp_{procs}p_MBps"] = sum(r) / 1e6
+    return {k: round(v, 1) for k, v in res.items()}
+
+
+def _zstd_worker(arg):
+    frames, seconds = arg
+    import ctypes
+    import zstd_oracle as zo
+    lib = zo.system_zstd()
+    o = ctypes.create_string_buffer(4096)
+    n, t0, k = 0, time.perf_counter(), 0
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(256):
+            f = frames[k % len(frames)]
+            k += 1
+            lib.ZSTD_decompress(o, 4096, f, len(f))
+        n += 256
+    return n * 4096 / (time.perf_counter() - t0)
+
+
 def _cpu_worker(arg):
     blk, seconds = arg
     import ctypes
@@ -103,6 +136,16 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
     cpu = None if args.no_cpu else cpu_lines(block_batch(64))
+    # the same blocks as zstd frames (libzstd level 1, LevelDB's default
+    # zstd_compression_level), for the device decoder
+    import zstd_oracle as zo
+    zlib = zo.system_zstd()
+    zframes = None
+    if zlib is not None:
+        h = block_batch(256)
+        zframes = [zo.lib_compress(zlib, h[i * 4096:(i + 1) * 4096].tobytes(), 1)
+                   for i in range(256)]
+    zcpu = None if args.no_cpu or zframes is None else zstd_cpu_lines(zframes)
     import torch
     import __graft_entry__ as g
     lvkv = g.load_package()
@@ -164,6 +207,25 @@ def main():
     }
     if cpu is not None:
         res["cpu_libsnappy_1_1_8"] = cpu
+    if zframes is not None:  # zstd: the device decoder over the 256 distinct frames, cycled
+        zf = [zframes[i % 256] for i in range(nb)]
+        zoff = np.zeros(nb, dtype=np.int64)
+        zoff[1:] = np.cumsum([len(f) for f in zf[:-1]])
+        zbuf = torch.from_numpy(np.frombuffer(b"".join(zf), dtype=np.uint8).copy()).to(dev)
+        zo_t = torch.from_numpy(zoff).to(dev)
+        zl_t = torch.tensor([len(f) for f in zf], dtype=torch.int32, device=dev)
+        zbytes = int(zl_t.to(torch.int64).sum())
+        t_z = timed(lambda: lvkv.lib.lvkv_zstd_uncompress_device(
+            zbuf.data_ptr(), zo_t.data_ptr(), zl_t.data_ptr(), udst.data_ptr(), off.data_ptr(),
+            cap.data_ptr(), ulen.data_ptr(), ust.data_ptr(), nb, L, stream.cuda_stream))
+        torch.cuda.synchronize()
+        assert int(ust.max()) == 0 and torch.equal(udst, src)
+        res["zstd_uncompress"] = {"us_per_launch": round(t_z * 1e6, 1),
+                                  "GBps_uncompressed": round(raw / t_z / 1e9, 2),
+                                  "hbm_GBps": round((raw + zbytes) / t_z / 1e9, 2),
+                                  "output_pct": round(100.0 * zbytes / raw, 2)}
+        if zcpu is not None:
+            res["cpu_libzstd_1_4_9"] = zcpu
     print(json.dumps(res), flush=True)
     (REPO / "gpurun_out").mkdir(exist_ok=True)
     (REPO / "gpurun_out" / "snappy_bench.json").write_text(json.dumps(res, indent=1))
