@@ -45,7 +45,7 @@ HIP_SOURCES = ["crc32c_kernel.hip", "crc32c_uniform.hip", "crc32c_compact.hip",
 ENGINE_KERNELS = "lvkv_engine_kernels.hip"
 HEADERS = ["lvkv_kernel_args.h", "lvkv_tables.h", "crc32c_device_common.h",
            "crc32c_uniform_common.h", "crc32c_compact_common.h", "crc32c_burst.h",
-           "crc32c_ragged_body.h", "lvkv_log_events.h"]
+           "crc32c_ragged_body.h", "lvkv_log_events.h", "lvkv_zstd_tables.h"]
 
 
 def _run(cmd: list[str], verbose: bool) -> None:

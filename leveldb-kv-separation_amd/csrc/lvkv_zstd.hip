@@ -17,6 +17,7 @@
 #include <stdint.h>
 
 #include "lvkv_snappy.h"
+#include "lvkv_zstd_tables.h"
 
 namespace lvkv {
 namespace {
@@ -214,27 +215,34 @@ __device__ bool build_fse(const int16_t* counts, uint32_t nsym, uint32_t log, ui
   }
   if (pos != 0) return false;
   __builtin_amdgcn_s_waitcnt(0xc07f);
-  // decode entries in table order: symbol s's k-th entry gets state nxt[s]++
-  for (uint32_t u = 0; u < size; ++u) {
-    const uint32_t s = table[u] & 255u;
-    const uint32_t ns = nxt[s];
-    if (lane == 0) nxt[s] = static_cast<uint16_t>(ns + 1u);
-    const uint32_t nbits = log - (31u - __builtin_clz(ns));
-    const uint32_t base = (ns << nbits) - size;
-    if (lane == 0) table[u] = s | (nbits << 8) | (base << 16);
+  // decode entries in table order: symbol s's k-th entry gets state
+  // nxt[s] + k. 64 entries a step: a lane's rank among the step's entries of
+  // its symbol, and whether a later one follows, from the other lanes'
+  // symbols (readlane); the last of each symbol carries nxt[s] on.
+  for (uint32_t c = 0; c < size; c += 64) {
+    const uint32_t u = c + lane;
+    const bool in = u < size;
+    const uint32_t s = in ? (table[u] & 255u) : 0x1000u + lane;
+    uint32_t before = 0, after = 0;
+    for (uint32_t j = 0; j < 64; ++j) {
+      const uint32_t sj = __builtin_amdgcn_readlane(s, j);
+      before += (sj == s && j < lane) ? 1u : 0u;
+      after += (sj == s && j > lane) ? 1u : 0u;
+    }
+    const uint32_t ns = (in ? nxt[s] : 1u) + before;
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // every lane has read nxt before it moves
+    if (in) {
+      const uint32_t nbits = log - (31u - __builtin_clz(ns));
+      const uint32_t base = (ns << nbits) - size;
+      table[u] = s | (nbits << 8) | (base << 16);
+      if (after == 0) nxt[s] = static_cast<uint16_t>(ns + 1u);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
   }
-  __builtin_amdgcn_s_waitcnt(0xc07f);
   return true;
 }
 
-// The predefined distributions (RFC 8878 §3.1.1.3.2.2)
-__constant__ int16_t kLLDefault[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
-                                       2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
-__constant__ int16_t kMLDefault[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1,
-                                       1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
-                                       1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
-__constant__ int16_t kOFDefault[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
-                                       1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+// Baselines and extra bits of the LL / ML codes (RFC 8878 §3.1.1.3.2.1)
 __constant__ uint32_t kLLBase[36] = {0,    1,    2,    3,     4,     5,     6,    7,    8,
                                      9,    10,   11,   12,    13,    14,    15,   16,   18,
                                      20,   22,   24,   28,    32,    40,    48,   64,   128,
@@ -572,14 +580,13 @@ __device__ bool literals(const Lds& L, uint32_t p, uint32_t end, uint32_t cap, b
 
 // A sequence table by mode into `table`; *log, *used. Uniform.
 __device__ bool seq_table(const Lds& L, uint32_t p, uint32_t end, uint32_t mode,
-                          const int16_t* dflt, uint32_t dn, uint32_t dlog, uint32_t max_sym,
+                          const uint32_t* dflt, uint32_t dlog, uint32_t max_sym,
                           uint32_t max_log, uint32_t* table, bool* have, uint32_t* log,
                           uint32_t* used, uint32_t lane, uint32_t* fail) {
   *used = 0;
-  if (mode == 0) {
-    for (uint32_t s = lane; s < dn; s += 64) L.cnt[s] = dflt[s];
+  if (mode == 0) {  // the predefined table (tools/gen_zstd_tables.py)
+    for (uint32_t u = lane; u < (1u << dlog); u += 64) table[u] = dflt[u];
     __builtin_amdgcn_s_waitcnt(0xc07f);
-    if (!build_fse(L.cnt, dn, dlog, table, L.nxt, lane)) return *fail = kFFseSpread, false;
     *log = dlog;
   } else if (mode == 1) {
     if (p >= end) return *fail = kFRle, false;
@@ -657,15 +664,15 @@ __device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
   const uint32_t modes = L.in[q];
   ++q;
   uint32_t u;
-  if (!seq_table(L, q, end, modes >> 6, kLLDefault, 36, 6, 35, 9, L.ll, &S.have_ll, &S.ll_log,
+  if (!seq_table(L, q, end, modes >> 6, kPredefLL, kPredefLLLog, 35, 9, L.ll, &S.have_ll, &S.ll_log,
                  &u, lane, fail))
     return false;
   q += u;
-  if (!seq_table(L, q, end, (modes >> 4) & 3u, kOFDefault, 29, 5, 31, 8, L.of, &S.have_of,
+  if (!seq_table(L, q, end, (modes >> 4) & 3u, kPredefOF, kPredefOFLog, 31, 8, L.of, &S.have_of,
                  &S.of_log, &u, lane, fail))
     return false;
   q += u;
-  if (!seq_table(L, q, end, (modes >> 2) & 3u, kMLDefault, 53, 6, 52, 9, L.ml, &S.have_ml,
+  if (!seq_table(L, q, end, (modes >> 2) & 3u, kPredefML, kPredefMLLog, 52, 9, L.ml, &S.have_ml,
                  &S.ml_log, &u, lane, fail))
     return false;
   q += u;
