@@ -86,7 +86,7 @@ def zstd_cpu_lines(frames, seconds: float = 2.0, procs: int = 16):
     res = {"uncomp_1t_MBps": one / 1e6}
     if procs > 1:
         with mp.get_context("fork").Pool(procs) as pool:
-            r = pool.map(_zstd_worker, [(frames[i * 64:(i + 1) * 64], seconds)
+            r = pool.map(_zstd_worker, [(frames[i * 16:(i + 1) * 16], seconds)
                                         for i in range(procs)])
         res[f"uncomp_{procs}p_MBps"] = sum(r) / 1e6
     return {k: round(v, 1) for k, v in res.items()}
