@@ -113,25 +113,27 @@ if want gate; then
   timeout -k 10 200 python tools/probe/gate_probe.py > $O/gate.log 2>&1 || { tail -20 $O/gate.log; exit 1; }
   grep -v amdgpu.ids $O/gate.log | tail -3
 fi
-if want snappy; then  # the device Snappy codec: parity, throughput, kernel trace
-  timeout -k 10 300 python -u -m pytest tests/test_snappy.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/snappy_tests.log 2>&1 \
+if want snappy; then  # the device codecs (Snappy, Zstd decode): parity, throughput, kernel trace
+  timeout -k 10 300 python -u -m pytest tests/test_snappy.py tests/test_zstd.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/snappy_tests.log 2>&1 \
     || { echo "snappy tests failed"; tail -40 $O/snappy_tests.log; exit 1; }
   tail -2 $O/snappy_tests.log
   timeout -k 10 200 python tools/snappy_bench.py > $O/snappy_bench.log 2>&1 || { tail -20 $O/snappy_bench.log; exit 1; }
   grep -v amdgpu.ids $O/snappy_bench.log | tail -2
+  timeout -k 10 120 python3 tools/snappy_bench.py --write-zstd-frames $O/zframes.bin > /dev/null 2>&1 || { echo "zstd frames failed"; exit 1; }
   D=$O/snappy_prof; rm -rf $D
-  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 tools/snappy_bench.py --no-cpu > $D.log 2>&1 \
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 tools/snappy_bench.py --no-cpu --zstd-frames $O/zframes.bin > $D.log 2>&1 \
     || { echo "snappy prof failed"; tail -20 $D.log; exit 1; }
   stats $D
 fi
 if want snappypmc; then
   i=0; mkdir -p $O/snappypmc
+  timeout -k 10 120 python3 tools/snappy_bench.py --write-zstd-frames $O/zframes.bin > /dev/null 2>&1 || { echo "zstd frames failed"; exit 1; }
   for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
              "SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
              "SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VMEM" \
              "FETCH_SIZE GRBM_GUI_ACTIVE"; do
     i=$((i+1)); D=$O/snappypmc/p$i; rm -rf $D
-    timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d $D -o run -- python3 tools/snappy_bench.py --no-cpu --steps 4 --warmup 1 > $D.log 2>&1 \
+    timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d $D -o run -- python3 tools/snappy_bench.py --no-cpu --steps 4 --warmup 1 --zstd-frames $O/zframes.bin > $D.log 2>&1 \
       || { echo "snappy pmc pass $i failed"; tail -5 $D.log; exit 1; }
   done
   python3 tools/pmc_table.py $O/snappypmc > $O/snappypmc.txt 2>&1 || true

@@ -134,17 +134,35 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--zstd-frames", default=None,
+                    help="read the zstd frames from this file instead of libzstd (profiled "
+                         "runs: the profiler's own zstd clashes with the library)")
+    ap.add_argument("--write-zstd-frames", default=None,
+                    help="write the zstd frames to this file and exit")
     args = ap.parse_args()
     cpu = None if args.no_cpu else cpu_lines(block_batch(64))
     # the same blocks as zstd frames (libzstd level 1, LevelDB's default
     # zstd_compression_level), for the device decoder
     import zstd_oracle as zo
-    zlib = zo.system_zstd()
     zframes = None
-    if zlib is not None:
-        h = block_batch(256)
-        zframes = [zo.lib_compress(zlib, h[i * 4096:(i + 1) * 4096].tobytes(), 1)
-                   for i in range(256)]
+    if args.zstd_frames:
+        blob = Path(args.zstd_frames).read_bytes()
+        zframes, p = [], 0
+        while p < len(blob):
+            n = int.from_bytes(blob[p:p + 4], "little")
+            zframes.append(blob[p + 4:p + 4 + n])
+            p += 4 + n
+        args.no_cpu = True
+    else:
+        zlib = zo.system_zstd()
+        if zlib is not None:
+            h = block_batch(256)
+            zframes = [zo.lib_compress(zlib, h[i * 4096:(i + 1) * 4096].tobytes(), 1)
+                       for i in range(256)]
+    if args.write_zstd_frames:
+        Path(args.write_zstd_frames).write_bytes(
+            b"".join(len(f).to_bytes(4, "little") + f for f in zframes))
+        return
     zcpu = None if args.no_cpu or zframes is None else zstd_cpu_lines(zframes)
     import torch
     import __graft_entry__ as g
