@@ -104,6 +104,23 @@ __device__ __forceinline__ uint32_t br_read(BitR& r, uint32_t n) {
   return br_bits(r, r.pos, n);
 }
 
+// n <= 56 bits at once (the window always holds 57 below its top)
+__device__ __forceinline__ uint64_t br_read64(BitR& r, uint32_t n) {
+  r.pos -= static_cast<int32_t>(n);
+  const int32_t p = r.pos, top = p + static_cast<int32_t>(n);
+  if (n == 0 || top <= 0) return 0;
+  const int32_t lo = p < 0 ? 0 : p;
+  if (r.cb < 0 || lo < 8 * r.cb || top > 8 * r.cb + 64) {
+    int32_t cb = ((top + 7) >> 3) - 8;
+    if (cb < 0) cb = 0;
+    r.cb = cb;
+    r.win = ld64(r.in, r.start + static_cast<uint32_t>(cb));
+  }
+  uint64_t v = r.win >> (lo - 8 * r.cb);
+  v &= (uint64_t{1} << (top - lo)) - 1u;
+  return v << (lo - p);
+}
+
 // ---- FSE tables (RFC 8878 §4.1; FSE_readNCount / FSE_buildDTable) --------
 // Decode entries: symbol | nbBits << 8 | baseline << 16.
 
@@ -262,7 +279,6 @@ __constant__ uint8_t kMLBits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
 struct Lds {
   uint8_t* in;      // the staged frame (+16 zero bytes)
   uint8_t* out;     // the frame's output
-  uint8_t* lits;    // a block's literals
   uint16_t* huf;    // Huffman decode table: symbol | nbBits << 8 (<= 2048)
   uint32_t* ll;     // FSE tables: 512 / 256 / 512 entries, and 64 for weights
   uint32_t* of;
@@ -281,7 +297,7 @@ __host__ __device__ constexpr uint32_t zstd_in_cap(uint32_t out_cap) {
 }
 __host__ __device__ constexpr uint32_t round16(uint32_t x) { return (x + 15u) & ~15u; }
 __host__ __device__ constexpr uint32_t zstd_lds_bytes(uint32_t out_cap) {
-  return round16(zstd_in_cap(out_cap) + 16u + 4u) + round16(out_cap) + round16(out_cap + 32u) +
+  return round16(zstd_in_cap(out_cap) + 16u + 4u) + round16(out_cap) +
          2u * kHufEntries + 4u * (kFseLL + kFseOF + kFseML + kFseW) + 272u + 512u + 512u;
 }
 
@@ -292,8 +308,6 @@ __device__ Lds lds_layout(uint8_t* smem, uint32_t out_cap) {
   o += round16(zstd_in_cap(out_cap) + 16u + 4u);
   L.out = smem + o;
   o += round16(out_cap);
-  L.lits = smem + o;
-  o += round16(out_cap + 32u);
   L.huf = reinterpret_cast<uint16_t*>(smem + o);
   o += 2u * kHufEntries;
   L.ll = reinterpret_cast<uint32_t*>(smem + o);
@@ -415,18 +429,41 @@ __device__ void huf_table(const Lds& L, uint32_t nw, uint32_t mb, uint32_t lane)
   __builtin_amdgcn_s_waitcnt(0xc07f);
 }
 
-// Huffman stream in[lo, hi) -> n symbols at dst; true when consumed exactly.
-// Per lane (the four streams run on lanes 0-3).
-__device__ __forceinline__ bool huf_stream(const Lds& L, uint32_t lo, uint32_t hi, uint32_t n,
-                                           uint32_t mb, uint8_t* dst) {
+// Symbols that start above bit `floor`, from bit position `pos` down (one
+// lane's segment of a stream at in[lo, ...)): the exit position; *count
+// symbols, the first `lim` of them written at dst (when dst is set).
+__device__ __forceinline__ int32_t huf_run(const Lds& L, uint32_t lo, int32_t pos, int32_t floor,
+                                           uint32_t mb, uint8_t* dst, uint32_t lim,
+                                           uint32_t* count) {
+  int32_t wlo = 0x7fffffff;
+  uint64_t win = 0;
+  const uint32_t mask = (1u << mb) - 1u;
   BitR r;
-  if (!br_init(r, L.in, lo, hi)) return false;
-  for (uint32_t i = 0; i < n; ++i) {
-    const uint32_t e = L.huf[br_bits(r, r.pos - static_cast<int32_t>(mb), mb)];
-    r.pos -= static_cast<int32_t>(e >> 8);
-    dst[i] = static_cast<uint8_t>(e & 255u);
+  r.in = L.in;
+  r.start = lo;
+  r.cb = -1;
+  uint32_t c = 0;
+  while (pos > floor) {
+    const int32_t p = pos - static_cast<int32_t>(mb);
+    uint32_t idx;
+    if (p >= 0) {
+      if (p < wlo) {
+        int32_t cb = ((pos + 7) >> 3) - 8;
+        if (cb < 0) cb = 0;
+        wlo = 8 * cb;
+        win = ld64(L.in, lo + static_cast<uint32_t>(cb));
+      }
+      idx = static_cast<uint32_t>(win >> (p - wlo)) & mask;
+    } else {
+      idx = br_bits(r, p, mb);  // bits below the start read as zeros
+    }
+    const uint32_t e = L.huf[idx];
+    pos -= static_cast<int32_t>(e >> 8);
+    if (dst != nullptr && c < lim) dst[c] = static_cast<uint8_t>(e & 255u);
+    ++c;
   }
-  return r.pos == 0;
+  *count = c;
+  return pos;
 }
 
 // ---- a frame --------------------------------------------------------------
@@ -491,12 +528,21 @@ struct ZArgs {
   uint32_t out_cap;
   uint32_t block_mode;  // ReadBlock mode: handles, type byte 2 only, LVKV_READ_*
   const uint8_t* vstatus;
+  uint64_t* stamps;  // probe build: 8 clock stamps a frame (nullptr: none)
 };
 
-// One compressed block's literals into L.lits; *nlit, *used. Uniform.
-__device__ bool literals(const Lds& L, uint32_t p, uint32_t end, uint32_t cap, bool* have_tree,
-                         uint32_t* mb_tree, uint32_t* nlit, uint32_t* used, uint32_t lane,
-                         uint32_t* fail) {
+// s_memtime into a frame's stamp slot k (probe build; lane 0, a vector store)
+__device__ __forceinline__ void zstamp(uint64_t* slot, uint32_t k, uint32_t lane) {
+  if (slot != nullptr && lane == 0) slot[k] = __builtin_amdgcn_s_memtime();
+}
+
+// One compressed block's literals at the end of the frame's output space
+// (out_end - n: the output, which grows from the front, reaches a literal
+// only once it is consumed; any block that would overrun fails its size
+// checks first); *nlit, *used. Uniform.
+__device__ bool literals(const Lds& L, uint32_t p, uint32_t end, uint32_t cap, uint8_t* out_end,
+                         bool* have_tree, uint32_t* mb_tree, uint32_t* nlit, uint32_t* used,
+                         uint32_t lane, uint32_t* fail, uint64_t* stamp) {
   if (end - p < 3u) return *fail = kFLitHdr, false;  // MIN_CBLOCK_SIZE
   const uint32_t b0 = L.in[p];
   const uint32_t type = b0 & 3u, sf = (b0 >> 2) & 3u;
@@ -517,12 +563,14 @@ __device__ bool literals(const Lds& L, uint32_t p, uint32_t end, uint32_t cap, b
     if (n > cap) return *fail = kFCap, false;
     if (type == 0) {
       if (p + hs + n > end) return *fail = kFLitSize, false;
-      for (uint32_t k = lane; k < n; k += 64) L.lits[k] = L.in[p + hs + k];
+      uint8_t* lits = out_end - n;
+      for (uint32_t k = lane; k < n; k += 64) lits[k] = L.in[p + hs + k];
       *used = hs + n;
     } else {
       if (p + hs + 1u > end) return *fail = kFLitSize, false;
       const uint8_t v = L.in[p + hs];
-      for (uint32_t k = lane; k < n; k += 64) L.lits[k] = v;
+      uint8_t* lits = out_end - n;
+      for (uint32_t k = lane; k < n; k += 64) lits[k] = v;
       *used = hs + 1u;
     }
     *nlit = n;
@@ -543,7 +591,9 @@ __device__ bool literals(const Lds& L, uint32_t p, uint32_t end, uint32_t cap, b
   if (type == 2) {
     uint32_t nw, mb, u;
     if (!huf_weights(L, q, qend, &nw, &mb, &u, lane, fail)) return false;
+    zstamp(stamp, 6, lane);
     huf_table(L, nw, mb, lane);
+    zstamp(stamp, 7, lane);
     *have_tree = true;
     *mb_tree = mb;
     q += u;
@@ -551,10 +601,11 @@ __device__ bool literals(const Lds& L, uint32_t p, uint32_t end, uint32_t cap, b
     return *fail = kFHufHdr, false;
   }
   const uint32_t mb = *mb_tree;
-  bool good;
-  if (sf == 0) {
-    good = lane == 0 ? huf_stream(L, q, qend, n, mb, L.lits) : true;
-  } else {
+  // the streams' bounds: one stream on 64 lanes, or four on 16 lanes each
+  const uint32_t S = sf == 0 ? 64u : 16u;
+  const uint32_t sid = lane / S, k = lane % S;
+  uint32_t slo = q, shi = qend, scnt = n, sbase = 0;
+  if (sf != 0) {
     if (qend - q < 10u) return *fail = kFJump, false;
     const uint32_t s1 = L.in[q] | static_cast<uint32_t>(L.in[q + 1]) << 8;
     const uint32_t s2 = L.in[q + 2] | static_cast<uint32_t>(L.in[q + 3]) << 8;
@@ -563,14 +614,52 @@ __device__ bool literals(const Lds& L, uint32_t p, uint32_t end, uint32_t cap, b
     if (d > qend) return *fail = kFJump, false;
     const uint32_t seg = (n + 3u) >> 2;
     if (3u * seg > n) return *fail = kFJump, false;
-    good = true;
-    if (lane < 4) {
-      const uint32_t lo = lane == 0 ? a : lane == 1 ? b : lane == 2 ? c : d;
-      const uint32_t hi = lane == 0 ? b : lane == 1 ? c : lane == 2 ? d : qend;
-      const uint32_t cnt = lane == 3 ? n - 3u * seg : seg;
-      good = huf_stream(L, lo, hi, cnt, mb, L.lits + lane * seg);
-    }
+    slo = sid == 0 ? a : sid == 1 ? b : sid == 2 ? c : d;
+    shi = sid == 0 ? b : sid == 1 ? c : sid == 2 ? d : qend;
+    scnt = sid == 3 ? n - 3u * seg : seg;
+    sbase = sid * seg;
   }
+  bool good = shi > slo && L.in[shi - 1] != 0;  // the end marker (br_init)
+  if (__ballot(!good)) return *fail = kFHufStream, false;
+  const int32_t P = static_cast<int32_t>(8u * (shi - slo - 1u) +
+                                         (31u - __builtin_clz(static_cast<uint32_t>(L.in[shi - 1]))));
+  // Self-synchronising parallel decode: lane k of a stream takes the symbols
+  // that start in bits (floor, top] of its segment. Pass A starts from the
+  // segment's top (a guess), then each lane redoes its segment from the
+  // exit of the lane before until no exit moves (the first lane's entry is
+  // exact, so a pass in which nothing moves has exact entries everywhere),
+  // then the symbols are written at their prefix-summed offsets.
+  const int32_t seglen = (P + static_cast<int32_t>(S) - 1) / static_cast<int32_t>(S);
+  const int32_t top = P - static_cast<int32_t>(k) * seglen;
+  int32_t floor = P - static_cast<int32_t>(k + 1u) * seglen;
+  if (floor < 0) floor = 0;
+  uint32_t cnt = 0;
+  int32_t x = huf_run(L, slo, top, floor, mb, nullptr, 0, &cnt);
+  for (uint32_t it = 0; it < S; ++it) {
+    int32_t entry = __shfl_up(x, 1, static_cast<int>(S));
+    if (k == 0) entry = P;
+    uint32_t c2 = 0;
+    const int32_t x2 = huf_run(L, slo, entry, floor, mb, nullptr, 0, &c2);
+    const bool moved = x2 != x;
+    x = x2;
+    cnt = c2;
+    if (!__ballot(moved)) break;
+  }
+  uint32_t incl = cnt;
+  for (uint32_t d = 1; d < S; d <<= 1) {
+    const uint32_t v = __shfl_up(incl, d, static_cast<int>(S));
+    if (k >= d) incl += v;
+  }
+  const uint32_t off = incl - cnt;
+  const uint32_t total = __shfl(incl, static_cast<int>(S - 1u), static_cast<int>(S));
+  const int32_t last = __shfl(x, static_cast<int>(S - 1u), static_cast<int>(S));
+  int32_t entry = __shfl_up(x, 1, static_cast<int>(S));
+  if (k == 0) entry = P;
+  uint32_t c3 = 0;
+  huf_run(L, slo, entry, floor, mb, out_end - n + sbase + off, scnt > off ? scnt - off : 0u,
+          &c3);
+  // the sequential decoder's verdict: exactly scnt symbols ending at bit 0
+  good = total == scnt && last == 0;
   if (__ballot(!good)) return *fail = kFHufStream, false;
   __builtin_amdgcn_s_waitcnt(0xc07f);
   *nlit = n;
@@ -611,6 +700,7 @@ __device__ bool seq_table(const Lds& L, uint32_t p, uint32_t end, uint32_t mode,
 }
 
 struct SeqState {
+  uint64_t* stamp;  // probe stamps of this frame, or nullptr
   bool have_ll, have_of, have_ml, have_tree;
   uint32_t ll_log, of_log, ml_log, mb_tree;
   uint32_t rep0, rep1, rep2;
@@ -632,8 +722,11 @@ __device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
                            uint32_t frame_start, uint32_t cap, SeqState& S, uint32_t lane,
                            uint32_t* fail) {
   uint32_t nlit, used;
-  if (!literals(L, p, end, cap - *op, &S.have_tree, &S.mb_tree, &nlit, &used, lane, fail))
+  if (!literals(L, p, end, cap - *op, L.out + cap, &S.have_tree, &S.mb_tree, &nlit, &used, lane,
+                fail, S.stamp))
     return false;
+  const uint8_t* lits = L.out + (cap - nlit);
+  zstamp(S.stamp, 2, lane);
   uint32_t q = p + used;
   if (q >= end) return *fail = kFSeqHdr, false;
   const uint32_t b0 = L.in[q];
@@ -656,7 +749,7 @@ __device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
   if (nseq == 0) {
     if (q != end) return *fail = kFSeqHdr, false;
     if (nlit > cap - *op) return *fail = kFCap, false;
-    lds_copy(L.out + *op, L.lits, nlit, 0, lane);
+    lds_copy(L.out + *op, lits, nlit, 0, lane);
     *op += nlit;
     return true;
   }
@@ -676,6 +769,7 @@ __device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
                  &S.ml_log, &u, lane, fail))
     return false;
   q += u;
+  zstamp(S.stamp, 3, lane);
   BitR r;
   if (!br_init(r, L.in, q, end)) return *fail = kFSeqBits, false;
   uint32_t sl = br_read(r, S.ll_log), so = br_read(r, S.of_log), sm = br_read(r, S.ml_log);
@@ -683,9 +777,22 @@ __device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
   for (uint32_t i = 0; i < nseq; ++i) {
     const uint32_t el = L.ll[sl], eo = L.of[so], em = L.ml[sm];
     const uint32_t llc = el & 255u, ofc = eo & 255u, mlc = em & 255u;
-    const uint32_t ofv = (1u << ofc) + br_read(r, ofc);
-    const uint32_t ml = kMLBase[mlc] + br_read(r, kMLBits[mlc]);
-    const uint32_t ll = kLLBase[llc] + br_read(r, kLLBits[llc]);
+    // the extra bits, offset then ML then LL, in one read when they fit
+    const uint32_t mlb = kMLBits[mlc], llb = kLLBits[llc];
+    uint32_t ofx, mlx, llx;
+    if (ofc + mlb + llb <= 56u) {
+      const uint64_t v = br_read64(r, ofc + mlb + llb);
+      llx = static_cast<uint32_t>(v) & ((1u << llb) - 1u);
+      mlx = static_cast<uint32_t>(v >> llb) & ((1u << mlb) - 1u);
+      ofx = static_cast<uint32_t>(v >> (llb + mlb));
+    } else {
+      ofx = br_read(r, ofc);
+      mlx = br_read(r, mlb);
+      llx = br_read(r, llb);
+    }
+    const uint32_t ofv = (1u << ofc) + ofx;
+    const uint32_t ml = kMLBase[mlc] + mlx;
+    const uint32_t ll = kLLBase[llc] + llx;
     uint32_t off;
     if (ofv > 3u) {
       off = ofv - 3u;
@@ -714,12 +821,16 @@ __device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
       if (off == 0) off = S.rep0 = 1;  // (1.4.9 forces a zero repeat offset to 1)
     }
     // the states, LL then ML then OF (also after the last sequence)
-    sl = (el >> 16) + br_read(r, (el >> 8) & 255u);
-    sm = (em >> 16) + br_read(r, (em >> 8) & 255u);
-    so = (eo >> 16) + br_read(r, (eo >> 8) & 255u);
+    {  // (<= 9 + 9 + 8 bits: one read)
+      const uint32_t nl = (el >> 8) & 255u, nm = (em >> 8) & 255u, no = (eo >> 8) & 255u;
+      const uint32_t v = static_cast<uint32_t>(br_read64(r, nl + nm + no));
+      sl = (el >> 16) + (v >> (nm + no));
+      sm = (em >> 16) + ((v >> no) & ((1u << nm) - 1u));
+      so = (eo >> 16) + (v & ((1u << no) - 1u));
+    }
     if (ll > nlit - lp) return *fail = kFLitOverrun, false;
     if (ll + ml > cap - *op) return *fail = kFCap, false;
-    lds_copy(L.out + *op, L.lits + lp, ll, 0, lane);
+    lds_copy(L.out + *op, lits + lp, ll, 0, lane);
     lp += ll;
     *op += ll;
     if (off > *op - frame_start) return *fail = kFOffset, false;
@@ -727,9 +838,10 @@ __device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
     *op += ml;
   }
   if (r.pos > 0) return *fail = kFSeqBits, false;
+  zstamp(S.stamp, 4, lane);
   const uint32_t rest = nlit - lp;
   if (rest > cap - *op) return *fail = kFCap, false;
-  lds_copy(L.out + *op, L.lits + lp, rest, 0, lane);
+  lds_copy(L.out + *op, lits + lp, rest, 0, lane);
   *op += rest;
   return true;
 }
@@ -831,8 +943,11 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
   if (csize > cap) return finish(kCap, csize > 0xFFFFFFFFull ? 0xFFFFFFFFu : csize, kFOk);
   if (csize > a.out_cap || n > zstd_in_cap(a.out_cap)) return finish(kBig, csize, kFOk);
   const Lds L = lds_layout(smem, a.out_cap);
+  uint64_t* stamp = a.stamps != nullptr ? a.stamps + 8u * b : nullptr;
+  zstamp(stamp, 0, lane);
   stage(L.in, src, n, 16, lane);
   __builtin_amdgcn_s_waitcnt(0);
+  zstamp(stamp, 1, lane);
   // ZSTD_decompressDCtx(dst, csize, src, n): frames one after another
   const uint32_t ocap = static_cast<uint32_t>(csize);
   uint32_t p = 0, op = 0, fail = kFOk;
@@ -880,6 +995,7 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
     uint32_t q = p + f.hsize;
     const uint32_t start = op;
     SeqState S{};
+    S.stamp = stamp;
     S.rep0 = 1;
     S.rep1 = 4;
     S.rep2 = 8;
@@ -981,10 +1097,15 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
     k0 = 4u * nd;
   }
   for (uint32_t k = k0 + lane; k < op; k += 64) dst[k] = L.out[k];
+  zstamp(stamp, 5, lane);
   finish(kOK, op, kFOk);
 }
 
 }  // namespace
+
+#ifdef LVKV_PROBE_BUILD
+uint64_t* g_zstd_stamps = nullptr;  // lvkv_debug_zstd_stamps (tools/probe)
+#endif
 
 uint32_t zstd_lds(uint32_t max_ulen) { return zstd_lds_bytes(max(16u, max_ulen)); }
 
@@ -995,7 +1116,10 @@ hipError_t launch_zstd_uncompress(const uint8_t* src, const uint64_t* src_off,
                                   uint32_t block_mode, const uint8_t* vstatus,
                                   hipStream_t stream) {
   ZArgs a{src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, detail, nblocks,
-          0, block_mode, vstatus};
+          0, block_mode, vstatus, nullptr};
+#ifdef LVKV_PROBE_BUILD
+  a.stamps = g_zstd_stamps;
+#endif
   a.out_cap = dst_cap == nullptr ? 0u : max(16u, max_ulen);
   const size_t lds = dst_cap == nullptr ? 16u : zstd_lds_bytes(a.out_cap);
   hipLaunchKernelGGL(zstd_uncompress_kernel, dim3(nblocks), dim3(64), lds, stream, a);

@@ -43,6 +43,7 @@ int lvkv_debug_read_bw(const void* d_data, uint64_t bytes, uint32_t* d_scratch,
  * iteration (16 iterations kept), slots 0 start, 1 placed, 2 next walked,
  * 3 wave 2's records done, 4 all records, 5 long records, 6 merged. */
 void lvkv_debug_log_stamps(uint64_t* d_stamps);
+void lvkv_debug_zstd_stamps(uint64_t* d_stamps);  /* 8 s_memtime stamps a zstd frame */
 void lvkv_debug_asm_stamps(uint64_t* d_stamps);
 /* Whole-SSTable verify phase stamps: 16 u64 per table (head slots 0-7; the
  * fused form's first CRC workgroup in table 0's slots 8-10). NULL: off. */
