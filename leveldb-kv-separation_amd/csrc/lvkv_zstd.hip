@@ -124,19 +124,42 @@ __device__ __forceinline__ uint64_t br_read64(BitR& r, uint32_t n) {
 // ---- FSE tables (RFC 8878 §4.1; FSE_readNCount / FSE_buildDTable) --------
 // Decode entries: symbol | nbBits << 8 | baseline << 16.
 
+// 256 staged bytes from in[a] (a 4-aligned) held across the wave, a dword a
+// lane, so that the serial header and weight decoders read them with
+// v_readlane (a few cycles) instead of an LDS round trip each.
+struct RegBytes {
+  const uint8_t* in;
+  uint32_t a;
+  uint32_t d;
+};
+__device__ __forceinline__ RegBytes reg_bytes(const uint8_t* in, uint32_t p, uint32_t lane) {
+  RegBytes r;
+  r.in = in;
+  r.a = p & ~3u;
+  r.d = reinterpret_cast<const uint32_t*>(in + r.a)[lane];
+  return r;
+}
+// 32 bits at in[p] (p >= r.a)
+__device__ __forceinline__ uint32_t rb32(const RegBytes& r, uint32_t p) {
+  const uint32_t b = p - r.a;
+  if (b + 8u > 256u) return ld32(r.in, p);
+  const uint32_t w0 = __builtin_amdgcn_readlane(r.d, b >> 2);
+  const uint32_t w1 = __builtin_amdgcn_readlane(r.d, (b >> 2) + 1u);
+  return __builtin_amdgcn_alignbyte(w1, w0, b & 3u);
+}
+
 // The table description at in[p, end): false when malformed. Scalar code.
 __device__ bool read_ncount(const uint8_t* in, uint32_t p, uint32_t end, uint32_t max_sym,
                             uint32_t max_log, int16_t* counts, uint32_t* nsym, uint32_t* log_out,
-                            uint32_t* used) {
+                            uint32_t* used, uint32_t lane) {
   if (end <= p) return false;
   const uint32_t len = end - p;
+  const RegBytes rg = reg_bytes(in, p, lane);
   // 32 bits at byte offset i of the description, zeros past its end
   auto rd32 = [&](uint32_t i) -> uint32_t {
-    if (i + 4 <= len) return ld32(in, p + i);
-    uint32_t v = 0;
-    for (uint32_t k = 0; k < 4; ++k)
-      if (i + k < len) v |= static_cast<uint32_t>(in[p + i + k]) << (8 * k);
-    return v;
+    if (i >= len) return 0u;
+    const uint32_t v = rb32(rg, p + i);
+    return i + 4u <= len ? v : v & ((1u << (8u * (len - i))) - 1u);
   };
   uint32_t ip = 0;
   uint32_t bits = rd32(0);
@@ -202,57 +225,93 @@ __device__ bool read_ncount(const uint8_t* in, uint32_t p, uint32_t end, uint32_
 }
 
 // Spread and decode entries for counts[0, nsym) at accuracy `log` into
-// table (1 << log entries). `scratch` holds the per-symbol next state.
-// Scalar: a table has at most 512 entries.
+// table (1 << log entries, <= 512). `nxt` holds the per-symbol next state,
+// `syms` (>= 512 bytes) the symbols in spread order.
+//
+// FSE_buildDTable walks the positions p_j = j * step mod size, skipping the
+// low-probability slots at the top, and gives the k-th position it keeps to
+// the k-th symbol of the counts laid end to end. Here every j at once: its
+// rank among the kept positions (ballot), the symbol of that rank (the
+// symbols' first ranks marked, then a running max), one scatter.
 __device__ bool build_fse(const int16_t* counts, uint32_t nsym, uint32_t log, uint32_t* table,
-                          uint16_t* nxt, uint32_t lane) {
+                          uint16_t* nxt, uint8_t* syms, uint32_t lane) {
   const uint32_t size = 1u << log;
-  int32_t high = static_cast<int32_t>(size) - 1;
-  // symbols with count -1 at the top; everyone's next state starts at its count
-  for (uint32_t s = 0; s < nsym; ++s) {
-    const int32_t c = counts[s];
-    if (c == -1) {
-      if (lane == 0) table[high] = s;
-      --high;
-      if (lane == 0) nxt[s] = 1;
-    } else if (lane == 0) {
-      nxt[s] = static_cast<uint16_t>(c);
+  const uint64_t below = (uint64_t{1} << lane) - 1u;
+  for (uint32_t r = lane; r < size; r += 64) syms[r] = 0;
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  // symbols with count -1 at the top, in order; next states start at the
+  // count (1 for those); each positive count's first rank marked
+  uint32_t nlow = 0, cum = 0;
+  for (uint32_t g = 0; g < nsym; g += 64) {
+    const uint32_t s = g + lane;
+    const int32_t c = s < nsym ? counts[s] : 0;
+    const bool low = c == -1;
+    const uint64_t m = __ballot(low);
+    if (low) table[size - 1u - (nlow + __popcll(m & below))] = s;
+    nlow += __popcll(m);
+    const uint32_t pc = c > 0 ? static_cast<uint32_t>(c) : 0u;
+    uint32_t incl = pc;
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t v = __shfl_up(incl, d);
+      if (lane >= d) incl += v;
     }
+    if (s < nsym) nxt[s] = static_cast<uint16_t>(low ? 1 : c);
+    if (pc != 0 && cum + incl - pc < size) syms[cum + incl - pc] = static_cast<uint8_t>(s);
+    cum += __shfl(incl, 63);
   }
+  const uint32_t kept = size - nlow;  // (high + 1)
+  if (nlow > size || cum != kept) return false;
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  // symbol of every rank: the running max of the marks (symbols ascend)
+  uint32_t carry = 0;
+  for (uint32_t r0 = 0; r0 < kept; r0 += 64) {
+    const uint32_t r = r0 + lane;
+    uint32_t v = r < kept ? syms[r] : 0u;
+    v = v > carry ? v : carry;
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(v, d);
+      if (lane >= d && o > v) v = o;
+    }
+    if (r < kept) syms[r] = static_cast<uint8_t>(v);
+    carry = __shfl(v, 63);
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
   const uint32_t step = (size >> 1) + (size >> 3) + 3u;
   const uint32_t mask = size - 1u;
-  uint32_t pos = 0;
-  for (uint32_t s = 0; s < nsym; ++s) {
-    const int32_t c = counts[s];
-    for (int32_t i = 0; i < c; ++i) {
-      if (lane == 0) table[pos] = s;
-      pos = (pos + step) & mask;
-      while (static_cast<int32_t>(pos) > high) pos = (pos + step) & mask;
-    }
+  uint32_t rank = 0;
+  for (uint32_t j0 = 0; j0 < size; j0 += 64) {
+    const uint32_t j = j0 + lane;
+    const uint32_t t = (j * step) & mask;
+    const bool keep = j < size && t < kept;
+    const uint64_t m = __ballot(keep);
+    if (keep) table[t] = syms[rank + __popcll(m & below)];
+    rank += __popcll(m);
   }
-  if (pos != 0) return false;
   __builtin_amdgcn_s_waitcnt(0xc07f);
   // decode entries in table order: symbol s's k-th entry gets state
   // nxt[s] + k. 64 entries a step: a lane's rank among the step's entries of
-  // its symbol, and whether a later one follows, from the other lanes'
-  // symbols (readlane); the last of each symbol carries nxt[s] on.
+  // its symbol (the lanes sharing its symbol, one ballot per distinct
+  // symbol); the last of each symbol carries nxt[s] on.
   for (uint32_t c = 0; c < size; c += 64) {
     const uint32_t u = c + lane;
     const bool in = u < size;
-    const uint32_t s = in ? (table[u] & 255u) : 0x1000u + lane;
-    uint32_t before = 0, after = 0;
-    for (uint32_t j = 0; j < 64; ++j) {
-      const uint32_t sj = __builtin_amdgcn_readlane(s, j);
-      before += (sj == s && j < lane) ? 1u : 0u;
-      after += (sj == s && j > lane) ? 1u : 0u;
+    const uint32_t s = in ? (table[u] & 255u) : 0x1000u;
+    uint64_t todo = __ballot(in), peers = 0;
+    while (todo) {
+      const uint32_t sl = __builtin_amdgcn_readlane(s, static_cast<uint32_t>(__builtin_ctzll(todo)));
+      const uint64_t m = __ballot(s == sl);
+      if (s == sl) peers = m;
+      todo &= ~m;
     }
+    const uint32_t before = __popcll(peers & below);
+    const bool last = (peers >> lane) == 1u;
     const uint32_t ns = (in ? nxt[s] : 1u) + before;
     __builtin_amdgcn_s_waitcnt(0xc07f);  // every lane has read nxt before it moves
     if (in) {
       const uint32_t nbits = log - (31u - __builtin_clz(ns));
       const uint32_t base = (ns << nbits) - size;
       table[u] = s | (nbits << 8) | (base << 16);
-      if (after == 0) nxt[s] = static_cast<uint16_t>(ns + 1u);
+      if (last) nxt[s] = static_cast<uint16_t>(ns + 1u);
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
   }
@@ -287,6 +346,7 @@ struct Lds {
   uint8_t* w;       // Huffman weights (256 + 1)
   int16_t* cnt;     // normalized counts scratch (256: the weights' FSE may name 256)
   uint16_t* nxt;    // FSE next-state scratch (256)
+  uint8_t* sym;     // FSE spread scratch (512)
 };
 
 constexpr uint32_t kHufEntries = 2048, kFseLL = 512, kFseOF = 256, kFseML = 512, kFseW = 64;
@@ -298,7 +358,7 @@ __host__ __device__ constexpr uint32_t zstd_in_cap(uint32_t out_cap) {
 __host__ __device__ constexpr uint32_t round16(uint32_t x) { return (x + 15u) & ~15u; }
 __host__ __device__ constexpr uint32_t zstd_lds_bytes(uint32_t out_cap) {
   return round16(zstd_in_cap(out_cap) + 16u + 4u) + round16(out_cap) +
-         2u * kHufEntries + 4u * (kFseLL + kFseOF + kFseML + kFseW) + 272u + 512u + 512u;
+         2u * kHufEntries + 4u * (kFseLL + kFseOF + kFseML + kFseW) + 272u + 512u + 512u + 512u;
 }
 
 __device__ Lds lds_layout(uint8_t* smem, uint32_t out_cap) {
@@ -323,15 +383,24 @@ __device__ Lds lds_layout(uint8_t* smem, uint32_t out_cap) {
   L.cnt = reinterpret_cast<int16_t*>(smem + o);
   o += 512u;
   L.nxt = reinterpret_cast<uint16_t*>(smem + o);
+  o += 512u;
+  L.sym = smem + o;
   return L;
 }
 
 // ---- Huffman (RFC 8878 §4.2; HUF_readStats / HUF_readDTableX1) -----------
 
+// s_memtime into a frame's stamp slot k (probe build; lane 0, a vector store)
+__device__ __forceinline__ void zstamp(uint64_t* slot, uint32_t k, uint32_t lane) {
+  if (slot != nullptr && lane == 0) slot[k] = __builtin_amdgcn_s_memtime();
+}
+
 // The tree description at in[p, end): weights into L.w (with the implied
 // last), *nw = symbols, *maxbits, *used. Scalar.
 __device__ bool huf_weights(const Lds& L, uint32_t p, uint32_t end, uint32_t* nw,
-                            uint32_t* maxbits, uint32_t* used, uint32_t lane, uint32_t* fail) {
+                            uint32_t* maxbits, uint32_t* used, uint32_t lane, uint32_t* fail,
+                            uint64_t* stamp) {
+  zstamp(stamp, 8, lane);
   if (p >= end) return *fail = kFHufHdr, false;
   const uint32_t hb = L.in[p];
   uint32_t n = 0;
@@ -347,35 +416,59 @@ __device__ bool huf_weights(const Lds& L, uint32_t p, uint32_t end, uint32_t* nw
   } else {  // FSE-compressed weights, two interleaved states
     if (hb == 0 || p + 1u + hb > end) return *fail = kFHufHdr, false;
     uint32_t nsym, log, nc;
-    if (!read_ncount(L.in, p + 1u, p + 1u + hb, 255u, 6u, L.cnt, &nsym, &log, &nc))
+    if (!read_ncount(L.in, p + 1u, p + 1u + hb, 255u, 6u, L.cnt, &nsym, &log, &nc, lane))
       return *fail = kFNcount, false;
-    if (!build_fse(L.cnt, nsym, log, L.wt, L.nxt, lane)) return *fail = kFFseSpread, false;
-    BitR r;
-    if (!br_init(r, L.in, p + 1u + nc, p + 1u + hb)) return *fail = kFHufWeights, false;
-    uint32_t s1 = br_read(r, log), s2 = br_read(r, log);
+    zstamp(stamp, 9, lane);
+    if (!build_fse(L.cnt, nsym, log, L.wt, L.nxt, L.sym, lane)) return *fail = kFFseSpread, false;
+    zstamp(stamp, 10, lane);
+    // the <= 64-entry table and the <= 127-byte stream in registers: each
+    // step is a readlane, a shift and an add (both states share the stream)
+    const uint32_t lo = p + 1u + nc, hi = p + 1u + hb;
+    if (hi <= lo || L.in[hi - 1] == 0) return *fail = kFHufWeights, false;
+    const uint32_t treg = L.wt[lane];
+    const RegBytes rg = reg_bytes(L.in, lo, lane);
+    const int32_t base = static_cast<int32_t>(8u * (lo - rg.a));
+    int32_t pos = static_cast<int32_t>(8u * (hi - lo - 1u) +
+                                       (31u - __builtin_clz(static_cast<uint32_t>(L.in[hi - 1]))));
+    auto rd = [&](uint32_t nb) -> uint32_t {  // br_read on the registers
+      pos -= static_cast<int32_t>(nb);
+      const int32_t top = pos + static_cast<int32_t>(nb);
+      if (nb == 0 || top <= 0) return 0u;
+      const int32_t l = pos < 0 ? 0 : pos;
+      const uint32_t q = static_cast<uint32_t>(base + l);
+      // (readlane returns int: widen through uint32_t, not by sign)
+      const uint32_t w0 = __builtin_amdgcn_readlane(rg.d, q >> 5);
+      const uint32_t w1 = __builtin_amdgcn_readlane(rg.d, (q >> 5) + 1u);
+      const uint64_t w = (static_cast<uint64_t>(w1) << 32) | w0;
+      const uint32_t v = static_cast<uint32_t>(w >> (q & 31u)) & ((1u << (top - l)) - 1u);
+      return v << (l - pos);
+    };
+    auto entry = [&](uint32_t s) -> uint32_t { return __builtin_amdgcn_readlane(treg, s); };
+    uint32_t s1 = rd(log), s2 = rd(log);
     for (;;) {
       if (n > 253u) return *fail = kFHufWeights, false;
-      uint32_t e = L.wt[s1];
+      uint32_t e = entry(s1);
       if (lane == 0) L.w[n] = static_cast<uint8_t>(e & 255u);
       ++n;
-      s1 = (e >> 16) + br_read(r, (e >> 8) & 255u);
-      if (r.pos < 0) {
-        if (lane == 0) L.w[n] = static_cast<uint8_t>(L.wt[s2] & 255u);
+      s1 = (e >> 16) + rd((e >> 8) & 255u);
+      if (pos < 0) {
+        if (lane == 0) L.w[n] = static_cast<uint8_t>(entry(s2) & 255u);
         ++n;
         break;
       }
       if (n > 253u) return *fail = kFHufWeights, false;
-      e = L.wt[s2];
+      e = entry(s2);
       if (lane == 0) L.w[n] = static_cast<uint8_t>(e & 255u);
       ++n;
-      s2 = (e >> 16) + br_read(r, (e >> 8) & 255u);
-      if (r.pos < 0) {
-        if (lane == 0) L.w[n] = static_cast<uint8_t>(L.wt[s1] & 255u);
+      s2 = (e >> 16) + rd((e >> 8) & 255u);
+      if (pos < 0) {
+        if (lane == 0) L.w[n] = static_cast<uint8_t>(entry(s1) & 255u);
         ++n;
         break;
       }
     }
     *used = 1u + hb;
+    zstamp(stamp, 11, lane);
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);
   // total weight, the implied last weight, and rank 1's count
@@ -409,22 +502,32 @@ __device__ bool huf_weights(const Lds& L, uint32_t p, uint32_t end, uint32_t* nw
 
 // Decode table: symbols by weight, then by symbol value, each over
 // 2^(w-1) entries of 2^maxbits.
+// A level at a time: its symbols listed in order (ballot ranks, into the
+// nxt scratch), then its entries filled 64 at a time from the list.
 __device__ void huf_table(const Lds& L, uint32_t nw, uint32_t mb, uint32_t lane) {
-  uint32_t pos = 0;
+  uint8_t* list = reinterpret_cast<uint8_t*>(L.nxt);
+  const uint64_t below = (uint64_t{1} << lane) - 1u;
+  uint32_t w[4];
+#pragma unroll
+  for (uint32_t g = 0; g < 4; ++g) {
+    const uint32_t s = 64u * g + lane;
+    w[g] = s < nw ? L.w[s] : 0u;
+  }
+  uint32_t pos = 0, lpos = 0;
   for (uint32_t wgt = 1; wgt <= mb; ++wgt) {
-    const uint32_t span = 1u << (wgt - 1u);
-    const uint32_t e = (mb + 1u - wgt) << 8;
-    for (uint32_t g = 0; g < nw; g += 64) {
-      const uint32_t s = g + lane;
-      uint64_t m = __ballot(s < nw && L.w[s] == wgt);
-      while (m) {
-        const uint32_t sym = g + static_cast<uint32_t>(__builtin_ctzll(m));
-        m &= m - 1u;
-        for (uint32_t k = lane; k < span; k += 64)
-          L.huf[pos + k] = static_cast<uint16_t>(sym | e);
-        pos += span;
-      }
+    const uint32_t lpos0 = lpos;
+#pragma unroll
+    for (uint32_t g = 0; g < 4; ++g) {
+      const bool mine = w[g] == wgt;
+      const uint64_t m = __ballot(mine);
+      if (mine) list[lpos + __popcll(m & below)] = static_cast<uint8_t>(64u * g + lane);
+      lpos += __popcll(m);
     }
+    const uint32_t n = (lpos - lpos0) << (wgt - 1u);
+    const uint32_t e = (mb + 1u - wgt) << 8;
+    for (uint32_t k = lane; k < n; k += 64)
+      L.huf[pos + k] = static_cast<uint16_t>(list[lpos0 + (k >> (wgt - 1u))] | e);
+    pos += n;
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);
 }
@@ -528,13 +631,9 @@ struct ZArgs {
   uint32_t out_cap;
   uint32_t block_mode;  // ReadBlock mode: handles, type byte 2 only, LVKV_READ_*
   const uint8_t* vstatus;
-  uint64_t* stamps;  // probe build: 8 clock stamps a frame (nullptr: none)
+  uint64_t* stamps;  // probe build: 16 clock stamps a frame (nullptr: none)
 };
 
-// s_memtime into a frame's stamp slot k (probe build; lane 0, a vector store)
-__device__ __forceinline__ void zstamp(uint64_t* slot, uint32_t k, uint32_t lane) {
-  if (slot != nullptr && lane == 0) slot[k] = __builtin_amdgcn_s_memtime();
-}
 
 // One compressed block's literals at the end of the frame's output space
 // (out_end - n: the output, which grows from the front, reaches a literal
@@ -590,7 +689,7 @@ __device__ bool literals(const Lds& L, uint32_t p, uint32_t end, uint32_t cap, u
   const uint32_t qend = p + hs + csize;
   if (type == 2) {
     uint32_t nw, mb, u;
-    if (!huf_weights(L, q, qend, &nw, &mb, &u, lane, fail)) return false;
+    if (!huf_weights(L, q, qend, &nw, &mb, &u, lane, fail, stamp)) return false;
     zstamp(stamp, 6, lane);
     huf_table(L, nw, mb, lane);
     zstamp(stamp, 7, lane);
@@ -687,9 +786,9 @@ __device__ bool seq_table(const Lds& L, uint32_t p, uint32_t end, uint32_t mode,
     *used = 1;
   } else if (mode == 2) {
     uint32_t nsym, lg, u;
-    if (!read_ncount(L.in, p, end, max_sym, max_log, L.cnt, &nsym, &lg, &u))
+    if (!read_ncount(L.in, p, end, max_sym, max_log, L.cnt, &nsym, &lg, &u, lane))
       return *fail = kFNcount, false;
-    if (!build_fse(L.cnt, nsym, lg, table, L.nxt, lane)) return *fail = kFFseSpread, false;
+    if (!build_fse(L.cnt, nsym, lg, table, L.nxt, L.sym, lane)) return *fail = kFFseSpread, false;
     *log = lg;
     *used = u;
   } else if (!*have) {
@@ -943,7 +1042,7 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
   if (csize > cap) return finish(kCap, csize > 0xFFFFFFFFull ? 0xFFFFFFFFu : csize, kFOk);
   if (csize > a.out_cap || n > zstd_in_cap(a.out_cap)) return finish(kBig, csize, kFOk);
   const Lds L = lds_layout(smem, a.out_cap);
-  uint64_t* stamp = a.stamps != nullptr ? a.stamps + 8u * b : nullptr;
+  uint64_t* stamp = a.stamps != nullptr ? a.stamps + 16u * b : nullptr;
   zstamp(stamp, 0, lane);
   stage(L.in, src, n, 16, lane);
   __builtin_amdgcn_s_waitcnt(0);

@@ -41,7 +41,7 @@ def main():
     cap = torch.full((nb,), 4096, dtype=torch.int32, device=dev)
     ol = torch.empty(nb, dtype=torch.int32, device=dev)
     st = torch.empty(nb, dtype=torch.uint8, device=dev)
-    stamps = torch.zeros(nb * 8, dtype=torch.int64, device=dev)
+    stamps = torch.zeros(nb * 16, dtype=torch.int64, device=dev)
     lib = ctypes.CDLL(str(REPO / "tools" / "probe" / "liblvkv_probe.so"))
     vp = ctypes.c_void_p
     lib.lvkv_debug_zstd_stamps.argtypes = [vp]
@@ -53,7 +53,7 @@ def main():
     assert lib.lvkv_zstd_uncompress_device(*args) == 0
     torch.cuda.synchronize()
     assert int(st.max()) == 0
-    s = stamps.view(nb, 8).cpu().numpy().astype(np.float64)
+    s = stamps.view(nb, 16).cpu().numpy().astype(np.float64)
     names = ["stage", "literals", "seq tables", "sequences", "out"]
     d = np.diff(s[:, :6], axis=1)
     med = {n: float(np.median(d[:, i])) for i, n in enumerate(names)}
@@ -61,6 +61,11 @@ def main():
     med["weights"] = float(np.median(s[:, 6] - s[:, 1]))
     med["huf table"] = float(np.median(s[:, 7] - s[:, 6]))
     med["streams"] = float(np.median(s[:, 2] - s[:, 7]))
+    fse = s[:, 11] > 0  # frames whose first tree has FSE-coded weights
+    for name, a, b in (("to weights", 1, 8), ("ncount", 8, 9), ("fse build", 9, 10),
+                       ("weight decode", 10, 11), ("weight checks", 11, 6)):
+        med[name] = float(np.median(s[fse, b] - s[fse, a])) if fse.any() else None
+    med["fse frames"] = int(fse.sum())
     print({"ticks_median": med, "total": tot})
 
 
