@@ -45,6 +45,19 @@ __device__ __forceinline__ uint64_t ld64(const uint8_t* b, uint32_t p) {
   return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
+// Wave-uniform reads. The parser's values are the same in every lane; an
+// LDS or global load still lands in a VGPR, and everything computed from it
+// would run as divergent code (exec masks, VALU), so the loads that steer
+// control flow go through v_readfirstlane into SGPRs.
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t ldb(const uint8_t* b, uint32_t p) { return uni(b[p]); }
+__device__ __forceinline__ uint32_t ld32u(const uint8_t* b, uint32_t p) { return uni(ld32(b, p)); }
+__device__ __forceinline__ uint64_t ld64u(const uint8_t* b, uint32_t p) {
+  const uint64_t v = ld64(b, p);
+  return (static_cast<uint64_t>(uni(static_cast<uint32_t>(v >> 32))) << 32) |
+         uni(static_cast<uint32_t>(v));
+}
+
 // Global -> LDS (4-aligned), as the Snappy kernels stage (aligned dword loads
 // at any source alignment, nothing read past the block's last dword).
 __device__ __forceinline__ void stage(uint8_t* dst, const uint8_t* src, uint32_t n, uint32_t pad,
@@ -77,13 +90,14 @@ __device__ __forceinline__ bool br_init(BitR& r, const uint8_t* in, uint32_t lo,
   r.cb = -1;
   r.win = 0;
   if (hi <= lo) return false;
-  const uint32_t last = in[hi - 1];
+  const uint32_t last = ldb(in, hi - 1);
   if (last == 0) return false;
   r.pos = static_cast<int32_t>(8u * (hi - lo - 1u) + (31u - __builtin_clz(last)));
   return true;
 }
 
-// bits [p, p + n) (n <= 32), zeros below 0
+// bits [p, p + n) (n <= 32), zeros below 0 (U: the reader is wave-uniform)
+template <bool U = true>
 __device__ __forceinline__ uint32_t br_bits(BitR& r, int32_t p, uint32_t n) {
   const int32_t top = p + static_cast<int32_t>(n);
   if (n == 0 || top <= 0) return 0;
@@ -92,7 +106,8 @@ __device__ __forceinline__ uint32_t br_bits(BitR& r, int32_t p, uint32_t n) {
     int32_t cb = ((top + 7) >> 3) - 8;
     if (cb < 0) cb = 0;
     r.cb = cb;
-    r.win = ld64(r.in, r.start + static_cast<uint32_t>(cb));
+    r.win = U ? ld64u(r.in, r.start + static_cast<uint32_t>(cb))
+              : ld64(r.in, r.start + static_cast<uint32_t>(cb));
   }
   uint64_t v = r.win >> (lo - 8 * r.cb);
   v &= (uint64_t{1} << (top - lo)) - 1u;
@@ -114,7 +129,7 @@ __device__ __forceinline__ uint64_t br_read64(BitR& r, uint32_t n) {
     int32_t cb = ((top + 7) >> 3) - 8;
     if (cb < 0) cb = 0;
     r.cb = cb;
-    r.win = ld64(r.in, r.start + static_cast<uint32_t>(cb));
+    r.win = ld64u(r.in, r.start + static_cast<uint32_t>(cb));
   }
   uint64_t v = r.win >> (lo - 8 * r.cb);
   v &= (uint64_t{1} << (top - lo)) - 1u;
@@ -142,7 +157,7 @@ __device__ __forceinline__ RegBytes reg_bytes(const uint8_t* in, uint32_t p, uin
 // 32 bits at in[p] (p >= r.a)
 __device__ __forceinline__ uint32_t rb32(const RegBytes& r, uint32_t p) {
   const uint32_t b = p - r.a;
-  if (b + 8u > 256u) return ld32(r.in, p);
+  if (b + 8u > 256u) return ld32u(r.in, p);
   const uint32_t w0 = __builtin_amdgcn_readlane(r.d, b >> 2);
   const uint32_t w1 = __builtin_amdgcn_readlane(r.d, (b >> 2) + 1u);
   return __builtin_amdgcn_alignbyte(w1, w0, b & 3u);
@@ -257,7 +272,7 @@ __device__ bool build_fse(const int16_t* counts, uint32_t nsym, uint32_t log, ui
     }
     if (s < nsym) nxt[s] = static_cast<uint16_t>(low ? 1 : c);
     if (pc != 0 && cum + incl - pc < size) syms[cum + incl - pc] = static_cast<uint8_t>(s);
-    cum += __shfl(incl, 63);
+    cum += uni(__shfl(incl, 63));
   }
   const uint32_t kept = size - nlow;  // (high + 1)
   if (nlow > size || cum != kept) return false;
@@ -273,7 +288,7 @@ __device__ bool build_fse(const int16_t* counts, uint32_t nsym, uint32_t log, ui
       if (lane >= d && o > v) v = o;
     }
     if (r < kept) syms[r] = static_cast<uint8_t>(v);
-    carry = __shfl(v, 63);
+    carry = uni(__shfl(v, 63));
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);
   const uint32_t step = (size >> 1) + (size >> 3) + 3u;
@@ -343,7 +358,6 @@ struct Lds {
   uint32_t* of;
   uint32_t* ml;
   uint32_t* wt;
-  uint8_t* w;       // Huffman weights (256 + 1)
   int16_t* cnt;     // normalized counts scratch (256: the weights' FSE may name 256)
   uint16_t* nxt;    // FSE next-state scratch (256)
   uint8_t* sym;     // FSE spread scratch (512)
@@ -358,7 +372,7 @@ __host__ __device__ constexpr uint32_t zstd_in_cap(uint32_t out_cap) {
 __host__ __device__ constexpr uint32_t round16(uint32_t x) { return (x + 15u) & ~15u; }
 __host__ __device__ constexpr uint32_t zstd_lds_bytes(uint32_t out_cap) {
   return round16(zstd_in_cap(out_cap) + 16u + 4u) + round16(out_cap) +
-         2u * kHufEntries + 4u * (kFseLL + kFseOF + kFseML + kFseW) + 272u + 512u + 512u + 512u;
+         2u * kHufEntries + 4u * (kFseLL + kFseOF + kFseML + kFseW) + 512u + 512u + 512u;
 }
 
 __device__ Lds lds_layout(uint8_t* smem, uint32_t out_cap) {
@@ -378,8 +392,6 @@ __device__ Lds lds_layout(uint8_t* smem, uint32_t out_cap) {
   o += 4u * kFseML;
   L.wt = reinterpret_cast<uint32_t*>(smem + o);
   o += 4u * kFseW;
-  L.w = smem + o;
-  o += 272u;
   L.cnt = reinterpret_cast<int16_t*>(smem + o);
   o += 512u;
   L.nxt = reinterpret_cast<uint16_t*>(smem + o);
@@ -390,27 +402,49 @@ __device__ Lds lds_layout(uint8_t* smem, uint32_t out_cap) {
 
 // ---- Huffman (RFC 8878 §4.2; HUF_readStats / HUF_readDTableX1) -----------
 
-// s_memtime into a frame's stamp slot k (probe build; lane 0, a vector store)
-__device__ __forceinline__ void zstamp(uint64_t* slot, uint32_t k, uint32_t lane) {
-  if (slot != nullptr && lane == 0) slot[k] = __builtin_amdgcn_s_memtime();
+// s_memtime into a frame's stamp slot k (probe build only: a vector store
+// from every lane, the same value, so that no lane-dependent branch splits
+// the parser's uniform control flow)
+__device__ __forceinline__ void zstamp(uint64_t* slot, uint32_t k, uint32_t) {
+#ifdef LVKV_PROBE_BUILD
+  if (slot != nullptr) slot[k] = __builtin_amdgcn_s_memtime();
+#else
+  (void)slot;
+  (void)k;
+#endif
 }
 
-// The tree description at in[p, end): weights into L.w (with the implied
-// last), *nw = symbols, *maxbits, *used. Scalar.
-__device__ bool huf_weights(const Lds& L, uint32_t p, uint32_t end, uint32_t* nw,
-                            uint32_t* maxbits, uint32_t* used, uint32_t lane, uint32_t* fail,
-                            uint64_t* stamp) {
+// The tree description at in[p, end): the weights in registers (symbol
+// 64 g + lane's in w[g], zeros past the last; with the implied last), *nw =
+// symbols, *maxbits, *used. Uniform control flow; no LDS stores in the
+// serial loop (a store there would make every step wait on lgkmcnt).
+__device__ bool huf_weights(const Lds& L, uint32_t p, uint32_t end, uint32_t (&w)[4],
+                            uint32_t* nw, uint32_t* maxbits, uint32_t* used, uint32_t lane,
+                            uint32_t* fail, uint64_t* stamp) {
   zstamp(stamp, 8, lane);
   if (p >= end) return *fail = kFHufHdr, false;
-  const uint32_t hb = L.in[p];
+  const uint32_t hb = ldb(L.in, p);
   uint32_t n = 0;
+#pragma unroll
+  for (uint32_t g = 0; g < 4; ++g) w[g] = 0;
+  // weight v of symbol i (uniform i): one lane of one register
+  auto put = [&](uint32_t i, uint32_t v) {
+    const bool me = lane == (i & 63u);
+#pragma unroll
+    for (uint32_t g = 0; g < 4; ++g)
+      if ((i >> 6) == g) w[g] = me ? v : w[g];
+  };
   if (hb >= 128) {  // direct 4-bit weights
     n = hb - 127u;
     const uint32_t nbytes = (n + 1u) >> 1;
     if (p + 1u + nbytes > end) return *fail = kFHufHdr, false;
-    for (uint32_t i = lane; i < n; i += 64) {
-      const uint32_t b = L.in[p + 1u + (i >> 1)];
-      L.w[i] = static_cast<uint8_t>((i & 1u) ? (b & 15u) : (b >> 4));
+#pragma unroll
+    for (uint32_t g = 0; g < 4; ++g) {
+      const uint32_t i = 64u * g + lane;
+      if (i < n) {
+        const uint32_t b = L.in[p + 1u + (i >> 1)];
+        w[g] = (i & 1u) ? (b & 15u) : (b >> 4);
+      }
     }
     *used = 1u + nbytes;
   } else {  // FSE-compressed weights, two interleaved states
@@ -424,76 +458,84 @@ __device__ bool huf_weights(const Lds& L, uint32_t p, uint32_t end, uint32_t* nw
     // the <= 64-entry table and the <= 127-byte stream in registers: each
     // step is a readlane, a shift and an add (both states share the stream)
     const uint32_t lo = p + 1u + nc, hi = p + 1u + hb;
-    if (hi <= lo || L.in[hi - 1] == 0) return *fail = kFHufWeights, false;
+    if (hi <= lo || ldb(L.in, hi - 1) == 0) return *fail = kFHufWeights, false;
     const uint32_t treg = L.wt[lane];
-    const RegBytes rg = reg_bytes(L.in, lo, lane);
-    const int32_t base = static_cast<int32_t>(8u * (lo - rg.a));
+    // lane k + 1 holds the stream's dword k, lane 0 zeros: bit x of the
+    // stream is bit x + 32 of the lanes' concatenation, and the bits below
+    // its start (x < 0, at most 12 of them) read as zeros with no test
+    const uint32_t sd = lane == 0 ? 0u : ld32(L.in, lo + 4u * (lane - 1u));
+    __builtin_amdgcn_s_waitcnt(0xc07f);
     int32_t pos = static_cast<int32_t>(8u * (hi - lo - 1u) +
-                                       (31u - __builtin_clz(static_cast<uint32_t>(L.in[hi - 1]))));
-    auto rd = [&](uint32_t nb) -> uint32_t {  // br_read on the registers
+                                       (31u - __builtin_clz(ldb(L.in, hi - 1))));
+    auto rd = [&](uint32_t nb) -> uint32_t {  // br_read on the registers (nb <= 6)
       pos -= static_cast<int32_t>(nb);
-      const int32_t top = pos + static_cast<int32_t>(nb);
-      if (nb == 0 || top <= 0) return 0u;
-      const int32_t l = pos < 0 ? 0 : pos;
-      const uint32_t q = static_cast<uint32_t>(base + l);
+      const uint32_t q = static_cast<uint32_t>(pos + 32);
       // (readlane returns int: widen through uint32_t, not by sign)
-      const uint32_t w0 = __builtin_amdgcn_readlane(rg.d, q >> 5);
-      const uint32_t w1 = __builtin_amdgcn_readlane(rg.d, (q >> 5) + 1u);
-      const uint64_t w = (static_cast<uint64_t>(w1) << 32) | w0;
-      const uint32_t v = static_cast<uint32_t>(w >> (q & 31u)) & ((1u << (top - l)) - 1u);
-      return v << (l - pos);
+      const uint32_t w0 = __builtin_amdgcn_readlane(sd, q >> 5);
+      const uint32_t w1 = __builtin_amdgcn_readlane(sd, (q >> 5) + 1u);
+      const uint64_t x = (static_cast<uint64_t>(w1) << 32) | w0;
+      return static_cast<uint32_t>(x >> (q & 31u)) & ((1u << nb) - 1u);
     };
     auto entry = [&](uint32_t s) -> uint32_t { return __builtin_amdgcn_readlane(treg, s); };
+    // (lane 0 stores the weights into the spread scratch, free again: one
+    // ds_write a weight, nothing waits on it inside the loop)
+    uint8_t* ws = L.sym;
     uint32_t s1 = rd(log), s2 = rd(log);
     for (;;) {
       if (n > 253u) return *fail = kFHufWeights, false;
       uint32_t e = entry(s1);
-      if (lane == 0) L.w[n] = static_cast<uint8_t>(e & 255u);
+      if (lane == 0) ws[n] = static_cast<uint8_t>(e);
       ++n;
       s1 = (e >> 16) + rd((e >> 8) & 255u);
       if (pos < 0) {
-        if (lane == 0) L.w[n] = static_cast<uint8_t>(entry(s2) & 255u);
+        if (lane == 0) ws[n] = static_cast<uint8_t>(entry(s2));
         ++n;
         break;
       }
       if (n > 253u) return *fail = kFHufWeights, false;
       e = entry(s2);
-      if (lane == 0) L.w[n] = static_cast<uint8_t>(e & 255u);
+      if (lane == 0) ws[n] = static_cast<uint8_t>(e);
       ++n;
       s2 = (e >> 16) + rd((e >> 8) & 255u);
       if (pos < 0) {
-        if (lane == 0) L.w[n] = static_cast<uint8_t>(entry(s1) & 255u);
+        if (lane == 0) ws[n] = static_cast<uint8_t>(entry(s1));
         ++n;
         break;
       }
     }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+#pragma unroll
+    for (uint32_t g = 0; g < 4; ++g) {
+      const uint32_t i = 64u * g + lane;
+      w[g] = i < n ? ws[i] : 0u;
+    }
     *used = 1u + hb;
     zstamp(stamp, 11, lane);
   }
-  __builtin_amdgcn_s_waitcnt(0xc07f);
   // total weight, the implied last weight, and rank 1's count
   uint32_t total = 0, bad = 0;
-  for (uint32_t i = lane; i < n; i += 64) {
-    const uint32_t x = L.w[i];
-    bad |= x > 11u;
-    total += (1u << x) >> 1;
+#pragma unroll
+  for (uint32_t g = 0; g < 4; ++g) {
+    bad |= w[g] > 11u;
+    total += (1u << (w[g] & 15u)) >> 1;
   }
   for (uint32_t d = 32; d >= 1; d >>= 1) {
     total += __shfl_xor(total, d);
     bad |= __shfl_xor(bad, d);
   }
+  total = uni(total);
+  bad = uni(bad);
   if (bad || total == 0) return *fail = kFHufWeights, false;
   const uint32_t mb = 32u - __builtin_clz(total);  // highbit(total) + 1
   if (mb > 11u) return *fail = kFHufWeights, false;
   const uint32_t rest = (1u << mb) - total;
   if (rest & (rest - 1u)) return *fail = kFHufWeights, false;
-  const uint32_t last = 32u - __builtin_clz(rest);
-  if (lane == 0) L.w[n] = static_cast<uint8_t>(last);
-  ++n;
-  __builtin_amdgcn_s_waitcnt(0xc07f);
+  put(n++, 32u - __builtin_clz(rest));
   uint32_t r1 = 0;
-  for (uint32_t i = lane; i < n; i += 64) r1 += L.w[i] == 1u ? 1u : 0u;
+#pragma unroll
+  for (uint32_t g = 0; g < 4; ++g) r1 += w[g] == 1u ? 1u : 0u;
   for (uint32_t d = 32; d >= 1; d >>= 1) r1 += __shfl_xor(r1, d);
+  r1 = uni(r1);
   if (r1 < 2u || (r1 & 1u)) return *fail = kFHufWeights, false;
   *nw = n;
   *maxbits = mb;
@@ -504,15 +546,9 @@ __device__ bool huf_weights(const Lds& L, uint32_t p, uint32_t end, uint32_t* nw
 // 2^(w-1) entries of 2^maxbits.
 // A level at a time: its symbols listed in order (ballot ranks, into the
 // nxt scratch), then its entries filled 64 at a time from the list.
-__device__ void huf_table(const Lds& L, uint32_t nw, uint32_t mb, uint32_t lane) {
+__device__ void huf_table(const Lds& L, const uint32_t (&w)[4], uint32_t mb, uint32_t lane) {
   uint8_t* list = reinterpret_cast<uint8_t*>(L.nxt);
   const uint64_t below = (uint64_t{1} << lane) - 1u;
-  uint32_t w[4];
-#pragma unroll
-  for (uint32_t g = 0; g < 4; ++g) {
-    const uint32_t s = 64u * g + lane;
-    w[g] = s < nw ? L.w[s] : 0u;
-  }
   uint32_t pos = 0, lpos = 0;
   for (uint32_t wgt = 1; wgt <= mb; ++wgt) {
     const uint32_t lpos0 = lpos;
@@ -558,7 +594,7 @@ __device__ __forceinline__ int32_t huf_run(const Lds& L, uint32_t lo, int32_t po
       }
       idx = static_cast<uint32_t>(win >> (p - wlo)) & mask;
     } else {
-      idx = br_bits(r, p, mb);  // bits below the start read as zeros
+      idx = br_bits<false>(r, p, mb);  // bits below the start read as zeros
     }
     const uint32_t e = L.huf[idx];
     pos -= static_cast<int32_t>(e >> 8);
@@ -643,7 +679,7 @@ __device__ bool literals(const Lds& L, uint32_t p, uint32_t end, uint32_t cap, u
                          bool* have_tree, uint32_t* mb_tree, uint32_t* nlit, uint32_t* used,
                          uint32_t lane, uint32_t* fail, uint64_t* stamp) {
   if (end - p < 3u) return *fail = kFLitHdr, false;  // MIN_CBLOCK_SIZE
-  const uint32_t b0 = L.in[p];
+  const uint32_t b0 = ldb(L.in, p);
   const uint32_t type = b0 & 3u, sf = (b0 >> 2) & 3u;
   if (type <= 1u) {  // raw / RLE
     uint32_t n, hs;
@@ -651,11 +687,10 @@ __device__ bool literals(const Lds& L, uint32_t p, uint32_t end, uint32_t cap, u
       n = b0 >> 3;
       hs = 1;
     } else if (sf == 1) {
-      n = (b0 >> 4) + (static_cast<uint32_t>(L.in[p + 1]) << 4);
+      n = (b0 >> 4) + (ldb(L.in, p + 1) << 4);
       hs = 2;
     } else {
-      n = (b0 >> 4) + (static_cast<uint32_t>(L.in[p + 1]) << 4) +
-          (static_cast<uint32_t>(L.in[p + 2]) << 12);
+      n = (b0 >> 4) + (ldb(L.in, p + 1) << 4) + (ldb(L.in, p + 2) << 12);
       hs = 3;
     }
     if (n > kBlockMax) return *fail = kFLitSize, false;
@@ -667,7 +702,7 @@ __device__ bool literals(const Lds& L, uint32_t p, uint32_t end, uint32_t cap, u
       *used = hs + n;
     } else {
       if (p + hs + 1u > end) return *fail = kFLitSize, false;
-      const uint8_t v = L.in[p + hs];
+      const uint8_t v = static_cast<uint8_t>(ldb(L.in, p + hs));
       uint8_t* lits = out_end - n;
       for (uint32_t k = lane; k < n; k += 64) lits[k] = v;
       *used = hs + 1u;
@@ -678,7 +713,7 @@ __device__ bool literals(const Lds& L, uint32_t p, uint32_t end, uint32_t cap, u
   const uint32_t hs = sf == 0 ? 3u : sf == 1 ? 3u : sf == 2 ? 4u : 5u;
   if (p + hs > end) return *fail = kFLitHdr, false;
   uint64_t hv = 0;
-  for (uint32_t k = 0; k < hs; ++k) hv |= static_cast<uint64_t>(L.in[p + k]) << (8 * k);
+  for (uint32_t k = 0; k < hs; ++k) hv |= static_cast<uint64_t>(ldb(L.in, p + k)) << (8 * k);
   const uint32_t bits = sf <= 1u ? 10u : sf == 2 ? 14u : 18u;
   const uint32_t n = static_cast<uint32_t>(hv >> 4) & ((1u << bits) - 1u);
   const uint32_t csize = static_cast<uint32_t>(hv >> (4 + bits)) & ((1u << bits) - 1u);
@@ -688,10 +723,10 @@ __device__ bool literals(const Lds& L, uint32_t p, uint32_t end, uint32_t cap, u
   uint32_t q = p + hs;
   const uint32_t qend = p + hs + csize;
   if (type == 2) {
-    uint32_t nw, mb, u;
-    if (!huf_weights(L, q, qend, &nw, &mb, &u, lane, fail, stamp)) return false;
+    uint32_t w[4], nw, mb, u;
+    if (!huf_weights(L, q, qend, w, &nw, &mb, &u, lane, fail, stamp)) return false;
     zstamp(stamp, 6, lane);
-    huf_table(L, nw, mb, lane);
+    huf_table(L, w, mb, lane);
     zstamp(stamp, 7, lane);
     *have_tree = true;
     *mb_tree = mb;
@@ -706,9 +741,9 @@ __device__ bool literals(const Lds& L, uint32_t p, uint32_t end, uint32_t cap, u
   uint32_t slo = q, shi = qend, scnt = n, sbase = 0;
   if (sf != 0) {
     if (qend - q < 10u) return *fail = kFJump, false;
-    const uint32_t s1 = L.in[q] | static_cast<uint32_t>(L.in[q + 1]) << 8;
-    const uint32_t s2 = L.in[q + 2] | static_cast<uint32_t>(L.in[q + 3]) << 8;
-    const uint32_t s3 = L.in[q + 4] | static_cast<uint32_t>(L.in[q + 5]) << 8;
+    const uint32_t s1 = ldb(L.in, q) | ldb(L.in, q + 1) << 8;
+    const uint32_t s2 = ldb(L.in, q + 2) | ldb(L.in, q + 3) << 8;
+    const uint32_t s3 = ldb(L.in, q + 4) | ldb(L.in, q + 5) << 8;
     const uint32_t a = q + 6u, b = a + s1, c = b + s2, d = c + s3;
     if (d > qend) return *fail = kFJump, false;
     const uint32_t seg = (n + 3u) >> 2;
@@ -778,7 +813,7 @@ __device__ bool seq_table(const Lds& L, uint32_t p, uint32_t end, uint32_t mode,
     *log = dlog;
   } else if (mode == 1) {
     if (p >= end) return *fail = kFRle, false;
-    const uint32_t s = L.in[p];
+    const uint32_t s = ldb(L.in, p);
     if (s > max_sym) return *fail = kFRle, false;
     if (lane == 0) table[0] = s;
     __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -828,7 +863,7 @@ __device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
   zstamp(S.stamp, 2, lane);
   uint32_t q = p + used;
   if (q >= end) return *fail = kFSeqHdr, false;
-  const uint32_t b0 = L.in[q];
+  const uint32_t b0 = ldb(L.in, q);
   uint32_t nseq;
   if (b0 == 0) {
     nseq = 0;
@@ -838,11 +873,11 @@ __device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
     q += 1;
   } else if (b0 < 255) {
     if (q + 2 > end) return *fail = kFSeqHdr, false;
-    nseq = ((b0 - 128u) << 8) + L.in[q + 1];
+    nseq = ((b0 - 128u) << 8) + ldb(L.in, q + 1);
     q += 2;
   } else {
     if (q + 3 > end) return *fail = kFSeqHdr, false;
-    nseq = L.in[q + 1] + (static_cast<uint32_t>(L.in[q + 2]) << 8) + 0x7F00u;
+    nseq = ldb(L.in, q + 1) + (ldb(L.in, q + 2) << 8) + 0x7F00u;
     q += 3;
   }
   if (nseq == 0) {
@@ -853,7 +888,7 @@ __device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
     return true;
   }
   if (q >= end) return *fail = kFSeqHdr, false;
-  const uint32_t modes = L.in[q];
+  const uint32_t modes = ldb(L.in, q);
   ++q;
   uint32_t u;
   if (!seq_table(L, q, end, modes >> 6, kPredefLL, kPredefLLLog, 35, 9, L.ll, &S.have_ll, &S.ll_log,
@@ -874,7 +909,7 @@ __device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
   uint32_t sl = br_read(r, S.ll_log), so = br_read(r, S.of_log), sm = br_read(r, S.ml_log);
   uint32_t lp = 0;
   for (uint32_t i = 0; i < nseq; ++i) {
-    const uint32_t el = L.ll[sl], eo = L.of[so], em = L.ml[sm];
+    const uint32_t el = uni(L.ll[sl]), eo = uni(L.of[so]), em = uni(L.ml[sm]);
     const uint32_t llc = el & 255u, ofc = eo & 255u, mlc = em & 255u;
     // the extra bits, offset then ML then LL, in one read when they fit
     const uint32_t mlb = kMLBits[mlc], llb = kLLBits[llc];
@@ -953,7 +988,7 @@ __device__ __forceinline__ uint64_t xxh_merge(uint64_t h, uint64_t v, uint64_t P
   return h * P1 + P4;
 }
 // (base 4-aligned; the bytes are base[o, o + n))
-__device__ uint64_t xxh64(const uint8_t* base, uint32_t o, uint32_t n) {
+__device__ __forceinline__ uint64_t xxh64(const uint8_t* base, uint32_t o, uint32_t n) {
   const uint64_t P1 = 11400714785074694791ull, P2 = 14029467366897019727ull,
                  P3 = 1609587929392839161ull, P4 = 9650029242287828579ull,
                  P5 = 2870177450012600261ull;
@@ -962,10 +997,10 @@ __device__ uint64_t xxh64(const uint8_t* base, uint32_t o, uint32_t n) {
   if (n >= 32) {
     uint64_t v1 = P1 + P2, v2 = P2, v3 = 0, v4 = 0 - P1;
     for (; i + 32 <= n; i += 32) {
-      v1 = rotl64(v1 + ld64(base, o + i) * P2, 31) * P1;
-      v2 = rotl64(v2 + ld64(base, o + i + 8) * P2, 31) * P1;
-      v3 = rotl64(v3 + ld64(base, o + i + 16) * P2, 31) * P1;
-      v4 = rotl64(v4 + ld64(base, o + i + 24) * P2, 31) * P1;
+      v1 = rotl64(v1 + ld64u(base, o + i) * P2, 31) * P1;
+      v2 = rotl64(v2 + ld64u(base, o + i + 8) * P2, 31) * P1;
+      v3 = rotl64(v3 + ld64u(base, o + i + 16) * P2, 31) * P1;
+      v4 = rotl64(v4 + ld64u(base, o + i + 24) * P2, 31) * P1;
     }
     h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
     h = xxh_merge(h, v1, P1, P2, P4);
@@ -977,16 +1012,16 @@ __device__ uint64_t xxh64(const uint8_t* base, uint32_t o, uint32_t n) {
   }
   h += n;
   for (; i + 8 <= n; i += 8) {
-    h ^= rotl64(ld64(base, o + i) * P2, 31) * P1;
+    h ^= rotl64(ld64u(base, o + i) * P2, 31) * P1;
     h = rotl64(h, 27) * P1 + P4;
   }
   if (i + 4 <= n) {
-    h ^= static_cast<uint64_t>(ld32(base, o + i)) * P1;
+    h ^= static_cast<uint64_t>(ld32u(base, o + i)) * P1;
     h = rotl64(h, 23) * P2 + P3;
     i += 4;
   }
   for (; i < n; ++i) {
-    h ^= base[o + i] * P5;
+    h ^= ldb(base, o + i) * P5;
     h = rotl64(h, 11) * P1;
   }
   h ^= h >> 33;
@@ -1002,8 +1037,11 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
   const uint32_t b = blockIdx.x;
   if (b >= a.nblocks) return;
   const uint32_t lane = threadIdx.x;
-  uint32_t n = a.src_len[b];
-  const uint8_t* src = a.src + a.src_off[b];
+  uint32_t n = uni(a.src_len[b]);
+  const uint64_t so = a.src_off[b];
+  const uint8_t* src =
+      a.src + ((static_cast<uint64_t>(uni(static_cast<uint32_t>(so >> 32))) << 32) |
+               uni(static_cast<uint32_t>(so)));
   auto finish = [&](uint32_t st, uint32_t ol, uint32_t why) {
     if (lane == 0) {
       a.status[b] = static_cast<uint8_t>(st);
@@ -1018,15 +1056,15 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
   const uint32_t kCap = a.block_mode ? LVKV_READ_CAPACITY : LVKV_SNAPPY_CAPACITY;
   const uint32_t kBig = a.block_mode ? LVKV_READ_TOO_LARGE : LVKV_SNAPPY_TOO_LARGE;
   if (a.block_mode) {  // only type-2 blocks whose checksum held (the rest are done)
-    if (src[n] != 2) return;
-    if (a.vstatus != nullptr && a.vstatus[b] != 0) return;
+    if (ldb(src, n) != 2) return;
+    if (a.vstatus != nullptr && uni(a.vstatus[b]) != 0) return;
   }
   // port::Zstd_GetUncompressedLength: ZSTD_getFrameContentSize, false on 0
   // (a skippable frame reads as 0; a malformed header as ERROR, passed on)
   uint64_t csize;
   {
-    auto rd = [&](uint32_t i) -> uint32_t { return src[i]; };
-    const uint32_t m = n >= 4 ? (src[0] | src[1] << 8 | src[2] << 16 | src[3] << 24) : 0u;
+    auto rd = [&](uint32_t i) -> uint32_t { return ldb(src, i); };
+    const uint32_t m = n >= 4 ? (rd(0) | rd(1) << 8 | rd(2) << 16 | rd(3) << 24) : 0u;
     if (n >= 4 && (m & 0xFFFFFFF0u) == 0x184D2A50u) {
       csize = n >= 8 ? 0 : ~uint64_t{1};
     } else {
@@ -1038,7 +1076,7 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
   if (a.dst_cap == nullptr)  // (unknown, malformed and > 4 GiB sizes: TOO_LARGE)
     return csize > 0xFFFFFFFFull ? finish(kBig, 0xFFFFFFFFu, kFOk)
                                  : finish(kOK, static_cast<uint32_t>(csize), kFOk);
-  const uint32_t cap = a.dst_cap[b];
+  const uint32_t cap = uni(a.dst_cap[b]);
   if (csize > cap) return finish(kCap, csize > 0xFFFFFFFFull ? 0xFFFFFFFFu : csize, kFOk);
   if (csize > a.out_cap || n > zstd_in_cap(a.out_cap)) return finish(kBig, csize, kFOk);
   const Lds L = lds_layout(smem, a.out_cap);
@@ -1052,20 +1090,22 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
   uint32_t p = 0, op = 0, fail = kFOk;
   bool ok = true;
   while (ok && p < n) {
+    p = uni(p);  // (loop-carried parser state: pinned uniform, see uni())
+    op = uni(op);
     const uint32_t rem = n - p;
     if (rem < 5) {  // (ZSTD_startingInputLength: input left over)
       ok = false;
       fail = kFTrailing;
       break;
     }
-    const uint32_t m = ld32(L.in, p);
+    const uint32_t m = ld32u(L.in, p);
     if ((m & 0xFFFFFFF0u) == 0x184D2A50u) {  // skippable frame
       if (rem < 8) {
         ok = false;
         fail = kFSkippable;
         break;
       }
-      const uint32_t sz = ld32(L.in, p + 4);
+      const uint32_t sz = ld32u(L.in, p + 4);
       if (sz > rem - 8) {
         ok = false;
         fail = kFSkippable;
@@ -1079,7 +1119,7 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
       fail = kFHeader;
       break;
     }
-    auto rd = [&](uint32_t i) -> uint32_t { return L.in[p + i]; };
+    auto rd = [&](uint32_t i) -> uint32_t { return ldb(L.in, p + i); };
     const Frame f = frame_header(rd, rem);
     if (!f.ok) {
       ok = false;
@@ -1099,13 +1139,14 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
     S.rep1 = 4;
     S.rep2 = 8;
     for (;;) {
+      q = uni(q);
+      op = uni(op);
       if (q + 3 > n) {
         ok = false;
         fail = kFBlockHdr;
         break;
       }
-      const uint32_t bh = L.in[q] | static_cast<uint32_t>(L.in[q + 1]) << 8 |
-                          static_cast<uint32_t>(L.in[q + 2]) << 16;
+      const uint32_t bh = ldb(L.in, q) | ldb(L.in, q + 1) << 8 | ldb(L.in, q + 2) << 16;
       q += 3;
       const uint32_t last = bh & 1u, btype = (bh >> 1) & 3u, bsize = bh >> 3;
       if (btype == 3) {
@@ -1124,7 +1165,7 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
           fail = kFCap;
           break;
         }
-        const uint8_t v = L.in[q];
+        const uint8_t v = static_cast<uint8_t>(ldb(L.in, q));
         for (uint32_t k = lane; k < bsize; k += 64) L.out[op + k] = v;
         op += bsize;
         q += 1;
@@ -1175,7 +1216,7 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
         fail = kFChecksum;
         break;
       }
-      const uint32_t want = ld32(L.in, q);
+      const uint32_t want = ld32u(L.in, q);
       if (static_cast<uint32_t>(xxh64(L.out, start, op - start)) != want) {
         ok = false;
         fail = kFChecksum;
