@@ -74,30 +74,17 @@ __device__ __forceinline__ void stage(uint8_t* dst, const uint8_t* src, uint32_t
 }
 
 // ---- backward bitstreams (RFC 8878 §4.1.1.1) ------------------------------
-// Bits [0, pos) of the stream, read from the top down; bits below 0 read as
-// zeros. A 64-bit window of the staged bytes is cached in registers.
+// Bits [0, pos) of a stream, read from the top down; bits below 0 read as
+// zeros. BitR: one lane's reader (a Huffman stream segment), a 64-bit window
+// of the staged bytes cached in its registers.
 struct BitR {
   const uint8_t* in;  // staged frame (4-aligned)
   uint32_t start;     // the stream's first byte in `in`
-  int32_t pos;        // bits left
   int32_t cb;         // window's first byte (relative), or -1
   uint64_t win;
 };
 
-__device__ __forceinline__ bool br_init(BitR& r, const uint8_t* in, uint32_t lo, uint32_t hi) {
-  r.in = in;
-  r.start = lo;
-  r.cb = -1;
-  r.win = 0;
-  if (hi <= lo) return false;
-  const uint32_t last = ldb(in, hi - 1);
-  if (last == 0) return false;
-  r.pos = static_cast<int32_t>(8u * (hi - lo - 1u) + (31u - __builtin_clz(last)));
-  return true;
-}
-
-// bits [p, p + n) (n <= 32), zeros below 0 (U: the reader is wave-uniform)
-template <bool U = true>
+// bits [p, p + n) (n <= 32), zeros below 0
 __device__ __forceinline__ uint32_t br_bits(BitR& r, int32_t p, uint32_t n) {
   const int32_t top = p + static_cast<int32_t>(n);
   if (n == 0 || top <= 0) return 0;
@@ -106,34 +93,53 @@ __device__ __forceinline__ uint32_t br_bits(BitR& r, int32_t p, uint32_t n) {
     int32_t cb = ((top + 7) >> 3) - 8;
     if (cb < 0) cb = 0;
     r.cb = cb;
-    r.win = U ? ld64u(r.in, r.start + static_cast<uint32_t>(cb))
-              : ld64(r.in, r.start + static_cast<uint32_t>(cb));
+    r.win = ld64(r.in, r.start + static_cast<uint32_t>(cb));
   }
   uint64_t v = r.win >> (lo - 8 * r.cb);
   v &= (uint64_t{1} << (top - lo)) - 1u;
   return static_cast<uint32_t>(v << (lo - p));
 }
 
-__device__ __forceinline__ uint32_t br_read(BitR& r, uint32_t n) {
-  r.pos -= static_cast<int32_t>(n);
-  return br_bits(r, r.pos, n);
+// The sequences' bitstream, read by the scalar unit from a window of 248
+// staged bytes held a dword a lane and reloaded from LDS when a read leaves
+// it (about every 60 sequences): a read is two v_readlane and a 64-bit
+// shift, with no LDS round trip to wait on. Bits below the stream's start
+// read as zeros (the window's lanes there hold zeros).
+struct RegBits {
+  const uint8_t* in;
+  uint32_t start;  // the stream's first byte in `in`
+  int32_t pos;     // bits left
+  int32_t wlo;     // the window's first bit (stream-relative, a multiple of 32)
+  uint32_t d;      // lane k: the stream's bits [wlo + 32 k, wlo + 32 k + 32)
+};
+__device__ __forceinline__ void rb_load(RegBits& r, int32_t top, uint32_t lane) {
+  r.wlo = ((top + 31) & ~31) - 1984;  // top - wlo <= 2015: lanes q >> 5 and + 1 <= 63
+  const int32_t b = (r.wlo >> 3) + 4 * static_cast<int32_t>(lane);
+  r.d = b < 0 ? 0u : ld32(r.in, r.start + static_cast<uint32_t>(b));
+  __builtin_amdgcn_s_waitcnt(0xc07f);
 }
-
-// n <= 56 bits at once (the window always holds 57 below its top)
-__device__ __forceinline__ uint64_t br_read64(BitR& r, uint32_t n) {
+// false: no end marker (br_init)
+__device__ __forceinline__ bool rb_init(RegBits& r, const uint8_t* in, uint32_t lo, uint32_t hi,
+                                        uint32_t lane) {
+  r.in = in;
+  r.start = lo;
+  if (hi <= lo) return false;
+  const uint32_t last = ldb(in, hi - 1);
+  if (last == 0) return false;
+  r.pos = static_cast<int32_t>(8u * (hi - lo - 1u) + (31u - __builtin_clz(last)));
+  rb_load(r, r.pos, lane);
+  return true;
+}
+// n <= 32 bits
+__device__ __forceinline__ uint32_t rb_read(RegBits& r, uint32_t n, uint32_t lane) {
   r.pos -= static_cast<int32_t>(n);
-  const int32_t p = r.pos, top = p + static_cast<int32_t>(n);
-  if (n == 0 || top <= 0) return 0;
-  const int32_t lo = p < 0 ? 0 : p;
-  if (r.cb < 0 || lo < 8 * r.cb || top > 8 * r.cb + 64) {
-    int32_t cb = ((top + 7) >> 3) - 8;
-    if (cb < 0) cb = 0;
-    r.cb = cb;
-    r.win = ld64u(r.in, r.start + static_cast<uint32_t>(cb));
-  }
-  uint64_t v = r.win >> (lo - 8 * r.cb);
-  v &= (uint64_t{1} << (top - lo)) - 1u;
-  return v << (lo - p);
+  if (r.pos < r.wlo) rb_load(r, r.pos + static_cast<int32_t>(n), lane);
+  const uint32_t q = static_cast<uint32_t>(r.pos - r.wlo);
+  // (readlane returns int: widen through uint32_t, not by sign)
+  const uint32_t w0 = __builtin_amdgcn_readlane(r.d, q >> 5);
+  const uint32_t w1 = __builtin_amdgcn_readlane(r.d, (q >> 5) + 1u);
+  const uint64_t x = (static_cast<uint64_t>(w1) << 32) | w0;
+  return static_cast<uint32_t>((x >> (q & 31u)) & ((uint64_t{1} << n) - 1u));
 }
 
 // ---- FSE tables (RFC 8878 §4.1; FSE_readNCount / FSE_buildDTable) --------
@@ -594,7 +600,7 @@ __device__ __forceinline__ int32_t huf_run(const Lds& L, uint32_t lo, int32_t po
       }
       idx = static_cast<uint32_t>(win >> (p - wlo)) & mask;
     } else {
-      idx = br_bits<false>(r, p, mb);  // bits below the start read as zeros
+      idx = br_bits(r, p, mb);  // bits below the start read as zeros
     }
     const uint32_t e = L.huf[idx];
     pos -= static_cast<int32_t>(e >> 8);
@@ -835,6 +841,10 @@ __device__ bool seq_table(const Lds& L, uint32_t p, uint32_t end, uint32_t mode,
 
 struct SeqState {
   uint64_t* stamp;  // probe stamps of this frame, or nullptr
+  // the LL / ML codes' baselines and extra bits, lane c holding code c's
+  // (base | bits << 24): a v_readlane a sequence instead of constant-memory
+  // loads (the u8 bit counts would be vector loads, waited on each time)
+  uint32_t llcode, mlcode;
   bool have_ll, have_of, have_ml, have_tree;
   uint32_t ll_log, of_log, ml_log, mb_tree;
   uint32_t rep0, rep1, rep2;
@@ -904,29 +914,38 @@ __device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
     return false;
   q += u;
   zstamp(S.stamp, 3, lane);
-  BitR r;
-  if (!br_init(r, L.in, q, end)) return *fail = kFSeqBits, false;
-  uint32_t sl = br_read(r, S.ll_log), so = br_read(r, S.of_log), sm = br_read(r, S.ml_log);
+  RegBits r;
+  if (!rb_init(r, L.in, q, end, lane)) return *fail = kFSeqBits, false;
+  // tables of <= 64 entries (the predefined ones, RLE, small FSE) are read
+  // from registers (v_readlane), larger ones from LDS
+  const bool sll = S.ll_log <= 6u, sof = S.of_log <= 6u, sml = S.ml_log <= 6u;
+  const uint32_t tll = L.ll[lane], tof = L.of[lane], tml = L.ml[lane];
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  auto entry = [&](bool small, uint32_t reg, const uint32_t* t, uint32_t s) -> uint32_t {
+    uint32_t e;
+    if (small)
+      e = __builtin_amdgcn_readlane(reg, s);
+    else
+      e = uni(t[s]);
+    return e;
+  };
+  uint32_t sl = rb_read(r, S.ll_log, lane), so = rb_read(r, S.of_log, lane),
+           sm = rb_read(r, S.ml_log, lane);
   uint32_t lp = 0;
   for (uint32_t i = 0; i < nseq; ++i) {
-    const uint32_t el = uni(L.ll[sl]), eo = uni(L.of[so]), em = uni(L.ml[sm]);
+    const uint32_t el = entry(sll, tll, L.ll, sl), eo = entry(sof, tof, L.of, so),
+                   em = entry(sml, tml, L.ml, sm);
     const uint32_t llc = el & 255u, ofc = eo & 255u, mlc = em & 255u;
-    // the extra bits, offset then ML then LL, in one read when they fit
-    const uint32_t mlb = kMLBits[mlc], llb = kLLBits[llc];
-    uint32_t ofx, mlx, llx;
-    if (ofc + mlb + llb <= 56u) {
-      const uint64_t v = br_read64(r, ofc + mlb + llb);
-      llx = static_cast<uint32_t>(v) & ((1u << llb) - 1u);
-      mlx = static_cast<uint32_t>(v >> llb) & ((1u << mlb) - 1u);
-      ofx = static_cast<uint32_t>(v >> (llb + mlb));
-    } else {
-      ofx = br_read(r, ofc);
-      mlx = br_read(r, mlb);
-      llx = br_read(r, llb);
-    }
+    const uint32_t lc = __builtin_amdgcn_readlane(S.llcode, llc);
+    const uint32_t mc = __builtin_amdgcn_readlane(S.mlcode, mlc);
+    const uint32_t mlb = mc >> 24, llb = lc >> 24;
+    // the extra bits: offset, then ML and LL in one read (<= 16 + 16)
+    const uint32_t ofx = rb_read(r, ofc, lane);
+    const uint32_t mlx_llx = rb_read(r, mlb + llb, lane);
+    const uint32_t llx = mlx_llx & ((1u << llb) - 1u), mlx = mlx_llx >> llb;
     const uint32_t ofv = (1u << ofc) + ofx;
-    const uint32_t ml = kMLBase[mlc] + mlx;
-    const uint32_t ll = kLLBase[llc] + llx;
+    const uint32_t ml = (mc & 0xFFFFFFu) + mlx;
+    const uint32_t ll = (lc & 0xFFFFFFu) + llx;
     uint32_t off;
     if (ofv > 3u) {
       off = ofv - 3u;
@@ -957,7 +976,7 @@ __device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
     // the states, LL then ML then OF (also after the last sequence)
     {  // (<= 9 + 9 + 8 bits: one read)
       const uint32_t nl = (el >> 8) & 255u, nm = (em >> 8) & 255u, no = (eo >> 8) & 255u;
-      const uint32_t v = static_cast<uint32_t>(br_read64(r, nl + nm + no));
+      const uint32_t v = rb_read(r, nl + nm + no, lane);
       sl = (el >> 16) + (v >> (nm + no));
       sm = (em >> 16) + ((v >> no) & ((1u << nm) - 1u));
       so = (eo >> 16) + (v & ((1u << no) - 1u));
@@ -1063,7 +1082,16 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
   // (a skippable frame reads as 0; a malformed header as ERROR, passed on)
   uint64_t csize;
   {
-    auto rd = [&](uint32_t i) -> uint32_t { return ldb(src, i); };
+    // the first 24 bytes (a frame header is at most 18) in one round of
+    // aligned dword loads, lanes 0-6; read back by v_readlane, not by a
+    // chain of dependent byte loads from global memory
+    const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src)) & 3u;
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src - mis);
+    const uint32_t hd = lane < 7u && 4u * lane < mis + n ? s32[lane] : 0u;
+    auto rd = [&](uint32_t i) -> uint32_t {  // byte i < min(n, 24)
+      const uint32_t q = i + mis;
+      return (static_cast<uint32_t>(__builtin_amdgcn_readlane(hd, q >> 2)) >> (8u * (q & 3u))) & 255u;
+    };
     const uint32_t m = n >= 4 ? (rd(0) | rd(1) << 8 | rd(2) << 16 | rd(3) << 24) : 0u;
     if (n >= 4 && (m & 0xFFFFFFF0u) == 0x184D2A50u) {
       csize = n >= 8 ? 0 : ~uint64_t{1};
@@ -1082,6 +1110,8 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
   const Lds L = lds_layout(smem, a.out_cap);
   uint64_t* stamp = a.stamps != nullptr ? a.stamps + 16u * b : nullptr;
   zstamp(stamp, 0, lane);
+  const uint32_t llcode = lane < 36u ? kLLBase[lane] | static_cast<uint32_t>(kLLBits[lane]) << 24 : 0u;
+  const uint32_t mlcode = lane < 53u ? kMLBase[lane] | static_cast<uint32_t>(kMLBits[lane]) << 24 : 0u;
   stage(L.in, src, n, 16, lane);
   __builtin_amdgcn_s_waitcnt(0);
   zstamp(stamp, 1, lane);
@@ -1135,6 +1165,8 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
     const uint32_t start = op;
     SeqState S{};
     S.stamp = stamp;
+    S.llcode = llcode;
+    S.mlcode = mlcode;
     S.rep0 = 1;
     S.rep1 = 4;
     S.rep2 = 8;
