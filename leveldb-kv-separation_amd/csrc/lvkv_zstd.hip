@@ -10,9 +10,10 @@
 // One wave per frame (64-thread workgroups), the frame staged in LDS. The
 // frame is a chain (headers, a Huffman tree, FSE tables, backward
 // bitstreams, sequences whose matches read earlier output), so control flow
-// is wave-uniform; the lanes copy literals and matches, fill decode tables,
-// and decode the four Huffman streams of a block side by side (lanes 0-3,
-// each with its own bit reader).
+// is wave-uniform and the serial chains run on the scalar unit from
+// registers (uni(), RegBits); the lanes build the decode tables, decode the
+// Huffman streams in self-synchronising segments, and copy literals and
+// matches.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -861,80 +862,30 @@ __device__ __forceinline__ void lds_copy(uint8_t* dst, const uint8_t* from, uint
   }
 }
 
-// A compressed block at in[p, end): output appended at out[*op, ...).
-__device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
-                           uint32_t frame_start, uint32_t cap, SeqState& S, uint32_t lane,
-                           uint32_t* fail) {
-  uint32_t nlit, used;
-  if (!literals(L, p, end, cap - *op, L.out + cap, &S.have_tree, &S.mb_tree, &nlit, &used, lane,
-                fail, S.stamp))
-    return false;
-  const uint8_t* lits = L.out + (cap - nlit);
-  zstamp(S.stamp, 2, lane);
-  uint32_t q = p + used;
-  if (q >= end) return *fail = kFSeqHdr, false;
-  const uint32_t b0 = ldb(L.in, q);
-  uint32_t nseq;
-  if (b0 == 0) {
-    nseq = 0;
-    q += 1;
-  } else if (b0 < 128) {
-    nseq = b0;
-    q += 1;
-  } else if (b0 < 255) {
-    if (q + 2 > end) return *fail = kFSeqHdr, false;
-    nseq = ((b0 - 128u) << 8) + ldb(L.in, q + 1);
-    q += 2;
-  } else {
-    if (q + 3 > end) return *fail = kFSeqHdr, false;
-    nseq = ldb(L.in, q + 1) + (ldb(L.in, q + 2) << 8) + 0x7F00u;
-    q += 3;
-  }
-  if (nseq == 0) {
-    if (q != end) return *fail = kFSeqHdr, false;
-    if (nlit > cap - *op) return *fail = kFCap, false;
-    lds_copy(L.out + *op, lits, nlit, 0, lane);
-    *op += nlit;
-    return true;
-  }
-  if (q >= end) return *fail = kFSeqHdr, false;
-  const uint32_t modes = ldb(L.in, q);
-  ++q;
-  uint32_t u;
-  if (!seq_table(L, q, end, modes >> 6, kPredefLL, kPredefLLLog, 35, 9, L.ll, &S.have_ll, &S.ll_log,
-                 &u, lane, fail))
-    return false;
-  q += u;
-  if (!seq_table(L, q, end, (modes >> 4) & 3u, kPredefOF, kPredefOFLog, 31, 8, L.of, &S.have_of,
-                 &S.of_log, &u, lane, fail))
-    return false;
-  q += u;
-  if (!seq_table(L, q, end, (modes >> 2) & 3u, kPredefML, kPredefMLLog, 52, 9, L.ml, &S.have_ml,
-                 &S.ml_log, &u, lane, fail))
-    return false;
-  q += u;
-  zstamp(S.stamp, 3, lane);
-  RegBits r;
-  if (!rb_init(r, L.in, q, end, lane)) return *fail = kFSeqBits, false;
-  // tables of <= 64 entries (the predefined ones, RLE, small FSE) are read
-  // from registers (v_readlane), larger ones from LDS
-  const bool sll = S.ll_log <= 6u, sof = S.of_log <= 6u, sml = S.ml_log <= 6u;
-  const uint32_t tll = L.ll[lane], tof = L.of[lane], tml = L.ml[lane];
-  __builtin_amdgcn_s_waitcnt(0xc07f);
+// The block's tables as the sequence loop reads them: the first 64 entries
+// in registers, and which tables fit there.
+struct Tabs {
+  uint32_t ll, of, ml;
+  bool sll, sof, sml;
+};
+
+// The nseq sequences of a block (RFC 8878 §3.1.1.4-5): decode, execute, and
+// the literals left after the last. Small: every table fits in registers.
+template <bool Small>
+__device__ __forceinline__ bool sequences(const Lds& L, RegBits& r, SeqState& S, const Tabs& T,
+                                          uint32_t nseq, uint32_t nlit, const uint8_t* lits,
+                                          uint32_t* op, uint32_t frame_start, uint32_t cap,
+                                          uint32_t lane, uint32_t* fail) {
   auto entry = [&](bool small, uint32_t reg, const uint32_t* t, uint32_t s) -> uint32_t {
-    uint32_t e;
-    if (small)
-      e = __builtin_amdgcn_readlane(reg, s);
-    else
-      e = uni(t[s]);
-    return e;
+    if (Small || small) return __builtin_amdgcn_readlane(reg, s);
+    return uni(t[s]);
   };
   uint32_t sl = rb_read(r, S.ll_log, lane), so = rb_read(r, S.of_log, lane),
            sm = rb_read(r, S.ml_log, lane);
   uint32_t lp = 0;
   for (uint32_t i = 0; i < nseq; ++i) {
-    const uint32_t el = entry(sll, tll, L.ll, sl), eo = entry(sof, tof, L.of, so),
-                   em = entry(sml, tml, L.ml, sm);
+    const uint32_t el = entry(T.sll, T.ll, L.ll, sl), eo = entry(T.sof, T.of, L.of, so),
+                   em = entry(T.sml, T.ml, L.ml, sm);
     const uint32_t llc = el & 255u, ofc = eo & 255u, mlc = em & 255u;
     const uint32_t lc = __builtin_amdgcn_readlane(S.llcode, llc);
     const uint32_t mc = __builtin_amdgcn_readlane(S.mlcode, mlc);
@@ -997,6 +948,74 @@ __device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
   lds_copy(L.out + *op, lits + lp, rest, 0, lane);
   *op += rest;
   return true;
+}
+
+
+// A compressed block at in[p, end): output appended at out[*op, ...).
+__device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
+                           uint32_t frame_start, uint32_t cap, SeqState& S, uint32_t lane,
+                           uint32_t* fail) {
+  uint32_t nlit, used;
+  if (!literals(L, p, end, cap - *op, L.out + cap, &S.have_tree, &S.mb_tree, &nlit, &used, lane,
+                fail, S.stamp))
+    return false;
+  const uint8_t* lits = L.out + (cap - nlit);
+  zstamp(S.stamp, 2, lane);
+  uint32_t q = p + used;
+  if (q >= end) return *fail = kFSeqHdr, false;
+  const uint32_t b0 = ldb(L.in, q);
+  uint32_t nseq;
+  if (b0 == 0) {
+    nseq = 0;
+    q += 1;
+  } else if (b0 < 128) {
+    nseq = b0;
+    q += 1;
+  } else if (b0 < 255) {
+    if (q + 2 > end) return *fail = kFSeqHdr, false;
+    nseq = ((b0 - 128u) << 8) + ldb(L.in, q + 1);
+    q += 2;
+  } else {
+    if (q + 3 > end) return *fail = kFSeqHdr, false;
+    nseq = ldb(L.in, q + 1) + (ldb(L.in, q + 2) << 8) + 0x7F00u;
+    q += 3;
+  }
+  if (nseq == 0) {
+    if (q != end) return *fail = kFSeqHdr, false;
+    if (nlit > cap - *op) return *fail = kFCap, false;
+    lds_copy(L.out + *op, lits, nlit, 0, lane);
+    *op += nlit;
+    return true;
+  }
+  if (q >= end) return *fail = kFSeqHdr, false;
+  const uint32_t modes = ldb(L.in, q);
+  ++q;
+  uint32_t u;
+  if (!seq_table(L, q, end, modes >> 6, kPredefLL, kPredefLLLog, 35, 9, L.ll, &S.have_ll, &S.ll_log,
+                 &u, lane, fail))
+    return false;
+  q += u;
+  if (!seq_table(L, q, end, (modes >> 4) & 3u, kPredefOF, kPredefOFLog, 31, 8, L.of, &S.have_of,
+                 &S.of_log, &u, lane, fail))
+    return false;
+  q += u;
+  if (!seq_table(L, q, end, (modes >> 2) & 3u, kPredefML, kPredefMLLog, 52, 9, L.ml, &S.have_ml,
+                 &S.ml_log, &u, lane, fail))
+    return false;
+  q += u;
+  zstamp(S.stamp, 3, lane);
+  RegBits r;
+  if (!rb_init(r, L.in, q, end, lane)) return *fail = kFSeqBits, false;
+  // tables of <= 64 entries (the predefined ones, RLE, small FSE: a small
+  // block's) are read from registers (v_readlane), larger ones from LDS; the
+  // loop is built twice so that the common all-small case carries no
+  // per-table branch (and no flags to spill)
+  const uint32_t tll = L.ll[lane], tof = L.of[lane], tml = L.ml[lane];
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  const Tabs T{tll, tof, tml, S.ll_log <= 6u, S.of_log <= 6u, S.ml_log <= 6u};
+  if (T.sll && T.sof && T.sml)
+    return sequences<true>(L, r, S, T, nseq, nlit, lits, op, frame_start, cap, lane, fail);
+  return sequences<false>(L, r, S, T, nseq, nlit, lits, op, frame_start, cap, lane, fail);
 }
 
 // XXH64 of out[0, n) (seed 0): the frame checksum. Scalar, from LDS.
