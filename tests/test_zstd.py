@@ -275,3 +275,74 @@ def test_predefined_tables_header_matches_oracle():
         got = [int(x.strip().rstrip("u"), 16) for x in m.group(1).split(",")]
         assert got == [s | (nb << 8) | (b << 16) for s, nb, b in table]
         assert f"kPredef{name}Log = {log};" in text
+
+
+# ---- multi-block frames (tests/golden/gen_zstd_stream.py) -----------------
+
+@pytest.fixture(scope="module")
+def sfx():
+    spec = json.loads((GOLDEN / "zstd_stream.json").read_text())
+    ins = _split((GOLDEN / "zstd_stream_inputs.bin").read_bytes(), spec["inputs"])
+    frames = _split((GOLDEN / "zstd_stream_frames.bin").read_bytes(), spec["frames"])
+    return ins, frames, spec
+
+
+def test_oracle_decodes_streamed_frames(sfx):
+    """Frames of several small blocks (a flush every 1-4 KiB): the later
+    blocks reuse the earlier one's Huffman tree (treeless literals) and FSE
+    tables (repeat mode), carry repeat offsets and reach back into earlier
+    blocks' output."""
+    ins, frames, spec = sfx
+    assert spec["counts"]["treeless"] > 100 and spec["counts"]["fse_repeat"] > 10
+    assert min(m[4] for m in spec["meta"]) >= 2
+    for f, m in zip(frames, spec["meta"]):
+        x = ins[m[0]]
+        assert zo.get_uncompressed_length(f) == len(x)
+        ok, got = zo.uncompress(f)
+        assert ok and got == x, m
+    lib = zo.system_zstd()
+    if lib is not None:
+        for f, m in zip(frames, spec["meta"]):
+            assert zo.lib_uncompress(lib, f) == (True, ins[m[0]])
+
+
+@pytest.mark.gpu
+def test_device_decodes_streamed_frames(lvkv, gpu, sfx):
+    import torch
+    ins, frames, spec = sfx
+    src, off, ln = _pack(torch, gpu, frames, skew=1)
+    dst, doff, dlen, st, why = lvkv.zstd_uncompress(src, off, ln, max_ulen=lvkv.SNAPPY_MAX_BLOCK,
+                                                    detail=True)
+    torch.cuda.synchronize()
+    st, why = st.cpu().tolist(), why.cpu().tolist()
+    got = _unpack(dst, doff, dlen)
+    for k, m in enumerate(spec["meta"]):
+        assert st[k] == lvkv.SNAPPY_OK, (k, m, st[k], why[k])
+        assert got[k] == ins[m[0]], (k, m)
+
+
+@pytest.mark.gpu
+def test_device_streamed_frames_damaged_against_oracle(lvkv, gpu, sfx):
+    """Bytes flipped in the multi-block frames: the device's verdict and bytes
+    are the oracle's (damage in a later block lands in the repeat paths)."""
+    import torch
+    _, frames, _ = sfx
+    rng = np.random.default_rng(77)
+    cap = lvkv.SNAPPY_MAX_BLOCK
+    blobs = []
+    for k in range(1500):
+        d = bytearray(frames[k % len(frames)])
+        for _ in range(int(rng.integers(1, 3))):
+            d[int(rng.integers(6, len(d)))] ^= 1 << int(rng.integers(0, 8))
+        blobs.append(bytes(d))
+    src, off, ln = _pack(torch, gpu, blobs, skew=2)
+    dst, doff, dlen, st, why = lvkv.zstd_uncompress(src, off, ln, max_ulen=cap, detail=True)
+    torch.cuda.synchronize()
+    st, why = st.cpu().tolist(), why.cpu().tolist()
+    got = _unpack(dst, doff, dlen)
+    for k, b in enumerate(blobs):
+        ok, want = zo.uncompress(b)
+        want_st = _want(lvkv, b, cap, ok=ok)
+        assert st[k] == want_st, (k, st[k], want_st, why[k])
+        if want_st == lvkv.SNAPPY_OK:
+            assert got[k] == want, k
