@@ -76,30 +76,8 @@ __device__ __forceinline__ void stage(uint8_t* dst, const uint8_t* src, uint32_t
 
 // ---- backward bitstreams (RFC 8878 §4.1.1.1) ------------------------------
 // Bits [0, pos) of a stream, read from the top down; bits below 0 read as
-// zeros. BitR: one lane's reader (a Huffman stream segment), a 64-bit window
-// of the staged bytes cached in its registers.
-struct BitR {
-  const uint8_t* in;  // staged frame (4-aligned)
-  uint32_t start;     // the stream's first byte in `in`
-  int32_t cb;         // window's first byte (relative), or -1
-  uint64_t win;
-};
-
-// bits [p, p + n) (n <= 32), zeros below 0
-__device__ __forceinline__ uint32_t br_bits(BitR& r, int32_t p, uint32_t n) {
-  const int32_t top = p + static_cast<int32_t>(n);
-  if (n == 0 || top <= 0) return 0;
-  const int32_t lo = p < 0 ? 0 : p;
-  if (r.cb < 0 || lo < 8 * r.cb || top > 8 * r.cb + 64) {
-    int32_t cb = ((top + 7) >> 3) - 8;
-    if (cb < 0) cb = 0;
-    r.cb = cb;
-    r.win = ld64(r.in, r.start + static_cast<uint32_t>(cb));
-  }
-  uint64_t v = r.win >> (lo - 8 * r.cb);
-  v &= (uint64_t{1} << (top - lo)) - 1u;
-  return static_cast<uint32_t>(v << (lo - p));
-}
+// zeros. The Huffman lanes cache a 64-bit window each (huf_run); the wave's
+// scalar readers use a register-held window (RegBits).
 
 // The sequences' bitstream, read by the scalar unit from a window of 248
 // staged bytes held a dword a lane and reloaded from LDS when a read leaves
@@ -584,25 +562,19 @@ __device__ __forceinline__ int32_t huf_run(const Lds& L, uint32_t lo, int32_t po
   int32_t wlo = 0x7fffffff;
   uint64_t win = 0;
   const uint32_t mask = (1u << mb) - 1u;
-  BitR r;
-  r.in = L.in;
-  r.start = lo;
-  r.cb = -1;
   uint32_t c = 0;
   while (pos > floor) {
     const int32_t p = pos - static_cast<int32_t>(mb);
-    uint32_t idx;
-    if (p >= 0) {
-      if (p < wlo) {
-        int32_t cb = ((pos + 7) >> 3) - 8;
-        if (cb < 0) cb = 0;
-        wlo = 8 * cb;
-        win = ld64(L.in, lo + static_cast<uint32_t>(cb));
-      }
-      idx = static_cast<uint32_t>(win >> (p - wlo)) & mask;
-    } else {
-      idx = br_bits(r, p, mb);  // bits below the start read as zeros
+    // the window holds bits [wlo, wlo + 64); near the stream's start (p < 0)
+    // it is the first 64 bits and the index shifts up, zeros below bit 0
+    if (p < wlo && wlo > 0) {
+      int32_t cb = ((pos + 7) >> 3) - 8;
+      if (cb < 0) cb = 0;
+      wlo = 8 * cb;
+      win = ld64(L.in, lo + static_cast<uint32_t>(cb));
     }
+    const int32_t d = p - wlo;
+    const uint32_t idx = static_cast<uint32_t>(d >= 0 ? win >> d : win << -d) & mask;
     const uint32_t e = L.huf[idx];
     pos -= static_cast<int32_t>(e >> 8);
     if (dst != nullptr && c < lim) dst[c] = static_cast<uint8_t>(e & 255u);
