@@ -564,21 +564,26 @@ __device__ __forceinline__ int32_t huf_run(const Lds& L, uint32_t lo, int32_t po
   const uint32_t mask = (1u << mb) - 1u;
   uint32_t c = 0;
   while (pos > floor) {
-    const int32_t p = pos - static_cast<int32_t>(mb);
-    // the window holds bits [wlo, wlo + 64); near the stream's start (p < 0)
-    // it is the first 64 bits and the index shifts up, zeros below bit 0
-    if (p < wlo && wlo > 0) {
+    // the window holds bits [wlo, wlo + 64): refilled so that it covers the
+    // next four symbols (<= 44 bits); near the stream's start it is the
+    // first 64 bits and an index below bit 0 shifts up, zeros below
+    if (pos - 4 * static_cast<int32_t>(mb) < wlo && wlo > 0) {
       int32_t cb = ((pos + 7) >> 3) - 8;
       if (cb < 0) cb = 0;
       wlo = 8 * cb;
       win = ld64(L.in, lo + static_cast<uint32_t>(cb));
     }
-    const int32_t d = p - wlo;
-    const uint32_t idx = static_cast<uint32_t>(d >= 0 ? win >> d : win << -d) & mask;
-    const uint32_t e = L.huf[idx];
-    pos -= static_cast<int32_t>(e >> 8);
-    if (dst != nullptr && c < lim) dst[c] = static_cast<uint8_t>(e & 255u);
-    ++c;
+    // four symbols without a branch: a lane past its floor reads and drops
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool live = pos > floor;
+      const int32_t d = pos - static_cast<int32_t>(mb) - wlo;
+      const uint32_t idx = static_cast<uint32_t>(d >= 0 ? win >> d : win << -d) & mask;
+      const uint32_t e = L.huf[idx];
+      if (dst != nullptr && live && c < lim) dst[c] = static_cast<uint8_t>(e & 255u);
+      pos -= live ? static_cast<int32_t>(e >> 8) : 0;
+      c += live ? 1u : 0u;
+    }
   }
   *count = c;
   return pos;
