@@ -1,3 +1,7 @@
+"""Prints the Zstd decoder's verdict and failure site for every fixture frame
+(tests/golden/zstd_*), at capacities 4096 and 49152, through the debug
+entry (zstd_uncompress(detail=True)). A GPU-box debugging aid, not a test.
+"""
 import json, sys, numpy as np, torch
 from pathlib import Path
 sys.path.insert(0, "/root/repo")
