@@ -25,6 +25,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "lvkv_zstd.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -88,38 +90,13 @@ int lvkv_snappy_uncompress_device(const void* d_src, const uint64_t* d_src_off,
                                   uint32_t* d_out_len, uint8_t* d_status, size_t nblocks,
                                   uint32_t max_ulen, void* stream);
 
-/* ---- Zstd frames (the read side of kZstdCompression) --------------------- */
-
-/*
- * port::Zstd_GetUncompressedLength (port/port_stdcxx.h:163-177) over a batch:
- * d_ulen[i] = ZSTD_getFrameContentSize of stream i, d_status[i] =
- * LVKV_SNAPPY_OK, LVKV_SNAPPY_BAD_LENGTH (the size is 0: an empty frame or a
- * skippable one) or LVKV_SNAPPY_TOO_LARGE (unknown, malformed, or past
- * 32 bits; d_ulen = 0xffffffff).
- */
-int lvkv_zstd_uncompressed_length_device(const void* d_src, const uint64_t* d_src_off,
-                                         const uint32_t* d_src_len, uint32_t* d_ulen,
-                                         uint8_t* d_status, size_t nblocks, void* stream);
-
-/*
- * port::Zstd_Uncompress (port/port_stdcxx.h:179-199) over a batch: stream i
- * decoded as ZSTD_decompressDCtx does (libzstd 1.4.9; frames one after
- * another, skippable frames skipped, checksums verified) into exactly its
- * content size at d_dst[d_dst_off[i], + d_dst_cap[i]). Statuses as
- * lvkv_snappy_uncompress_device: OK, BAD_LENGTH (content size 0), BAD_CONTENTS
- * (any ZSTD_isError), CAPACITY (content size past d_dst_cap[i], or unknown),
- * TOO_LARGE (past max_ulen, or a stream longer than ZSTD_compressBound of
- * it). max_ulen <= LVKV_SNAPPY_MAX_BLOCK. No compressor: zstd's bytes come
- * from its match finder and entropy heuristics (the host library's).
- */
-int lvkv_zstd_uncompress_device(const void* d_src, const uint64_t* d_src_off,
-                                const uint32_t* d_src_len, void* d_dst, const uint64_t* d_dst_off,
-                                const uint32_t* d_dst_cap, uint32_t* d_out_len, uint8_t* d_status,
-                                size_t nblocks, uint32_t max_ulen, void* stream);
+/* ---- Zstd: include/lvkv_zstd.h (its entry points moved there in round 6; the
+ * LVKV_SNAPPY_* status names stay valid for zstd calls: LVKV_ZSTD_* has the
+ * same values) ---------------------------------------------------------- */
 
 /* ---- the block writer and reader around the codec ----------------------- */
 
-/* Scratch for lvkv_sst_write_blocks_device with compression 1. */
+/* Scratch for lvkv_sst_write_blocks_device with compression 1 or 2. */
 size_t lvkv_sst_write_scratch_bytes(size_t nblocks, uint32_t max_len);
 
 /*
@@ -127,13 +104,15 @@ size_t lvkv_sst_write_scratch_bytes(size_t nblocks, uint32_t max_len);
  * (table/table_builder.cc:141-209): block i = d_raw[d_raw_off[i], +
  * d_raw_len[i]) (each at most max_len bytes), written in order from file
  * offset `file_offset` of d_file (the image of the file; d_file[0] is file
- * offset 0): with compression 1 (kSnappyCompression) the snappy form when it
- * is smaller than raw - raw/8, else raw with type 0; the type byte; the
+ * offset 0): with compression 1 (kSnappyCompression) or 2
+ * (kZstdCompression, at zstd_compression_level 1) the compressed form when
+ * it is smaller than raw - raw/8, else raw with type 0; the type byte; the
  * masked CRC32C of contents + type (the batch CRC kernel). d_handle_off /
  * d_handle_size = the BlockHandles, d_type = the kept type, d_end[0] = the
  * file offset after the last trailer (Rep::offset). compression 0 writes
  * every block raw (no scratch needed). d_file must hold the whole output:
- * at most sum(raw + 5) bytes from file_offset.
+ * at most sum(raw + 5) bytes from file_offset. A block longer than max_len
+ * is kept raw (the caller's bound sized the scratch).
  */
 int lvkv_sst_write_blocks_device(const void* d_raw, const uint64_t* d_raw_off,
                                  const uint32_t* d_raw_len, size_t nblocks, int compression,
@@ -141,6 +120,19 @@ int lvkv_sst_write_blocks_device(const void* d_raw, const uint64_t* d_raw_off,
                                  uint64_t file_offset, uint64_t* d_handle_off,
                                  uint32_t* d_handle_size, uint8_t* d_type, uint64_t* d_end,
                                  void* stream);
+
+/*
+ * The same with Options::zstd_compression_level (include/leveldb/options.h:
+ * 141) for compression 2: levels <= 2 except 0 (ZSTD_fast at every block
+ * size the device takes) and max_len <= LVKV_ZSTD_COMPRESS_MAX_BLOCK; other
+ * values are LVKV_ERR_INVALID (the host's libzstd path).
+ */
+int lvkv_sst_write_blocks_level_device(const void* d_raw, const uint64_t* d_raw_off,
+                                       const uint32_t* d_raw_len, size_t nblocks, int compression,
+                                       int zstd_level, uint32_t max_len, void* d_scratch,
+                                       void* d_file, uint64_t file_offset, uint64_t* d_handle_off,
+                                       uint32_t* d_handle_size, uint8_t* d_type, uint64_t* d_end,
+                                       void* stream);
 
 /* ReadBlock verdicts */
 #define LVKV_READ_OK 0

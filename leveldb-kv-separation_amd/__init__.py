@@ -156,6 +156,13 @@ def _load() -> ctypes.CDLL:
     L.lvkv_sst_write_blocks_device.argtypes = [vp, vp, vp, sz, i32, u32, vp, vp, u64, vp, vp, vp,
                                                vp, vp]
     L.lvkv_sst_write_blocks_device.restype = i32
+    L.lvkv_sst_write_blocks_level_device.argtypes = [vp, vp, vp, sz, i32, i32, u32, vp, vp, u64,
+                                                     vp, vp, vp, vp, vp]
+    L.lvkv_sst_write_blocks_level_device.restype = i32
+    L.lvkv_zstd_compress_bound.argtypes = [sz]
+    L.lvkv_zstd_compress_bound.restype = sz
+    L.lvkv_zstd_compress_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, sz, u32, i32, vp]
+    L.lvkv_zstd_compress_device.restype = i32
     L.lvkv_sst_read_blocks_device.argtypes = [vp, vp, vp, sz, i32, vp, vp, vp, vp, vp, u32, vp]
     L.lvkv_sst_read_blocks_device.restype = i32
     L.lvkv_strerror.argtypes = [i32]
@@ -598,6 +605,58 @@ def snappy_uncompress(src, offsets, lengths, *, max_ulen: int, dst=None, dst_off
     return dst, dst_offsets, out_len, status
 
 
+ZSTD_OK, ZSTD_BAD_LENGTH, ZSTD_BAD_CONTENTS, ZSTD_CAPACITY, ZSTD_TOO_LARGE, \
+    ZSTD_UNSUPPORTED = range(6)
+ZSTD_MAX_BLOCK = 49152
+ZSTD_COMPRESS_MAX_BLOCK = 20480
+
+
+def zstd_compress_bound(n: int) -> int:
+    """ZSTD_compressBound (libzstd 1.4.9)."""
+    return int(_lib.lvkv_zstd_compress_bound(n))
+
+
+def zstd_compress(src, offsets, lengths, *, level: int = 1, max_len: Optional[int] = None,
+                  dst=None, dst_offsets=None, stream=None):
+    """Batched port::Zstd_Compress(level, block) (port/port_stdcxx.h:133-161) of
+    block i = src[offsets[i] : offsets[i] + lengths[i]]: libzstd 1.4.9's frame
+    as ZSTD_compress2 writes it after getCParams(level, max(n, 1)) +
+    setCParams. Without dst, every block gets ZSTD_compressBound bytes,
+    packed. Returns (dst uint8, dst_offsets int64, frame lengths int32,
+    status uint8: ZSTD_OK / ZSTD_TOO_LARGE / ZSTD_UNSUPPORTED)."""
+    torch = _torch()
+    n = offsets.numel()
+    dev = src.device
+    if lengths.numel() != n:
+        raise ValueError("offsets and lengths differ in length")
+    if max_len is None:
+        max_len = int(lengths.max().item()) if n else 0
+    if not 0 <= max_len <= ZSTD_COMPRESS_MAX_BLOCK:
+        raise ValueError(f"max_len must be in [0, {ZSTD_COMPRESS_MAX_BLOCK}]")
+    if dst is None:
+        lens = lengths.to(torch.int64)
+        room = lens + (lens >> 8) + torch.clamp((131072 - lens) >> 11, min=0)
+        dst_offsets = _packed_offsets(torch, room, dev)
+        dst = torch.empty(max(1, int(room.sum().item())) if n else 1, dtype=torch.uint8,
+                          device=dev)
+    elif dst_offsets is None:
+        raise ValueError("dst needs dst_offsets")
+    out_len = torch.empty(n, dtype=torch.int32, device=dev)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    if n:
+        with torch.cuda.device(dev):
+            rc = _lib.lvkv_zstd_compress_device(
+                _dev_ptr(src, "src", (torch.uint8, torch.int8)),
+                _dev_ptr(offsets, "offsets", (torch.int64,)),
+                _dev_ptr(lengths, "lengths", (torch.int32,)),
+                _dev_ptr(dst, "dst", (torch.uint8, torch.int8)),
+                _dev_ptr(dst_offsets, "dst_offsets", (torch.int64,), n),
+                _dev_ptr(out_len, "out_len"), _dev_ptr(status, "status"), n, int(max_len),
+                int(level), _stream_handle(stream, dev))
+        _check("lvkv_zstd_compress_device", rc)
+    return dst, dst_offsets, out_len, status
+
+
 READ_OK, READ_CHECKSUM, READ_BAD_TYPE, READ_SNAPPY_LENGTH, READ_SNAPPY_CONTENTS, \
     READ_ZSTD_LENGTH, READ_CAPACITY, READ_TOO_LARGE, READ_ZSTD_CONTENTS = range(9)
 
@@ -664,7 +723,7 @@ def zstd_uncompress(src, offsets, lengths, *, max_ulen: int, dst=None, dst_offse
 
 
 def sst_write_blocks(raw, offsets, lengths, *, compression: int = 1, max_len: Optional[int] = None,
-                     file=None, file_offset: int = 0, stream=None):
+                     file=None, file_offset: int = 0, zstd_level: int = 1, stream=None):
     """Batched TableBuilder::WriteBlock + WriteRawBlock (table/table_builder.cc:
     141-209): blocks raw[offsets[i] : offsets[i] + lengths[i]] written in order
     from file_offset of the file image `file` (allocated when None: file_offset
@@ -683,20 +742,20 @@ def sst_write_blocks(raw, offsets, lengths, *, compression: int = 1, max_len: Op
     typ = torch.empty(n, dtype=torch.uint8, device=dev)
     end = torch.empty(1, dtype=torch.int64, device=dev)
     scratch = None
-    if compression == 1 and n:
+    if compression in (1, 2) and n:
         scratch = torch.empty(int(_lib.lvkv_sst_write_scratch_bytes(n, max_len)),
                               dtype=torch.uint8, device=dev)
     with torch.cuda.device(dev):
-        rc = _lib.lvkv_sst_write_blocks_device(
+        rc = _lib.lvkv_sst_write_blocks_level_device(
             _dev_ptr(raw, "raw", (torch.uint8, torch.int8)) if n else None,
             _dev_ptr(offsets, "offsets", (torch.int64,)) if n else None,
             _dev_ptr(lengths, "lengths", (torch.int32,), n) if n else None, n, compression,
-            max_len, _dev_ptr(scratch, "scratch") if scratch is not None else None,
+            int(zstd_level), max_len, _dev_ptr(scratch, "scratch") if scratch is not None else None,
             _dev_ptr(file, "file", (torch.uint8, torch.int8)), file_offset,
             _dev_ptr(hoff, "hoff") if n else None, _dev_ptr(hsize, "hsize") if n else None,
             _dev_ptr(typ, "type") if n else None, _dev_ptr(end, "end"),
             _stream_handle(stream, dev))
-    _check("lvkv_sst_write_blocks_device", rc)
+    _check("lvkv_sst_write_blocks_level_device", rc)
     return file, hoff, hsize, typ, end
 
 

@@ -39,7 +39,8 @@ HOST_SOURCES = ["lvkv_tables.cpp", "lvkv_cpu_crc32c.cpp", "leveldb_crc32c_shim.c
 # HIP sources: kernels and the runtime-facing C-ABI.
 HIP_SOURCES = ["crc32c_kernel.hip", "crc32c_uniform.hip", "crc32c_compact.hip",
                "crc32c_ragged.hip", "lvkv_sst_table.hip", "lvkv_log_blocks.hip",
-               "lvkv_log_assemble.hip", "lvkv_snappy.hip", "lvkv_zstd.hip", "lvkv_capi.cpp", "lvkv_engine.cpp"]
+               "lvkv_log_assemble.hip", "lvkv_snappy.hip", "lvkv_zstd.hip",
+               "lvkv_zstd_compress.hip", "lvkv_capi.cpp", "lvkv_engine.cpp"]
 # Kernels of the AQL engine: compiled alone into a gfx950 code object that is
 # embedded in the library (.incbin) and loaded through the HSA loader.
 ENGINE_KERNELS = "lvkv_engine_kernels.hip"

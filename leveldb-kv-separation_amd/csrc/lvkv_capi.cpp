@@ -89,7 +89,12 @@ hipError_t launch_sst_write_blocks(const uint8_t* raw, const uint64_t* raw_off,
                                    const uint32_t* raw_len, uint32_t nblocks, int compression,
                                    uint32_t max_len, uint8_t* scratch, uint8_t* file,
                                    uint64_t file_offset, uint64_t* hoff, uint32_t* hsize,
-                                   uint8_t* type, uint64_t* end, hipStream_t stream);
+                                   uint8_t* type, uint64_t* end, int zstd_level,
+                                   hipStream_t stream);
+hipError_t launch_zstd_compress(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
+                                uint8_t* dst, const uint64_t* dst_off, uint32_t* dst_len,
+                                uint8_t* status, uint32_t nblocks, uint32_t max_len, int level,
+                                uint64_t dst_stride, hipStream_t stream);
 hipError_t launch_sst_read_blocks(const uint8_t* file, const uint64_t* hoff, const uint32_t* hsize,
                                   uint32_t nblocks, uint8_t* out, const uint64_t* out_off,
                                   const uint32_t* out_cap, uint32_t* out_len, uint8_t* status,
@@ -917,20 +922,61 @@ size_t lvkv_sst_write_scratch_bytes(size_t nblocks, uint32_t max_len) {
   return nblocks * (snappy_write_stride(max_len) + 5);
 }
 
+size_t lvkv_zstd_compress_bound(size_t n) {
+  return n + (n >> 8) + (n < (size_t{128} << 10) ? ((size_t{128} << 10) - n) >> 11 : 0);
+}
+
+int lvkv_zstd_compress_device(const void* d_src, const uint64_t* d_src_off,
+                              const uint32_t* d_src_len, void* d_dst, const uint64_t* d_dst_off,
+                              uint32_t* d_dst_len, uint8_t* d_status, size_t nblocks,
+                              uint32_t max_len, int level, void* stream) {
+  if (nblocks == 0) return LVKV_OK;
+  if (!d_src || !d_src_off || !d_src_len || !d_dst || !d_dst_off || !d_dst_len || !d_status ||
+      nblocks > kMaxBlocksPerLaunch || max_len > LVKV_ZSTD_COMPRESS_MAX_BLOCK)
+    return LVKV_ERR_INVALID;
+  int rc = LVKV_OK;
+  if (current_ctx(&rc) == nullptr) return rc;
+  const hipError_t e = launch_zstd_compress(
+      static_cast<const uint8_t*>(d_src), d_src_off, d_src_len, static_cast<uint8_t*>(d_dst),
+      d_dst_off, d_dst_len, d_status, static_cast<uint32_t>(nblocks), max_len, level, 0,
+      static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? LVKV_OK : hip_fail(e);
+}
+
 int lvkv_sst_write_blocks_device(const void* d_raw, const uint64_t* d_raw_off,
                                  const uint32_t* d_raw_len, size_t nblocks, int compression,
                                  uint32_t max_len, void* d_scratch, void* d_file,
                                  uint64_t file_offset, uint64_t* d_handle_off,
                                  uint32_t* d_handle_size, uint8_t* d_type, uint64_t* d_end,
                                  void* stream) {
-  if (!d_end || (compression != 0 && compression != 1)) return LVKV_ERR_INVALID;
-  if (nblocks == 0) {
-    const hipError_t e = hipMemcpyAsync(d_end, &file_offset, 8, hipMemcpyHostToDevice,
-                                        static_cast<hipStream_t>(stream));
+  return lvkv_sst_write_blocks_level_device(d_raw, d_raw_off, d_raw_len, nblocks, compression, 1,
+                                            max_len, d_scratch, d_file, file_offset, d_handle_off,
+                                            d_handle_size, d_type, d_end, stream);
+}
+
+int lvkv_sst_write_blocks_level_device(const void* d_raw, const uint64_t* d_raw_off,
+                                       const uint32_t* d_raw_len, size_t nblocks, int compression,
+                                       int zstd_level, uint32_t max_len, void* d_scratch,
+                                       void* d_file, uint64_t file_offset, uint64_t* d_handle_off,
+                                       uint32_t* d_handle_size, uint8_t* d_type, uint64_t* d_end,
+                                       void* stream) {
+  if (!d_end || compression < 0 || compression > 2) return LVKV_ERR_INVALID;
+  // kZstdCompression on the device: the ZSTD_fast levels (<= 2; 0 means 3)
+  // and blocks the compressor's LDS plan holds
+  if (compression == 2 &&
+      (zstd_level == 0 || zstd_level > 2 || max_len > LVKV_ZSTD_COMPRESS_MAX_BLOCK))
+    return LVKV_ERR_INVALID;
+  if (nblocks == 0) {  // d_end = file_offset, by the layout kernel (no host pointer kept)
+    int rc = LVKV_OK;
+    if (current_ctx(&rc) == nullptr) return rc;
+    const hipError_t e = launch_sst_write_blocks(nullptr, nullptr, nullptr, 0, compression, 0,
+                                                 nullptr, nullptr, file_offset, nullptr, nullptr,
+                                                 nullptr, d_end, zstd_level,
+                                                 static_cast<hipStream_t>(stream));
     return e == hipSuccess ? LVKV_OK : hip_fail(e);
   }
   if (!d_raw || !d_raw_off || !d_raw_len || !d_file || !d_handle_off || !d_handle_size ||
-      !d_type || (compression == 1 && !d_scratch) || nblocks > kMaxBlocksPerLaunch)
+      !d_type || (compression != 0 && !d_scratch) || nblocks > kMaxBlocksPerLaunch)
     return LVKV_ERR_INVALID;
   int rc = LVKV_OK;
   if (current_ctx(&rc) == nullptr) return rc;
@@ -938,7 +984,7 @@ int lvkv_sst_write_blocks_device(const void* d_raw, const uint64_t* d_raw_off,
   hipError_t e = launch_sst_write_blocks(
       static_cast<const uint8_t*>(d_raw), d_raw_off, d_raw_len, static_cast<uint32_t>(nblocks),
       compression, max_len, static_cast<uint8_t*>(d_scratch), static_cast<uint8_t*>(d_file),
-      file_offset, d_handle_off, d_handle_size, d_type, d_end, hs);
+      file_offset, d_handle_off, d_handle_size, d_type, d_end, zstd_level, hs);
   if (e != hipSuccess) return hip_fail(e);
   // the trailers: Mask(CRC32C(contents + type)) by the batch CRC kernel
   return lvkv_sst_fill_trailers_device(d_file, d_handle_off, d_handle_size, nullptr, nblocks,

@@ -293,6 +293,7 @@ struct CompressArgs {
   uint32_t nblocks;
   uint32_t frag_cap;    // the largest fragment the LDS holds (<= kFrag)
   uint64_t dst_stride;  // dst_off == nullptr: block b's output at b * dst_stride
+  uint32_t max_len;     // dst_off == nullptr: the stride's sizing; longer blocks are TOO_LARGE
 };
 
 __global__ void __launch_bounds__(64) snappy_compress_kernel(CompressArgs a) {
@@ -306,7 +307,9 @@ __global__ void __launch_bounds__(64) snappy_compress_kernel(CompressArgs a) {
   uint8_t* in = smem;
   uint32_t* slots = reinterpret_cast<uint32_t*>(smem + in_bytes);  // 256
   uint16_t* table = reinterpret_cast<uint16_t*>(slots + 256);
-  if (min(len, kFrag) > a.frag_cap) {  // the caller's max_len was too small
+  // the caller's max_len was too small: the fragment does not fit the LDS,
+  // or (fixed stride) the output would run into the next block's slot
+  if (min(len, kFrag) > a.frag_cap || (a.dst_off == nullptr && len > a.max_len)) {
     if (lane == 0) {
       a.dst_len[b] = 0;
       a.status[b] = LVKV_SNAPPY_TOO_LARGE;
@@ -443,8 +446,9 @@ __global__ void __launch_bounds__(64) snappy_uncompress_kernel(UncompressArgs a)
           ok = false;
           break;
         }
-        // (64-bit: a 4-byte length of 0xffffffff is 2^32, not 0)
-        len64 = ((t8 >> 8) & ((uint64_t{1} << (8 * k)) - 1u)) + 1u;
+        // snappy adds the 1 in uint32: a 4-byte length of 0xffffffff wraps
+        // to an empty literal (libsnappy 1.1.8 accepts 03fcffffffff08616263)
+        len64 = (((t8 >> 8) & ((uint64_t{1} << (8 * k)) - 1u)) + 1u) & 0xffffffffu;
         ip += k;
       }
       if (len64 > n - ip || len64 > ulen - op) {
@@ -524,7 +528,8 @@ __global__ void __launch_bounds__(1024) sst_layout_kernel(const uint32_t* raw_le
                                                           const uint32_t* clen, const uint8_t* cst,
                                                           uint32_t n, uint64_t file_offset,
                                                           uint64_t* hoff, uint32_t* hsize,
-                                                          uint8_t* type, uint64_t* end) {
+                                                          uint8_t* type, uint64_t* end,
+                                                          uint32_t ctype) {
   __shared__ uint64_t wsum[17];
   const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
   uint64_t carry = file_offset;
@@ -540,7 +545,7 @@ __global__ void __launch_bounds__(1024) sst_layout_kernel(const uint32_t* raw_le
         const uint32_t L = raw_len[i];
         const bool c = clen != nullptr && cst[i] == LVKV_SNAPPY_OK && clen[i] < L - L / 8u;
         sz[j] = c ? clen[i] : L;
-        ty[j] = c ? 1 : 0;
+        ty[j] = c ? static_cast<uint8_t>(ctype) : 0;
         local += sz[j] + 5u;
       }
     }
@@ -596,31 +601,50 @@ __global__ void __launch_bounds__(256) sst_place_kernel(const uint8_t* raw, cons
 
 }  // namespace
 
+// A block's compressed scratch slot: room for either codec's bound
+// (snappy::MaxCompressedLength, ZSTD_compressBound).
 uint64_t snappy_write_stride(uint32_t max_len) {
-  return (snappy_in_cap(max_len) + 15u) & ~uint64_t{15};
+  const uint64_t zb = uint64_t{max_len} + (max_len >> 8) +
+                      (max_len < (128u << 10) ? ((128u << 10) - max_len) >> 11 : 0u);
+  const uint64_t sb = snappy_in_cap(max_len);
+  return ((sb > zb ? sb : zb) + 15u) & ~uint64_t{15};
 }
+
+hipError_t launch_zstd_compress(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
+                                uint8_t* dst, const uint64_t* dst_off, uint32_t* dst_len,
+                                uint8_t* status, uint32_t nblocks, uint32_t max_len, int level,
+                                uint64_t dst_stride, hipStream_t stream);
 
 hipError_t launch_sst_write_blocks(const uint8_t* raw, const uint64_t* raw_off,
                                    const uint32_t* raw_len, uint32_t nblocks, int compression,
                                    uint32_t max_len, uint8_t* scratch, uint8_t* file,
                                    uint64_t file_offset, uint64_t* hoff, uint32_t* hsize,
-                                   uint8_t* type, uint64_t* end, hipStream_t stream) {
+                                   uint8_t* type, uint64_t* end, int zstd_level,
+                                   hipStream_t stream) {
   const uint64_t stride = snappy_write_stride(max_len);
   uint32_t* clen = nullptr;
   uint8_t* cst = nullptr;
-  if (compression == 1) {
+  if (compression == 1 && nblocks != 0) {
     clen = reinterpret_cast<uint32_t*>(scratch + stride * nblocks);
     cst = reinterpret_cast<uint8_t*>(clen + nblocks);
-    CompressArgs a{raw, raw_off, raw_len, scratch, nullptr, clen, cst, nblocks, 0, stride};
+    CompressArgs a{raw, raw_off, raw_len, scratch, nullptr, clen, cst, nblocks, 0, stride, max_len};
     a.frag_cap = max(16u, min(max_len, kFrag));
     const uint32_t in_bytes = (a.frag_cap + 16u + 15u) & ~15u;
     uint32_t t = 256;
     while (t < kMaxTable && t < a.frag_cap) t <<= 1;
     const size_t lds = in_bytes + 1024u + 2u * t;
     hipLaunchKernelGGL(snappy_compress_kernel, dim3(nblocks), dim3(64), lds, stream, a);
+  } else if (compression == 2 && nblocks != 0) {  // kZstdCompression
+    clen = reinterpret_cast<uint32_t*>(scratch + stride * nblocks);
+    cst = reinterpret_cast<uint8_t*>(clen + nblocks);
+    const hipError_t e = launch_zstd_compress(raw, raw_off, raw_len, scratch, nullptr, clen, cst,
+                                              nblocks, max_len, zstd_level, stride, stream);
+    if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(sst_layout_kernel, dim3(1), dim3(1024), 0, stream, raw_len, clen, cst,
-                     nblocks, file_offset, hoff, hsize, type, end);
+                     nblocks, file_offset, hoff, hsize, type, end,
+                     static_cast<uint32_t>(compression == 2 ? 2 : 1));
+  if (nblocks == 0) return hipGetLastError();  // (the layout stored end = file_offset)
   hipLaunchKernelGGL(sst_place_kernel, dim3(nblocks), dim3(256), 0, stream, raw, raw_off,
                      scratch, stride, hoff, hsize, type, file);
   return hipGetLastError();

@@ -338,7 +338,7 @@ __constant__ uint8_t kMLBits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
 struct Lds {
   uint8_t* in;      // the staged frame (+16 zero bytes)
   uint8_t* out;     // the frame's output
-  uint16_t* huf;    // Huffman decode table: symbol | nbBits << 8 (<= 2048)
+  uint16_t* huf;    // Huffman decode table: symbol | nbBits << 8 (<= 4096)
   uint32_t* ll;     // FSE tables: 512 / 256 / 512 entries, and 64 for weights
   uint32_t* of;
   uint32_t* ml;
@@ -348,7 +348,7 @@ struct Lds {
   uint8_t* sym;     // FSE spread scratch (512)
 };
 
-constexpr uint32_t kHufEntries = 2048, kFseLL = 512, kFseOF = 256, kFseML = 512, kFseW = 64;
+constexpr uint32_t kHufEntries = 4096, kFseLL = 512, kFseOF = 256, kFseML = 512, kFseW = 64;
 
 __host__ __device__ constexpr uint32_t zstd_in_cap(uint32_t out_cap) {
   // ZSTD_compressBound(out_cap) (1.4.9): every frame the library writes
@@ -512,7 +512,8 @@ __device__ bool huf_weights(const Lds& L, uint32_t p, uint32_t end, uint32_t (&w
   bad = uni(bad);
   if (bad || total == 0) return *fail = kFHufWeights, false;
   const uint32_t mb = 32u - __builtin_clz(total);  // highbit(total) + 1
-  if (mb > 11u) return *fail = kFHufWeights, false;
+  // HUF_TABLELOG_MAX: a tree of up to 12 bits decodes (1.4.9's DTable holds 12)
+  if (mb > 12u) return *fail = kFHufWeights, false;
   const uint32_t rest = (1u << mb) - total;
   if (rest & (rest - 1u)) return *fail = kFHufWeights, false;
   put(n++, 32u - __builtin_clz(rest));

@@ -215,7 +215,8 @@ def uncompress(src: bytes) -> Tuple[int, bytes]:
                 k = ln - 60
                 if i + k > len(src):
                     return BAD_CONTENTS, b""
-                ln = int.from_bytes(src[i: i + k], "little") + 1
+                # snappy adds the 1 in uint32 (0xffffffff wraps to 0)
+                ln = (int.from_bytes(src[i: i + k], "little") + 1) & 0xFFFFFFFF
                 i += k
             if i + ln > len(src) or len(out) + ln > n:
                 return BAD_CONTENTS, b""
@@ -261,10 +262,11 @@ def _crc():
     return m
 
 
-def write_blocks(raws, compression: int, file_offset: int = 0):
+def write_blocks(raws, compression: int, file_offset: int = 0, zstd_level: int = 1):
     """TableBuilder::WriteBlock + WriteRawBlock (table/table_builder.cc:141-209)
     for each raw block in order: (file bytes from file_offset, handles
-    [(offset, size)], types)."""
+    [(offset, size)], types). Compression 2 is kZstdCompression through
+    oracle/zstd_encoder.py (port::Zstd_Compress at zstd_level, :172-185)."""
     crc = _crc()
     out = bytearray()
     handles, types = [], []
@@ -275,6 +277,14 @@ def write_blocks(raws, compression: int, file_offset: int = 0):
             c = compress(raw)
             if len(c) < len(raw) - len(raw) // 8:  # :160-168
                 contents, typ = c, 1
+        elif compression == 2:
+            try:
+                from oracle import zstd_encoder as ze
+            except ImportError:  # (oracle/ itself on sys.path)
+                import zstd_encoder as ze
+            c = ze.compress(raw, zstd_level)
+            if len(c) < len(raw) - len(raw) // 8:  # :172-185
+                contents, typ = c, 2
         handles.append((file_offset + len(out), len(contents)))
         types.append(typ)
         out += contents

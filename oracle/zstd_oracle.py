@@ -252,7 +252,7 @@ def huf_weights(data: bytes, p: int, end: int):
     if total == 0:
         raise Corrupt("huf: no weights")
     maxbits = total.bit_length()  # highbit(total) + 1
-    if maxbits > 11:
+    if maxbits > 12:  # HUF_TABLELOG_MAX (weights stay <= 11)
         raise Corrupt("huf: tree too deep")
     rest = (1 << maxbits) - total
     if rest & (rest - 1):

@@ -99,7 +99,10 @@ def damaged(streams):
               bytes([0xFF, 0xFF, 0xFF, 0xFF, 0x10]),                     # varint too long
               bytes([0x80, 0x80, 0x80, 0x80, 0x80, 0x00]),
               bytes([3, 0xFC, 0xFF, 0xFF, 0xFF, 0xFF]) + b"abc",         # literal of 2^32
-              bytes([0]), b"", bytes([1]), bytes([2, 0x04]) + b"xy" + bytes([0x00]) + b"z"]
+              bytes([0]), b"", bytes([1]), bytes([2, 0x04]) + b"xy" + bytes([0x00]) + b"z",
+              # 4-byte literal length 0xffffffff: + 1 wraps in uint32 to an
+              # empty literal (libsnappy decodes this to b"abc", status 0)
+              bytes([3, 0xFC, 0xFF, 0xFF, 0xFF, 0xFF, 0x08]) + b"abc"]
     return cases
 
 

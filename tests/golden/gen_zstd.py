@@ -73,9 +73,12 @@ def main():
             f = f[: int(rng.integers(1, len(f) + 1))]
         if k % 7 == 0:
             f += rng.integers(0, 256, int(rng.integers(1, 6)), dtype=np.uint8).tobytes()
-        f = bytes(f)
+        dam.append(bytes(f))
+    # hand-made: literals under a 12-bit single-stream Huffman tree
+    # (HUF_TABLELOG_MAX; libzstd decodes it to four zero bytes)
+    dam.append(bytes.fromhex("28b52ffd20047500004280028cbbba9876543210550100"))
+    for f in dam:
         ok, out = zo.lib_uncompress(lib, f)
-        dam.append(f)
         verdicts.append({"ok": 2 if ok is None else int(ok), "n": len(out),
                          "sha256": hashlib.sha256(out).hexdigest() if ok else None})
     blob = {"inputs": [len(x) for x in ins], "frames": [len(f) for f in frames], "meta": meta,

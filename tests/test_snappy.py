@@ -249,6 +249,11 @@ def test_device_codec_empty_batch(lvkv, gpu):
     assert dl.numel() == 0 and st.numel() == 0
     _, _, dl, st = lvkv.snappy_uncompress(z8, e64, e32, max_ulen=4096)
     assert dl.numel() == 0 and st.numel() == 0
+    for comp in (0, 1):  # no blocks: Rep::offset stays where it was
+        _, _, _, _, end = lvkv.sst_write_blocks(z8, e64, e32, compression=comp,
+                                                file_offset=987654321)
+        torch.cuda.synchronize()
+        assert int(end.item()) == 987654321
 
 
 # ---- WriteBlock / ReadBlock around the codec -------------------------------
@@ -302,6 +307,28 @@ def test_device_write_blocks_matches_oracle(lvkv, gpu, compression, file_offset)
     assert int(end.item()) == file_offset + len(img)
     got = file.cpu().numpy()[file_offset:file_offset + len(img)].tobytes()
     assert got == img
+
+
+@pytest.mark.gpu
+def test_device_write_blocks_longer_than_max_len_stay_raw(lvkv, gpu):
+    """A block longer than the call's max_len (here >= 64 KiB, so the LDS
+    would take it) must not run past its fixed-stride scratch slot: it is
+    TOO_LARGE for the compressor and the layout keeps it raw.
+    Every block still reads back to its bytes."""
+    import torch
+    from tools.db_bench_data import block_batch
+    bench = block_batch(40).tobytes()
+    raws = [bench[:5000], bench[7:7 + 70000], bench[100:4196], bench[:65536]]
+    src, off, ln = _pack(torch, gpu, raws, skew=1)
+    file, hoff, hsize, typ, end = lvkv.sst_write_blocks(src, off, ln, compression=1,
+                                                        max_len=65536)
+    torch.cuda.synchronize()
+    types = typ.cpu().tolist()
+    assert types[1] == 0 and types[0] == types[2] == types[3] == 1
+    img = file.cpu().numpy().tobytes()
+    for raw, o, s in zip(raws, hoff.cpu().tolist(), hsize.cpu().tolist()):
+        assert so.read_block(img, o, s) == (so.READ_OK, raw)
+    assert int(end.item()) == sum(hsize.cpu().tolist()) + 5 * len(raws)
 
 
 @pytest.mark.gpu
