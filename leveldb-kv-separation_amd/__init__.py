@@ -631,8 +631,7 @@ def zstd_compress(src, offsets, lengths, *, level: int = 1, max_len: Optional[in
         raise ValueError("offsets and lengths differ in length")
     if max_len is None:
         max_len = int(lengths.max().item()) if n else 0
-    if not 0 <= max_len <= ZSTD_COMPRESS_MAX_BLOCK:
-        raise ValueError(f"max_len must be in [0, {ZSTD_COMPRESS_MAX_BLOCK}]")
+    # (max_len past ZSTD_COMPRESS_MAX_BLOCK: the C-ABI's LVKV_ERR_INVALID)
     if dst is None:
         lens = lengths.to(torch.int64)
         room = lens + (lens >> 8) + torch.clamp((131072 - lens) >> 11, min=0)

@@ -1348,7 +1348,7 @@ __device__ void match_block(const uint8_t* in, uint32_t n, TIdx* table, uint32_t
       cand = uni(__builtin_amdgcn_readlane(kind == 2 ? c0 : c1, J)) - 1u;
     }
     const uint32_t ki = ~vmask ? static_cast<uint32_t>(__builtin_ctzll(~vmask)) : 64u;
-    const bool end = J >= ki;  // the loop runs past ilimit before a hit
+    const bool end = ki < 64 && J >= ki;  // the loop runs past ilimit before a hit
     // the window's table writes: steps 0..min(J, 63), each hash's last
     const uint32_t Jw = J < 64 ? J : 63u;
     const bool part = valid && lane <= Jw;
