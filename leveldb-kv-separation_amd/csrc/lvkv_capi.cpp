@@ -32,6 +32,7 @@ extern uint64_t* g_asm_stamps;
 extern uint64_t* g_sst_stamps;
 extern uint32_t g_log_knobs;
 extern uint64_t* g_zstd_stamps;
+extern uint64_t* g_zstdc_stamps;
 hipError_t launch_crc32c_probe(const KernelArgs& args, int variant,
                                int num_groups, hipStream_t stream);
 hipError_t launch_read_bw(const void* p, uint64_t bytes, uint32_t* out,
@@ -1182,6 +1183,7 @@ void lvkv_debug_asm_stamps(uint64_t* d_stamps) { g_asm_stamps = d_stamps; }
 void lvkv_debug_sst_stamps(uint64_t* d_stamps) { g_sst_stamps = d_stamps; }
 void lvkv_debug_log_knobs(uint32_t knobs) { g_log_knobs = knobs; }
 void lvkv_debug_zstd_stamps(uint64_t* d_stamps) { g_zstd_stamps = d_stamps; }
+void lvkv_debug_zstdc_stamps(uint64_t* d_stamps) { g_zstdc_stamps = d_stamps; }
 static uint64_t* g_debug_stamps = nullptr;
 
 void lvkv_debug_set_stamps(uint64_t* d_stamps) { g_debug_stamps = d_stamps; }

@@ -77,7 +77,7 @@ __device__ __forceinline__ void stage(uint8_t* dst, const uint8_t* src, uint32_t
 // W | H << 8 | minMatch << 16 of ZSTD_defaultCParameters' fast rows; 0 where
 // the strategy is not ZSTD_fast. Table 0: > 256 KiB, 1: <= 256 KiB, 2: <=
 // 128 KiB, 3: <= 16 KiB; row 0 is the base row of the negative levels.
-__host__ __device__ uint32_t zstd_fast_row(uint32_t tid, uint32_t row) {
+__host__ __device__ __forceinline__ uint32_t zstd_fast_row(uint32_t tid, uint32_t row) {
   constexpr uint32_t r00 = 19 | 13 << 8 | 6 << 16, r01 = 19 | 14 << 8 | 7 << 16,
                      r02 = 20 | 16 << 8 | 6 << 16;
   constexpr uint32_t r10 = 18 | 13 << 8 | 5 << 16, r11 = 18 | 14 << 8 | 6 << 16;
@@ -108,7 +108,7 @@ struct ZParams {
 // The parameters ZSTD_compress2 runs with for port::Zstd_Compress(level, n
 // bytes): getCParams(level, max(n, 1)) set field by field over the context's
 // level-3 row, adjusted to the pledged size (the same fit again).
-__host__ __device__ ZParams zstd_port_params(int level, uint32_t n) {
+__host__ __device__ __forceinline__ ZParams zstd_port_params(int level, uint32_t n) {
   ZParams p{0, 0, 0, 0, 0};
   if (level == 0 || level > 2) return p;
   const uint32_t s = n ? n : 1u;
@@ -140,7 +140,6 @@ constexpr uint32_t kEStLL = 2048;    // u16[512] FSE next states
 constexpr uint32_t kEStML = 3072;    // u16[512]
 constexpr uint32_t kEStOF = 4096;    // u16[256]
 constexpr uint32_t kEStW = 4608;     // u16[64]
-constexpr uint32_t kENorm = 4736;    // i16[64] normalized counts
 constexpr uint32_t kENxt = 4864;     // u16[64] per-symbol next slot
 constexpr uint32_t kESpread = 4992;  // u8[512] symbol of each spread rank
 constexpr uint32_t kEPosSym = 5504;  // u8[512] symbol of each table position
@@ -162,7 +161,23 @@ struct ZcArgs {
   uint64_t dst_stride;  // dst_off == nullptr: block b's frame at b * dst_stride
   // LDS offsets
   uint32_t o_tbl, o_tag, o_lit, o_sll, o_sof, smax;
+  uint64_t* stamps;  // probe build: 16 clock stamps a block (nullptr: none)
 };
+
+// s_memtime into stamp slot k of the block's LDS stamp area (probe build
+// only; copied to a.stamps at the end, so that no global store or pointer
+// test sits between the phases)
+#ifndef ZC_STAMP_MASK
+#define ZC_STAMP_MASK 0xFFFFu
+#endif
+__device__ __forceinline__ void zcstamp(uint64_t* slot, uint32_t k) {
+#ifdef LVKV_PROBE_BUILD
+  if (((ZC_STAMP_MASK >> k) & 1u) && threadIdx.x == 0) slot[k] = __builtin_amdgcn_s_memtime();
+#else
+  (void)slot;
+  (void)k;
+#endif
+}
 
 // ---- LL / ML codes (ZSTD_LLcode / ZSTD_MLcode) -----------------------------
 
@@ -256,9 +271,11 @@ __device__ __forceinline__ uint32_t fse_opt_log(uint32_t max_log, uint32_t src, 
 }
 
 // FSE_normalizeCount (+ FSE_normalizeM2) over counts held a symbol a lane
-// (cnt, symbols < 64): the result into norm[] (LDS). Uniform serial code.
-__device__ void fse_normalize(uint32_t cnt, uint32_t tl, uint32_t total, uint32_t max_sym,
-                              bool low_prob, int16_t* norm, uint32_t lane) {
+// (cnt, symbols < 64): returns this lane's normalized count (0 past
+// max_sym). The wave works on the counts together; the serial parts are
+// reductions and ballots.
+__device__ __forceinline__ int32_t fse_normalize(uint32_t cnt, uint32_t tl, uint32_t total, uint32_t max_sym,
+                                 bool low_prob, uint32_t lane) {
   const int32_t low = low_prob ? -1 : 1;
   const uint32_t scale = 62u - tl;
   const uint64_t step = (uint64_t{1} << 62) / total;
@@ -296,11 +313,7 @@ __device__ void fse_normalize(uint32_t cnt, uint32_t tl, uint32_t total, uint32_
   const uint64_t lm = __ballot(big && p == largest_p && largest_p > 0);
   const uint32_t largest = lm ? static_cast<uint32_t>(__builtin_ctzll(lm)) : 0u;
   const int32_t nl = static_cast<int32_t>(uni(__builtin_amdgcn_readlane(static_cast<uint32_t>(p), largest)));
-  if (-still < (nl >> 1)) {
-    if (lane <= max_sym) norm[lane] = static_cast<int16_t>(lane == largest ? p + still : p);
-    lds_sync();
-    return;
-  }
+  if (-still < (nl >> 1)) return lane == largest ? p + still : p;
   // FSE_normalizeM2
   const int16_t kNA = -2;
   uint32_t distributed = 0;
@@ -379,12 +392,12 @@ __device__ void fse_normalize(uint32_t cnt, uint32_t tl, uint32_t total, uint32_
       }
     }
   }
-  if (lane <= max_sym) norm[lane] = static_cast<int16_t>(q);
-  lds_sync();
+  return lane <= max_sym ? q : 0;
 }
 
-// FSE_writeNCount of norm[0..max_sym] at accuracy tl through bw.
-__device__ void fse_write_ncount(const int16_t* norm, uint32_t max_sym, uint32_t tl, BitW& bw,
+// FSE_writeNCount of the normalized counts (a symbol a lane, symbols
+// 0..max_sym) at accuracy tl through bw. Uniform serial code on readlanes.
+__device__ __forceinline__ void fse_write_ncount(int32_t normv, uint32_t max_sym, uint32_t tl, BitW& bw,
                                  uint32_t lane) {
   bw_add(bw, tl - 5u, 4, lane);
   int32_t remaining = (1 << tl) + 1;
@@ -392,12 +405,14 @@ __device__ void fse_write_ncount(const int16_t* norm, uint32_t max_sym, uint32_t
   uint32_t nb = tl + 1u;
   uint32_t s = 0;
   const uint32_t alpha = max_sym + 1u;
+  const uint64_t nzm = __ballot(normv != 0);
   bool prev0 = false;
   while (s < alpha && remaining > 1) {
     if (prev0) {
       uint32_t start = s;
-      while (s < alpha && uni(static_cast<uint32_t>(norm[s])) == 0) ++s;
-      if (s == alpha) break;
+      const uint64_t ahead = nzm >> s;  // the next non-zero symbol
+      s = ahead ? s + static_cast<uint32_t>(__builtin_ctzll(ahead)) : alpha;
+      if (s >= alpha) break;
       while (s >= start + 24u) {
         start += 24u;
         bw_add(bw, 0xFFFFu, 16, lane);
@@ -408,7 +423,7 @@ __device__ void fse_write_ncount(const int16_t* norm, uint32_t max_sym, uint32_t
       }
       bw_add(bw, s - start, 2, lane);
     }
-    int32_t count = static_cast<int16_t>(uni(static_cast<uint32_t>(static_cast<uint16_t>(norm[s]))));
+    int32_t count = static_cast<int32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(normv), s));
     ++s;
     const int32_t mx = (2 * threshold - 1) - remaining;
     remaining -= count < 0 ? -count : count;
@@ -416,6 +431,7 @@ __device__ void fse_write_ncount(const int16_t* norm, uint32_t max_sym, uint32_t
     if (count >= threshold) count += mx;
     bw_add(bw, static_cast<uint32_t>(count), nb - (count < mx ? 1u : 0u), lane);
     prev0 = count == 1;
+    if (remaining < 1) break;  // (a bad distribution: FSE_writeNCount's error)
     while (remaining < threshold) {
       --nb;
       threshold >>= 1;
@@ -425,14 +441,14 @@ __device__ void fse_write_ncount(const int16_t* norm, uint32_t max_sym, uint32_t
 
 // FSE_buildCTable_wksp for norm[0..max_sym] (max_sym < 64) at accuracy tl:
 // next states into st[], and per symbol (lane s) the transform dnb / dfs.
-__device__ void fse_build_ctable(const int16_t* norm, uint32_t max_sym, uint32_t tl, uint16_t* st,
+__device__ __forceinline__ void fse_build_ctable(int32_t normv, uint32_t max_sym, uint32_t tl, uint16_t* st,
                                  uint8_t* ent, uint32_t lane, uint32_t* dnb_out, int32_t* dfs_out) {
   uint8_t* spread = ent + kESpread;
   uint8_t* psym = ent + kEPosSym;
   uint16_t* nxt = reinterpret_cast<uint16_t*>(ent + kENxt);
   const uint32_t size = 1u << tl;
   const uint64_t below = (uint64_t{1} << lane) - 1u;
-  const int32_t c = lane <= max_sym ? norm[lane] : 0;
+  const int32_t c = lane <= max_sym ? normv : 0;
   const bool lowp = c == -1;
   const uint32_t take = lowp ? 1u : (c > 0 ? static_cast<uint32_t>(c) : 0u);
   uint32_t cum = take;
@@ -524,27 +540,38 @@ __device__ void fse_build_ctable(const int16_t* norm, uint32_t max_sym, uint32_t
   *dfs_out = dfs;
 }
 
-// FSE state coder over a table whose transforms sit a symbol a lane.
+// FSE state coder over a table whose transforms sit a symbol a lane. A
+// table of <= 64 states is also held a state a lane (stv), so that the
+// serial coders read it with v_readlane instead of an LDS round trip.
 struct FseC {
   const uint16_t* st;
+  uint32_t stv;  // lane u: st[u] (reg tables)
   uint32_t dnb;  // lane s: symbol s's deltaNbBits
   int32_t dfs;   // lane s: deltaFindState
   uint32_t log;
+  bool reg;
 };
+__device__ __forceinline__ void fse_regs(FseC& t, uint32_t lane) {
+  t.reg = t.log <= 6;
+  if (t.reg) t.stv = lane < (1u << t.log) ? t.st[lane] : 0u;
+}
+__device__ __forceinline__ uint32_t fse_state(const FseC& t, int32_t idx) {
+  return t.reg ? __builtin_amdgcn_readlane(t.stv, static_cast<uint32_t>(idx)) : uni(t.st[idx]);
+}
 __device__ __forceinline__ uint32_t fse_init(const FseC& t, uint32_t sym) {
-  const uint32_t dnb = uni(__builtin_amdgcn_readlane(t.dnb, sym));
-  const int32_t dfs = static_cast<int32_t>(uni(__builtin_amdgcn_readlane(static_cast<uint32_t>(t.dfs), sym)));
+  const uint32_t dnb = __builtin_amdgcn_readlane(t.dnb, sym);
+  const int32_t dfs = static_cast<int32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(t.dfs), sym));
   const uint32_t nbo = (dnb + (1u << 15)) >> 16;
   const uint32_t v = (nbo << 16) - dnb;
-  return uni(t.st[static_cast<int32_t>(v >> nbo) + dfs]);
+  return fse_state(t, static_cast<int32_t>(v >> nbo) + dfs);
 }
 __device__ __forceinline__ uint32_t fse_enc(const FseC& t, uint32_t state, uint32_t sym, BitW& bw,
                                             uint32_t lane) {
-  const uint32_t dnb = uni(__builtin_amdgcn_readlane(t.dnb, sym));
-  const int32_t dfs = static_cast<int32_t>(uni(__builtin_amdgcn_readlane(static_cast<uint32_t>(t.dfs), sym)));
+  const uint32_t dnb = __builtin_amdgcn_readlane(t.dnb, sym);
+  const int32_t dfs = static_cast<int32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(t.dfs), sym));
   const uint32_t nbo = (state + dnb) >> 16;
   bw_add(bw, state, nbo, lane);
-  return uni(t.st[static_cast<int32_t>(state >> nbo) + dfs]);
+  return fse_state(t, static_cast<int32_t>(state >> nbo) + dfs);
 }
 
 // ---- Huffman (huf_compress.c) -----------------------------------------------
@@ -557,7 +584,7 @@ struct HNode {
 };
 
 // HUF_setMaxHeight over node[0..last] (node = huffNode, node[-1] the barrier)
-__device__ uint32_t huf_set_max_height(HNode* node, int32_t last, uint32_t max_nb) {
+__device__ __forceinline__ uint32_t huf_set_max_height(HNode* node, int32_t last, uint32_t max_nb) {
   const uint32_t largest = uni(node[last].nb);
   if (largest <= max_nb) return largest;
   int32_t total = 0;
@@ -621,10 +648,39 @@ __device__ uint32_t huf_set_max_height(HNode* node, int32_t last, uint32_t max_n
   return max_nb;
 }
 
+// 256-entry arrays held a value a lane in 4 VGPRs: element i at lane i & 63
+// of register i >> 6 (i uniform).
+__device__ __forceinline__ uint32_t rd256(const uint32_t (&a)[4], uint32_t i) {
+  const uint32_t g = i >> 6;
+  const uint32_t v = g == 0 ? a[0] : (g == 1 ? a[1] : (g == 2 ? a[2] : a[3]));
+  return __builtin_amdgcn_readlane(v, i & 63u);
+}
+__device__ __forceinline__ void wr256(uint32_t (&a)[4], uint32_t i, uint32_t v) {
+  const uint32_t g = i >> 6, l = i & 63u;
+  const bool me = threadIdx.x == l;  // (v_cmp + v_cndmask: a lane write)
+  a[0] = (g == 0 && me) ? v : a[0];
+  a[1] = (g == 1 && me) ? v : a[1];
+  a[2] = (g == 2 && me) ? v : a[2];
+  a[3] = (g == 3 && me) ? v : a[3];
+}
+// lane-varying gather from a 256-entry register array
+__device__ __forceinline__ uint32_t gather256(const uint32_t (&a)[4], uint32_t i) {
+  const int addr = static_cast<int>((i & 63u) << 2);
+  const uint32_t v0 = __builtin_amdgcn_ds_bpermute(addr, static_cast<int>(a[0]));
+  const uint32_t v1 = __builtin_amdgcn_ds_bpermute(addr, static_cast<int>(a[1]));
+  const uint32_t v2 = __builtin_amdgcn_ds_bpermute(addr, static_cast<int>(a[2]));
+  const uint32_t v3 = __builtin_amdgcn_ds_bpermute(addr, static_cast<int>(a[3]));
+  const uint32_t g = i >> 6;
+  return g == 0 ? v0 : (g == 1 ? v1 : (g == 2 ? v2 : v3));
+}
+
 // HUF_buildCTable_wksp: counts a symbol a lane x 4 (c[g] for g * 64 + lane),
 // symbols 0..max_sym. Codes go to huf[s] = code | nbBits << 16. Returns the
-// table's max bits.
-__device__ uint32_t huf_build(const uint32_t (&c)[4], uint32_t max_sym, uint32_t max_nb,
+// table's max bits. The sorted leaves, the created nodes' counts, the
+// parents and the depths live in registers (rd256 / wr256): the merges and
+// the depth walk are chains of v_readlane / v_writelane, not LDS round
+// trips. node0 (LDS) serves the rank scatter and the rare HUF_setMaxHeight.
+__device__ __forceinline__ uint32_t huf_build(const uint32_t (&c)[4], uint32_t max_sym, uint32_t max_nb,
                               HNode* node0, uint32_t* huf, uint32_t lane) {
   HNode* node = node0 + 1;
   // HUF_sort: decreasing count, ties in symbol order -- each symbol's rank
@@ -635,7 +691,7 @@ __device__ uint32_t huf_build(const uint32_t (&c)[4], uint32_t max_sym, uint32_t
     const uint32_t top = max_sym - g2 * 64u < 63u ? max_sym - g2 * 64u : 63u;
     for (uint32_t l = 0; l <= top; ++l) {
       const uint32_t t = g2 * 64u + l;
-      const uint32_t ct = uni(__builtin_amdgcn_readlane(c[g2], l));
+      const uint32_t ct = __builtin_amdgcn_readlane(c[g2], l);
 #pragma unroll
       for (uint32_t g = 0; g < 4; ++g) {
         const uint32_t s = g * 64u + lane;
@@ -643,13 +699,6 @@ __device__ uint32_t huf_build(const uint32_t (&c)[4], uint32_t max_sym, uint32_t
       }
     }
   }
-  for (uint32_t k = lane; k < 512; k += 64) {
-    node0[k].count = 0;
-    node0[k].parent = 0;
-    node0[k].byte = 0;
-    node0[k].nb = 0;
-  }
-  lds_sync();
   uint32_t nnz = 0;
 #pragma unroll
   for (uint32_t g = 0; g < 4; ++g) {
@@ -661,74 +710,102 @@ __device__ uint32_t huf_build(const uint32_t (&c)[4], uint32_t max_sym, uint32_t
     nnz += __popcll(__ballot(s <= max_sym && c[g] != 0));
   }
   lds_sync();
-  const int32_t non_null = static_cast<int32_t>(nnz) - 1;
-  constexpr int32_t kStart = 256;
-  int32_t low_s = non_null;
-  int32_t node_nb = kStart;
-  const int32_t node_root = node_nb + low_s - 1;
-  int32_t low_n = node_nb;
-  for (int32_t k = node_nb + 1 + static_cast<int32_t>(lane); k <= node_root; k += 64)
-    node[k].count = 1u << 30;
-  if (lane == 0) {
-    node[node_nb].count = node[low_s].count + node[low_s - 1].count;
-    node[low_s].parent = static_cast<uint16_t>(node_nb);
-    node[low_s - 1].parent = static_cast<uint16_t>(node_nb);
-    node0[0].count = 1u << 31;
+  // the sorted leaves, a rank a lane
+  uint32_t L[4], S[4];
+#pragma unroll
+  for (uint32_t g = 0; g < 4; ++g) {
+    const uint32_t r = g * 64u + lane;
+    L[g] = r <= max_sym ? node[r].count : 0u;
+    S[g] = r <= max_sym ? node[r].byte : 0u;
   }
-  lds_sync();
-  ++node_nb;
+  const uint32_t non_null = nnz - 1u;  // (nnz >= 2: one symbol is the RLE case)
+  constexpr uint32_t kBarrier = 1u << 31, kUnmade = 1u << 30;
+  // created node k (k = node number - 256): counts IC, parents of leaves PL
+  // and of created nodes PI (as created-node numbers)
+  uint32_t IC[4] = {kUnmade, kUnmade, kUnmade, kUnmade}, PL[4] = {0, 0, 0, 0},
+           PI[4] = {0, 0, 0, 0};
+  const uint32_t root = non_null - 1u;  // the last created node
+  int32_t low_s = static_cast<int32_t>(non_null);
+  {
+    const uint32_t c1 = rd256(L, non_null), c0 = rd256(L, non_null - 1u);
+    wr256(IC, 0, c1 + c0);
+    wr256(PL, non_null, 0);
+    wr256(PL, non_null - 1u, 0);
+  }
   low_s -= 2;
-  // the merges: two smallest of the sorted leaves (from low_s down) and the
-  // created nodes (from low_n up), ties to the created node
-  uint32_t cs = uni(node[low_s].count), cn = uni(node[low_n].count);
-  while (node_nb <= node_root) {
-    int32_t n1, n2;
+  uint32_t low_n = 0, made = 1;
+  uint32_t cs = low_s >= 0 ? rd256(L, static_cast<uint32_t>(low_s)) : kBarrier;
+  uint32_t cn = rd256(IC, 0);
+  while (made <= root) {
     uint32_t c1, c2;
+    // n1
     if (cs < cn) {
-      n1 = low_s--;
       c1 = cs;
-      cs = uni(node[low_s].count);
+      wr256(PL, static_cast<uint32_t>(low_s), made);
+      --low_s;
+      cs = low_s >= 0 ? rd256(L, static_cast<uint32_t>(low_s)) : kBarrier;
     } else {
-      n1 = low_n++;
       c1 = cn;
-      cn = uni(node[low_n].count);
+      wr256(PI, low_n, made);
+      ++low_n;
+      cn = low_n < made ? rd256(IC, low_n) : kUnmade;
     }
+    // n2
     if (cs < cn) {
-      n2 = low_s--;
       c2 = cs;
-      cs = uni(node[low_s].count);
+      wr256(PL, static_cast<uint32_t>(low_s), made);
+      --low_s;
+      cs = low_s >= 0 ? rd256(L, static_cast<uint32_t>(low_s)) : kBarrier;
     } else {
-      n2 = low_n++;
       c2 = cn;
-      cn = uni(node[low_n].count);
+      wr256(PI, low_n, made);
+      ++low_n;
+      cn = low_n < made ? rd256(IC, low_n) : kUnmade;
     }
-    if (lane == 0) {
-      node[node_nb].count = c1 + c2;
-      node[n1].parent = static_cast<uint16_t>(node_nb);
-      node[n2].parent = static_cast<uint16_t>(node_nb);
+    wr256(IC, made, c1 + c2);
+    if (low_n == made) cn = c1 + c2;
+    ++made;
+  }
+  // depths: the created nodes from the root down, then every leaf at once
+  uint32_t DI[4] = {0, 0, 0, 0};
+  for (int32_t k = static_cast<int32_t>(root) - 1; k >= 0; --k)
+    wr256(DI, static_cast<uint32_t>(k), rd256(DI, rd256(PI, static_cast<uint32_t>(k))) + 1u);
+  uint32_t NB[4];
+  uint32_t deepest = 0;
+#pragma unroll
+  for (uint32_t g = 0; g < 4; ++g) {
+    const uint32_t r = g * 64u + lane;
+    const uint32_t d = gather256(DI, PL[g]) + 1u;
+    NB[g] = r <= non_null ? d : 0u;
+  }
+  deepest = rd256(NB, non_null);
+  if (deepest > max_nb) {  // HUF_setMaxHeight (on the LDS nodes)
+#pragma unroll
+    for (uint32_t g = 0; g < 4; ++g) {
+      const uint32_t r = g * 64u + lane;
+      if (r <= max_sym) node[r].nb = static_cast<uint8_t>(NB[g]);
     }
+    if (lane == 0) node0[0].nb = 0;
     lds_sync();
-    if (low_n == node_nb) cn = c1 + c2;  // (the node just made is next in line)
-    ++node_nb;
-  }
-  // depths: internal nodes from the root down, then the leaves
-  if (lane == 0) node[node_root].nb = 0;
-  lds_sync();
-  for (int32_t k = node_root - 1; k >= kStart; --k) {
-    if (lane == 0) node[k].nb = static_cast<uint8_t>(node[node[k].parent].nb + 1u);
+    max_nb = huf_set_max_height(node, static_cast<int32_t>(non_null), max_nb);
     lds_sync();
+#pragma unroll
+    for (uint32_t g = 0; g < 4; ++g) {
+      const uint32_t r = g * 64u + lane;
+      NB[g] = r <= non_null ? node[r].nb : 0u;
+    }
+  } else {
+    max_nb = deepest;
   }
-  for (int32_t k = static_cast<int32_t>(lane); k <= non_null; k += 64)
-    node[k].nb = static_cast<uint8_t>(node[node[k].parent].nb + 1u);
-  lds_sync();
-  max_nb = huf_set_max_height(node, non_null, max_nb);
-  lds_sync();
   // codes: valPerRank from the counts per bit length, then each symbol's
   // rank among the symbols of its length in symbol order
-  uint32_t nbs[4] = {0, 0, 0, 0};
-  for (int32_t k = static_cast<int32_t>(lane); k <= static_cast<int32_t>(max_sym); k += 64)
-    huf[node[k].byte] = k <= non_null ? static_cast<uint32_t>(node[k].nb) << 16 : 0u;
+#pragma unroll
+  for (uint32_t g = 0; g < 4; ++g) {
+    const uint32_t r = g * 64u + lane;
+    if (r <= max_sym) huf[S[g]] = NB[g] << 16;
+  }
   lds_sync();
+  uint32_t nbs[4];
 #pragma unroll
   for (uint32_t g = 0; g < 4; ++g) {
     const uint32_t s = g * 64u + lane;
@@ -775,7 +852,7 @@ __device__ uint32_t huf_build(const uint32_t (&c)[4], uint32_t max_sym, uint32_t
 
 // ---- the literals section (ZSTD_compressLiterals) ---------------------------
 
-__device__ uint32_t raw_literals(uint8_t* out, const uint8_t* lits, uint32_t n, uint32_t lane) {
+__device__ __forceinline__ uint32_t raw_literals(uint8_t* out, const uint8_t* lits, uint32_t n, uint32_t lane) {
   const uint32_t fl = 1u + (n > 31) + (n > 4095);
   if (lane == 0) {
     if (fl == 1) {
@@ -796,7 +873,7 @@ __device__ uint32_t raw_literals(uint8_t* out, const uint8_t* lits, uint32_t n, 
   return fl + n;
 }
 
-__device__ uint32_t rle_literals(uint8_t* out, const uint8_t* lits, uint32_t n, uint32_t lane) {
+__device__ __forceinline__ uint32_t rle_literals(uint8_t* out, const uint8_t* lits, uint32_t n, uint32_t lane) {
   const uint32_t fl = 1u + (n > 31) + (n > 4095);
   if (lane == 0) {
     if (fl == 1) {
@@ -820,7 +897,7 @@ __device__ uint32_t rle_literals(uint8_t* out, const uint8_t* lits, uint32_t n, 
 // HUF_writeCTable's weights through FSE (HUF_compressWeights) into buf (LDS,
 // dword-aligned): returns the bytes (0: no FSE form). w[g] = weight of
 // symbol g * 64 + lane for symbols < nw.
-__device__ uint32_t huf_compress_weights(const uint32_t (&w)[4], uint32_t nw, uint8_t* ent,
+__device__ __forceinline__ uint32_t huf_compress_weights(const uint32_t (&w)[4], uint32_t nw, uint8_t* ent,
                                          uint8_t* buf, uint32_t lane) {
   if (nw <= 1) return 0;
   // histogram of the weights (0..12): a value a lane
@@ -842,11 +919,10 @@ __device__ uint32_t huf_compress_weights(const uint32_t (&w)[4], uint32_t nw, ui
   mc = uni(mc);
   if (mc == nw || mc == 1) return 0;
   const uint32_t tl = fse_opt_log(6, nw, max_sym, 2);
-  int16_t* norm = reinterpret_cast<int16_t*>(ent + kENorm);
-  fse_normalize(cnt, tl, nw, max_sym, false, norm, lane);
+  const int32_t normv = fse_normalize(cnt, tl, nw, max_sym, false, lane);
   BitW bw;
   bw_init(bw, buf, 0);
-  fse_write_ncount(norm, max_sym, tl, bw, lane);
+  fse_write_ncount(normv, max_sym, tl, bw, lane);
   bw_flush(bw, lane);
   lds_sync();
   const uint32_t nc = bw_end(bw);
@@ -854,9 +930,10 @@ __device__ uint32_t huf_compress_weights(const uint32_t (&w)[4], uint32_t nw, ui
   FseC t;
   t.st = reinterpret_cast<uint16_t*>(ent + kEStW);
   t.log = tl;
-  fse_build_ctable(norm, max_sym, tl, reinterpret_cast<uint16_t*>(ent + kEStW), ent, lane, &t.dnb,
+  fse_build_ctable(normv, max_sym, tl, reinterpret_cast<uint16_t*>(ent + kEStW), ent, lane, &t.dnb,
                    &t.dfs);
   lds_sync();
+  fse_regs(t, lane);
   // the weights from the end, two interleaved states
   auto wat = [&](uint32_t i) -> uint32_t {
     const uint32_t g = i >> 6, l = i & 63u;
@@ -893,8 +970,8 @@ __device__ uint32_t huf_compress_weights(const uint32_t (&w)[4], uint32_t nw, ui
 }
 
 // The literals section into out (LDS, dword-aligned): its size.
-__device__ uint32_t compress_literals(uint8_t* out, const uint8_t* lits, uint32_t n, bool disable,
-                                      uint8_t* ent, HNode* nodes, uint32_t lane) {
+__device__ __forceinline__ uint32_t compress_literals(uint8_t* out, const uint8_t* lits, uint32_t n, bool disable,
+                                      uint8_t* ent, HNode* nodes, uint32_t lane, uint64_t* stamp) {
   if (disable || n <= 63) return raw_literals(out, lits, n, lane);
   uint32_t* cnt = reinterpret_cast<uint32_t*>(ent + kECnt);
   for (uint32_t k = lane; k < 256; k += 64) cnt[k] = 0;
@@ -927,7 +1004,9 @@ __device__ uint32_t compress_literals(uint8_t* out, const uint8_t* lits, uint32_
   // HUF_optimalTableLog, the tree, its description
   const uint32_t huf_log = fse_opt_log(11, n, max_sym, 1);
   uint32_t* huf = reinterpret_cast<uint32_t*>(ent + kEHuf);
+  zcstamp(stamp, 8);
   const uint32_t mb = huf_build(c, max_sym, huf_log, nodes, huf, lane);
+  zcstamp(stamp, 9);
   uint32_t w[4];
 #pragma unroll
   for (uint32_t g = 0; g < 4; ++g) {
@@ -937,6 +1016,7 @@ __device__ uint32_t compress_literals(uint8_t* out, const uint8_t* lits, uint32_
   }
   uint8_t* wbuf = ent + kEWts;
   uint32_t hsize = huf_compress_weights(w, max_sym, ent, wbuf, lane);
+  zcstamp(stamp, 10);
   bool fse_form = hsize > 1 && hsize < max_sym / 2u;
   if (!fse_form) {
     if (max_sym > 128) return raw_literals(out, lits, n, lane);  // (HUF_writeCTable error)
@@ -973,6 +1053,7 @@ __device__ uint32_t compress_literals(uint8_t* out, const uint8_t* lits, uint32_
   const uint32_t total = hsize + jump + sz[0] + sz[1] + sz[2] + sz[3];
   if (total >= n - 1u) return raw_literals(out, lits, n, lane);  // HUF: not worth it
   if (total >= n - min_gain) return raw_literals(out, lits, n, lane);
+  zcstamp(stamp, 11);
   // pack: zero the streams' dwords, OR each chunk's bits in
   const uint32_t s0 = lh + hsize + jump;
   uint32_t* ow = reinterpret_cast<uint32_t*>(out);
@@ -1089,7 +1170,7 @@ __device__ __forceinline__ int32_t default_norm(uint32_t table, uint32_t s) {
 }
 
 // One of the three tables: type, description bytes through bw, the CTable.
-__device__ uint32_t seq_table(uint32_t table, const uint8_t* codes, uint32_t nbseq, uint8_t* ent,
+__device__ __forceinline__ uint32_t seq_table(uint32_t table, const uint8_t* codes, uint32_t nbseq, uint8_t* ent,
                               uint16_t* st, BitW& bw, FseC* t, uint32_t* desc_at, uint32_t lane) {
   uint32_t* cnt = reinterpret_cast<uint32_t*>(ent + kECnt);
   if (lane < 64) cnt[lane] = 0;
@@ -1109,7 +1190,6 @@ __device__ uint32_t seq_table(uint32_t table, const uint8_t* codes, uint32_t nbs
   const uint32_t dlog = table == 1 ? 5u : 6u;
   const bool allowed = table == 1 ? max_sym <= 28u : true;
   const uint32_t type = select_type(most, nbseq, dlog, allowed);
-  int16_t* norm = reinterpret_cast<int16_t*>(ent + kENorm);
   t->st = st;
   *desc_at = 0xFFFFFFFFu;
   if (type == 1) {  // FSE_buildCTable_rle: one state, no bits
@@ -1121,14 +1201,15 @@ __device__ uint32_t seq_table(uint32_t table, const uint8_t* codes, uint32_t nbs
     t->dfs = 0;
     t->log = 0;
     lds_sync();
+    fse_regs(*t, lane);
     return type;
   }
   uint32_t tl, ms;
+  int32_t normv;
   if (type == 0) {
     tl = dlog;
     ms = table == 0 ? 35u : (table == 1 ? 28u : 52u);
-    if (lane <= ms) norm[lane] = static_cast<int16_t>(default_norm(table, lane));
-    lds_sync();
+    normv = lane <= ms ? default_norm(table, lane) : 0;
   } else {
     const uint32_t fse_log = table == 1 ? 8u : 9u;
     tl = fse_opt_log(fse_log, nbseq, max_sym, 2);
@@ -1139,9 +1220,9 @@ __device__ uint32_t seq_table(uint32_t table, const uint8_t* codes, uint32_t nbs
       if (lane == last) c -= 1u;
       --n1;
     }
-    fse_normalize(c, tl, n1, max_sym, n1 >= 2048, norm, lane);
+    normv = fse_normalize(c, tl, n1, max_sym, n1 >= 2048, lane);
     *desc_at = bw_end(bw);
-    fse_write_ncount(norm, max_sym, tl, bw, lane);
+    fse_write_ncount(normv, max_sym, tl, bw, lane);
     // (the description ends on a byte: the next starts on a fresh one)
     const uint32_t pad = (8u - (bw.n & 7u)) & 7u;
     bw_add(bw, 0, pad, lane);
@@ -1149,9 +1230,10 @@ __device__ uint32_t seq_table(uint32_t table, const uint8_t* codes, uint32_t nbs
   }
   bw_flush(bw, lane);
   lds_sync();
-  fse_build_ctable(norm, ms, tl, st, ent, lane, &t->dnb, &t->dfs);
+  fse_build_ctable(normv, ms, tl, st, ent, lane, &t->dnb, &t->dfs);
   t->log = tl;
   lds_sync();
+  fse_regs(*t, lane);
   return type;
 }
 
@@ -1159,7 +1241,7 @@ __device__ uint32_t seq_table(uint32_t table, const uint8_t* codes, uint32_t nbs
 
 // A frame's header (ZSTD_writeFrameHeader): content size, single segment
 // when the window covers it. Returns its bytes (written by lane 0 to g).
-__device__ uint32_t frame_header(uint8_t* g, uint32_t wlog, uint32_t n, uint32_t lane) {
+__device__ __forceinline__ uint32_t frame_header(uint8_t* g, uint32_t wlog, uint32_t n, uint32_t lane) {
   const uint32_t single = (1u << wlog) >= n ? 1u : 0u;
   const uint32_t fcs = (n >= 256u) + (n >= 65536u + 256u);
   uint32_t p = 0;
@@ -1248,7 +1330,7 @@ __device__ __forceinline__ void store_seq(Seqs& s, const uint8_t* in, uint32_t a
 // ZSTD_compressBlock_fast_generic over the whole frame in[0, n) (one block:
 // n <= the window), 64 steps a window.
 template <typename TIdx>
-__device__ void match_block(const uint8_t* in, uint32_t n, TIdx* table, uint32_t* tags,
+__device__ __forceinline__ void match_block(const uint8_t* in, uint32_t n, TIdx* table, uint32_t* tags,
                             const ZParams& zp, Seqs& sq, uint32_t lane) {
   const uint32_t hlog = zp.hlog, mls = zp.mls;
   const uint32_t ss = zp.tl + (zp.tl ? 0u : 1u) + 1u;
@@ -1474,6 +1556,13 @@ __global__ void __launch_bounds__(64) zstd_compress_kernel(ZcArgs a) {
       a.status[b] = static_cast<uint8_t>(st);
     }
   };
+#ifdef LVKV_PROBE_BUILD
+  __shared__ uint64_t stamp_lds[16];
+  uint64_t* stamp = stamp_lds;
+#else
+  uint64_t* stamp = nullptr;
+#endif
+  zcstamp(stamp, 0);
   const ZParams zp = zstd_port_params(a.level, n);
   if (!zp.ok) return finish(LVKV_ZSTD_UNSUPPORTED, 0);
   if (n > a.max_len) return finish(LVKV_ZSTD_TOO_LARGE, 0);
@@ -1506,14 +1595,17 @@ __global__ void __launch_bounds__(64) zstd_compress_kernel(ZcArgs a) {
     for (uint32_t k = lane; k < kTags; k += 64) tags[k] = 0xFFFFFFFFu;
   }
   lds_sync();
+  zcstamp(stamp, 1);
   match_block<TIdx>(in, n, table, tags, zp, sq, lane);
+  zcstamp(stamp, 2);
   // ---- entropy (the input region becomes the block's staging buffer)
   uint8_t* out = in;
   uint8_t* ent = reinterpret_cast<uint8_t*>(table);
   HNode* nodes = reinterpret_cast<HNode*>(tags);
   const uint32_t nseq = sq.nseq;
   const uint32_t limit = n - ((n >> 6) + 2u);  // a body at least this long: raw
-  uint32_t pos = compress_literals(out, sq.lits, sq.nlit, zp.tl > 0, ent, nodes, lane);
+  uint32_t pos = compress_literals(out, sq.lits, sq.nlit, zp.tl > 0, ent, nodes, lane, stamp);
+  zcstamp(stamp, 3);
   if (pos + 1u >= limit) return raw_block();  // (the smallest body: + the count byte)
   // sequences header
   if (lane == 0) {
@@ -1554,14 +1646,29 @@ __global__ void __launch_bounds__(64) zstd_compress_kernel(ZcArgs a) {
     const uint32_t ty_ml = seq_table(2, mlc, nseq, ent, reinterpret_cast<uint16_t*>(ent + kEStML),
                                      bw, &tml, &at_ml, lane);
     uint32_t last_nc = at_ml != 0xFFFFFFFFu ? at_ml : (at_of != 0xFFFFFFFFu ? at_of : at_ll);
+    zcstamp(stamp, 4);
     if (lane == 0) out[seq_head] = static_cast<uint8_t>((ty_ll << 6) + (ty_of << 4) + (ty_ml << 2));
     lds_sync();
     // the backward bitstream (ZSTD_encodeSequences)
     const uint32_t bs_start = bw_end(bw);
     bw_init(bw, out, bs_start);
+    // the sequences 64 at a time in registers (lane k: sequence base + k),
+    // read by the serial coder with v_readlane
+    uint32_t base = (nseq - 1u) & ~63u;
+    uint32_t rv = 0, ro = 0, rc = 0;
+    auto load = [&](uint32_t b0) {
+      const uint32_t k = b0 + lane;
+      rv = k < nseq ? sq.sll[k] : 0u;
+      ro = k < nseq ? sq.sof[k] : 0u;
+      rc = k < nseq ? (llc[k] | (static_cast<uint32_t>(ofc[k]) << 8) |
+                       (static_cast<uint32_t>(mlc[k]) << 16))
+                    : 0u;
+    };
+    load(base);
     uint32_t i = nseq - 1u;
-    uint32_t v = uni(sq.sll[i]), of = uni(sq.sof[i]);
-    uint32_t cl = uni(llc[i]), co = uni(ofc[i]), cm = uni(mlc[i]);
+    uint32_t v = __builtin_amdgcn_readlane(rv, i - base), of = __builtin_amdgcn_readlane(ro, i - base);
+    uint32_t cc = __builtin_amdgcn_readlane(rc, i - base);
+    uint32_t cl = cc & 255u, co = (cc >> 8) & 255u, cm = cc >> 16;
     uint32_t sm = fse_init(tml, cm), so = fse_init(tof, co), sl = fse_init(tll, cl);
     bw_add(bw, v & 0xFFFFu, ll_bits(cl), lane);
     bw_add(bw, v >> 16, ml_bits(cm), lane);
@@ -1569,11 +1676,16 @@ __global__ void __launch_bounds__(64) zstd_compress_kernel(ZcArgs a) {
     bool over = false;
     while (i > 0) {
       --i;
-      v = uni(sq.sll[i]);
-      of = uni(sq.sof[i]);
-      cl = uni(llc[i]);
-      co = uni(ofc[i]);
-      cm = uni(mlc[i]);
+      if (i < base) {
+        base -= 64u;
+        load(base);
+      }
+      v = __builtin_amdgcn_readlane(rv, i - base);
+      of = __builtin_amdgcn_readlane(ro, i - base);
+      cc = __builtin_amdgcn_readlane(rc, i - base);
+      cl = cc & 255u;
+      co = (cc >> 8) & 255u;
+      cm = cc >> 16;
       so = fse_enc(tof, so, co, bw, lane);
       sm = fse_enc(tml, sm, cm, bw, lane);
       sl = fse_enc(tll, sl, cl, bw, lane);
@@ -1586,6 +1698,7 @@ __global__ void __launch_bounds__(64) zstd_compress_kernel(ZcArgs a) {
       }
     }
     if (over) return raw_block();
+    zcstamp(stamp, 5);
     bw_add(bw, sm, tml.log, lane);
     bw_add(bw, so, tof.log, lane);
     bw_add(bw, sl, tll.log, lane);
@@ -1602,6 +1715,11 @@ __global__ void __launch_bounds__(64) zstd_compress_kernel(ZcArgs a) {
   if (lane < 3) g[fh + lane] = static_cast<uint8_t>(bh >> (8u * lane));
   for (uint32_t k = lane; k < pos; k += 64) g[fh + 3u + k] = out[k];
   finish(LVKV_ZSTD_OK, fh + 3u + pos);
+  zcstamp(stamp, 6);
+#ifdef LVKV_PROBE_BUILD
+  lds_sync();
+  if (a.stamps != nullptr && lane < 16) a.stamps[16u * b + lane] = stamp[lane];
+#endif
 }
 
 }  // namespace
@@ -1645,6 +1763,8 @@ uint32_t zstd_compress_lds(uint32_t max_len, int level) {
   return zstd_compress_plan(max_len < 16u ? 16u : max_len, level).lds;
 }
 
+uint64_t* g_zstdc_stamps = nullptr;  // lvkv_debug_zstdc_stamps (tools/probe)
+
 hipError_t launch_zstd_compress(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
                                 uint8_t* dst, const uint64_t* dst_off, uint32_t* dst_len,
                                 uint8_t* status, uint32_t nblocks, uint32_t max_len, int level,
@@ -1652,7 +1772,7 @@ hipError_t launch_zstd_compress(const uint8_t* src, const uint64_t* src_off, con
   const uint32_t cap = max_len < 16u ? 16u : max_len;
   const ZstdCompressPlan p = zstd_compress_plan(cap, level);
   ZcArgs a{src, src_off, src_len, dst, dst_off, dst_len, status, nblocks, level, max_len,
-           dst_stride, p.o_tbl, p.o_tag, p.o_lit, p.o_sll, p.o_sof, p.smax};
+           dst_stride, p.o_tbl, p.o_tag, p.o_lit, p.o_sll, p.o_sof, p.smax, g_zstdc_stamps};
   hipLaunchKernelGGL(zstd_compress_kernel<uint16_t>, dim3(nblocks), dim3(64), p.lds, stream, a);
   return hipGetLastError();
 }

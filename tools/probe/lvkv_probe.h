@@ -44,6 +44,10 @@ int lvkv_debug_read_bw(const void* d_data, uint64_t bytes, uint32_t* d_scratch,
  * 3 wave 2's records done, 4 all records, 5 long records, 6 merged. */
 void lvkv_debug_log_stamps(uint64_t* d_stamps);
 void lvkv_debug_zstd_stamps(uint64_t* d_stamps);  /* 8 s_memtime stamps a zstd frame */
+/* 16 s_memtime stamps a block of the zstd compressor: 0 start, 1 staged, 2
+ * matched, 8 literals counted, 9 tree built, 10 weights coded, 11 streams
+ * sized, 3 literals done, 4 sequence tables, 5 sequence bits, 6 end. */
+void lvkv_debug_zstdc_stamps(uint64_t* d_stamps);
 void lvkv_debug_asm_stamps(uint64_t* d_stamps);
 /* Whole-SSTable verify phase stamps: 16 u64 per table (head slots 0-7; the
  * fused form's first CRC workgroup in table 0's slots 8-10). NULL: off. */

@@ -92,6 +92,28 @@ def zstd_cpu_lines(frames, seconds: float = 2.0, procs: int = 16):
     return {k: round(v, 1) for k, v in res.items()}
 
 
+def zstd_compress_cpu_lines(blocks: np.ndarray, seconds: float = 2.0, procs: int = 16):
+    """libzstd 1.4.9 through port::Zstd_Compress's calls, per 4 KiB block at
+    level 1 (oracle/zstd_port_bench, a C harness): one core and `procs`
+    processes."""
+    import subprocess
+    import tempfile
+    exe = REPO / "oracle" / "zstd_port_bench"
+    if not exe.exists():
+        return None
+    with tempfile.NamedTemporaryFile(suffix=".bin") as f:
+        f.write(blocks.tobytes())
+        f.flush()
+        res = {}
+        for p in (1, procs):
+            out = subprocess.run([str(exe), f.name, "4096", "1", str(seconds), str(p)],
+                                 capture_output=True, text=True, check=True).stdout
+            r = json.loads(out)
+            res[f"comp_{'1t' if p == 1 else f'{p}p'}_MBps"] = r["MBps"]
+            res["output_pct"] = r["output_pct"]
+    return res
+
+
 def _zstd_worker(arg):
     frames, seconds = arg
     import ctypes
@@ -164,6 +186,7 @@ def main():
             b"".join(len(f).to_bytes(4, "little") + f for f in zframes))
         return
     zcpu = None if args.no_cpu or zframes is None else zstd_cpu_lines(zframes)
+    zccpu = None if args.no_cpu else zstd_compress_cpu_lines(block_batch(256))
     import torch
     import __graft_entry__ as g
     lvkv = g.load_package()
@@ -244,6 +267,33 @@ def main():
                                   "output_pct": round(100.0 * zbytes / raw, 2)}
         if zcpu is not None:
             res["cpu_libzstd_1_4_9"] = zcpu
+    # zstd compress (port::Zstd_Compress at level 1, LevelDB's default): the
+    # device compressor over the nb blocks, one launch
+    zb = L + (L >> 8) + ((131072 - L) >> 11)
+    zdst = torch.empty(nb * zb, dtype=torch.uint8, device=dev)
+    zdoff = torch.arange(nb, dtype=torch.int64, device=dev) * zb
+    zlen, zst = torch.empty_like(dlen), torch.empty_like(st)
+    t_zc = timed(lambda: lvkv.lib.lvkv_zstd_compress_device(
+        src.data_ptr(), off.data_ptr(), ln.data_ptr(), zdst.data_ptr(), zdoff.data_ptr(),
+        zlen.data_ptr(), zst.data_ptr(), nb, L, 1, stream.cuda_stream))
+    torch.cuda.synchronize()
+    assert int(zst.max()) == 0
+    zc_bytes = int(zlen.to(torch.int64).sum())
+    # parity on a sample (tests/test_zstd_write.py covers the rest): the
+    # library's own frame through the port's calls, or the oracle's
+    import zstd_encoder as ze
+    zlib_w = ze.system_zstd_writer()
+    zh = zdst.cpu().numpy()
+    for i in range(0, nb, max(1, nb // 64)):
+        blk = host[i * L:(i + 1) * L].tobytes()
+        want = ze.lib_port_compress(zlib_w, blk, 1) if zlib_w else ze.compress(blk, 1)
+        assert zh[i * zb:i * zb + int(zlen[i])].tobytes() == want, i
+    res["zstd_compress"] = {"us_per_launch": round(t_zc * 1e6, 1),
+                            "GBps_uncompressed": round(raw / t_zc / 1e9, 2),
+                            "hbm_GBps": round((raw + zc_bytes) / t_zc / 1e9, 2),
+                            "output_pct": round(100.0 * zc_bytes / raw, 2), "level": 1}
+    if zccpu is not None:
+        res["cpu_libzstd_1_4_9_port_compress"] = zccpu
     print(json.dumps(res), flush=True)
     (REPO / "gpurun_out").mkdir(exist_ok=True)
     (REPO / "gpurun_out" / "snappy_bench.json").write_text(json.dumps(res, indent=1))
