@@ -512,6 +512,142 @@ __global__ void __launch_bounds__(64) snappy_uncompress_kernel(UncompressArgs a)
   finish(LVKV_SNAPPY_OK, ulen);
 }
 
+// Blocks the LDS path hands back (TOO_LARGE: a longer output than the
+// call's LDS staging, or a stream past MaxCompressedLength of it) decoded
+// straight into the HBM output, any size (table/format.cc:120-135 reads
+// any block): the stream through an 8 KiB LDS window, the output written to
+// the destination as it is produced and its last 32 KiB also kept in an LDS
+// ring. A copy from within the ring reads LDS; a farther one reads the
+// destination, where every byte that old has landed: the wave waits for
+// its stores (vmcnt(0)) each time the output crosses 8 KiB. Runs after
+// snappy_uncompress_kernel over the same batch; a block it did not mark
+// TOO_LARGE exits at once.
+constexpr uint32_t kBigWin = 8192, kBigRing = 32768, kBigChunk = 32;
+
+__device__ __forceinline__ void snappy_big_block(const UncompressArgs& a, uint32_t b, uint8_t* smem, uint32_t lane) {
+  const uint32_t n = a.src_len[b];
+  const uint8_t* src = a.src + a.src_off[b];
+  // (ReadBlock mode: only snappy blocks; a zstd block's status is the zstd
+  // kernel's, launched next)
+  if (a.block_mode && __builtin_amdgcn_readfirstlane(src[n]) != 1u) return;
+  uint8_t* dst = a.dst + a.dst_off[b];
+  uint8_t* win = smem;                  // src[wbase, wbase + kBigWin) + 16 zero bytes
+  uint8_t* ring = smem + kBigWin + 16;  // out[p] at ring[p % kBigRing]
+  auto finish = [&](uint32_t st, uint32_t ol) {
+    if (lane == 0) {
+      a.status[b] = static_cast<uint8_t>(
+          a.block_mode ? (st == LVKV_SNAPPY_OK ? LVKV_READ_OK : LVKV_READ_SNAPPY_CONTENTS) : st);
+      a.out_len[b] = ol;
+    }
+  };
+  uint32_t ulen = 0;
+  const uint32_t pl = preamble(src, n, &ulen);  // (checked by the LDS path)
+  uint32_t wbase = 0, wlen = 0;
+  auto window = [&](uint32_t at) {  // the window from at (4-aligned)
+    wbase = at & ~3u;
+    wlen = n - wbase < kBigWin ? n - wbase : kBigWin;
+    stage(win, src + wbase, wlen, 16, lane);
+    __builtin_amdgcn_s_waitcnt(0);
+  };
+  window(pl);
+  uint32_t ip = pl, op = 0, flushed_at = 0;
+  bool ok = true;
+  while (ip < n) {
+    if (ip + 5u > wbase + wlen && wbase + wlen < n) window(ip);
+    const uint64_t t8 = ld64(win, ip - wbase);
+    const uint32_t tag = static_cast<uint32_t>(t8) & 255u;
+    ++ip;
+    if ((tag & 3u) == 0) {
+      uint64_t len64 = (tag >> 2) + 1u;
+      if (len64 > 60) {
+        const uint32_t k = static_cast<uint32_t>(len64) - 60u;
+        if (ip + k > n) {
+          ok = false;
+          break;
+        }
+        len64 = (((t8 >> 8) & ((uint64_t{1} << (8 * k)) - 1u)) + 1u) & 0xffffffffu;
+        ip += k;
+      }
+      if (len64 > n - ip || len64 > ulen - op) {
+        ok = false;
+        break;
+      }
+      const uint32_t len = static_cast<uint32_t>(len64);
+      // the bytes from global memory into the output and the ring
+      for (uint32_t k = lane; k < len; k += 64) {
+        const uint8_t v = src[ip + k];
+        dst[op + k] = v;
+        ring[(op + k) & (kBigRing - 1u)] = v;
+      }
+      ip += len;
+      op += len;
+    } else {
+      uint32_t len, off;
+      if ((tag & 3u) == 1) {
+        if (ip + 1 > n) {
+          ok = false;
+          break;
+        }
+        len = ((tag >> 2) & 7u) + 4u;
+        off = ((tag >> 5) << 8) | static_cast<uint32_t>((t8 >> 8) & 255u);
+        ip += 1;
+      } else if ((tag & 3u) == 2) {
+        if (ip + 2 > n) {
+          ok = false;
+          break;
+        }
+        len = (tag >> 2) + 1u;
+        off = static_cast<uint32_t>((t8 >> 8) & 0xffffu);
+        ip += 2;
+      } else {
+        if (ip + 4 > n) {
+          ok = false;
+          break;
+        }
+        len = (tag >> 2) + 1u;
+        off = static_cast<uint32_t>((t8 >> 8) & 0xffffffffu);
+        ip += 4;
+      }
+      if (off == 0 || off > op || len > ulen - op) {
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // (the ring's earlier bytes have landed)
+      if (lane < len) {
+        const uint32_t k = off >= len ? lane : lane % off;
+        const uint32_t from = op - off + k;
+        const uint8_t v = off <= kBigRing - 64u ? ring[from & (kBigRing - 1u)] : dst[from];
+        dst[op + lane] = v;
+        ring[(op + lane) & (kBigRing - 1u)] = v;
+      }
+      op += len;
+    }
+    if (op - flushed_at >= kBigWin) {  // every byte before flushed_at is in HBM
+      __builtin_amdgcn_s_waitcnt(0);
+      flushed_at = op;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  if (!ok || op != ulen) return finish(LVKV_SNAPPY_BAD_CONTENTS, ulen);
+  finish(LVKV_SNAPPY_OK, ulen);
+}
+
+// One workgroup per 32 blocks: their statuses in one load, then the marked
+// ones one after another (a batch without big blocks costs a short launch).
+__global__ void __launch_bounds__(64) snappy_uncompress_big_kernel(UncompressArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t b0 = blockIdx.x * kBigChunk;
+  const uint32_t mark = a.block_mode ? LVKV_READ_TOO_LARGE : LVKV_SNAPPY_TOO_LARGE;
+  const bool mine = lane < kBigChunk && b0 + lane < a.nblocks && a.status[b0 + lane] == mark;
+  uint64_t todo = __ballot(mine);
+  while (todo) {
+    const uint32_t b = b0 + static_cast<uint32_t>(__builtin_ctzll(todo));
+    todo &= todo - 1u;
+    snappy_big_block(a, b, smem, lane);
+  }
+}
+
 // ---- TableBuilder::WriteBlock over a batch (table/table_builder.cc:141-209) --
 
 __device__ __forceinline__ uint64_t shfl_up64(uint64_t v, uint32_t d) {
@@ -659,6 +795,8 @@ hipError_t launch_sst_read_blocks(const uint8_t* file, const uint64_t* hoff, con
   a.out_cap = max(16u, max_ulen);
   const size_t lds = ((snappy_in_cap(a.out_cap) + 16u + 15u) & ~15u) + ((a.out_cap + 15u) & ~15u);
   hipLaunchKernelGGL(snappy_uncompress_kernel, dim3(nblocks), dim3(64), lds, stream, a);
+  hipLaunchKernelGGL(snappy_uncompress_big_kernel, dim3((nblocks + kBigChunk - 1u) / kBigChunk),
+                     dim3(64), kBigWin + 16u + kBigRing, stream, a);
   return hipGetLastError();
 }
 
@@ -686,6 +824,10 @@ hipError_t launch_snappy_uncompress(const uint8_t* src, const uint64_t* src_off,
                                         : ((snappy_in_cap(a.out_cap) + 16u + 15u) & ~15u) +
                                               ((a.out_cap + 15u) & ~15u);
   hipLaunchKernelGGL(snappy_uncompress_kernel, dim3(nblocks), dim3(64), lds, stream, a);
+  if (dst_cap != nullptr)  // (the blocks past the LDS staging, any size)
+    hipLaunchKernelGGL(snappy_uncompress_big_kernel,
+                       dim3((nblocks + kBigChunk - 1u) / kBigChunk), dim3(64),
+                       kBigWin + 16u + kBigRing, stream, a);
   return hipGetLastError();
 }
 

@@ -338,7 +338,9 @@ __constant__ uint8_t kMLBits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
 struct Lds {
   uint8_t* in;      // the staged frame (+16 zero bytes)
   uint8_t* out;     // the frame's output
-  uint16_t* huf;    // Huffman decode table: symbol | nbBits << 8 (<= 4096)
+  uint16_t* huf;    // Huffman decode table: symbol | nbBits << 8 (2048; a 12-bit
+                    // tree in split form, huf_table)
+  uint8_t* hside;   // a 12-bit tree's second symbols of its split entries (128)
   uint32_t* ll;     // FSE tables: 512 / 256 / 512 entries, and 64 for weights
   uint32_t* of;
   uint32_t* ml;
@@ -348,7 +350,7 @@ struct Lds {
   uint8_t* sym;     // FSE spread scratch (512)
 };
 
-constexpr uint32_t kHufEntries = 4096, kFseLL = 512, kFseOF = 256, kFseML = 512, kFseW = 64;
+constexpr uint32_t kHufEntries = 2048, kFseLL = 512, kFseOF = 256, kFseML = 512, kFseW = 64;
 
 __host__ __device__ constexpr uint32_t zstd_in_cap(uint32_t out_cap) {
   // ZSTD_compressBound(out_cap) (1.4.9): every frame the library writes
@@ -357,7 +359,7 @@ __host__ __device__ constexpr uint32_t zstd_in_cap(uint32_t out_cap) {
 __host__ __device__ constexpr uint32_t round16(uint32_t x) { return (x + 15u) & ~15u; }
 __host__ __device__ constexpr uint32_t zstd_lds_bytes(uint32_t out_cap) {
   return round16(zstd_in_cap(out_cap) + 16u + 4u) + round16(out_cap) +
-         2u * kHufEntries + 4u * (kFseLL + kFseOF + kFseML + kFseW) + 512u + 512u + 512u;
+         2u * kHufEntries + 128u + 4u * (kFseLL + kFseOF + kFseML + kFseW) + 512u + 512u + 512u;
 }
 
 __device__ Lds lds_layout(uint8_t* smem, uint32_t out_cap) {
@@ -369,6 +371,8 @@ __device__ Lds lds_layout(uint8_t* smem, uint32_t out_cap) {
   o += round16(out_cap);
   L.huf = reinterpret_cast<uint16_t*>(smem + o);
   o += 2u * kHufEntries;
+  L.hside = smem + o;
+  o += 128u;
   L.ll = reinterpret_cast<uint32_t*>(smem + o);
   o += 4u * kFseLL;
   L.of = reinterpret_cast<uint32_t*>(smem + o);
@@ -532,9 +536,15 @@ __device__ bool huf_weights(const Lds& L, uint32_t p, uint32_t end, uint32_t (&w
 // 2^(w-1) entries of 2^maxbits.
 // A level at a time: its symbols listed in order (ballot ranks, into the
 // nxt scratch), then its entries filled 64 at a time from the list.
+// A 12-bit tree (HUF_TABLELOG_MAX) keeps 2048 entries indexed by the top 11
+// bits: its weight-1 symbols (12-bit codes, an even count, first in the
+// table) pair up into split entries (nbBits field 15; the symbol of the
+// 12th bit 0 in the entry, of bit 1 in hside), every other level fills
+// 2^(w-2) entries with its real bit count.
 __device__ void huf_table(const Lds& L, const uint32_t (&w)[4], uint32_t mb, uint32_t lane) {
   uint8_t* list = reinterpret_cast<uint8_t*>(L.nxt);
   const uint64_t below = (uint64_t{1} << lane) - 1u;
+  const bool wide = mb == 12u;
   uint32_t pos = 0, lpos = 0;
   for (uint32_t wgt = 1; wgt <= mb; ++wgt) {
     const uint32_t lpos0 = lpos;
@@ -545,10 +555,21 @@ __device__ void huf_table(const Lds& L, const uint32_t (&w)[4], uint32_t mb, uin
       if (mine) list[lpos + __popcll(m & below)] = static_cast<uint8_t>(64u * g + lane);
       lpos += __popcll(m);
     }
-    const uint32_t n = (lpos - lpos0) << (wgt - 1u);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    const uint32_t cnt = lpos - lpos0;
+    if (wide && wgt == 1u) {  // pairs of 12-bit codes
+      for (uint32_t k = lane; 2u * k < cnt; k += 64) {
+        L.huf[k] = static_cast<uint16_t>(list[lpos0 + 2u * k] | (15u << 8));
+        L.hside[k] = list[lpos0 + 2u * k + 1u];
+      }
+      pos += cnt >> 1;
+      continue;
+    }
+    const uint32_t sh = wide ? wgt - 2u : wgt - 1u;  // log2 of a symbol's span
+    const uint32_t n = cnt << sh;
     const uint32_t e = (mb + 1u - wgt) << 8;
     for (uint32_t k = lane; k < n; k += 64)
-      L.huf[pos + k] = static_cast<uint16_t>(list[lpos0 + (k >> (wgt - 1u))] | e);
+      L.huf[pos + k] = static_cast<uint16_t>(list[lpos0 + (k >> sh)] | e);
     pos += n;
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -557,6 +578,7 @@ __device__ void huf_table(const Lds& L, const uint32_t (&w)[4], uint32_t mb, uin
 // Symbols that start above bit `floor`, from bit position `pos` down (one
 // lane's segment of a stream at in[lo, ...)): the exit position; *count
 // symbols, the first `lim` of them written at dst (when dst is set).
+template <bool Wide>
 __device__ __forceinline__ int32_t huf_run(const Lds& L, uint32_t lo, int32_t pos, int32_t floor,
                                            uint32_t mb, uint8_t* dst, uint32_t lim,
                                            uint32_t* count) {
@@ -566,7 +588,7 @@ __device__ __forceinline__ int32_t huf_run(const Lds& L, uint32_t lo, int32_t po
   uint32_t c = 0;
   while (pos > floor) {
     // the window holds bits [wlo, wlo + 64): refilled so that it covers the
-    // next four symbols (<= 44 bits); near the stream's start it is the
+    // next four symbols (<= 48 bits); near the stream's start it is the
     // first 64 bits and an index below bit 0 shifts up, zeros below
     if (pos - 4 * static_cast<int32_t>(mb) < wlo && wlo > 0) {
       int32_t cb = ((pos + 7) >> 3) - 8;
@@ -580,7 +602,13 @@ __device__ __forceinline__ int32_t huf_run(const Lds& L, uint32_t lo, int32_t po
       const bool live = pos > floor;
       const int32_t d = pos - static_cast<int32_t>(mb) - wlo;
       const uint32_t idx = static_cast<uint32_t>(d >= 0 ? win >> d : win << -d) & mask;
-      const uint32_t e = L.huf[idx];
+      uint32_t e;
+      if (Wide) {  // 2048 entries by the top 11 of 12 bits; split entries
+        e = L.huf[idx >> 1];
+        if ((e >> 8) == 15u) e = ((idx & 1u) ? L.hside[idx >> 1] : (e & 255u)) | (12u << 8);
+      } else {
+        e = L.huf[idx];
+      }
       if (dst != nullptr && live && c < lim) dst[c] = static_cast<uint8_t>(e & 255u);
       pos -= live ? static_cast<int32_t>(e >> 8) : 0;
       c += live ? 1u : 0u;
@@ -588,6 +616,12 @@ __device__ __forceinline__ int32_t huf_run(const Lds& L, uint32_t lo, int32_t po
   }
   *count = c;
   return pos;
+}
+__device__ __forceinline__ int32_t huf_run_any(const Lds& L, uint32_t lo, int32_t pos,
+                                               int32_t floor, uint32_t mb, uint8_t* dst,
+                                               uint32_t lim, uint32_t* count) {
+  return mb == 12u ? huf_run<true>(L, lo, pos, floor, mb, dst, lim, count)
+                   : huf_run<false>(L, lo, pos, floor, mb, dst, lim, count);
 }
 
 // ---- a frame --------------------------------------------------------------
@@ -753,12 +787,12 @@ __device__ bool literals(const Lds& L, uint32_t p, uint32_t end, uint32_t cap, u
   int32_t floor = P - static_cast<int32_t>(k + 1u) * seglen;
   if (floor < 0) floor = 0;
   uint32_t cnt = 0;
-  int32_t x = huf_run(L, slo, top, floor, mb, nullptr, 0, &cnt);
+  int32_t x = huf_run_any(L, slo, top, floor, mb, nullptr, 0, &cnt);
   for (uint32_t it = 0; it < S; ++it) {
     int32_t entry = __shfl_up(x, 1, static_cast<int>(S));
     if (k == 0) entry = P;
     uint32_t c2 = 0;
-    const int32_t x2 = huf_run(L, slo, entry, floor, mb, nullptr, 0, &c2);
+    const int32_t x2 = huf_run_any(L, slo, entry, floor, mb, nullptr, 0, &c2);
     const bool moved = x2 != x;
     x = x2;
     cnt = c2;
@@ -775,7 +809,7 @@ __device__ bool literals(const Lds& L, uint32_t p, uint32_t end, uint32_t cap, u
   int32_t entry = __shfl_up(x, 1, static_cast<int>(S));
   if (k == 0) entry = P;
   uint32_t c3 = 0;
-  huf_run(L, slo, entry, floor, mb, out_end - n + sbase + off, scnt > off ? scnt - off : 0u,
+  huf_run_any(L, slo, entry, floor, mb, out_end - n + sbase + off, scnt > off ? scnt - off : 0u,
           &c3);
   // the sequential decoder's verdict: exactly scnt symbols ending at bit 0
   good = total == scnt && last == 0;
