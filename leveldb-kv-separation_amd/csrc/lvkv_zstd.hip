@@ -357,18 +357,25 @@ __host__ __device__ constexpr uint32_t zstd_in_cap(uint32_t out_cap) {
   return out_cap + (out_cap >> 8) + (out_cap < (128u << 10) ? ((128u << 10) - out_cap) >> 11 : 0u);
 }
 __host__ __device__ constexpr uint32_t round16(uint32_t x) { return (x + 15u) & ~15u; }
+constexpr uint32_t kTabBytes =
+    2u * kHufEntries + 128u + 4u * (kFseLL + kFseOF + kFseML + kFseW) + 512u + 512u + 512u;
 __host__ __device__ constexpr uint32_t zstd_lds_bytes(uint32_t out_cap) {
-  return round16(zstd_in_cap(out_cap) + 16u + 4u) + round16(out_cap) +
-         2u * kHufEntries + 128u + 4u * (kFseLL + kFseOF + kFseML + kFseW) + 512u + 512u + 512u;
+  return round16(zstd_in_cap(out_cap) + 16u + 4u) + round16(out_cap) + kTabBytes;
 }
+// The HBM-output kernel's input window: a compressed block (< 128 KiB) from
+// any 4-aligned start, + slack for the register-window reads past its end.
+constexpr uint32_t kZWin = (128u << 10) + 64u, kZWinBytes = kZWin + 512u, kZBigChunk = 32;
+constexpr uint32_t kZBigLds = kZWinBytes + kTabBytes;
 
-__device__ Lds lds_layout(uint8_t* smem, uint32_t out_cap) {
+// in_bytes of input staging, then out_bytes of output (0: the output is in
+// HBM), then the tables
+__device__ __forceinline__ Lds lds_layout(uint8_t* smem, uint32_t in_bytes, uint32_t out_bytes) {
   Lds L;
   uint32_t o = 0;
   L.in = smem;
-  o += round16(zstd_in_cap(out_cap) + 16u + 4u);
+  o += in_bytes;
   L.out = smem + o;
-  o += round16(out_cap);
+  o += out_bytes;
   L.huf = reinterpret_cast<uint16_t*>(smem + o);
   o += 2u * kHufEntries;
   L.hside = smem + o;
@@ -861,6 +868,7 @@ struct SeqState {
   bool have_ll, have_of, have_ml, have_tree;
   uint32_t ll_log, of_log, ml_log, mb_tree;
   uint32_t rep0, rep1, rep2;
+  uint32_t flushed;  // HBM-output mode: every output byte below it has landed
 };
 
 // Copies n bytes from LDS `from` to out[op, ...): lanes 64 at a time. An
@@ -883,7 +891,7 @@ struct Tabs {
 
 // The nseq sequences of a block (RFC 8878 §3.1.1.4-5): decode, execute, and
 // the literals left after the last. Small: every table fits in registers.
-template <bool Small>
+template <bool Small, bool Global>
 __device__ __forceinline__ bool sequences(const Lds& L, RegBits& r, SeqState& S, const Tabs& T,
                                           uint32_t nseq, uint32_t nlit, const uint8_t* lits,
                                           uint32_t* op, uint32_t frame_start, uint32_t cap,
@@ -950,6 +958,12 @@ __device__ __forceinline__ bool sequences(const Lds& L, RegBits& r, SeqState& S,
     lp += ll;
     *op += ll;
     if (off > *op - frame_start) return *fail = kFOffset, false;
+    // (HBM output: a match that reads bytes whose stores may still be in
+    // flight waits for them; recent offsets do, far ones mostly do not)
+    if (Global && *op - off + (ml < off ? ml : off) > S.flushed) {
+      __builtin_amdgcn_s_waitcnt(0);
+      S.flushed = *op;
+    }
     lds_copy(L.out + *op, L.out + (*op - off), ml, off, lane);
     *op += ml;
   }
@@ -964,6 +978,9 @@ __device__ __forceinline__ bool sequences(const Lds& L, RegBits& r, SeqState& S,
 
 
 // A compressed block at in[p, end): output appended at out[*op, ...).
+// Global: out is the HBM destination (the literals' stores land before
+// the sequences read them).
+template <bool Global>
 __device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
                            uint32_t frame_start, uint32_t cap, SeqState& S, uint32_t lane,
                            uint32_t* fail) {
@@ -971,6 +988,7 @@ __device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
   if (!literals(L, p, end, cap - *op, L.out + cap, &S.have_tree, &S.mb_tree, &nlit, &used, lane,
                 fail, S.stamp))
     return false;
+  if (Global) __builtin_amdgcn_s_waitcnt(0);
   const uint8_t* lits = L.out + (cap - nlit);
   zstamp(S.stamp, 2, lane);
   uint32_t q = p + used;
@@ -1026,8 +1044,8 @@ __device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
   __builtin_amdgcn_s_waitcnt(0xc07f);
   const Tabs T{tll, tof, tml, S.ll_log <= 6u, S.of_log <= 6u, S.ml_log <= 6u};
   if (T.sll && T.sof && T.sml)
-    return sequences<true>(L, r, S, T, nseq, nlit, lits, op, frame_start, cap, lane, fail);
-  return sequences<false>(L, r, S, T, nseq, nlit, lits, op, frame_start, cap, lane, fail);
+    return sequences<true, Global>(L, r, S, T, nseq, nlit, lits, op, frame_start, cap, lane, fail);
+  return sequences<false, Global>(L, r, S, T, nseq, nlit, lits, op, frame_start, cap, lane, fail);
 }
 
 // XXH64 of out[0, n) (seed 0): the frame checksum. Scalar, from LDS.
@@ -1082,11 +1100,100 @@ __device__ __forceinline__ uint64_t xxh64(const uint8_t* base, uint32_t o, uint3
   return h;
 }
 
-__global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const uint32_t b = blockIdx.x;
-  if (b >= a.nblocks) return;
-  const uint32_t lane = threadIdx.x;
+// XXH64 of p[0, n) in HBM (seed 0; any alignment): 1 KiB a round, four
+// aligned dwords a lane (none starting past the end), the next round's
+// loads issued before this round's 32 stripes are folded in by v_readlane.
+__device__ __forceinline__ uint64_t xxh64_hbm(const uint8_t* p, uint32_t n, uint32_t lane) {
+  const uint64_t P1 = 11400714785074694791ull, P2 = 14029467366897019727ull,
+                 P3 = 1609587929392839161ull, P4 = 9650029242287828579ull,
+                 P5 = 2870177450012600261ull;
+  const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)) & 3u;
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(p - mis);
+  const uint32_t nd = (mis + n + 3u) >> 2;
+  // register j of round c: bytes p[1024 c + 256 j + 4 lane, + 4)
+  auto fetch = [&](uint32_t c, uint32_t* w) {
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint32_t i = 256u * c + 64u * j + lane;
+      const uint32_t lo = i < nd ? d[i] : 0u;
+      const uint32_t hi = mis != 0 && i + 1u < nd ? d[i + 1u] : 0u;
+      w[j] = __builtin_amdgcn_alignbyte(hi, lo, mis);
+    }
+  };
+  auto dw = [&](const uint32_t* w, uint32_t b) -> uint32_t {  // the dword at round byte b
+    const uint32_t j = b >> 8;
+    const uint32_t v = j == 0 ? w[0] : j == 1 ? w[1] : j == 2 ? w[2] : w[3];
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(v, (b >> 2) & 63u));
+  };
+  auto qw = [&](const uint32_t* w, uint32_t b) -> uint64_t {
+    return static_cast<uint64_t>(dw(w, b + 4u)) << 32 | dw(w, b);
+  };
+  auto rnd = [&](uint64_t v, uint64_t x) { return rotl64(v + x * P2, 31) * P1; };
+  uint32_t w[4], wn[4];
+  fetch(0, w);
+  uint32_t i = 0, c = 0;
+  uint64_t h;
+  if (n >= 32) {
+    uint64_t v1 = P1 + P2, v2 = P2, v3 = 0, v4 = 0 - P1;
+    for (;;) {
+      fetch(c + 1u, wn);
+      bool more = true;
+#pragma unroll
+      for (uint32_t s = 0; s < 32; ++s) {
+        if (more && i + 32u <= n) {
+          v1 = rnd(v1, qw(w, 32u * s));
+          v2 = rnd(v2, qw(w, 32u * s + 8u));
+          v3 = rnd(v3, qw(w, 32u * s + 16u));
+          v4 = rnd(v4, qw(w, 32u * s + 24u));
+          i += 32u;
+        } else {
+          more = false;
+        }
+      }
+      if (!more) break;
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) w[j] = wn[j];
+      ++c;
+    }
+    h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+    h = xxh_merge(h, v1, P1, P2, P4);
+    h = xxh_merge(h, v2, P1, P2, P4);
+    h = xxh_merge(h, v3, P1, P2, P4);
+    h = xxh_merge(h, v4, P1, P2, P4);
+  } else {
+    h = P5;
+  }
+  h += n;
+  // the < 32 bytes left, all in round c's registers
+  for (; i + 8u <= n; i += 8u) {
+    h ^= rotl64(qw(w, i & 1023u) * P2, 31) * P1;
+    h = rotl64(h, 27) * P1 + P4;
+  }
+  if (i + 4u <= n) {
+    h ^= static_cast<uint64_t>(dw(w, i & 1023u)) * P1;
+    h = rotl64(h, 23) * P2 + P3;
+    i += 4u;
+  }
+  for (; i < n; ++i) {
+    h ^= ((dw(w, i & 1020u) >> (8u * (i & 3u))) & 255u) * P5;
+    h = rotl64(h, 11) * P1;
+  }
+  h ^= h >> 33;
+  h *= P2;
+  h ^= h >> 29;
+  h *= P3;
+  h ^= h >> 32;
+  return h;
+}
+
+// One stream b (RFC 8878 frames one after another). LDS mode: the stream
+// staged whole, the output built in LDS and copied out; a stream past the
+// staging is marked TOO_LARGE. Global (zstd_uncompress_big_kernel, for the
+// streams so marked): the input read through a window of one block at a
+// time (kZWin), the output written straight into the HBM destination.
+template <bool Global>
+__device__ __forceinline__ void zstd_stream(const ZArgs& a, uint32_t b, uint8_t* smem,
+                                            uint32_t lane) {
   uint32_t n = uni(a.src_len[b]);
   const uint64_t so = a.src_off[b];
   const uint8_t* src =
@@ -1107,7 +1214,8 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
   const uint32_t kBig = a.block_mode ? LVKV_READ_TOO_LARGE : LVKV_SNAPPY_TOO_LARGE;
   if (a.block_mode) {  // only type-2 blocks whose checksum held (the rest are done)
     if (ldb(src, n) != 2) return;
-    if (a.vstatus != nullptr && uni(a.vstatus[b]) != 0) return;
+    // (Global: the mark this kernel's LDS pass left is the verdict slot)
+    if (!Global && a.vstatus != nullptr && uni(a.vstatus[b]) != 0) return;
   }
   // port::Zstd_GetUncompressedLength: ZSTD_getFrameContentSize, false on 0
   // (a skippable frame reads as 0; a malformed header as ERROR, passed on)
@@ -1137,14 +1245,38 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
                                  : finish(kOK, static_cast<uint32_t>(csize), kFOk);
   const uint32_t cap = uni(a.dst_cap[b]);
   if (csize > cap) return finish(kCap, csize > 0xFFFFFFFFull ? 0xFFFFFFFFu : csize, kFOk);
-  if (csize > a.out_cap || n > zstd_in_cap(a.out_cap)) return finish(kBig, csize, kFOk);
-  const Lds L = lds_layout(smem, a.out_cap);
+  if (!Global && (csize > a.out_cap || n > zstd_in_cap(a.out_cap)))
+    return finish(kBig, csize, kFOk);
+  uint8_t* const dst = a.dst + a.dst_off[b];
+  Lds L = Global ? lds_layout(smem, kZWinBytes, 0)
+                 : lds_layout(smem, round16(zstd_in_cap(a.out_cap) + 16u + 4u), round16(a.out_cap));
+  uint8_t* const win = L.in;
+  if (Global) L.out = dst;
   uint64_t* stamp = a.stamps != nullptr ? a.stamps + 16u * b : nullptr;
   zstamp(stamp, 0, lane);
   const uint32_t llcode = lane < 36u ? kLLBase[lane] | static_cast<uint32_t>(kLLBits[lane]) << 24 : 0u;
   const uint32_t mlcode = lane < 53u ? kMLBase[lane] | static_cast<uint32_t>(kMLBits[lane]) << 24 : 0u;
-  stage(L.in, src, n, 16, lane);
-  __builtin_amdgcn_s_waitcnt(0);
+  // the staged input: in[wbase, wend) (LDS mode: all of it)
+  uint32_t wbase = 0, wend = n;
+  auto ensure = [&](uint32_t lo, uint32_t hi) {  // in[lo, min(hi, n)) staged
+    if (!Global) return;
+    hi = hi < n ? hi : n;
+    if (lo >= wbase && hi <= wend) return;
+    __builtin_amdgcn_s_waitcnt(0);  // (reads of the old window done)
+    wbase = lo & ~3u;
+    const uint32_t wl = n - wbase < kZWin ? n - wbase : kZWin;
+    wend = wbase + wl;
+    stage(win, src + wbase, wl, 16, lane);
+    __builtin_amdgcn_s_waitcnt(0);
+    L.in = win - wbase;
+  };
+  if (Global) {
+    wend = 0;
+    ensure(0, 32);
+  } else {
+    stage(L.in, src, n, 16, lane);
+    __builtin_amdgcn_s_waitcnt(0);
+  }
   zstamp(stamp, 1, lane);
   // ZSTD_decompressDCtx(dst, csize, src, n): frames one after another
   const uint32_t ocap = static_cast<uint32_t>(csize);
@@ -1159,6 +1291,7 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
       fail = kFTrailing;
       break;
     }
+    ensure(p, p + 32u);
     const uint32_t m = ld32u(L.in, p);
     if ((m & 0xFFFFFFF0u) == 0x184D2A50u) {  // skippable frame
       if (rem < 8) {
@@ -1201,6 +1334,7 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
     S.rep0 = 1;
     S.rep1 = 4;
     S.rep2 = 8;
+    S.flushed = start;
     for (;;) {
       q = uni(q);
       op = uni(op);
@@ -1209,6 +1343,7 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
         fail = kFBlockHdr;
         break;
       }
+      ensure(q, q + 3u);
       const uint32_t bh = ldb(L.in, q) | ldb(L.in, q + 1) << 8 | ldb(L.in, q + 2) << 16;
       q += 3;
       const uint32_t last = bh & 1u, btype = (bh >> 1) & 3u, bsize = bh >> 3;
@@ -1228,6 +1363,7 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
           fail = kFCap;
           break;
         }
+        ensure(q, q + 1u);
         const uint8_t v = static_cast<uint8_t>(ldb(L.in, q));
         for (uint32_t k = lane; k < bsize; k += 64) L.out[op + k] = v;
         op += bsize;
@@ -1249,7 +1385,11 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
             fail = kFCap;
             break;
           }
-          for (uint32_t k = lane; k < bsize; k += 64) L.out[op + k] = L.in[q + k];
+          if (Global) {  // (HBM to HBM; a raw block may pass the window)
+            for (uint32_t k = lane; k < bsize; k += 64) L.out[op + k] = src[q + k];
+          } else {
+            for (uint32_t k = lane; k < bsize; k += 64) L.out[op + k] = L.in[q + k];
+          }
           op += bsize;
         } else {
           if (bsize < 3) {
@@ -1257,7 +1397,8 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
             fail = kFLitHdr;
             break;
           }
-          if (!comp_block(L, q, q + bsize, &op, start, ocap, S, lane, &fail)) {
+          ensure(q, q + bsize);
+          if (!comp_block<Global>(L, q, q + bsize, &op, start, ocap, S, lane, &fail)) {
             ok = false;
             break;
           }
@@ -1279,8 +1420,16 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
         fail = kFChecksum;
         break;
       }
+      ensure(q, q + 4u);
       const uint32_t want = ld32u(L.in, q);
-      if (static_cast<uint32_t>(xxh64(L.out, start, op - start)) != want) {
+      uint64_t h;
+      if (Global) {
+        __builtin_amdgcn_s_waitcnt(0);
+        h = xxh64_hbm(dst + start, op - start, lane);
+      } else {
+        h = xxh64(L.out, start, op - start);
+      }
+      if (static_cast<uint32_t>(h) != want) {
         ok = false;
         fail = kFChecksum;
         break;
@@ -1289,19 +1438,46 @@ __global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
     }
     p = q;
   }
+  if (Global) __builtin_amdgcn_s_waitcnt(0);
   if (!ok) return finish(kBad, ocap, fail);
   if (op != ocap) return finish(kBad, ocap, kFContentSize);  // (short output)
-  uint8_t* dst = a.dst + a.dst_off[b];
-  uint32_t k0 = 0;
-  if ((reinterpret_cast<uintptr_t>(dst) & 3u) == 0) {
-    const uint32_t nd = op >> 2;
-    for (uint32_t i = lane; i < nd; i += 64)
-      reinterpret_cast<uint32_t*>(dst)[i] = reinterpret_cast<const uint32_t*>(L.out)[i];
-    k0 = 4u * nd;
+  if (!Global) {
+    uint32_t k0 = 0;
+    if ((reinterpret_cast<uintptr_t>(dst) & 3u) == 0) {
+      const uint32_t nd = op >> 2;
+      for (uint32_t i = lane; i < nd; i += 64)
+        reinterpret_cast<uint32_t*>(dst)[i] = reinterpret_cast<const uint32_t*>(L.out)[i];
+      k0 = 4u * nd;
+    }
+    for (uint32_t k = k0 + lane; k < op; k += 64) dst[k] = L.out[k];
   }
-  for (uint32_t k = k0 + lane; k < op; k += 64) dst[k] = L.out[k];
   zstamp(stamp, 5, lane);
   finish(kOK, op, kFOk);
+}
+
+__global__ void __launch_bounds__(64) zstd_uncompress_kernel(ZArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t b = blockIdx.x;
+  if (b >= a.nblocks) return;
+  zstd_stream<false>(a, b, smem, threadIdx.x);
+}
+
+// The streams zstd_uncompress_kernel marked TOO_LARGE (a frame past the LDS
+// staging, ReadBlock's any-size blocks), run after it on the same stream: a
+// workgroup per 32 streams, their statuses in one load, the marked ones one
+// after another (a batch without one costs a short launch).
+__global__ void __launch_bounds__(64) zstd_uncompress_big_kernel(ZArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t b0 = blockIdx.x * kZBigChunk;
+  const uint32_t mark = a.block_mode ? LVKV_READ_TOO_LARGE : LVKV_SNAPPY_TOO_LARGE;
+  const bool mine = lane < kZBigChunk && b0 + lane < a.nblocks && a.status[b0 + lane] == mark;
+  uint64_t todo = __ballot(mine);
+  while (todo) {
+    const uint32_t b = b0 + static_cast<uint32_t>(__builtin_ctzll(todo));
+    todo &= todo - 1u;
+    zstd_stream<true>(a, b, smem, lane);
+  }
 }
 
 }  // namespace
@@ -1326,6 +1502,10 @@ hipError_t launch_zstd_uncompress(const uint8_t* src, const uint64_t* src_off,
   a.out_cap = dst_cap == nullptr ? 0u : max(16u, max_ulen);
   const size_t lds = dst_cap == nullptr ? 16u : zstd_lds_bytes(a.out_cap);
   hipLaunchKernelGGL(zstd_uncompress_kernel, dim3(nblocks), dim3(64), lds, stream, a);
+  if (dst_cap != nullptr && nblocks != 0)  // (the streams past the LDS staging, any size)
+    hipLaunchKernelGGL(zstd_uncompress_big_kernel,
+                       dim3((nblocks + kZBigChunk - 1u) / kZBigChunk), dim3(64), kZBigLds,
+                       stream, a);
   return hipGetLastError();
 }
 

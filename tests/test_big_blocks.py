@@ -154,3 +154,114 @@ def test_device_read_blocks_big_snappy_blocks(lvkv, gpu, big):
         d = out.cpu().numpy()
         for r, o in zip(raws, ooff.cpu().tolist()):
             assert d[o:o + len(r)].tobytes() == r
+
+
+def _with_checksum(f: bytes, x: bytes) -> bytes:
+    """Frame f with its checksum flag set and XXH64(x)'s low 32 bits after
+    its last block (the library's ZSTD_c_checksumFlag frame)."""
+    import xxhash
+    b = bytearray(f)
+    b[4] |= 4
+    return bytes(b) + (xxhash.xxh64(x, seed=0).intdigest() & 0xFFFFFFFF).to_bytes(4, "little")
+
+
+def _zstd_cases(ins, zst):
+    """(stream, expected output or None): the library's big frames, checksummed
+    copies, a skippable frame before one, two frames in one stream (the
+    second overflows the first's content size), and damaged copies."""
+    want = [ins[k // 2] for k in range(len(zst))]
+    cases = list(zip(zst, want))
+    for k in (0, 8, 12, 13, 16):  # 64 KiB, 256 KiB, 1 MiB (levels 1, 3), 300,000
+        cases.append((_with_checksum(zst[k], want[k]), want[k]))
+    # (a stream that opens with a skippable frame has no length: BAD_LENGTH)
+    cases.append((b"\x50\x2a\x4d\x18" + (5).to_bytes(4, "little") + b"skip!" + zst[12], None))
+    cases.append((zst[8] + zst[2], None))
+    rng = np.random.default_rng(9)
+    for k in (0, 8, 12, 13, 16):
+        b = bytearray(zst[k])
+        b[int(rng.integers(len(b) // 2, len(b)))] ^= 0x21
+        cases.append((bytes(b), None))
+        cases.append((zst[k][:len(zst[k]) - 100], None))
+        c = bytearray(_with_checksum(zst[k], want[k]))
+        c[-1] ^= 1
+        cases.append((bytes(c), None))
+    return cases
+
+
+@pytest.fixture(scope="module")
+def zcases(big):
+    """_zstd_cases with the oracle's verdict on each: (stream, want, ok, out)."""
+    ins, _, zst = big
+    return [(f, x) + tuple(zo.uncompress(f)) for f, x in _zstd_cases(ins, zst)]
+
+
+def test_oracle_big_zstd_cases(zcases):
+    bad = 0
+    for f, x, ok, out in zcases:
+        if x is not None:
+            assert ok and out == x
+        else:
+            bad += not ok
+    assert bad >= 10  # (a changed byte can land where it changes nothing checked)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_ulen", [4096, 49152])
+def test_device_zstd_decodes_big_frames(lvkv, gpu, zcases, max_ulen):
+    """Frames of 64 KiB - 1 MiB (one to eight 128 KiB blocks) through the
+    HBM-output kernel, checksums included; damaged ones get the oracle's
+    verdict."""
+    import torch
+    streams = [c[0] for c in zcases]
+    sizes = [zo.get_uncompressed_length(f) or 0 for f in streams]
+    src, off, ln = _pack(torch, gpu, streams, skew=3)
+    dst, doff, cap = _outbuf(torch, gpu, sizes)
+    _, _, olen, st, why = lvkv.zstd_uncompress(src, off, ln, max_ulen=max_ulen, dst=dst,
+                                               dst_offsets=doff, dst_caps=cap, detail=True)
+    torch.cuda.synchronize()
+    st, why, olen = st.cpu().tolist(), why.cpu().tolist(), olen.cpu().tolist()
+    d = dst.cpu().numpy()
+    for k, ((f, _, ok, out), o) in enumerate(zip(zcases, doff.cpu().tolist())):
+        if zo.get_uncompressed_length(f) is None:
+            want = lvkv.SNAPPY_BAD_LENGTH
+        else:
+            want = lvkv.SNAPPY_OK if ok else lvkv.SNAPPY_BAD_CONTENTS
+        assert st[k] == want, (k, len(f), st[k], want, why[k])
+        if ok:
+            assert olen[k] == len(out)
+            assert d[o:o + len(out)].tobytes() == out, k
+
+
+@pytest.mark.gpu
+def test_device_read_blocks_big_zstd_blocks(lvkv, gpu, big):
+    """ReadBlock over an image of big zstd blocks (library frames) between
+    small snappy and raw ones: every block reads back at max_ulen 8192."""
+    import torch
+    ins, snap, zst = big
+    crc = so._crc()
+    img = bytearray()
+    handles, raws = [], []
+
+    def put(contents, t, raw):
+        handles.append((len(img), len(contents)))
+        raws.append(raw)
+        img.extend(contents + bytes([t]))
+        img.extend(crc.mask(crc.extend(crc.value(contents), bytes([t]))).to_bytes(4, "little"))
+
+    small = ins[0][:3000]
+    for k, z in enumerate(zst):
+        put(z, 2, ins[k // 2])
+        put(so.compress(small), 1, small)
+        put(small, 0, small)
+    file = torch.from_numpy(np.frombuffer(bytes(img), dtype=np.uint8).copy()).to(gpu)
+    ho = torch.tensor([h[0] for h in handles], dtype=torch.int64, device=gpu)
+    hs = torch.tensor([h[1] for h in handles], dtype=torch.int32, device=gpu)
+    out, ooff, cap = _outbuf(torch, gpu, [len(r) for r in raws])
+    for verify in (True, False):
+        _, _, olen, st = lvkv.sst_read_blocks(file, ho, hs, max_ulen=8192, verify=verify,
+                                              out=out, out_offsets=ooff, out_caps=cap)
+        torch.cuda.synchronize()
+        assert st.cpu().tolist() == [lvkv.READ_OK] * len(raws)
+        d = out.cpu().numpy()
+        for r, o in zip(raws, ooff.cpu().tolist()):
+            assert d[o:o + len(r)].tobytes() == r

@@ -173,8 +173,7 @@ def _expected_device_verdict(lvkv, d, v, cap):
     ulen = so.uncompressed_length(d)
     if ulen > cap:
         return lvkv.SNAPPY_CAPACITY
-    if len(d) > so.max_compressed_length(cap):
-        return lvkv.SNAPPY_TOO_LARGE
+    # (a stream past the LDS staging is decoded by the HBM-output kernel)
     return v["status"]
 
 
@@ -413,8 +412,6 @@ def test_device_uncompress_fuzz_against_oracle(lvkv, gpu):
         ul = so.uncompressed_length(s)
         if ost != so.BAD_LENGTH and ul is not None and ul > cap:
             want = lvkv.SNAPPY_CAPACITY
-        elif ost != so.BAD_LENGTH and len(s) > so.max_compressed_length(cap):
-            want = lvkv.SNAPPY_TOO_LARGE
         else:
             want = ost
         assert st[i] == want, (i, s[:12].hex(), st[i], want)
