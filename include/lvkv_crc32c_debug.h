@@ -52,14 +52,6 @@ int lvkv_engine_set_variant(struct lvkv_engine* engine, int variant, int ordered
 /* Kernel of LVKV_FLAG_FINAL uniform dispatches (the last before a wait):
  * -1 = as the overlapped ones (default), 0 or 1 as above. */
 int lvkv_engine_set_final_variant(struct lvkv_engine* engine, int variant);
-/* Device-written completion (on = 1): a LVKV_FLAG_FINAL overlapped uniform
- * dispatch stores its CRCs write-through and its last workgroup stores a flag
- * in host memory; a wait whose every queue ends in such a dispatch spins on
- * those flags instead of the packets' completion signals. LVKV_ERR_INVALID
- * if the engine could not allocate the flags. */
-int lvkv_engine_set_flag_wait(struct lvkv_engine* engine, int on);
-/* Waits that took the flag path, and waits that fell back to signals. */
-int lvkv_engine_flag_stats(struct lvkv_engine* engine, uint64_t* waits, uint64_t* fallbacks);
 /* Ordered (overlapped = 0) or overlapped dispatches run `kernel` (a
  * UniformArgs kernel of the given shape, symbol name with ".kd") from a
  * separate gfx950 code object in memory (tools/probe/build.sh) instead of the

@@ -126,10 +126,6 @@ def _load() -> ctypes.CDLL:
     L.lvkv_engine_shape.restype = i32
     L.lvkv_debug_engine_kernarg_cache.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]
     L.lvkv_debug_engine_kernarg_cache.restype = i32
-    L.lvkv_engine_set_flag_wait.argtypes = [vp, i32]
-    L.lvkv_engine_set_flag_wait.restype = i32
-    L.lvkv_engine_flag_stats.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]
-    L.lvkv_engine_flag_stats.restype = i32
     L.lvkv_engine_profile.argtypes = [vp, i32]
     L.lvkv_engine_profile.restype = i32
     L.lvkv_engine_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double),
@@ -1104,17 +1100,6 @@ class Engine:
         _check("lvkv_debug_engine_kernarg_cache",
                _lib.lvkv_debug_engine_kernarg_cache(self.handle, ctypes.byref(h), ctypes.byref(m)))
         return int(h.value), int(m.value)
-
-    def set_flag_wait(self, on: bool) -> None:
-        """Device-written completion of FINAL dispatches (lvkv_engine_set_flag_wait)."""
-        _check("lvkv_engine_set_flag_wait", _lib.lvkv_engine_set_flag_wait(self.handle, int(on)))
-
-    def flag_stats(self) -> Tuple[int, int]:
-        """(waits on device-written flags, waits that fell back to signals)."""
-        w, f = ctypes.c_uint64(), ctypes.c_uint64()
-        _check("lvkv_engine_flag_stats",
-               _lib.lvkv_engine_flag_stats(self.handle, ctypes.byref(w), ctypes.byref(f)))
-        return int(w.value), int(f.value)
 
     def queues(self, n: int = 0) -> int:
         r = int(_lib.lvkv_engine_queues(self.handle, n))

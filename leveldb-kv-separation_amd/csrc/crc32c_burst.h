@@ -44,9 +44,6 @@ enum : int {
   kBurstSplit4 = 256,  // ... as 4 independent 4-row groups
   kBurstPipe1 = 512,   // chain-pipelined: walk chain c, then issue chain c + 1
   kBurstPipe2 = 1024,  // ... two chains ahead: walk c, then issue c + 2
-  kBurstSysOut = 2048, // CRCs stored write-through (sc1: drop the L2 line, land in
-                       // HBM), for a dispatch that signals its own completion
-                       // (lvkv_ek_uniform_flag: no L2 write-back needed)
 };
 
 namespace {
@@ -86,14 +83,6 @@ __device__ __forceinline__ void burst_stamp(const UniformArgs& a, uint32_t gw, i
     const uint64_t t = __builtin_amdgcn_s_memrealtime();
     if (lane_id() == 0) a.stamps[gw * 8u + slot] = t;
   }
-}
-
-template <int F>
-__device__ __forceinline__ void burst_out(const UniformArgs& a, uint32_t i, uint32_t v) {
-  if (F & kBurstSysOut)
-    __hip_atomic_store(a.out + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else
-    a.out[i] = v;
 }
 
 template <int F>
@@ -159,7 +148,7 @@ __device__ __forceinline__ void burst_body(const UniformArgs& a, const UniGeo& g
     x = wave_xor_dpp(x);
     if (lane == 0 && live)
 #pragma unroll
-      for (int c = 0; c < NV; ++c) burst_out<F>(a, blk[c], x);
+      for (int c = 0; c < NV; ++c) a.out[blk[c]] = x;
     return;
   }
 
@@ -210,7 +199,7 @@ __device__ __forceinline__ void burst_body(const UniformArgs& a, const UniGeo& g
           if (FULL || static_cast<uint32_t>(j) < g.rows) st = row_step_c(lds, st, w[c][j], keys);
         crc = wave_xor_dpp(lane_end_shift_c(lds, st, lane_base)) ^ 0xffffffffu;
       }
-      if (lane == 0 && live) burst_out<F>(a, blk[c], a.mask ? crc_mask(crc) : crc);
+      if (lane == 0 && live) a.out[blk[c]] = a.mask ? crc_mask(crc) : crc;
       if (c < 2) burst_stamp<F>(a, gw, 6 + c);
       __builtin_amdgcn_sched_barrier(0);
       if (c + D < NV) load_rows(c + D, c + D + 1);
@@ -291,7 +280,7 @@ __device__ __forceinline__ void burst_body(const UniformArgs& a, const UniGeo& g
     }
     if (lane == 0 && live) {
 #pragma unroll
-      for (int c = 0; c < NV; ++c) burst_out<F>(a, blk[c], a.mask ? crc_mask(crc[c]) : crc[c]);
+      for (int c = 0; c < NV; ++c) a.out[blk[c]] = a.mask ? crc_mask(crc[c]) : crc[c];
     }
     burst_stamp<F>(a, gw, 4);
     return;
@@ -320,7 +309,7 @@ __device__ __forceinline__ void burst_body(const UniformArgs& a, const UniGeo& g
     crc[c] = wave_xor_dpp(lane_end_shift_c(lds, st[c], lane_base)) ^ 0xffffffffu;
   if (lane == 0 && live) {
 #pragma unroll
-    for (int c = 0; c < NV; ++c) burst_out<F>(a, blk[c], a.mask ? crc_mask(crc[c]) : crc[c]);
+    for (int c = 0; c < NV; ++c) a.out[blk[c]] = a.mask ? crc_mask(crc[c]) : crc[c];
   }
   burst_stamp<F>(a, gw, 4);
 }

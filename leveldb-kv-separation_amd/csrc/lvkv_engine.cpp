@@ -100,20 +100,12 @@ constexpr KernelSpec kSpecs[] = {
     {"lvkv_ek_ragged_small.kd", nullptr, 8, 4, 2, kArgsRagged},
     {"lvkv_ek_ragged_burst.kd", nullptr, 8, 4, 1, kArgsRagged},
     {"lvkv_ek_ragged_burst_small.kd", nullptr, 8, 6, 1, kArgsRagged},
-    {"lvkv_ek_uniform_flag.kd", nullptr, 8, 5, 1, kArgsUniform},
-    {"lvkv_ek_uniform_wt.kd", nullptr, 8, 5, 1, kArgsUniform},
 };
 constexpr int kNumSpecs = static_cast<int>(sizeof(kSpecs) / sizeof(kSpecs[0]));
 constexpr int kNumUniformSpecs = 2;  // lvkv_engine_set_variant's choices
 // general-layout kernels: persistent runs (two workgroups per CU, rounds of
 // 16 / 32 blocks), and one round per dispatch (one workgroup per CU)
 constexpr int kRaggedSpec = 2, kRaggedSmallSpec = 3, kBurstSpec = 4, kBurstSmallSpec = 5;
-// a FINAL overlapped uniform dispatch under the device-written completion
-constexpr int kFlagSpec = 6;
-// the other overlapped uniform dispatches then (write-through CRC stores)
-constexpr int kWtSpec = 7;
-constexpr bool kFlagWriteThrough = true;  // experiment switch (LVKV_FLAG_WB in the kernels)
-constexpr uint32_t kFlagSlots = 256;  // completion counters / host flags
 constexpr uint32_t kBurstRows = 17, kBurstSmallRows = 8;  // chunk rows of the SST / small shapes
 static_assert(sizeof(EngineRaggedArgs) <= 256 && sizeof(UniformArgs) <= 256, "kernarg slot");
 
@@ -253,18 +245,6 @@ struct Engine {
   bool fin_ok = false;
   uint64_t q_last[kQueues] = {};   // 1 + index of the queue's last dispatch since the fence
   uint64_t q_final[kQueues] = {};  // 1 + index of its last FINAL dispatch
-  // Device-written completion (lvkv_engine_set_flag_wait): a FINAL uniform
-  // dispatch runs lvkv_ek_uniform_flag with counter / flag slot s; its last
-  // workgroup stores done_flag[s] = 1 in host memory, and a wait whose every
-  // queue ends in such a dispatch spins on those flags instead of fin_sig.
-  bool flag_wait = false;
-  uint32_t* done_ctr = nullptr;            // kFlagSlots, VRAM (zeroed)
-  volatile uint32_t* done_flag = nullptr;  // kFlagSlots, fine-grained host memory
-  uint64_t flag_next = 0;
-  uint64_t flag_owner[kFlagSlots] = {};    // 1 + the dispatch that last used the slot
-  uint32_t q_flag[kQueues] = {};           // 1 + slot of the queue's last dispatch (0: none)
-  bool dirty = false;  // a dispatch since the last fence stored through the L2 (needs a release)
-  uint64_t flag_waits = 0, flag_fallbacks = 0;
 
   uint64_t next = 0;    // dispatches submitted
   uint64_t fenced = 0;  // every dispatch before this index is known complete
@@ -329,8 +309,6 @@ void destroy(Engine* e) {
   if (e->fence_ok) hsa_signal_destroy(e->fence_sig);
   if (e->fin_ok) hsa_signal_destroy(e->fin_sig);
   if (e->hold_ok) hsa_signal_destroy(e->hold_sig);
-  if (e->done_ctr) hsa_amd_memory_pool_free(e->done_ctr);
-  if (e->done_flag) hsa_amd_memory_pool_free(const_cast<uint32_t*>(e->done_flag));
   if (e->kernarg) {
     if (e->kernarg_vram)
       hsa_amd_memory_pool_free(e->kernarg);
@@ -375,62 +353,6 @@ bool alloc_kernargs(Engine& e) {
     return false;
   return hsa_memory_allocate(karg, kSlots * kSlotBytes, reinterpret_cast<void**>(&e.kernarg)) ==
          HSA_STATUS_SUCCESS;
-}
-
-struct FinePool {
-  hsa_amd_memory_pool_t pool;
-  bool found;
-};
-
-// The CPU agent's fine-grained system-memory pool (host flags the GPU writes).
-hsa_status_t find_fine_pool(hsa_amd_memory_pool_t pool, void* data) {
-  hsa_amd_segment_t seg;
-  uint32_t flags = 0;
-  bool alloc = false;
-  if (hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) !=
-          HSA_STATUS_SUCCESS ||
-      seg != HSA_AMD_SEGMENT_GLOBAL ||
-      hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags) !=
-          HSA_STATUS_SUCCESS ||
-      !(flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_FINE_GRAINED) ||
-      hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED,
-                                   &alloc) != HSA_STATUS_SUCCESS ||
-      !alloc)
-    return HSA_STATUS_SUCCESS;
-  FinePool* f = static_cast<FinePool*>(data);
-  f->pool = pool;
-  f->found = true;
-  return HSA_STATUS_INFO_BREAK;
-}
-
-// Counters (VRAM, zeroed) and host flags of the device-written completion;
-// false leaves the engine on completion signals only.
-bool alloc_flags(Engine& e) {
-  PoolFind vram{{}, false};
-  hsa_amd_agent_iterate_memory_pools(e.agent, find_vram_pool, &vram);
-  hsa_agent_t cpu{};
-  hsa_iterate_agents(find_cpu, &cpu);
-  FinePool fine{{}, false};
-  if (cpu.handle != 0) hsa_amd_agent_iterate_memory_pools(cpu, find_fine_pool, &fine);
-  if (!vram.found || !fine.found) return false;
-  void* c = nullptr;
-  void* f = nullptr;
-  if (hsa_amd_memory_pool_allocate(vram.pool, kFlagSlots * 4, 0, &c) != HSA_STATUS_SUCCESS)
-    return false;
-  if (hsa_amd_memory_fill(c, 0, kFlagSlots) != HSA_STATUS_SUCCESS ||
-      hsa_amd_memory_pool_allocate(fine.pool, 4096, 0, &f) != HSA_STATUS_SUCCESS) {
-    hsa_amd_memory_pool_free(c);
-    return false;
-  }
-  if (hsa_amd_agents_allow_access(1, &e.agent, nullptr, f) != HSA_STATUS_SUCCESS) {
-    hsa_amd_memory_pool_free(c);
-    hsa_amd_memory_pool_free(f);
-    return false;
-  }
-  memset(f, 0, 4096);
-  e.done_ctr = static_cast<uint32_t*>(c);
-  e.done_flag = static_cast<volatile uint32_t*>(f);
-  return true;
 }
 
 int create(int device, Engine** out) {
@@ -496,7 +418,6 @@ int create(int device, Engine** out) {
     }
   }
   ok = ok && alloc_kernargs(*e);
-  if (ok) (void)alloc_flags(*e);  // (optional: lvkv_engine_set_flag_wait needs it)
   ok = ok && hsa_signal_create(0, 0, nullptr, &e->fence_sig) == HSA_STATUS_SUCCESS;
   e->fence_ok = ok;
   ok = ok && hsa_signal_create(0, 0, nullptr, &e->fin_sig) == HSA_STATUS_SUCCESS;
@@ -555,26 +476,6 @@ bool wait_signal(Engine& e, hsa_signal_t sig) {
       e.queue_error = kStuck;
       return false;
     }
-  }
-}
-
-// Waits until the device stores done_flag[s] (a FINAL dispatch's last
-// workgroup); false on a queue error or a stuck device.
-bool wait_flag(Engine& e, uint32_t s) {
-  double deadline = 0;
-  for (uint64_t spin = 0;; ++spin) {
-    if (__atomic_load_n(&e.done_flag[s], __ATOMIC_ACQUIRE) != 0) return true;
-    if ((spin & 1023u) == 1023u) {
-      if (e.queue_error) return false;
-      const double t = now_s();
-      if (deadline == 0) {
-        deadline = t + e.stuck_s;
-      } else if (t > deadline) {
-        e.queue_error = kStuck;
-        return false;
-      }
-    }
-    __builtin_ia32_pause();
   }
 }
 
@@ -637,27 +538,6 @@ void collect_profile(Engine& e, uint32_t s) {
 // (the wait ends instead of spinning forever).
 int fence(Engine& e) {
   if (e.queue_error) return LVKV_ERR_HIP;
-  if (e.flag_wait) {
-    // every queue with dispatches since the last fence ends in a flagged
-    // FINAL one (barrier bit: it ran after the queue's earlier packets):
-    // their host flags say everything is done and its results are in HBM
-    bool any = false, flagged = true;
-    for (int q = 0; q < kQueues; ++q) {
-      if (e.q_last[q] == 0) continue;
-      any = true;
-      if (e.q_final[q] != e.q_last[q] || e.q_flag[q] == 0) flagged = false;
-    }
-    if (any && flagged && (!kFlagWriteThrough || !e.dirty)) {
-      for (int q = 0; q < kQueues; ++q)
-        if (e.q_last[q] != 0 && !wait_flag(e, e.q_flag[q] - 1u)) return LVKV_ERR_HIP;
-      for (int q = 0; q < kQueues; ++q) e.q_last[q] = e.q_final[q] = e.q_flag[q] = 0;
-      e.fenced = e.next;
-      e.dirty = false;
-      ++e.flag_waits;
-      return e.queue_error ? LVKV_ERR_HIP : LVKV_OK;
-    }
-    if (any) ++e.flag_fallbacks;
-  }
   int need = 0;
   for (int q = 0; q < kQueues; ++q)
     if (e.q_last[q] != 0 && e.q_final[q] != e.q_last[q]) ++need;
@@ -687,9 +567,8 @@ int fence(Engine& e) {
   e.cur = keep;
   if (need && !wait_signal(e, e.fence_sig)) return LVKV_ERR_HIP;
   if (!wait_signal(e, e.fin_sig)) return LVKV_ERR_HIP;
-  for (int q = 0; q < kQueues; ++q) e.q_last[q] = e.q_final[q] = e.q_flag[q] = 0;
+  for (int q = 0; q < kQueues; ++q) e.q_last[q] = e.q_final[q] = 0;
   e.fenced = e.next;
-  e.dirty = false;
   // oldest first: dispatch n used slot n % kProfSlots
   for (uint32_t i = 0; i < kProfSlots; ++i)
     collect_profile(e, static_cast<uint32_t>((e.next + i) % kProfSlots));
@@ -747,7 +626,7 @@ uint8_t* kernarg_slot(Engine& e, uint64_t n, const void* args, size_t size) {
 // queue n % nq (consecutive dispatches side by side); else that queue.
 int dispatch(Engine& e, const EngineKernel& k, const void* args, size_t size, uint32_t ngroups,
              bool acquire, bool barrier, bool system_acquire, int queue = -1,
-             bool final = false, int flag_slot = -1, bool write_through = false) {
+             bool final = false) {
   if (e.queue_error) return LVKV_ERR_HIP;
   const uint64_t n = e.next;
   // Kernarg slot n % kSlots was last used by dispatch n - kSlots.
@@ -797,9 +676,6 @@ int dispatch(Engine& e, const EngineKernel& k, const void* args, size_t size, ui
   publish(e, p, header, 1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS, idx);
   e.q_last[e.cur] = n + 1;
   if (final) e.q_final[e.cur] = n + 1;
-  e.q_flag[e.cur] = flag_slot >= 0 ? static_cast<uint32_t>(flag_slot) + 1u : 0u;
-  if (flag_slot >= 0) e.flag_owner[flag_slot] = n + 1;
-  if (!write_through) e.dirty = true;
   e.next = n + 1;
   return LVKV_OK;
 }
@@ -963,30 +839,12 @@ int lvkv_engine_crc32c_uniform(lvkv_engine* eng, const void* d_base, uint64_t st
       const uint64_t area = groups * k.waves * 8;
       a.stamps = e->stamps + (e->stamp_next++ % e->stamp_areas) * area;
     }
-    // a FINAL overlapped dispatch under the device-written completion: the
-    // same shape, CRCs stored write-through, its own counter and host flag
-    const bool fin = (flags & LVKV_FLAG_FINAL) != 0 && i + 1 == nd;
-    const EngineKernel& kf = e->kern[kFlagSpec];
-    const bool wt = kFlagWriteThrough && e->flag_wait && !ordered && !e->profiling && !e->stamps && !e->probe_on &&
-                    k.waves == kf.waves && k.chains == kf.chains && k.per_cu == kf.per_cu;
-    const bool flagged = fin && e->flag_wait && !ordered && !e->profiling && !e->stamps &&
-                         !e->probe_on && k.waves == kf.waves && k.chains == kf.chains &&
-                         k.per_cu == kf.per_cu;
-    int slot = -1;
-    if (flagged) {
-      slot = static_cast<int>(e->flag_next++ % kFlagSlots);
-      // (the slot's previous dispatch has finished: its flag is free to reset)
-      if (e->flag_owner[slot] > e->fenced && fence(*e) != LVKV_OK) return LVKV_ERR_HIP;
-      e->done_flag[slot] = 0;
-      a.done_ctr = e->done_ctr + slot;
-      a.done_flag = const_cast<uint32_t*>(e->done_flag + slot);
-    }
     // every dispatch acquires: overlapped ones rotate over queues, so
     // dispatch i > 0 may start before (or during) dispatch 0's acquire on
     // another queue
-    const int rc = dispatch(*e, flagged ? kf : wt ? e->kern[kWtSpec] : k, &a, sizeof(a),
-                            a.ngroups, /*acquire=*/true, /*barrier=*/ordered,
-                            (flags & LVKV_FLAG_SYSTEM_ACQUIRE) != 0, queue, fin, slot, wt);
+    const int rc = dispatch(*e, k, &a, sizeof(a), a.ngroups, /*acquire=*/true,
+                            /*barrier=*/ordered, (flags & LVKV_FLAG_SYSTEM_ACQUIRE) != 0, queue,
+                            (flags & LVKV_FLAG_FINAL) != 0 && i + 1 == nd);
     if (rc != LVKV_OK) return rc;
     done += n;
   }
@@ -1140,26 +998,6 @@ int lvkv_engine_set_variant(lvkv_engine* eng, int variant, int ordered_variant) 
   if (e->fenced != e->next && fence(*e) != LVKV_OK) return LVKV_ERR_HIP;
   e->variant = variant;
   e->ordered_variant = ordered_variant;
-  return LVKV_OK;
-}
-
-int lvkv_engine_set_flag_wait(lvkv_engine* eng, int on) {
-  if (eng == nullptr) return LVKV_ERR_INVALID;
-  Engine* e = reinterpret_cast<Engine*>(eng);
-  std::lock_guard<std::mutex> lk(e->mu);
-  if (on && e->done_ctr == nullptr) return LVKV_ERR_INVALID;
-  // (a switch drains first: no wait sees a half-flagged set of queues)
-  if (e->fenced != e->next && fence(*e) != LVKV_OK) return LVKV_ERR_HIP;
-  e->flag_wait = on != 0;
-  return LVKV_OK;
-}
-
-int lvkv_engine_flag_stats(lvkv_engine* eng, uint64_t* waits, uint64_t* fallbacks) {
-  if (eng == nullptr || waits == nullptr || fallbacks == nullptr) return LVKV_ERR_INVALID;
-  Engine* e = reinterpret_cast<Engine*>(eng);
-  std::lock_guard<std::mutex> lk(e->mu);
-  *waits = e->flag_waits;
-  *fallbacks = e->flag_fallbacks;
   return LVKV_OK;
 }
 

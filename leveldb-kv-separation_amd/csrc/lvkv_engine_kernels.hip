@@ -16,32 +16,6 @@
 
 namespace {
 constexpr int kLds = lvkv::kCompactLdsBytes / 4;
-
-// The dispatch's completion, written by the device (lvkv_engine_set_flag_wait):
-// every wave's write-through CRC stores drained (vmcnt 0), the workgroup's
-// barrier, then one lane adds to the dispatch's counter (agent scope); the
-// workgroup whose add comes last resets it and stores 1 to the host flag the
-// engine's wait spins on (MI355X_MICROARCH.md's sc1-store / counter form:
-// no L2 write-back, which the packet processor's end-of-kernel release and
-// signal would take several microseconds for).
-template <bool WB>
-__device__ __forceinline__ void signal_done(const lvkv::UniformArgs& a) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (WB) {  // this XCD's L2 written back (every earlier dispatch's stores too)
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    const uint32_t old =
-        __hip_atomic_fetch_add(a.done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1u == a.ngroups) {
-      __hip_atomic_store(a.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(a.done_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-}
 }
 
 // Production: one 512-thread workgroup per CU per dispatch, 8 waves x 5
@@ -62,31 +36,6 @@ extern "C" __global__ void __launch_bounds__(512, 2)
     lvkv_ek_uniform_pair(lvkv::UniformArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLds];
   lvkv::burst_kernel_body<lvkv::kBurstPipe1, 8, 3>(a, lds, a.ngroups);
-}
-
-// The overlapped kernel for a FINAL dispatch under the device-written
-// completion: CRCs stored write-through, then signal_done.
-extern "C" __global__ void __launch_bounds__(512, 2)
-    lvkv_ek_uniform_flag(lvkv::UniformArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kLds];
-#ifdef LVKV_FLAG_WB
-  lvkv::burst_kernel_body<lvkv::kBurstLate, 8, 5>(a, lds, a.ngroups);
-  signal_done<true>(a);
-#else
-  lvkv::burst_kernel_body<lvkv::kBurstLate | lvkv::kBurstSysOut, 8, 5>(a, lds, a.ngroups);
-  signal_done<false>(a);
-#endif
-}
-
-// The overlapped kernel of the other dispatches under the device-written
-// completion: CRCs stored write-through and drained before the waves end, so
-// a flagged FINAL dispatch's flag covers every dispatch before it (none of
-// them leaves a dirty L2 line for a release to write back).
-extern "C" __global__ void __launch_bounds__(512, 2)
-    lvkv_ek_uniform_wt(lvkv::UniformArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kLds];
-  lvkv::burst_kernel_body<lvkv::kBurstLate | lvkv::kBurstSysOut, 8, 5>(a, lds, a.ngroups);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // Timestamp builds of the two (per-wave s_memrealtime into

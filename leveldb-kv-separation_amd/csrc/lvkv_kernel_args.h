@@ -140,11 +140,6 @@ struct UniformArgs {
   uint32_t ngroups;           // workgroups of the launch (engine dispatches)
   uint32_t zcol[32];          // zcol[k] = Z_256(1 << k): the row tables are
                               // generated in-kernel from these columns
-  // device-written completion (lvkv_ek_uniform_flag; nullptr elsewhere): each
-  // workgroup counts itself in *done_ctr after its write-through stores have
-  // landed; the last resets it and stores 1 to *done_flag (host memory)
-  uint32_t* done_ctr;
-  uint32_t* done_flag;
 };
 
 // Arguments of the engine's general-layout kernels (lvkv_ek_ragged*,
