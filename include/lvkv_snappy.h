@@ -14,10 +14,13 @@
  * HAVE_SNAPPY=0, port/port_stdcxx.h:90-133). The compressor emits exactly
  * the bytes of snappy::RawCompress 1.1.8; the decompressor accepts exactly
  * the streams snappy::RawUncompress accepts and produces the same bytes.
- * The device keeps a block in LDS: blocks up to LVKV_SNAPPY_MAX_BLOCK bytes
- * uncompressed (LevelDB's blocks are ~block_size, 4 KiB by default); a block
- * beyond what the call was sized for is reported per block
- * (LVKV_SNAPPY_TOO_LARGE) and is the caller's to handle on the host.
+ * The decoders keep a block in LDS up to the call's max_ulen (at most
+ * LVKV_SNAPPY_MAX_BLOCK; LevelDB's blocks are ~block_size, 4 KiB by
+ * default); a block past that, of any size (block_size is a user option,
+ * include/leveldb/options.h:101), is decoded by a second kernel of the same
+ * call straight into its destination, so a valid block never comes back
+ * TOO_LARGE from a decoder. The compressor holds the block in LDS and
+ * reports a block past its max_len as LVKV_SNAPPY_TOO_LARGE.
  */
 #ifndef LVKV_SNAPPY_H_
 #define LVKV_SNAPPY_H_
@@ -39,9 +42,9 @@ extern "C" {
                                       block contents" (table/format.cc:127-131) */
 #define LVKV_SNAPPY_CAPACITY 3     /* the block's uncompressed length exceeds d_dst_cap[i]
                                       (out_len says how much it needs) */
-#define LVKV_SNAPPY_TOO_LARGE 4    /* beyond the call's max_len / max_ulen (or, for a
-                                      stream, longer than MaxCompressedLength(max_ulen):
-                                      valid only with padded elements no encoder writes) */
+#define LVKV_SNAPPY_TOO_LARGE 4    /* compressor: a block longer than max_len; decoders:
+                                      only the length-only calls (an unknown or > 32-bit
+                                      zstd content size) */
 
 #define LVKV_SNAPPY_MAX_BLOCK 49152u /* largest max_ulen of the decompressor */
 
@@ -79,8 +82,10 @@ int lvkv_snappy_uncompressed_length_device(const void* d_src, const uint64_t* d_
  * d_dst[d_dst_off[i], + d_dst_cap[i]): d_out_len[i] = its uncompressed
  * length (when the preamble decodes), d_status[i] = one of the statuses
  * above; on LVKV_SNAPPY_BAD_CONTENTS the destination holds garbage, as
- * after a failed RawUncompress. max_ulen (<= LVKV_SNAPPY_MAX_BLOCK) bounds
- * the uncompressed length the call handles and sizes its LDS. Replaces
+ * after a failed RawUncompress. max_ulen (<= LVKV_SNAPPY_MAX_BLOCK) sizes
+ * the LDS staging; a stream past it (a longer block, or one longer than
+ * MaxCompressedLength(max_ulen)) is decoded from HBM into HBM by a second
+ * kernel on the same stream, with the same verdicts. Replaces
  * port::Snappy_Uncompress (port/port_stdcxx.h:121-133) in ReadBlock
  * (table/format.cc:126-135).
  */
@@ -142,7 +147,8 @@ int lvkv_sst_write_blocks_level_device(const void* d_raw, const uint64_t* d_raw_
 #define LVKV_READ_SNAPPY_CONTENTS 4 /* "corrupted snappy compressed block contents" (:127-131) */
 #define LVKV_READ_ZSTD_LENGTH 5     /* "corrupted zstd compressed block length" (:140-143) */
 #define LVKV_READ_CAPACITY 6        /* contents longer than d_out_cap[i] (d_out_len says) */
-#define LVKV_READ_TOO_LARGE 7       /* beyond max_ulen (see LVKV_SNAPPY_TOO_LARGE) */
+#define LVKV_READ_TOO_LARGE 7       /* (no longer returned: blocks past max_ulen are
+                                       decoded from HBM; kept for the numbering) */
 #define LVKV_READ_ZSTD_CONTENTS 8   /* "corrupted zstd compressed block contents" (:145-149) */
 
 /*

@@ -34,11 +34,13 @@ extern "C" {
 #define LVKV_ZSTD_BAD_CONTENTS 2 /* Zstd_Uncompress failed: "corrupted zstd compressed
                                     block contents" (table/format.cc:145-149) */
 #define LVKV_ZSTD_CAPACITY 3     /* the content size exceeds d_dst_cap[i] (or is unknown) */
-#define LVKV_ZSTD_TOO_LARGE 4    /* beyond the call's max_len / max_ulen */
+#define LVKV_ZSTD_TOO_LARGE 4    /* compressor: a block longer than max_len; length-only
+                                    call: an unknown or > 32-bit content size */
 #define LVKV_ZSTD_UNSUPPORTED 5  /* compressor: the level's strategy at this size is not
                                     ZSTD_fast (levels >= 3, 0, and 2 for 128-256 KiB) */
 
-#define LVKV_ZSTD_MAX_BLOCK 49152u          /* largest max_ulen of the decompressor */
+#define LVKV_ZSTD_MAX_BLOCK 49152u          /* largest max_ulen of the decompressor (its LDS
+                                               staging; longer frames are decoded from HBM) */
 #define LVKV_ZSTD_COMPRESS_MAX_BLOCK 20480u /* largest max_len of the compressor (its LDS plan:
                                                the block, its hash table, literals, sequences) */
 
@@ -79,9 +81,11 @@ int lvkv_zstd_uncompressed_length_device(const void* d_src, const uint64_t* d_sr
  * another, skippable frames skipped, checksums verified) into exactly its
  * content size at d_dst[d_dst_off[i], + d_dst_cap[i]). Statuses: OK,
  * BAD_LENGTH (content size 0), BAD_CONTENTS (any ZSTD_isError), CAPACITY
- * (content size past d_dst_cap[i], or unknown), TOO_LARGE (past max_ulen, or
- * a stream longer than ZSTD_compressBound of it). max_ulen <=
- * LVKV_ZSTD_MAX_BLOCK.
+ * (content size past d_dst_cap[i], or unknown). max_ulen (<=
+ * LVKV_ZSTD_MAX_BLOCK) sizes the LDS staging: a frame past it (a longer
+ * content size, or a stream longer than ZSTD_compressBound(max_ulen)) is
+ * decoded by a second kernel on the same stream, its input through a
+ * 128 KiB LDS window and its output straight into d_dst.
  */
 int lvkv_zstd_uncompress_device(const void* d_src, const uint64_t* d_src_off,
                                 const uint32_t* d_src_len, void* d_dst, const uint64_t* d_dst_off,

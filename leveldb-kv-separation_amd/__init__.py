@@ -574,9 +574,10 @@ def snappy_uncompress(src, offsets, lengths, *, max_ulen: int, dst=None, dst_off
                       dst_caps=None, stream=None):
     """Batched port::Snappy_Uncompress (port/port_stdcxx.h:121-133) as
     ReadBlock runs it (table/format.cc:120-135). Without dst, every stream
-    gets max_ulen bytes. Returns (dst uint8, dst_offsets int64, uncompressed
-    lengths int32, status uint8: SNAPPY_OK / BAD_LENGTH / BAD_CONTENTS /
-    CAPACITY / TOO_LARGE)."""
+    gets max_ulen bytes. max_ulen sizes the LDS staging; a longer stream is
+    decoded from HBM by the call's second kernel. Returns (dst uint8,
+    dst_offsets int64, uncompressed lengths int32, status uint8: SNAPPY_OK /
+    BAD_LENGTH / BAD_CONTENTS / CAPACITY)."""
     torch = _torch()
     n = offsets.numel()
     dev = src.device
