@@ -37,11 +37,23 @@ namespace lvkv {
 namespace {
 
 constexpr uint32_t kTags = 1024;  // window-scratch slots (u32)
+constexpr uint32_t kLitStage = 32;  // the literals' offset in the frame slot (past the header)
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-// Every lane's LDS operations so far are ordered before what follows (one
-// wave: a compiler barrier plus lgkmcnt(0)).
-__device__ __forceinline__ void lds_sync() { __syncthreads(); }
+// Every lane's LDS operations so far are ordered before what follows. The
+// workgroup is one wave, and one wave's LDS instructions execute in issue
+// order (the counted lgkmcnt waits rest on it), so a later LDS access of any
+// lane sees every earlier one: only the compiler must not move LDS accesses
+// across this point -- no lgkmcnt(0) wait, which __syncthreads() would add
+// (the loaded values' own waits stay). The CPU SIMT emulator (threads, not
+// one instruction stream) keeps the barrier.
+__device__ __forceinline__ void lds_sync() {
+#ifdef LVKV_SIMT_EMU
+  __syncthreads();
+#else
+  asm volatile("" ::: "memory");
+#endif
+}
 
 __host__ __device__ __forceinline__ uint32_t hibit(uint32_t v) { return 31u - __builtin_clz(v); }
 
@@ -1310,9 +1322,9 @@ __device__ __forceinline__ uint32_t zcount(const uint8_t* in, uint32_t a, uint32
 }
 
 struct Seqs {
-  uint8_t* lits;
+  uint8_t* lits;  // the match finder's: the block's frame slot in HBM (kLitStage)
   uint32_t* sll;  // litLength | mlBase << 16
-  uint32_t* sof;  // offset code + 1
+  uint16_t* sof;  // offset code + 1 (<= max_len + 3)
   uint32_t nlit, nseq;
 };
 
@@ -1321,7 +1333,7 @@ __device__ __forceinline__ void store_seq(Seqs& s, const uint8_t* in, uint32_t a
   for (uint32_t k = lane; k < litlen; k += 64) s.lits[s.nlit + k] = in[anchor + k];
   if (lane == 0) {
     s.sll[s.nseq] = litlen | (mlbase << 16);
-    s.sof[s.nseq] = offcode + 1u;
+    s.sof[s.nseq] = static_cast<uint16_t>(offcode + 1u);
   }
   s.nlit += litlen;
   s.nseq += 1u;
@@ -1582,9 +1594,13 @@ __global__ void __launch_bounds__(64) zstd_compress_kernel(ZcArgs a) {
   TIdx* table = reinterpret_cast<TIdx*>(smem + a.o_tbl);
   uint32_t* tags = reinterpret_cast<uint32_t*>(smem + a.o_tag);
   Seqs sq;
-  sq.lits = smem + a.o_lit;
+  // the literals go to the block's own frame slot in HBM while the table is
+  // in use (room: ZSTD_compressBound(n) - n >= kLitStage + 22 for n <=
+  // LVKV_ZSTD_COMPRESS_MAX_BLOCK), then into the dead table's LDS for the
+  // entropy stage: one LDS region less, one more workgroup a CU
+  sq.lits = g + kLitStage;
   sq.sll = reinterpret_cast<uint32_t*>(smem + a.o_sll);
-  sq.sof = reinterpret_cast<uint32_t*>(smem + a.o_sof);
+  sq.sof = reinterpret_cast<uint16_t*>(smem + a.o_sof);
   sq.nlit = 0;
   sq.nseq = 0;
   stage(in, src, n, 16, lane);
@@ -1597,6 +1613,13 @@ __global__ void __launch_bounds__(64) zstd_compress_kernel(ZcArgs a) {
   lds_sync();
   zcstamp(stamp, 1);
   match_block<TIdx>(in, n, table, tags, zp, sq, lane);
+  {
+    __builtin_amdgcn_s_waitcnt(0);  // (every lane's literal stores have landed)
+    uint8_t* lits = smem + a.o_lit;
+    for (uint32_t k = lane; k < sq.nlit; k += 64) lits[k] = g[kLitStage + k];
+    sq.lits = lits;
+    lds_sync();
+  }
   zcstamp(stamp, 2);
   // ---- entropy (the input region becomes the block's staging buffer)
   uint8_t* out = in;
@@ -1730,8 +1753,10 @@ struct ZstdCompressPlan {
 
 // The LDS plan for blocks up to max_len at `level`: the staged block (+ room
 // for a body that runs past it before the raw decision), the hash table (the
-// largest hash log any size up to max_len gets; u16 entries), the window
-// slots (then the Huffman nodes), the literals and the sequences.
+// largest hash log any size up to max_len gets; u16 entries; after the match
+// finder, the entropy scratch and the literals), the window slots (then the
+// Huffman nodes) and the sequences. 31.3 KB for 4 KiB blocks: 5 workgroups
+// a CU.
 ZstdCompressPlan zstd_compress_plan(uint32_t max_len, int level) {
   ZstdCompressPlan p{};
   uint32_t hmax = 6;
@@ -1742,19 +1767,21 @@ ZstdCompressPlan zstd_compress_plan(uint32_t max_len, int level) {
     }
   }
   p.smax = max_len / 4u + 2u;
+  // the table region: the hash table, then (entropy stage) the scratch and
+  // after it the literals
   const uint32_t ent = kECodes + 3u * round16(p.smax);
-  const uint32_t tbl = (2u << hmax) > ent ? (2u << hmax) : ent;
+  const uint32_t ent_lits = ent + round16(max_len + 16u);
+  const uint32_t tbl = (2u << hmax) > ent_lits ? (2u << hmax) : ent_lits;
   uint32_t o = round16(max_len + 512u);
   p.o_tbl = o;
+  p.o_lit = o + ent;
   o += round16(tbl);
   p.o_tag = o;
   o += 4u * kTags;
-  p.o_lit = o;
-  o += round16(max_len + 16u);
   p.o_sll = o;
   o += 4u * round16(p.smax);
   p.o_sof = o;
-  o += 4u * round16(p.smax);
+  o += 2u * round16(p.smax);
   p.lds = o;
   return p;
 }

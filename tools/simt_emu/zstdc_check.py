@@ -16,7 +16,8 @@ import numpy as np
 REPO = Path(__file__).resolve().parent.parent.parent
 sys.path.insert(0, str(REPO))
 sys.path.insert(0, str(REPO / "tests"))
-from oracle import zstd_encoder as ze  # noqa: E402
+sys.path.insert(0, str(REPO / "oracle"))
+import zstd_encoder as ze  # noqa: E402
 
 
 def blocks(kind, args):
