@@ -688,10 +688,12 @@ __device__ __forceinline__ uint32_t gather256(const uint32_t (&a)[4], uint32_t i
 
 // HUF_buildCTable_wksp: counts a symbol a lane x 4 (c[g] for g * 64 + lane),
 // symbols 0..max_sym. Codes go to huf[s] = code | nbBits << 16. Returns the
-// table's max bits. The sorted leaves, the created nodes' counts, the
-// parents and the depths live in registers (rd256 / wr256): the merges and
-// the depth walk are chains of v_readlane / v_writelane, not LDS round
-// trips. node0 (LDS) serves the rank scatter and the rare HUF_setMaxHeight.
+// table's max bits. The sorted leaves and the created nodes' counts live in
+// registers: the merge is a chain of v_readlane and lane writes (no LDS
+// round trip), recording only where each pick came from; the parents are
+// then placed all at once and the depths found by pointer jumping. node0
+// (LDS) serves the rank scatter, the parents' scatter and the rare
+// HUF_setMaxHeight.
 __device__ __forceinline__ uint32_t huf_build(const uint32_t (&c)[4], uint32_t max_sym, uint32_t max_nb,
                               HNode* node0, uint32_t* huf, uint32_t lane) {
   HNode* node = node0 + 1;
@@ -732,56 +734,112 @@ __device__ __forceinline__ uint32_t huf_build(const uint32_t (&c)[4], uint32_t m
   }
   const uint32_t non_null = nnz - 1u;  // (nnz >= 2: one symbol is the RLE case)
   constexpr uint32_t kBarrier = 1u << 31, kUnmade = 1u << 30;
-  // created node k (k = node number - 256): counts IC, parents of leaves PL
-  // and of created nodes PI (as created-node numbers)
-  uint32_t IC[4] = {kUnmade, kUnmade, kUnmade, kUnmade}, PL[4] = {0, 0, 0, 0},
-           PI[4] = {0, 0, 0, 0};
+  // The two-queue merge (sorted leaves from the smallest, created nodes in
+  // order): created node k's count in IC (lane k & 63 of IC[k >> 6]), and
+  // per step only which queue each of its two picks came from (DEC: bit 0
+  // the first pick was a leaf, bit 1 the second), both lane writes into a
+  // register fixed per group of 64 steps. The parents follow from
+  // the pick order afterwards, all at once.
+  uint32_t IC[4] = {kUnmade, kUnmade, kUnmade, kUnmade}, DEC[4] = {0, 0, 0, 0};
   const uint32_t root = non_null - 1u;  // the last created node
   int32_t low_s = static_cast<int32_t>(non_null);
   {
     const uint32_t c1 = rd256(L, non_null), c0 = rd256(L, non_null - 1u);
-    wr256(IC, 0, c1 + c0);
-    wr256(PL, non_null, 0);
-    wr256(PL, non_null - 1u, 0);
+    IC[0] = lane == 0 ? c1 + c0 : IC[0];
+    DEC[0] = lane == 0 ? 3u : DEC[0];  // node 0: the two smallest leaves
   }
   low_s -= 2;
-  uint32_t low_n = 0, made = 1;
+  uint32_t low_n = 0;
   uint32_t cs = low_s >= 0 ? rd256(L, static_cast<uint32_t>(low_s)) : kBarrier;
   uint32_t cn = rd256(IC, 0);
-  while (made <= root) {
-    uint32_t c1, c2;
-    // n1
-    if (cs < cn) {
-      c1 = cs;
-      wr256(PL, static_cast<uint32_t>(low_s), made);
-      --low_s;
-      cs = low_s >= 0 ? rd256(L, static_cast<uint32_t>(low_s)) : kBarrier;
-    } else {
-      c1 = cn;
-      wr256(PI, low_n, made);
-      ++low_n;
-      cn = low_n < made ? rd256(IC, low_n) : kUnmade;
+#pragma unroll
+  for (uint32_t g = 0; g < 4; ++g) {
+    if (64u * g > root) break;
+    for (uint32_t l = g == 0 ? 1u : 0u; l < 64u; ++l) {
+      const uint32_t made = 64u * g + l;
+      if (made > root) break;
+      uint32_t c1, c2, dec = 0;
+      if (cs < cn) {
+        c1 = cs;
+        dec = 1;
+        --low_s;
+        cs = low_s >= 0 ? rd256(L, static_cast<uint32_t>(low_s)) : kBarrier;
+      } else {
+        c1 = cn;
+        ++low_n;
+        cn = low_n < made ? rd256(IC, low_n) : kUnmade;
+      }
+      if (cs < cn) {
+        c2 = cs;
+        dec |= 2;
+        --low_s;
+        cs = low_s >= 0 ? rd256(L, static_cast<uint32_t>(low_s)) : kBarrier;
+      } else {
+        c2 = cn;
+        ++low_n;
+        cn = low_n < made ? rd256(IC, low_n) : kUnmade;
+      }
+      IC[g] = lane == l ? c1 + c2 : IC[g];
+      DEC[g] = lane == l ? dec : DEC[g];
+      if (low_n == made) cn = c1 + c2;
     }
-    // n2
-    if (cs < cn) {
-      c2 = cs;
-      wr256(PL, static_cast<uint32_t>(low_s), made);
-      --low_s;
-      cs = low_s >= 0 ? rd256(L, static_cast<uint32_t>(low_s)) : kBarrier;
-    } else {
-      c2 = cn;
-      wr256(PI, low_n, made);
-      ++low_n;
-      cn = low_n < made ? rd256(IC, low_n) : kUnmade;
-    }
-    wr256(IC, made, c1 + c2);
-    if (low_n == made) cn = c1 + c2;
-    ++made;
   }
-  // depths: the created nodes from the root down, then every leaf at once
-  uint32_t DI[4] = {0, 0, 0, 0};
-  for (int32_t k = static_cast<int32_t>(root) - 1; k >= 0; --k)
-    wr256(DI, static_cast<uint32_t>(k), rd256(DI, rd256(PI, static_cast<uint32_t>(k))) + 1u);
+  // Parents from the pick order: step m's picks are slots 2m and 2m + 1; the
+  // r-th leaf pick takes leaf non_null - r, the q-th created-node pick node
+  // q, and both get parent m. Scattered through LDS (u8: parents <= 254),
+  // after the sort's nodes.
+  uint8_t* par_l = reinterpret_cast<uint8_t*>(node0 + 257);
+  uint8_t* par_i = par_l + 256;
+  {
+    const uint64_t below = (uint64_t{1} << lane) - 1u;
+    uint32_t carry = 0;
+#pragma unroll
+    for (uint32_t g = 0; g < 4; ++g) {
+      const uint32_t m = 64u * g + lane;
+      const bool on = m <= root;
+      const bool l0 = on && (DEC[g] & 1u), l1 = on && (DEC[g] & 2u);
+      const uint64_t b0 = __ballot(l0), b1 = __ballot(l1);
+      const uint32_t pre = carry + __popcll(b0 & below) + __popcll(b1 & below);
+      if (on) {
+        const uint32_t r1 = pre + (l0 ? 1u : 0u);
+        if (l0) par_l[non_null - pre] = static_cast<uint8_t>(m);
+        else par_i[2u * m - pre] = static_cast<uint8_t>(m);
+        if (l1) par_l[non_null - r1] = static_cast<uint8_t>(m);
+        else par_i[2u * m + 1u - r1] = static_cast<uint8_t>(m);
+      }
+      carry += __popcll(b0) + __popcll(b1);
+    }
+  }
+  lds_sync();
+  uint32_t PL[4], PI[4];
+#pragma unroll
+  for (uint32_t g = 0; g < 4; ++g) {
+    const uint32_t k = 64u * g + lane;
+    PL[g] = k <= non_null ? par_l[k] : 0u;
+    PI[g] = k < root ? par_i[k] : k;  // (the root and past it: their own parent)
+  }
+  // depths of the created nodes: pointer jumping to the root (8 rounds:
+  // depth <= 254)
+  uint32_t DI[4], AN[4];
+#pragma unroll
+  for (uint32_t g = 0; g < 4; ++g) {
+    const uint32_t k = 64u * g + lane;
+    DI[g] = k < root ? 1u : 0u;
+    AN[g] = PI[g];
+  }
+  for (int round = 0; round < 8; ++round) {
+    uint32_t nd[4], na[4];
+#pragma unroll
+    for (uint32_t g = 0; g < 4; ++g) {
+      nd[g] = DI[g] + gather256(DI, AN[g]);
+      na[g] = gather256(AN, AN[g]);
+    }
+#pragma unroll
+    for (uint32_t g = 0; g < 4; ++g) {
+      DI[g] = nd[g];
+      AN[g] = na[g];
+    }
+  }
   uint32_t NB[4];
   uint32_t deepest = 0;
 #pragma unroll

@@ -119,6 +119,8 @@ inline void launch(K kernel, dim3 grid, size_t lds, A... args) {
 #define __shfl_xor(v, m) emu::shfl_xor((v), static_cast<uint32_t>(m))
 #define __builtin_amdgcn_readlane(v, l) emu::xread((v), static_cast<uint32_t>(l))
 #define __builtin_amdgcn_readfirstlane(v) emu::xread((v), 0u)
+#define __builtin_amdgcn_writelane(v, l, old) \
+  (emu::tid.x == static_cast<uint32_t>(l) ? static_cast<uint32_t>(v) : static_cast<uint32_t>(old))
 #define __builtin_amdgcn_ds_bpermute(a, v) emu::xread((v), static_cast<uint32_t>((a) >> 2))
 #define __builtin_amdgcn_alignbyte(hi, lo, s) \
   static_cast<uint32_t>(((static_cast<uint64_t>(hi) << 32) | static_cast<uint32_t>(lo)) >> (8u * ((s) & 3u)))
