@@ -964,6 +964,48 @@ __device__ __forceinline__ uint32_t rle_literals(uint8_t* out, const uint8_t* li
   return fl + 1u;
 }
 
+// Packs `count` (<= 256) bit chunks, chunk e = the low nb[e >> 6] bits of
+// val[e >> 6] at lane e & 63, one after another from bit `bit0` of words
+// (LDS; the bits below bit0 are kept, the rest of the words the stream
+// covers are zeroed first): an exclusive scan of the counts places every
+// chunk, and each lane ORs its chunks into the one or two words they touch.
+// Chunks of 0-32 bits. Returns the bit after the last chunk.
+__device__ __forceinline__ uint32_t pack_bits(uint32_t* words, uint32_t bit0, const uint32_t (&val)[4],
+                                              const uint32_t (&nb)[4], uint32_t count, uint32_t lane) {
+  uint32_t off[4];
+  uint32_t carry = bit0;
+#pragma unroll
+  for (uint32_t g = 0; g < 4; ++g) {
+    const uint32_t n = 64u * g + lane < count ? nb[g] : 0u;
+    uint32_t incl = n;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t v = __shfl_up(incl, d);
+      if (lane >= d) incl += v;
+    }
+    off[g] = carry + incl - n;
+    carry += uni(__shfl(incl, 63));
+  }
+  const uint32_t w0 = bit0 >> 5, w1 = (carry + 31u) >> 5;
+  for (uint32_t k = w0 + lane; k < w1; k += 64) {
+    const uint32_t keep = k == w0 ? (bit0 & 31u) : 0u;
+    words[k] = keep ? words[k] & ((1u << keep) - 1u) : 0u;
+  }
+  lds_sync();
+#pragma unroll
+  for (uint32_t g = 0; g < 4; ++g) {
+    const uint32_t n = 64u * g + lane < count ? nb[g] : 0u;
+    if (n != 0) {
+      const uint64_t v = static_cast<uint64_t>(val[g] & (n == 32u ? 0xFFFFFFFFu : (1u << n) - 1u))
+                         << (off[g] & 31u);
+      atomicOr(&words[off[g] >> 5], static_cast<uint32_t>(v));
+      if ((off[g] & 31u) + n > 32u) atomicOr(&words[(off[g] >> 5) + 1u], static_cast<uint32_t>(v >> 32));
+    }
+  }
+  lds_sync();
+  return carry;
+}
+
 // HUF_writeCTable's weights through FSE (HUF_compressWeights) into buf (LDS,
 // dword-aligned): returns the bytes (0: no FSE form). w[g] = weight of
 // symbol g * 64 + lane for symbols < nw.
@@ -1004,39 +1046,74 @@ __device__ __forceinline__ uint32_t huf_compress_weights(const uint32_t (&w)[4],
                    &t.dfs);
   lds_sync();
   fse_regs(t, lane);
-  // the weights from the end, two interleaved states
+  // The weights from the end, two interleaved states (FSE_compress_usingCTable):
+  // the states are two independent chains, so they run first, each step's
+  // (bits, count) recorded in emission order; the lanes then pack the stream
+  // at once (pack_bits). Chain A takes the indices with i = nw - 1 (mod 2),
+  // chain B the others, each from its highest index down; emission step e
+  // (e = 0..nw-3) encodes index nw - 3 - e: chain A's on even e. A is s1
+  // when nw is odd, s2 when it is even.
   auto wat = [&](uint32_t i) -> uint32_t {
     const uint32_t g = i >> 6, l = i & 63u;
     const uint32_t v = g == 0 ? w[0] : (g == 1 ? w[1] : (g == 2 ? w[2] : w[3]));
     return uni(__builtin_amdgcn_readlane(v, l));
   };
-  bw_init(bw, buf, nc);
-  uint32_t ip = nw;
-  uint32_t s1, s2;
-  if (nw & 1u) {
-    s1 = fse_init(t, wat(--ip));
-    s2 = fse_init(t, wat(--ip));
-    s1 = fse_enc(t, s1, wat(--ip), bw, lane);
-  } else {
-    s2 = fse_init(t, wat(--ip));
-    s1 = fse_init(t, wat(--ip));
+  uint32_t sa = fse_init(t, wat(nw - 1u)), sb = fse_init(t, wat(nw - 2u));
+  const bool odd = (nw & 1u) != 0;
+  const uint32_t E = nw - 2u;
+  // per step, in parallel: its symbol's (deltaNbBits, deltaFindState)
+  uint32_t DNB[4], DFS[4];
+#pragma unroll
+  for (uint32_t g = 0; g < 4; ++g) {
+    const uint32_t e = 64u * g + lane;
+    // (every lane joins the gather: a lane-permute reads inactive lanes as 0)
+    const uint32_t gw = gather256(w, e < E ? nw - 3u - e : 0u);
+    const uint32_t sym = e < E ? gw : 0u;
+    DNB[g] = __shfl(t.dnb, static_cast<int>(sym));
+    DFS[g] = __shfl(static_cast<uint32_t>(t.dfs), static_cast<int>(sym));
   }
-  if ((nw - 2u) & 2u) {
-    s2 = fse_enc(t, s2, wat(--ip), bw, lane);
-    s1 = fse_enc(t, s1, wat(--ip), bw, lane);
+  // the two chains a step each per turn (independent: they overlap); each
+  // step's state before it recorded at its lane
+  uint32_t VAL[4] = {0, 0, 0, 0}, NBT[4] = {0, 0, 0, 0};
+  auto step = [&](uint32_t st, uint32_t dnb, uint32_t dfs) -> uint32_t {
+    const uint32_t nbo = (st + dnb) >> 16;
+    return fse_state(t, static_cast<int32_t>(st >> nbo) + static_cast<int32_t>(dfs));
+  };
+#pragma unroll
+  for (uint32_t g = 0; g < 4; ++g) {
+    if (64u * g >= E) break;
+    for (uint32_t l = 0; l < 64u; l += 2u) {
+      const uint32_t e = 64u * g + l;
+      if (e >= E) break;
+      const uint32_t da = __builtin_amdgcn_readlane(DNB[g], l), fa = __builtin_amdgcn_readlane(DFS[g], l);
+      VAL[g] = lane == l ? sa : VAL[g];
+      if (e + 1u < E) {
+        const uint32_t db = __builtin_amdgcn_readlane(DNB[g], l + 1u),
+                       fb = __builtin_amdgcn_readlane(DFS[g], l + 1u);
+        VAL[g] = lane == l + 1u ? sb : VAL[g];
+        sa = step(sa, da, fa);
+        sb = step(sb, db, fb);
+      } else {
+        sa = step(sa, da, fa);
+      }
+    }
   }
-  while (ip > 0) {
-    s2 = fse_enc(t, s2, wat(--ip), bw, lane);
-    s1 = fse_enc(t, s1, wat(--ip), bw, lane);
-    s2 = fse_enc(t, s2, wat(--ip), bw, lane);
-    s1 = fse_enc(t, s1, wat(--ip), bw, lane);
+#pragma unroll
+  for (uint32_t g = 0; g < 4; ++g) NBT[g] = 64u * g + lane < E ? (VAL[g] + DNB[g]) >> 16 : 0u;
+  // the flush: s2 then s1, the end mark
+  const uint32_t s2 = odd ? sb : sa, s1 = odd ? sa : sb;
+  const uint32_t tail_v[3] = {s2, s1, 1u}, tail_n[3] = {tl, tl, 1u};
+#pragma unroll
+  for (uint32_t k = 0; k < 3; ++k) {
+    const uint32_t e = E + k, g = e >> 6, l = e & 63u;
+#pragma unroll
+    for (uint32_t gg = 0; gg < 4; ++gg) {
+      VAL[gg] = (gg == g && lane == l) ? tail_v[k] : VAL[gg];
+      NBT[gg] = (gg == g && lane == l) ? tail_n[k] : NBT[gg];
+    }
   }
-  bw_add(bw, s2, tl, lane);
-  bw_add(bw, s1, tl, lane);
-  bw_add(bw, 1u, 1, lane);
-  bw_flush(bw, lane);
-  lds_sync();
-  return bw_end(bw);
+  const uint32_t bits = pack_bits(reinterpret_cast<uint32_t*>(buf), 8u * nc, VAL, NBT, E + 3u, lane);
+  return (bits + 7u) >> 3;
 }
 
 // The literals section into out (LDS, dword-aligned): its size.
@@ -1350,12 +1427,21 @@ __device__ __forceinline__ uint32_t zhash(const uint8_t* in, uint32_t p, uint32_
   return static_cast<uint32_t>((v * prime) >> (64u - hlog));
 }
 
+// a / b for a, b < 2^16, b > 0: a float reciprocal and one correction (the
+// estimate is within one), not the ~35-instruction integer division
+__device__ __forceinline__ uint32_t udiv16(uint32_t a, uint32_t b) {
+  uint32_t q = static_cast<uint32_t>(static_cast<float>(a) * __builtin_amdgcn_rcpf(static_cast<float>(b)));
+  if (q * b > a) --q;
+  else if ((q + 1u) * b <= a) ++q;
+  return q;
+}
+
 // ip0 - anchor after j steps from d0 (step = d >> 7 + ss)
 __device__ __forceinline__ uint32_t step_pos(uint32_t d, uint32_t k, uint32_t ss) {
   while (k) {
     const uint32_t q = d >> 7, st = q + ss;
     const uint32_t rem = ((q + 1u) << 7) - d;
-    const uint32_t nseg = (rem + st - 1u) / st;
+    const uint32_t nseg = udiv16(rem + st - 1u, st);
     if (k <= nseg) {
       d += k * st;
       break;

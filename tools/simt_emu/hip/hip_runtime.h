@@ -124,6 +124,7 @@ inline void launch(K kernel, dim3 grid, size_t lds, A... args) {
 #define __builtin_amdgcn_ds_bpermute(a, v) emu::xread((v), static_cast<uint32_t>((a) >> 2))
 #define __builtin_amdgcn_alignbyte(hi, lo, s) \
   static_cast<uint32_t>(((static_cast<uint64_t>(hi) << 32) | static_cast<uint32_t>(lo)) >> (8u * ((s) & 3u)))
+#define __builtin_amdgcn_rcpf(x) (1.0f / (x))
 #define __builtin_amdgcn_s_memtime() 0ull
 #define __builtin_amdgcn_wave_barrier() ((void)0)
 #define __builtin_amdgcn_s_waitcnt(x) ((void)0)
