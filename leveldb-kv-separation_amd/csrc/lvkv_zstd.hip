@@ -224,8 +224,18 @@ __device__ bool read_ncount(const uint8_t* in, uint32_t p, uint32_t end, uint32_
   return true;
 }
 
+// A decode entry as the table keeps it, symbol | nextState << 6 (u16:
+// symbols < 64, next states < 1024), expanded to symbol | nbBits << 8 |
+// baseline << 16: nbBits = log - highbit(nextState), baseline = (nextState
+// << nbBits) - (1 << log) (FSE_buildDTable's own formulas).
+__device__ __forceinline__ uint32_t fse_entry(uint32_t e16, uint32_t log) {
+  const uint32_t ns = e16 >> 6;
+  const uint32_t nb = log - (31u - __builtin_clz(ns));
+  return (e16 & 63u) | (nb << 8) | (((ns << nb) - (1u << log)) << 16);
+}
+
 // Spread and decode entries for counts[0, nsym) at accuracy `log` into
-// table (1 << log entries, <= 512). `nxt` holds the per-symbol next state,
+// table (1 << log u16 entries, <= 512). `nxt` holds the per-symbol next state,
 // `syms` (>= 512 bytes) the symbols in spread order.
 //
 // FSE_buildDTable walks the positions p_j = j * step mod size, skipping the
@@ -233,7 +243,7 @@ __device__ bool read_ncount(const uint8_t* in, uint32_t p, uint32_t end, uint32_
 // the k-th symbol of the counts laid end to end. Here every j at once: its
 // rank among the kept positions (ballot), the symbol of that rank (the
 // symbols' first ranks marked, then a running max), one scatter.
-__device__ bool build_fse(const int16_t* counts, uint32_t nsym, uint32_t log, uint32_t* table,
+__device__ bool build_fse(const int16_t* counts, uint32_t nsym, uint32_t log, uint16_t* table,
                           uint16_t* nxt, uint8_t* syms, uint32_t lane) {
   const uint32_t size = 1u << log;
   const uint64_t below = (uint64_t{1} << lane) - 1u;
@@ -295,7 +305,7 @@ __device__ bool build_fse(const int16_t* counts, uint32_t nsym, uint32_t log, ui
   for (uint32_t c = 0; c < size; c += 64) {
     const uint32_t u = c + lane;
     const bool in = u < size;
-    const uint32_t s = in ? (table[u] & 255u) : 0x1000u;
+    const uint32_t s = in ? (table[u] & 63u) : 0x1000u;
     uint64_t todo = __ballot(in), peers = 0;
     while (todo) {
       const uint32_t sl = __builtin_amdgcn_readlane(s, static_cast<uint32_t>(__builtin_ctzll(todo)));
@@ -308,9 +318,7 @@ __device__ bool build_fse(const int16_t* counts, uint32_t nsym, uint32_t log, ui
     const uint32_t ns = (in ? nxt[s] : 1u) + before;
     __builtin_amdgcn_s_waitcnt(0xc07f);  // every lane has read nxt before it moves
     if (in) {
-      const uint32_t nbits = log - (31u - __builtin_clz(ns));
-      const uint32_t base = (ns << nbits) - size;
-      table[u] = s | (nbits << 8) | (base << 16);
+      table[u] = static_cast<uint16_t>(s | (ns << 6));  // (fse_entry expands it)
       if (last) nxt[s] = static_cast<uint16_t>(ns + 1u);
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -341,10 +349,10 @@ struct Lds {
   uint16_t* huf;    // Huffman decode table: symbol | nbBits << 8 (2048; a 12-bit
                     // tree in split form, huf_table)
   uint8_t* hside;   // a 12-bit tree's second symbols of its split entries (128)
-  uint32_t* ll;     // FSE tables: 512 / 256 / 512 entries, and 64 for weights
-  uint32_t* of;
-  uint32_t* ml;
-  uint32_t* wt;
+  uint16_t* ll;     // FSE tables: 512 / 256 / 512 entries, and 64 for weights
+  uint16_t* of;     // (u16: symbol | nextState << 6, fse_entry)
+  uint16_t* ml;
+  uint16_t* wt;
   int16_t* cnt;     // normalized counts scratch (256: the weights' FSE may name 256)
   uint16_t* nxt;    // FSE next-state scratch (256)
   uint8_t* sym;     // FSE spread scratch (512)
@@ -358,7 +366,7 @@ __host__ __device__ constexpr uint32_t zstd_in_cap(uint32_t out_cap) {
 }
 __host__ __device__ constexpr uint32_t round16(uint32_t x) { return (x + 15u) & ~15u; }
 constexpr uint32_t kTabBytes =
-    2u * kHufEntries + 128u + 4u * (kFseLL + kFseOF + kFseML + kFseW) + 512u + 512u + 512u;
+    2u * kHufEntries + 128u + 2u * (kFseLL + kFseOF + kFseML + kFseW) + 512u + 512u + 512u;
 __host__ __device__ constexpr uint32_t zstd_lds_bytes(uint32_t out_cap) {
   return round16(zstd_in_cap(out_cap) + 16u + 4u) + round16(out_cap) + kTabBytes;
 }
@@ -380,14 +388,14 @@ __device__ __forceinline__ Lds lds_layout(uint8_t* smem, uint32_t in_bytes, uint
   o += 2u * kHufEntries;
   L.hside = smem + o;
   o += 128u;
-  L.ll = reinterpret_cast<uint32_t*>(smem + o);
-  o += 4u * kFseLL;
-  L.of = reinterpret_cast<uint32_t*>(smem + o);
-  o += 4u * kFseOF;
-  L.ml = reinterpret_cast<uint32_t*>(smem + o);
-  o += 4u * kFseML;
-  L.wt = reinterpret_cast<uint32_t*>(smem + o);
-  o += 4u * kFseW;
+  L.ll = reinterpret_cast<uint16_t*>(smem + o);
+  o += 2u * kFseLL;
+  L.of = reinterpret_cast<uint16_t*>(smem + o);
+  o += 2u * kFseOF;
+  L.ml = reinterpret_cast<uint16_t*>(smem + o);
+  o += 2u * kFseML;
+  L.wt = reinterpret_cast<uint16_t*>(smem + o);
+  o += 2u * kFseW;
   L.cnt = reinterpret_cast<int16_t*>(smem + o);
   o += 512u;
   L.nxt = reinterpret_cast<uint16_t*>(smem + o);
@@ -455,7 +463,7 @@ __device__ bool huf_weights(const Lds& L, uint32_t p, uint32_t end, uint32_t (&w
     // step is a readlane, a shift and an add (both states share the stream)
     const uint32_t lo = p + 1u + nc, hi = p + 1u + hb;
     if (hi <= lo || ldb(L.in, hi - 1) == 0) return *fail = kFHufWeights, false;
-    const uint32_t treg = L.wt[lane];
+    const uint32_t treg = fse_entry(L.wt[lane], log);
     // lane k + 1 holds the stream's dword k, lane 0 zeros: bit x of the
     // stream is bit x + 32 of the lanes' concatenation, and the bits below
     // its start (x < 0, at most 12 of them) read as zeros with no test
@@ -830,18 +838,21 @@ __device__ bool literals(const Lds& L, uint32_t p, uint32_t end, uint32_t cap, u
 // A sequence table by mode into `table`; *log, *used. Uniform.
 __device__ bool seq_table(const Lds& L, uint32_t p, uint32_t end, uint32_t mode,
                           const uint32_t* dflt, uint32_t dlog, uint32_t max_sym,
-                          uint32_t max_log, uint32_t* table, bool* have, uint32_t* log,
+                          uint32_t max_log, uint16_t* table, bool* have, uint32_t* log,
                           uint32_t* used, uint32_t lane, uint32_t* fail) {
   *used = 0;
   if (mode == 0) {  // the predefined table (tools/gen_zstd_tables.py)
-    for (uint32_t u = lane; u < (1u << dlog); u += 64) table[u] = dflt[u];
+    for (uint32_t u = lane; u < (1u << dlog); u += 64) {  // (to the u16 form)
+      const uint32_t e = dflt[u], nb = (e >> 8) & 255u;
+      table[u] = static_cast<uint16_t>((e & 255u) | ((((e >> 16) + (1u << dlog)) >> nb) << 6));
+    }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     *log = dlog;
   } else if (mode == 1) {
     if (p >= end) return *fail = kFRle, false;
     const uint32_t s = ldb(L.in, p);
     if (s > max_sym) return *fail = kFRle, false;
-    if (lane == 0) table[0] = s;
+    if (lane == 0) table[0] = static_cast<uint16_t>(s | (1u << 6));  // (log 0: nextState 1)
     __builtin_amdgcn_s_waitcnt(0xc07f);
     *log = 0;
     *used = 1;
@@ -896,16 +907,17 @@ __device__ __forceinline__ bool sequences(const Lds& L, RegBits& r, SeqState& S,
                                           uint32_t nseq, uint32_t nlit, const uint8_t* lits,
                                           uint32_t* op, uint32_t frame_start, uint32_t cap,
                                           uint32_t lane, uint32_t* fail) {
-  auto entry = [&](bool small, uint32_t reg, const uint32_t* t, uint32_t s) -> uint32_t {
+  auto entry = [&](bool small, uint32_t reg, const uint16_t* t, uint32_t lg, uint32_t s) -> uint32_t {
     if (Small || small) return __builtin_amdgcn_readlane(reg, s);
-    return uni(t[s]);
+    return fse_entry(uni(t[s]), lg);
   };
   uint32_t sl = rb_read(r, S.ll_log, lane), so = rb_read(r, S.of_log, lane),
            sm = rb_read(r, S.ml_log, lane);
   uint32_t lp = 0;
   for (uint32_t i = 0; i < nseq; ++i) {
-    const uint32_t el = entry(T.sll, T.ll, L.ll, sl), eo = entry(T.sof, T.of, L.of, so),
-                   em = entry(T.sml, T.ml, L.ml, sm);
+    const uint32_t el = entry(T.sll, T.ll, L.ll, S.ll_log, sl),
+                   eo = entry(T.sof, T.of, L.of, S.of_log, so),
+                   em = entry(T.sml, T.ml, L.ml, S.ml_log, sm);
     const uint32_t llc = el & 255u, ofc = eo & 255u, mlc = em & 255u;
     const uint32_t lc = __builtin_amdgcn_readlane(S.llcode, llc);
     const uint32_t mc = __builtin_amdgcn_readlane(S.mlcode, mlc);
@@ -1040,7 +1052,8 @@ __device__ bool comp_block(const Lds& L, uint32_t p, uint32_t end, uint32_t* op,
   // block's) are read from registers (v_readlane), larger ones from LDS; the
   // loop is built twice so that the common all-small case carries no
   // per-table branch (and no flags to spill)
-  const uint32_t tll = L.ll[lane], tof = L.of[lane], tml = L.ml[lane];
+  const uint32_t tll = fse_entry(L.ll[lane], S.ll_log), tof = fse_entry(L.of[lane], S.of_log),
+                 tml = fse_entry(L.ml[lane], S.ml_log);
   __builtin_amdgcn_s_waitcnt(0xc07f);
   const Tabs T{tll, tof, tml, S.ll_log <= 6u, S.of_log <= 6u, S.ml_log <= 6u};
   if (T.sll && T.sof && T.sml)
