@@ -223,6 +223,24 @@ def test_device_compress_ragged_against_oracle(lvkv, gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("level", [2, -1, -5])
+def test_device_compress_ragged_other_levels(lvkv, gpu, level):
+    """400 blocks of 0-20 KiB at levels 2 (the fast strategy below 128 KiB)
+    and -1, -5 (literal compression off): the device's frame is the oracle's
+    at every one."""
+    import torch
+    rng = np.random.default_rng(400 + level)
+    blobs = _fuzz_inputs(rng, 340, 6000) + _fuzz_inputs(rng, 60, 20481)
+    src, off, ln = _pack(torch, gpu, blobs, skew=3)
+    dst, doff, dlen, st = lvkv.zstd_compress(src, off, ln, level=level, max_len=20480)
+    torch.cuda.synchronize()
+    assert st.cpu().tolist() == [lvkv.ZSTD_OK] * len(blobs)
+    got = _unpack(dst, doff, dlen)
+    bad = [k for k, (x, g) in enumerate(zip(blobs, got)) if g != ze.compress(x, level)]
+    assert not bad, f"level {level}: device frame differs from the oracle on {bad[:20]} ({len(bad)})"
+
+
+@pytest.mark.gpu
 def test_device_compress_statuses(lvkv, gpu):
     import torch
     from tools.db_bench_data import block_batch
