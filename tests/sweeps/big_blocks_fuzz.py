@@ -6,7 +6,7 @@ max_ulen 4,096 so that nearly every block takes the HBM-output kernels, and
 compared with its input. Prints one JSON line; writes
 gpurun_out/big_blocks_fuzz.json.
 
-    python tools/big_blocks_fuzz.py [M] [seed]
+    python tests/sweeps/big_blocks_fuzz.py [M] [seed]
 """
 from __future__ import annotations
 
@@ -16,7 +16,7 @@ from pathlib import Path
 
 import numpy as np
 
-REPO = Path(__file__).resolve().parent.parent
+REPO = Path(__file__).resolve().parent.parent.parent
 sys.path.insert(0, str(REPO))
 sys.path.insert(0, str(REPO / "oracle"))
 

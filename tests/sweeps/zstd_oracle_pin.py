@@ -1,8 +1,9 @@
 """Pins oracle/zstd_encoder.py to libzstd 1.4.9 (this container's
 /opt/conda/lib) on many fresh inputs, driven as port::Zstd_Compress drives
-the library (CPU; evidence beside tests/test_zstd_write.py's 400-input fuzz).
+the library (CPU; evidence beside tests/test_zstd_write.py's 400-input fuzz; writes
+gpurun_out/zstd_oracle_pin.json).
 
-    python tools/zstd_oracle_pin.py [N] [seed] [levels, comma-separated]
+    python tests/sweeps/zstd_oracle_pin.py [N] [seed] [levels, comma-separated]
 """
 from __future__ import annotations
 
@@ -12,7 +13,7 @@ from pathlib import Path
 
 import numpy as np
 
-REPO = Path(__file__).resolve().parent.parent
+REPO = Path(__file__).resolve().parent.parent.parent
 sys.path.insert(0, str(REPO))
 sys.path.insert(0, str(REPO / "tests"))
 sys.path.insert(0, str(REPO / "oracle"))
@@ -42,4 +43,5 @@ def main():
 
 if __name__ == "__main__":
     r = main()
-    (REPO / "profiles" / "r06_zstd_oracle_pin.json").write_text(json.dumps(r, indent=1))
+    (REPO / "gpurun_out").mkdir(exist_ok=True)
+    (REPO / "gpurun_out" / "zstd_oracle_pin.json").write_text(json.dumps(r, indent=1))

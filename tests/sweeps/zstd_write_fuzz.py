@@ -5,7 +5,7 @@ skewed, repeats, key/value entries; 0-20 KiB), every device frame compared
 byte for byte with oracle/zstd_encoder.py and decoded back by the device
 decoder. Prints one JSON line; writes gpurun_out/zstd_write_fuzz.json.
 
-    python tools/zstd_write_fuzz.py [N] [seed] [levels, comma-separated; default 1,-1]
+    python tests/sweeps/zstd_write_fuzz.py [N] [seed] [levels, comma-separated; default 1,-1]
 """
 from __future__ import annotations
 
@@ -16,7 +16,7 @@ from pathlib import Path
 
 import numpy as np
 
-REPO = Path(__file__).resolve().parent.parent
+REPO = Path(__file__).resolve().parent.parent.parent
 sys.path.insert(0, str(REPO))
 sys.path.insert(0, str(REPO / "tests"))
 sys.path.insert(0, str(REPO / "oracle"))
